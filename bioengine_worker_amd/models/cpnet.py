@@ -1,0 +1,321 @@
+"""Cellpose CPnet (cyto3-style residual U-Net with style vector), MI355X-native.
+
+Two views of the same network:
+
+* :class:`CPnet` — an ``nn.Module`` whose module tree and parameter names mirror cellpose 3's
+  ``CPnet`` (``downsample.down.res_down_k``, ``upsample.up.res_up_k``, ``make_style``, ``output``,
+  ``diam_mean``/``diam_labels``), so a cellpose ``state_dict`` loads unchanged.  It is the fp32
+  PyTorch oracle and the autograd path for training.  The architecture is re-derived from the
+  cellpose algorithm (the reference only reaches it through the EXT ``cellpose==3.1.1.2`` pin,
+  ``apps/model-runner/runtime_deployment.py:19``; cyto3 named at
+  ``apps/cellpose-finetuning/main.py:2234``).
+* :class:`CPnetEngine` — the inference engine: NHWC bf16 activations, every conv a single fused
+  HIP kernel launch (BN fold + ReLU + style shift + skip add + maxpool/upsample in the loader,
+  residual add + bias in the epilogue), style vector from a fused HIP reduction.
+
+Default channel plan: ``nbase = [2, 32, 64, 128, 256]``, 3 outputs (dY, dX, cellprob).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import conv as convops
+from ..ops import style as styleops
+
+
+def _norm(c: int, kind: str) -> nn.Module:
+    if kind == "batch":
+        return nn.BatchNorm2d(c, eps=1e-5, momentum=0.05)
+    if kind == "group":
+        g = 8 if c % 8 == 0 else 1
+        return nn.GroupNorm(g, c, eps=1e-5)
+    raise ValueError(kind)
+
+
+def batchconv(cin, cout, sz, norm="batch"):
+    return nn.Sequential(_norm(cin, norm), nn.ReLU(inplace=True), nn.Conv2d(cin, cout, sz, padding=sz // 2))
+
+
+def batchconv0(cin, cout, sz, norm="batch"):
+    return nn.Sequential(_norm(cin, norm), nn.Conv2d(cin, cout, sz, padding=sz // 2))
+
+
+class resdown(nn.Module):
+    def __init__(self, cin, cout, sz, norm="batch"):
+        super().__init__()
+        self.conv = nn.Sequential()
+        self.proj = batchconv0(cin, cout, 1, norm)
+        for t in range(4):
+            self.conv.add_module(f"conv_{t}", batchconv(cin if t == 0 else cout, cout, sz, norm))
+
+    def forward(self, x):
+        x = self.proj(x) + self.conv[1](self.conv[0](x))
+        x = x + self.conv[3](self.conv[2](x))
+        return x
+
+
+class downsample(nn.Module):
+    def __init__(self, nbase, sz, norm="batch"):
+        super().__init__()
+        self.down = nn.Sequential()
+        self.maxpool = nn.MaxPool2d(2, 2)
+        for n in range(len(nbase) - 1):
+            self.down.add_module(f"res_down_{n}", resdown(nbase[n], nbase[n + 1], sz, norm))
+
+    def forward(self, x):
+        xd = []
+        for n in range(len(self.down)):
+            y = self.maxpool(xd[n - 1]) if n > 0 else x
+            xd.append(self.down[n](y))
+        return xd
+
+
+class batchconvstyle(nn.Module):
+    def __init__(self, cin, cout, style_channels, sz, norm="batch"):
+        super().__init__()
+        self.concatenation = False
+        self.conv = batchconv(cin, cout, sz, norm)
+        self.full = nn.Linear(style_channels, cout)
+
+    def forward(self, style, x, y=None):
+        if y is not None:
+            x = x + y
+        feat = self.full(style)
+        return self.conv(x + feat.unsqueeze(-1).unsqueeze(-1))
+
+
+class resup(nn.Module):
+    def __init__(self, cin, cout, style_channels, sz, norm="batch"):
+        super().__init__()
+        self.conv = nn.Sequential()
+        self.conv.add_module("conv_0", batchconv(cin, cout, sz, norm))
+        self.conv.add_module("conv_1", batchconvstyle(cout, cout, style_channels, sz, norm))
+        self.conv.add_module("conv_2", batchconvstyle(cout, cout, style_channels, sz, norm))
+        self.conv.add_module("conv_3", batchconvstyle(cout, cout, style_channels, sz, norm))
+        self.proj = batchconv0(cin, cout, 1, norm)
+
+    def forward(self, x, y, style):
+        x = self.proj(x) + self.conv[1](style, self.conv[0](x), y=y)
+        x = x + self.conv[3](style, self.conv[2](style, x))
+        return x
+
+
+class make_style(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.flatten = nn.Flatten()
+
+    def forward(self, x0):
+        style = F.avg_pool2d(x0, kernel_size=x0.shape[2:])
+        style = self.flatten(style)
+        return style / torch.sum(style ** 2, dim=1, keepdim=True) ** 0.5
+
+
+class upsample(nn.Module):
+    def __init__(self, nbase, sz, norm="batch"):
+        super().__init__()
+        self.upsampling = nn.Upsample(scale_factor=2, mode="nearest")
+        self.up = nn.Sequential()
+        for n in range(1, len(nbase)):
+            self.up.add_module(f"res_up_{n - 1}", resup(nbase[n], nbase[n - 1], nbase[-1], sz, norm))
+
+    def forward(self, style, xd):
+        x = self.up[-1](xd[-1], xd[-1], style)
+        for n in range(len(self.up) - 2, -1, -1):
+            x = self.upsampling(x)
+            x = self.up[n](x, xd[n], style)
+        return x
+
+
+class CPnet(nn.Module):
+    """cellpose-3 compatible CPnet (module/parameter names match cellpose ``CPnet``)."""
+
+    def __init__(self, nbase=(2, 32, 64, 128, 256), nout=3, sz=3, diam_mean=30.0, norm="batch", style_on=True):
+        super().__init__()
+        nbase = list(nbase)
+        self.nbase = nbase
+        self.nout = nout
+        self.sz = sz
+        self.norm_kind = norm
+        self.style_on = style_on
+        self.downsample = downsample(nbase, sz, norm)
+        nbaseup = nbase[1:] + [nbase[-1]]
+        self.upsample = upsample(nbaseup, sz, norm)
+        self.make_style = make_style()
+        self.output = batchconv(nbaseup[0], nout, 1, norm)
+        self.diam_mean = nn.Parameter(torch.ones(1) * diam_mean, requires_grad=False)
+        self.diam_labels = nn.Parameter(torch.ones(1) * diam_mean, requires_grad=False)
+
+    @property
+    def nchan(self):
+        return self.nbase[0]
+
+    def forward(self, data):
+        T0 = self.downsample(data)
+        style = self.make_style(T0[-1])
+        style0 = style
+        if not self.style_on:
+            style = style * 0
+        T1 = self.upsample(style, T0)
+        T1 = self.output(T1)
+        return T1, style0, T0
+
+    def randomize_(self, seed: int = 0) -> "CPnet":
+        """Random-init weights *and* BN running statistics (the benches run on random-init models)."""
+        g = torch.Generator().manual_seed(seed)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                fan_in = m.in_channels * m.kernel_size[0] * m.kernel_size[1]
+                m.weight.data = torch.randn(m.weight.shape, generator=g) * (1.0 / fan_in) ** 0.5
+                if m.bias is not None:
+                    m.bias.data = torch.randn(m.bias.shape, generator=g) * 0.01
+            elif isinstance(m, nn.Linear):
+                m.weight.data = torch.randn(m.weight.shape, generator=g) * (1.0 / m.in_features) ** 0.5
+                m.bias.data = torch.randn(m.bias.shape, generator=g) * 0.01
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.data = 1.0 + 0.1 * torch.randn(m.weight.shape, generator=g)
+                m.bias.data = 0.1 * torch.randn(m.bias.shape, generator=g)
+                m.running_mean.data = 0.1 * torch.randn(m.running_mean.shape, generator=g)
+                m.running_var.data = 1.0 + 0.1 * torch.rand(m.running_var.shape, generator=g)
+            elif isinstance(m, nn.GroupNorm):
+                m.weight.data = 1.0 + 0.1 * torch.randn(m.weight.shape, generator=g)
+                m.bias.data = 0.1 * torch.randn(m.bias.shape, generator=g)
+        return self
+
+
+# ----------------------------------------------------------------------------------------------
+# Fused inference engine
+# ----------------------------------------------------------------------------------------------
+
+def _bn_fold(bn: nn.Module, device) -> tuple[torch.Tensor, torch.Tensor]:
+    if isinstance(bn, nn.BatchNorm2d):
+        s = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+        t = bn.bias.detach().float() - bn.running_mean.detach().float() * s
+        return s.to(device).contiguous(), t.to(device).contiguous()
+    raise TypeError("CPnetEngine folds eval-mode BatchNorm only; GroupNorm nets run the autograd path")
+
+
+def _pad_vec(v: torch.Tensor, n: int, fill: float) -> torch.Tensor:
+    if v.numel() == n:
+        return v
+    out = torch.full((n,), fill, dtype=v.dtype, device=v.device)
+    out[: v.numel()] = v
+    return out
+
+
+class _FConv:
+    """One fused conv: packed weights + folded pre-activation affine."""
+
+    def __init__(self, seq: nn.Sequential, relu: bool, device, cin_pad=None, cout_pad_to=None):
+        bn, conv = seq[0], seq[-1]
+        self.pc = convops.PackedConv.from_weight(conv.weight, conv.bias, cin_pad=cin_pad, cout_pad_to=cout_pad_to).to(device)
+        s, t = _bn_fold(bn, device)
+        self.scale = _pad_vec(s, self.pc.cin_pad, 0.0)
+        self.shift = _pad_vec(t, self.pc.cin_pad, 0.0)
+        self.relu = relu
+
+    def __call__(self, x, *, x2=None, shift=None, residual=None, inmode="none", out_nchw_f32=False, cout_valid=None):
+        return convops.fused_conv2d(x, self.pc, x2=x2, scale=self.scale, shift=self.shift if shift is None else shift,
+                                    relu=self.relu, residual=residual, inmode=inmode, out_nchw_f32=out_nchw_f32,
+                                    cout_valid=cout_valid)
+
+
+class CPnetEngine:
+    """Inference engine for an eval-mode (BatchNorm) :class:`CPnet`.
+
+    ``forward(x)``: ``x`` NHWC bf16 [B, H, W, cin_pad] (H, W multiples of 8) ->
+    (flows+cellprob NCHW fp32 [B, nout, H, W], style fp32 [B, nbase[-1]]).
+    """
+
+    def __init__(self, net: CPnet, device):
+        net = net.eval()
+        self.device = torch.device(device)
+        self.nout = net.nout
+        self.nchan = net.nchan
+        self.cin_pad = convops._round_up(net.nchan, 8)
+        d = self.device
+        self.down = []
+        for n, blk in enumerate(net.downsample.down):
+            cin_pad = self.cin_pad if n == 0 else None
+            self.down.append(dict(
+                proj=_FConv(blk.proj, False, d, cin_pad),
+                c0=_FConv(blk.conv[0], True, d, cin_pad),
+                c1=_FConv(blk.conv[1], True, d),
+                c2=_FConv(blk.conv[2], True, d),
+                c3=_FConv(blk.conv[3], True, d),
+            ))
+        self.up = []
+        for blk in net.upsample.up:
+            e = dict(proj=_FConv(blk.proj, False, d), c0=_FConv(blk.conv[0], True, d))
+            for k in (1, 2, 3):
+                bcs = blk.conv[k]
+                e[f"c{k}"] = _FConv(bcs.conv, True, d)
+                e[f"full{k}"] = (bcs.full.weight.detach().float().to(d), bcs.full.bias.detach().float().to(d))
+            self.up.append(e)
+        self.out = _FConv(net.output, True, d, cout_pad_to=16)
+        self.style_on = net.style_on
+        # Stack every style Linear into one GEMM: feats = style @ Wall^T + ball, then per-conv
+        # shift[n, c] = feat[n, c] * s[c] + t[c]  (batchconvstyle folded into the next conv prologue).
+        ws, bs, ss, ts = [], [], [], []
+        self._feat_slices = []
+        off = 0
+        for i, e in enumerate(self.up):
+            for k in (1, 2, 3):
+                w, b = e[f"full{k}"]
+                conv = e[f"c{k}"]
+                ws.append(w); bs.append(b)
+                ss.append(conv.scale[: w.shape[0]]); ts.append(conv.shift[: w.shape[0]])
+                self._feat_slices.append((i, k, off, w.shape[0]))
+                off += w.shape[0]
+        self.style_w = torch.cat(ws, 0).contiguous()
+        self.style_b = torch.cat(bs, 0).contiguous()
+        self.style_s = torch.cat(ss, 0).contiguous()
+        self.style_t = torch.cat(ts, 0).contiguous()
+
+    def _style_shifts(self, style: torch.Tensor) -> dict:
+        st = style if self.style_on else torch.zeros_like(style)
+        shifts_all = styleops.style_shifts(st, self.style_w, self.style_b, self.style_s, self.style_t)
+        out = {}
+        for (i, k, off, c) in self._feat_slices:
+            out[(i, k)] = shifts_all[:, off: off + c].contiguous()
+        return out
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor):
+        xd = []
+        h = x
+        for n, e in enumerate(self.down):
+            im = "pool2" if n > 0 else "none"
+            src = x if n == 0 else xd[-1]
+            proj = e["proj"](src, inmode=im)
+            h = e["c0"](src, inmode=im)
+            x1 = e["c1"](h, residual=proj)
+            h = e["c2"](x1)
+            xd.append(e["c3"](h, residual=x1))
+        style = styleops.make_style(xd[-1])
+        shifts = self._style_shifts(style)
+        nup = len(self.up)
+        xcur = xd[-1]
+        for i in range(nup - 1, -1, -1):
+            e = self.up[i]
+            im = "none" if i == nup - 1 else "up2"
+            y = xd[i] if i < nup - 1 else xd[-1]
+            proj = e["proj"](xcur, inmode=im)
+            h0 = e["c0"](xcur, inmode=im)
+            x1 = e["c1"](h0, x2=y, shift=shifts[(i, 1)], residual=proj)
+            h2 = e["c2"](x1, shift=shifts[(i, 2)])
+            xcur = e["c3"](h2, shift=shifts[(i, 3)], residual=x1)
+        y = self.out(xcur, out_nchw_f32=True, cout_valid=self.nout)
+        return y, style
+
+    __call__ = forward
+
+
+def to_nhwc_input(x_nchw: torch.Tensor, cin_pad: int) -> torch.Tensor:
+    """NCHW float -> NHWC bf16 with channels zero-padded to ``cin_pad``."""
+    N, C, H, W = x_nchw.shape
+    out = torch.zeros(N, H, W, cin_pad, dtype=torch.bfloat16, device=x_nchw.device)
+    out[..., :C] = x_nchw.permute(0, 2, 3, 1)
+    return out

@@ -1,0 +1,198 @@
+"""Fused pre-activation NHWC conv2d (HIP kernel ``csrc/kernels/conv2d_nhwc.hip``).
+
+``fused_conv2d`` computes::
+
+    out = conv_k( relu?( (inxform(x) [+ x2]) * scale[c] + shift[n, c] ) ) [+ bias] [+ residual]
+
+with ``inxform`` in {identity, nearest-upsample x2, maxpool 2x2}.  This covers every conv in the
+Cellpose CPnet (cellpose ``batchconv``/``batchconv0``/``batchconvstyle``: BN -> ReLU -> Conv, the
+style-vector add and the skip add; reference reaches these via cellpose EXT modules, SURVEY.md §2.5
+K1) and the pre-activation blocks of BioImage.IO U-Nets.
+
+Activations are NHWC bf16 (channels padded to a multiple of 8); weights are repacked once into the
+kernel's tap-major K layout by :class:`PackedConv`.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+
+INMODES = {"none": 0, "up2": 1, "pool2": 2}
+
+
+def _round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+@dataclass
+class PackedConv:
+    """Conv weights repacked for the MFMA kernel.
+
+    ``wp``  : bf16 [cout_pad, nchunk, KP] (device tensor), K index = tap * ck + c within a chunk.
+    ``w``   : fp32 [cout, cin, ks, ks] original weights (reference path / re-packing).
+    """
+
+    w: torch.Tensor
+    bias: torch.Tensor | None
+    ks: int
+    cin: int
+    cin_pad: int
+    cout: int
+    cout_pad: int
+    ck: int
+    tco: int
+    kp: int
+    wp: torch.Tensor | None = None
+
+    @staticmethod
+    def choose(cin_pad: int, cout: int) -> tuple[int, int]:
+        ck = 8 if cin_pad % 32 else 32
+        if cout <= 16:
+            tco = 16
+        elif cout <= 32:
+            tco = 32
+        else:
+            tco = 64
+        return ck, tco
+
+    @classmethod
+    def from_weight(cls, weight: torch.Tensor, bias: torch.Tensor | None = None, cin_pad: int | None = None,
+                    cout_pad_to: int | None = None) -> "PackedConv":
+        cout, cin, ks, ks2 = weight.shape
+        assert ks == ks2 and ks in (1, 3), "only 1x1 / 3x3 convs"
+        cin_pad = cin_pad or _round_up(cin, 8)
+        if cin_pad % 32 and cin_pad != 8:
+            cin_pad = _round_up(cin_pad, 32)
+        ck, tco = cls.choose(cin_pad, cout)
+        cout_k = max(cout, cout_pad_to or 0)
+        cout_pad = _round_up(cout_k, tco)
+        kp = ((ks * ks * ck + 31) // 32) * 32
+        w = weight.detach().float()
+        pc = cls(w=w, bias=None if bias is None else bias.detach().float(), ks=ks, cin=cin, cin_pad=cin_pad,
+                 cout=cout, cout_pad=cout_pad, ck=ck, tco=tco, kp=kp)
+        pc.wp = pc._pack(w)
+        return pc
+
+    def _pack(self, w: torch.Tensor) -> torch.Tensor:
+        ks, ck = self.ks, self.ck
+        nchunk = self.cin_pad // ck
+        wz = torch.zeros(self.cout_pad, self.cin_pad, ks, ks, dtype=torch.float32, device=w.device)
+        wz[: self.cout, : self.cin] = w
+        # [Cout, ks, ks, Cin] -> [Cout, taps, nchunk, ck] -> [Cout, nchunk, taps*ck]
+        t = wz.permute(0, 2, 3, 1).reshape(self.cout_pad, ks * ks, nchunk, ck)
+        t = t.permute(0, 2, 1, 3).reshape(self.cout_pad, nchunk, ks * ks * ck)
+        if self.kp > ks * ks * ck:
+            t = F.pad(t, (0, self.kp - ks * ks * ck))
+        return t.to(torch.bfloat16).contiguous()
+
+    def to(self, device) -> "PackedConv":
+        self.w = self.w.to(device)
+        if self.bias is not None:
+            self.bias = self.bias.to(device)
+        if self.wp is not None:
+            self.wp = self.wp.to(device)
+        return self
+
+    def refresh(self, weight: torch.Tensor, bias: torch.Tensor | None = None) -> None:
+        """Re-pack after a weight update (training)."""
+        self.w = weight.detach().float()
+        if bias is not None:
+            self.bias = bias.detach().float()
+        self.wp = self._pack(self.w)
+
+
+register = _native.register_hip_signatures
+
+
+def _act_ref(x, x2, scale, shift, relu, inmode):
+    # x: NHWC float
+    xt = x.permute(0, 3, 1, 2)
+    if inmode == "up2":
+        xt = F.interpolate(xt, scale_factor=2, mode="nearest")
+    elif inmode == "pool2":
+        xt = F.max_pool2d(xt, 2, 2)
+    if x2 is not None:
+        xt = xt + x2.permute(0, 3, 1, 2).float()
+    C = xt.shape[1]
+    if scale is not None:
+        xt = xt * scale.view(1, C, 1, 1)
+    if shift is not None:
+        sh = shift.view(-1, C, 1, 1) if shift.dim() == 2 else shift.view(1, C, 1, 1)
+        xt = xt + sh
+    if relu:
+        xt = torch.relu(xt)
+    return xt
+
+
+def fused_conv2d_ref(x, pc: PackedConv, x2=None, scale=None, shift=None, relu=False, residual=None,
+                     inmode="none", out_nchw_f32=False, cout_valid=None, act_dtype=torch.bfloat16):
+    """PyTorch fp32 reference (and CPU path).  The activated input is rounded to ``act_dtype``
+    exactly like the kernel's LDS staging, so GPU-vs-reference differences are accumulation-order only."""
+    a = _act_ref(x.float(), x2, scale, shift, relu, inmode)
+    if act_dtype is not None:
+        a = a.to(act_dtype).float()
+    w = pc.w.to(a.device)
+    if w.shape[1] < a.shape[1]:
+        w = F.pad(w, (0, 0, 0, 0, 0, a.shape[1] - w.shape[1]))
+    wq = w.to(torch.bfloat16).float() if act_dtype is not None else w
+    y = F.conv2d(a, wq, None, padding=pc.ks // 2)
+    if pc.bias is not None:
+        y = y + pc.bias.to(y.device).view(1, -1, 1, 1)
+    if out_nchw_f32:
+        cv = cout_valid or pc.cout
+        return y[:, :cv].contiguous()
+    y = y.permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype).contiguous()
+
+
+def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=None, relu=False, residual=None,
+                 inmode: str = "none", out_nchw_f32: bool = False, cout_valid: int | None = None) -> torch.Tensor:
+    """Fused conv on NHWC activations.  ``x`` is [N, Hs, Ws, Cin_pad] bf16 (GPU) or any float (CPU)."""
+    N, Hs, Ws, Cin = x.shape
+    if inmode == "up2":
+        H, W = Hs * 2, Ws * 2
+    elif inmode == "pool2":
+        H, W = Hs // 2, Ws // 2
+    else:
+        H, W = Hs, Ws
+    if not x.is_cuda:
+        return fused_conv2d_ref(x, pc, x2, scale, shift, relu, residual, inmode, out_nchw_f32, cout_valid,
+                                act_dtype=torch.bfloat16 if x.dtype == torch.bfloat16 else None)
+    assert x.dtype == torch.bfloat16 and x.is_contiguous(), "fused_conv2d expects contiguous NHWC bf16"
+    assert Cin == pc.cin_pad, f"input channels {Cin} != packed cin {pc.cin_pad}"
+    if pc.wp.device != x.device:
+        pc.to(x.device)
+    cout_valid = cout_valid or pc.cout
+    if out_nchw_f32:
+        out = torch.empty(N, cout_valid, H, W, device=x.device, dtype=torch.float32)
+        cout_store = pc.cout_pad
+    else:
+        assert pc.cout % 4 == 0
+        out = torch.empty(N, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
+        cout_store = pc.cout
+    if x2 is not None:
+        assert x2.shape == (N, H, W, Cin) and x2.dtype == torch.bfloat16 and x2.is_contiguous()
+    if residual is not None:
+        assert residual.shape == (N, H, W, pc.cout) and residual.dtype == torch.bfloat16 and residual.is_contiguous()
+    if scale is not None:
+        assert scale.dtype == torch.float32 and scale.numel() == Cin
+    pshift_ns = 0
+    if shift is not None:
+        assert shift.dtype == torch.float32 and shift.is_contiguous()
+        pshift_ns = Cin if shift.dim() == 2 else 0
+        if shift.dim() == 2:
+            assert shift.shape == (N, Cin)
+    _native.call(
+        "be_conv2d_nhwc",
+        _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns, int(bool(relu)),
+        _native.ptr(pc.wp), _native.ptr(pc.bias), _native.ptr(residual), _native.ptr(out),
+        N, H, W, Hs, Ws, Cin, cout_store, cout_valid, pc.ks, pc.ck, pc.tco, INMODES[inmode], int(out_nchw_f32),
+        _native.stream(x.device),
+    )
+    return out

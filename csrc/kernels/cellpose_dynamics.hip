@@ -1,0 +1,229 @@
+// Cellpose mask recovery on the GPU: flow following + histogram seeds + seed expansion + labels.
+//
+// Semantics follow the Cellpose algorithm (cellpose 3 dynamics.compute_masks / follow_flows /
+// get_masks_torch, EXT; invoked by the reference through model.eval(..., niter, cellprob_threshold)
+// at apps/cellpose-finetuning/main.py:3559-3567 and the model-runner cellpose pin), re-derived and
+// checked against bioengine_worker_amd/cellpose/reference.py.  SURVEY.md §2.5 K3/K4.
+//
+// MI355X mapping:
+//  * follow_flows: one lane per foreground pixel runs all `niter` Euler steps with its position in
+//    registers; the (dy, dx) field is an interleaved float2 image (one 8-byte gather per bilinear
+//    corner) that stays L2/MALL-resident across the steps.  The end point is binned straight into
+//    the padded histogram with an integer atomic, so no point list round-trips through HBM.
+//  * seeds: 5x5 local-max test on the histogram, compacted with one atomic per seed into a per-image
+//    key list (count << 32 | raster index) that torch.sort orders exactly like cellpose's argsort.
+//  * expansion: one wave per seed, its 11x11 window in LDS, 5 dilations, labels committed with
+//    atomicMax (seeds are rank-ordered by count, so "last writer wins" == max rank).
+#include "common.h"
+
+namespace {
+
+constexpr int RPAD = 20;
+
+__device__ __forceinline__ float2 ldflow(const float2* __restrict__ f, int H, int W, int y, int x) {
+  if (y < 0 || y >= H || x < 0 || x >= W) return make_float2(0.f, 0.f);
+  return f[y * W + x];
+}
+
+// flow2: [B, H, W] float2 (dy, dx) already masked by cellprob > thr and divided by 5.
+// fg: [B, H, W] uint8.  hist: [B, H+2R, W+2R] int32 (zeroed).  pos: [B, H, W] int32 (-1 for bg).
+__global__ __launch_bounds__(256) void follow_flows_kernel(const float2* __restrict__ flow2, const uint8_t* __restrict__ fg,
+                                                           int* __restrict__ hist, int* __restrict__ pos, int B, int H,
+                                                           int W, int niter) {
+  const int HW = H * W;
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)B * HW) return;
+  const int b = (int)(gid / HW);
+  const int pix = (int)(gid % HW);
+  if (!fg[gid]) {
+    pos[gid] = -1;
+    return;
+  }
+  const float2* f = flow2 + (size_t)b * HW;
+  float py = (float)(pix / W), px = (float)(pix % W);
+  const float sy_scale = (H > 1) ? (float)H / (float)(H - 1) : 0.f;
+  const float sx_scale = (W > 1) ? (float)W / (float)(W - 1) : 0.f;
+  const float ymax = (float)(H - 1), xmax = (float)(W - 1);
+  for (int t = 0; t < niter; ++t) {
+    // grid_sample(align_corners=False) position for normalised coordinate 2p/(L-1)-1
+    const float sy = py * sy_scale - 0.5f;
+    const float sx = px * sx_scale - 0.5f;
+    const float fy = floorf(sy), fx = floorf(sx);
+    const int y0 = (int)fy, x0 = (int)fx;
+    const float wy = sy - fy, wx = sx - fx;
+    const float2 a = ldflow(f, H, W, y0, x0);
+    const float2 bq = ldflow(f, H, W, y0, x0 + 1);
+    const float2 c = ldflow(f, H, W, y0 + 1, x0);
+    const float2 d = ldflow(f, H, W, y0 + 1, x0 + 1);
+    const float w00 = (1.f - wy) * (1.f - wx), w01 = (1.f - wy) * wx, w10 = wy * (1.f - wx), w11 = wy * wx;
+    const float dy = a.x * w00 + bq.x * w01 + c.x * w10 + d.x * w11;
+    const float dx = a.y * w00 + bq.y * w01 + c.y * w10 + d.y * w11;
+    py = fminf(fmaxf(py + dy, 0.f), ymax);
+    px = fminf(fmaxf(px + dx, 0.f), xmax);
+  }
+  const int Wp = W + 2 * RPAD;
+  int iy = (int)py + RPAD, ix = (int)px + RPAD;
+  iy = min(max(iy, 0), H + RPAD - 1);
+  ix = min(max(ix, 0), W + RPAD - 1);
+  const int lin = iy * Wp + ix;
+  pos[gid] = lin;
+  atomicAdd(hist + (size_t)b * (H + 2 * RPAD) * Wp + lin, 1);
+}
+
+// Seeds: h > 10 and h == max over the 5x5 neighbourhood (zero outside).
+__global__ __launch_bounds__(256) void seeds_kernel(const int* __restrict__ hist, int B, int Hp, int Wp,
+                                                    long long* __restrict__ keys, int* __restrict__ nseeds, int cap) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int HWp = Hp * Wp;
+  if (gid >= (long long)B * HWp) return;
+  const int b = (int)(gid / HWp), lin = (int)(gid % HWp);
+  const int* h = hist + (size_t)b * HWp;
+  const int v = h[lin];
+  if (v <= 10) return;
+  const int y = lin / Wp, x = lin % Wp;
+  int m = 0;
+  for (int dy = -2; dy <= 2; ++dy) {
+    const int yy = y + dy;
+    if (yy < 0 || yy >= Hp) continue;
+    for (int dx = -2; dx <= 2; ++dx) {
+      const int xx = x + dx;
+      if (xx < 0 || xx >= Wp) continue;
+      m = max(m, h[yy * Wp + xx]);
+    }
+  }
+  if (v < m) return;
+  const int k = atomicAdd(nseeds + b, 1);
+  if (k < cap) keys[(size_t)b * cap + k] = ((long long)v << 32) | (long long)lin;
+}
+
+// One wave per seed: 11x11 window of (hist > 2), 5 dilations from the centre, commit rank+1.
+__global__ __launch_bounds__(256) void expand_kernel(const int* __restrict__ hist, const long long* __restrict__ keys_sorted,
+                                                     const int* __restrict__ nseeds, int B, int Hp, int Wp, int cap,
+                                                     int kmax, int* __restrict__ M1) {
+  __shared__ uint8_t win[4][2][128];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long sid = (long long)blockIdx.x * 4 + wave;  // seed slot = b * kmax + k
+  const int b = (int)(sid / kmax), k = (int)(sid % kmax);
+  const bool active = (b < B) && (k < min(nseeds[b], cap));
+  int sy = 0, sx = 0;
+  const int* h = hist + (size_t)b * Hp * Wp;
+  if (active) {
+    const long long key = keys_sorted[(size_t)b * cap + k];
+    const int lin = (int)(key & 0xffffffffLL);
+    sy = lin / Wp;
+    sx = lin % Wp;
+  }
+  uint8_t* cur = win[wave][0];
+  uint8_t* nxt = win[wave][1];
+  bool sup[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int c = lane + 64 * r;
+    sup[r] = false;
+    if (active && c < 121) {
+      const int yy = sy - 5 + c / 11, xx = sx - 5 + c % 11;
+      sup[r] = (yy >= 0 && yy < Hp && xx >= 0 && xx < Wp) && h[yy * Wp + xx] > 2;
+    }
+    if (c < 128) cur[c] = (c == 60) ? 1 : 0;  // centre (5,5)
+  }
+  __syncthreads();
+  for (int it = 0; it < 5; ++it) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = lane + 64 * r;
+      if (c < 121) {
+        const int cy = c / 11, cx = c % 11;
+        uint8_t any = 0;
+        for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int yy = cy + dy, xx = cx + dx;
+            if (yy >= 0 && yy < 11 && xx >= 0 && xx < 11) any |= cur[yy * 11 + xx];
+          }
+        nxt[c] = (any && sup[r]) ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    uint8_t* t = cur; cur = nxt; nxt = t;
+  }
+  if (active) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = lane + 64 * r;
+      if (c < 121 && cur[c]) {
+        const int yy = sy - 5 + c / 11, xx = sx - 5 + c % 11;
+        atomicMax(M1 + (size_t)b * Hp * Wp + yy * Wp + xx, k + 1);
+      }
+    }
+  }
+}
+
+// Per-pixel label from its end point; count pixels per label.
+__global__ __launch_bounds__(256) void label_lookup_kernel(const int* __restrict__ pos, const int* __restrict__ M1, int B,
+                                                           int HW, int HWp, int* __restrict__ M0, int* __restrict__ counts,
+                                                           int nlab) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)B * HW) return;
+  const int b = (int)(gid / HW);
+  const int p = pos[gid];
+  int lab = 0;
+  if (p >= 0) lab = M1[(size_t)b * HWp + p];
+  M0[gid] = lab;
+  if (lab > 0) atomicAdd(counts + (size_t)b * nlab + lab, 1);
+}
+
+// flow2 = (dY, dX) * (cellprob > thr) / 5 from a [B, 3, H, W] network output; fg mask.
+__global__ __launch_bounds__(256) void prep_flow_kernel(const float* __restrict__ y, int B, int H, int W, float thr,
+                                                        float2* __restrict__ flow2, uint8_t* __restrict__ fg) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int HW = H * W;
+  if (gid >= (long long)B * HW) return;
+  const int b = (int)(gid / HW), p = (int)(gid % HW);
+  const float* yb = y + (size_t)b * 3 * HW;
+  const bool f = yb[2 * HW + p] > thr;
+  fg[gid] = f;
+  flow2[gid] = f ? make_float2(yb[p] * 0.2f, yb[HW + p] * 0.2f) : make_float2(0.f, 0.f);
+}
+
+}  // namespace
+
+extern "C" {
+
+int be_cp_prep_flow(const float* y, int B, int H, int W, float thr, void* flow2, void* fg, hipStream_t s) {
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(prep_flow_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, y, B, H, W, thr, (float2*)flow2,
+                     (uint8_t*)fg);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_follow_flows(const void* flow2, const void* fg, int* hist, int* pos, int B, int H, int W, int niter,
+                       hipStream_t s) {
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(follow_flows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float2*)flow2,
+                     (const uint8_t*)fg, hist, pos, B, H, W, niter);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_seeds(const int* hist, int B, int Hp, int Wp, long long* keys, int* nseeds, int cap, hipStream_t s) {
+  const long long n = (long long)B * Hp * Wp;
+  hipLaunchKernelGGL(seeds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hist, B, Hp, Wp, keys, nseeds, cap);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_expand(const int* hist, const long long* keys_sorted, const int* nseeds, int B, int Hp, int Wp, int cap,
+                 int kmax, int* M1, hipStream_t s) {
+  const long long nslots = (long long)B * kmax;
+  if (nslots == 0) return 0;
+  hipLaunchKernelGGL(expand_kernel, dim3((unsigned)((nslots + 3) / 4)), dim3(256), 0, s, hist, keys_sorted, nseeds, B, Hp,
+                     Wp, cap, kmax, M1);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_label_lookup(const int* pos, const int* M1, int B, int HW, int HWp, int* M0, int* counts, int nlab,
+                       hipStream_t s) {
+  const long long n = (long long)B * HW;
+  hipLaunchKernelGGL(label_lookup_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pos, M1, B, HW, HWp, M0, counts,
+                     nlab);
+  return BE_CHECK_LAUNCH();
+}
+
+}  // extern "C"

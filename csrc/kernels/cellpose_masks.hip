@@ -1,0 +1,279 @@
+// Per-mask Cellpose post-processing: bounding boxes, heat-diffusion flows (masks_to_flows),
+// flow-error QC and hole filling.  SURVEY.md §2.5 K5 (flow QC, flow_threshold at
+// apps/cellpose-finetuning/main.py:5005-5012), K6 (fill holes / min_size), K10 (label -> flow
+// training targets, invoked at main.py:1370-1387).  Oracle: bioengine_worker_amd/cellpose/reference.py.
+//
+// MI355X mapping: one workgroup per mask.  The mask's bounding box (+1 ring) is staged in LDS
+// (membership bytes + two fp32 heat buffers), the whole Jacobi diffusion runs on-chip with one
+// barrier per half-step, and only log(1 + T) of the mask pixels goes back to HBM.  Masks whose box
+// exceeds the LDS budget run the same code on a per-mask global scratch slab (same block, so
+// __syncthreads still orders the sweeps).  Centres are exact medians from row/column histograms in
+// LDS, ties broken in raster order with a 64-bit atomicMin key.
+#include "common.h"
+
+namespace {
+
+constexpr int MT = 256;
+
+// bbox[b, lab] = (ymin, ymax, xmin, xmax); init (INT_MAX, -1, INT_MAX, -1) by the caller.
+__global__ __launch_bounds__(256) void bbox_kernel(const int* __restrict__ M, int B, int H, int W, int nlab,
+                                                   int* __restrict__ bbox) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int HW = H * W;
+  if (gid >= (long long)B * HW) return;
+  const int lab = M[gid];
+  if (lab <= 0) return;
+  const int b = (int)(gid / HW), p = (int)(gid % HW);
+  const int y = p / W, x = p % W;
+  int* bb = bbox + ((size_t)b * nlab + lab) * 4;
+  atomicMin(bb + 0, y);
+  atomicMax(bb + 1, y);
+  atomicMin(bb + 2, x);
+  atomicMax(bb + 3, x);
+}
+
+struct MaskJob {
+  int b, lab, y0, x0, ly, lx;  // box origin (inclusive) and extent
+  long long scratch;           // float offset into the global scratch arena (big masks), else -1
+};
+
+// Heat diffusion of one mask; writes L = log(1 + T) for its pixels into Lout [B, H, W].
+template <bool USE_LDS>
+__global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs, int H,
+                                                     int W, const int* __restrict__ niter_img, float* __restrict__ scratch,
+                                                     float* __restrict__ Lout) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const MaskJob J = jobs[blockIdx.x];
+  const int RY = J.ly + 2, RX = J.lx + 2, R = RY * RX;
+  float* T0;
+  float* T1;
+  int* hy;
+  int* hx;
+  unsigned char* inm;
+  if (USE_LDS) {
+    T0 = reinterpret_cast<float*>(smem);
+    T1 = T0 + R;
+    hy = reinterpret_cast<int*>(T1 + R);
+    hx = hy + RY;
+    inm = reinterpret_cast<unsigned char*>(hx + RX);
+  } else {
+    T0 = scratch + J.scratch;
+    T1 = T0 + R;
+    hy = reinterpret_cast<int*>(T1 + R);
+    hx = hy + RY;
+    inm = reinterpret_cast<unsigned char*>(hx + RX);
+  }
+  __shared__ unsigned long long best;
+  __shared__ int total;
+  const int tid = threadIdx.x;
+  const int* Mb = M + (size_t)J.b * H * W;
+  for (int e = tid; e < R; e += MT) { T0[e] = 0.f; T1[e] = 0.f; }
+  for (int e = tid; e < RY; e += MT) hy[e] = 0;
+  for (int e = tid; e < RX; e += MT) hx[e] = 0;
+  if (tid == 0) { best = ~0ull; total = 0; }
+  __syncthreads();
+  int cnt = 0;
+  for (int e = tid; e < R; e += MT) {
+    const int ry = e / RX, rx = e % RX;
+    const int y = J.y0 + ry - 1, x = J.x0 + rx - 1;
+    unsigned char m = 0;
+    if (ry >= 1 && ry <= J.ly && rx >= 1 && rx <= J.lx) m = (Mb[y * W + x] == J.lab);
+    inm[e] = m;
+    if (m) { atomicAdd(&hy[ry], 1); atomicAdd(&hx[rx], 1); ++cnt; }
+  }
+  atomicAdd(&total, cnt);
+  __syncthreads();
+  // exact medians (numpy semantics: mean of the two middle values for even counts)
+  __shared__ float med[2];
+  if (tid < 2) {
+    const int* h = tid == 0 ? hy : hx;
+    const int L = tid == 0 ? RY : RX;
+    const int n = total;
+    const int k1 = (n - 1) / 2, k2 = n / 2;
+    int acc = 0, v1 = -1, v2 = -1;
+    for (int i = 0; i < L; ++i) {
+      const int c = h[i];
+      if (v1 < 0 && acc + c > k1) v1 = i;
+      if (v2 < 0 && acc + c > k2) { v2 = i; break; }
+      acc += c;
+    }
+    med[tid] = 0.5f * (float)(v1 + v2);
+  }
+  __syncthreads();
+  for (int e = tid; e < R; e += MT) {
+    if (!inm[e]) continue;
+    const float dy = (float)(e / RX) - med[0], dx = (float)(e % RX) - med[1];
+    const float d = dx * dx + dy * dy;
+    const unsigned long long key = ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)e;
+    atomicMin(&best, key);
+  }
+  __syncthreads();
+  const int ce = (int)(best & 0xffffffffu);
+  const int niter = niter_img[J.b];
+  float* cur = T0;
+  float* nxt = T1;
+  for (int it = 0; it < niter; ++it) {
+    if (tid == 0) cur[ce] += 1.f;
+    __syncthreads();
+    for (int e = tid; e < R; e += MT) {
+      if (!inm[e]) continue;
+      float s = 0.f;
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int q = e + dy * RX + dx;
+          s += inm[q] ? cur[q] : 0.f;
+        }
+      nxt[e] = s * (1.f / 9.f);
+    }
+    __syncthreads();
+    float* t = cur; cur = nxt; nxt = t;
+  }
+  float* Lb = Lout + (size_t)J.b * H * W;
+  for (int e = tid; e < R; e += MT) {
+    if (!inm[e]) continue;
+    const int y = J.y0 + e / RX - 1, x = J.x0 + e % RX - 1;
+    Lb[y * W + x] = log1pf(cur[e]);
+  }
+}
+
+// mu = normalised central-difference gradient of L inside masks; per-mask squared error vs dP/5.
+// dp: optional [B, 2(or 3), H, W] network output (channel stride H*W, image stride dp_bstride).
+__global__ __launch_bounds__(256) void flow_grad_kernel(const int* __restrict__ M, const float* __restrict__ L, int B, int H,
+                                                        int W, float* __restrict__ mu, const float* __restrict__ dp,
+                                                        long long dp_bstride, float* __restrict__ err, int nlab) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int HW = H * W;
+  if (gid >= (long long)B * HW) return;
+  const int lab = M[gid];
+  const int b = (int)(gid / HW), p = (int)(gid % HW);
+  const int y = p / W, x = p % W;
+  float gy = 0.f, gx = 0.f;
+  if (lab > 0) {
+    const float* Lb = L + (size_t)b * HW;
+    const float up = y > 0 ? Lb[p - W] : 0.f, dn = y < H - 1 ? Lb[p + W] : 0.f;
+    const float lf = x > 0 ? Lb[p - 1] : 0.f, rt = x < W - 1 ? Lb[p + 1] : 0.f;
+    gy = dn - up;
+    gx = rt - lf;
+    const float nrm = sqrtf(gy * gy + gx * gx) + 1e-30f;
+    gy /= nrm;
+    gx /= nrm;
+    if (dp && err) {
+      const float* db = dp + (size_t)b * dp_bstride;
+      const float ey = gy - db[p] * 0.2f, ex = gx - db[HW + p] * 0.2f;
+      atomicAdd(err + (size_t)b * nlab + lab, ey * ey + ex * ex);
+    }
+  }
+  if (mu) {
+    mu[(size_t)b * 2 * HW + p] = gy;
+    mu[(size_t)b * 2 * HW + HW + p] = gx;
+  }
+}
+
+// Hole filling: background of the box (+1 ring) that is 4-connected to the ring is "outside";
+// everything else in the box is the filled mask.  Writes lut[lab] into out (atomicMax for claimed
+// hole pixels, plain for own pixels).  Masks with lut[lab] == 0 are skipped by the caller.
+template <bool USE_LDS>
+__global__ __launch_bounds__(MT) void fill_holes_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs, int H,
+                                                        int W, const int* __restrict__ lut, int nlab,
+                                                        unsigned char* __restrict__ scratch, int* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const MaskJob J = jobs[blockIdx.x];
+  const int RY = J.ly + 2, RX = J.lx + 2, R = RY * RX;
+  unsigned char* st = USE_LDS ? smem : scratch + J.scratch;  // 0 = inside/undecided, 1 = mask, 2 = outside
+  __shared__ int changed;
+  const int tid = threadIdx.x;
+  const int* Mb = M + (size_t)J.b * H * W;
+  for (int e = tid; e < R; e += MT) {
+    const int ry = e / RX, rx = e % RX;
+    unsigned char v;
+    if (ry == 0 || ry == RY - 1 || rx == 0 || rx == RX - 1) {
+      v = 2;
+    } else {
+      v = (Mb[(J.y0 + ry - 1) * W + (J.x0 + rx - 1)] == J.lab) ? 1 : 0;
+    }
+    st[e] = v;
+  }
+  if (tid == 0) changed = 0;
+  __syncthreads();
+  for (;;) {
+    int ch = 0;
+    for (int e = tid; e < R; e += MT) {
+      if (st[e] != 0) continue;
+      const int ry = e / RX, rx = e % RX;
+      if ((ry > 0 && st[e - RX] == 2) || (ry < RY - 1 && st[e + RX] == 2) || (rx > 0 && st[e - 1] == 2) ||
+          (rx < RX - 1 && st[e + 1] == 2)) {
+        st[e] = 2;
+        ch = 1;
+      }
+    }
+    if (ch) changed = 1;
+    __syncthreads();
+    const int c = changed;
+    __syncthreads();  // everyone has read the flag before it is reset
+    if (!c) break;
+    if (tid == 0) changed = 0;
+    __syncthreads();
+  }
+  const int newlab = lut[(size_t)J.b * nlab + J.lab];
+  int* ob = out + (size_t)J.b * H * W;
+  for (int e = tid; e < R; e += MT) {
+    const unsigned char v = st[e];
+    if (v == 2) continue;
+    const int ry = e / RX, rx = e % RX;
+    const int idx = (J.y0 + ry - 1) * W + (J.x0 + rx - 1);
+    if (v == 1) {
+      atomicMax(ob + idx, newlab);
+    } else if (Mb[idx] == 0) {
+      atomicMax(ob + idx, newlab);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int be_cp_bbox(const int* M, int B, int H, int W, int nlab, int* bbox, hipStream_t s) {
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(bbox_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, B, H, W, nlab, bbox);
+  return BE_CHECK_LAUNCH();
+}
+
+// jobs: device array of MaskJob (7 x int64-aligned fields: see struct); lds_bytes > 0 => LDS variant.
+int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, float* scratch,
+                  float* Lout, int lds_bytes, hipStream_t s) {
+  if (njobs == 0) return 0;
+  if (lds_bytes > 0)
+    hipLaunchKernelGGL((diffuse_kernel<true>), dim3(njobs), dim3(MT), lds_bytes, s, M, (const MaskJob*)jobs, H, W, niter_img,
+                       scratch, Lout);
+  else
+    hipLaunchKernelGGL((diffuse_kernel<false>), dim3(njobs), dim3(MT), 0, s, M, (const MaskJob*)jobs, H, W, niter_img, scratch,
+                       Lout);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_flow_grad(const int* M, const float* L, int B, int H, int W, float* mu, const float* dp, long long dp_bstride,
+                    float* err, int nlab, hipStream_t s) {
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(flow_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, L, B, H, W, mu, dp, dp_bstride,
+                     err, nlab);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_fill_holes(const int* M, const void* jobs, int njobs, int H, int W, const int* lut, int nlab, void* scratch,
+                     int* out, int lds_bytes, hipStream_t s) {
+  if (njobs == 0) return 0;
+  if (lds_bytes > 0)
+    hipLaunchKernelGGL((fill_holes_kernel<true>), dim3(njobs), dim3(MT), lds_bytes, s, M, (const MaskJob*)jobs, H, W, lut, nlab,
+                       (unsigned char*)scratch, out);
+  else
+    hipLaunchKernelGGL((fill_holes_kernel<false>), dim3(njobs), dim3(MT), 0, s, M, (const MaskJob*)jobs, H, W, lut, nlab,
+                       (unsigned char*)scratch, out);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_mask_job_bytes() { return (int)sizeof(MaskJob); }
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernel library.
+//
+// Every kernel in csrc/kernels is written for gfx950 only: 64-lane waves,
+// MFMA 16x16x32 bf16 tiles, 160 KiB LDS per CU.  Host entry points are plain
+// C ABI functions (`be_*`) that take raw device pointers and a hipStream_t so
+// the Python layer (bioengine_worker_amd/ops/_native.py) can call them on
+// PyTorch's current stream without pulling torch headers into the build.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (8 bf16)
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // MFMA 16x16 accumulator
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+#define BE_WAVE 64
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even, NaN preserved
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap of a linear block id (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): blocks that share an XCD (id % 8) get a contiguous range of logical tiles so that
+// neighbouring tiles, which share halo rows and weight panels, hit the same private L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = orig % 8;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / 8;
+}
+
+#define BE_CHECK_LAUNCH() ((int)hipGetLastError())

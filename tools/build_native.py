@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Build the native libraries of bioengine_worker_amd in-tree.
+
+* ``libbe_hip.so``     — every ``csrc/kernels/*.hip`` compiled with ``hipcc --offload-arch=gfx950``
+  (CDNA4 only; no other targets, no CUDA, no hipify).
+* ``libbe_runtime.so`` — the host runtime in ``csrc/runtime/*.cpp`` (request batcher, shared-memory
+  ring, tile planner, CPU mask post-processing) compiled with g++; it has no GPU dependency so it
+  also runs in CPU-only CI.
+
+Objects are cached under ``build/`` keyed by source mtime + flags, so rebuilding after editing one
+kernel recompiles only that file.  Usage: ``python tools/build_native.py [--only hip|runtime] [-j N]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+OUT_DIR = ROOT / "bioengine_worker_amd" / "_native"
+BUILD = ROOT / "build" / "native"
+ARCH = os.environ.get("BE_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_lib_dir() -> str | None:
+    try:
+        import importlib.util
+
+        spec = importlib.util.find_spec("torch")
+        if spec is None or spec.origin is None:
+            return None
+        return str(Path(spec.origin).parent / "lib")
+    except Exception:
+        return None
+
+
+HIP_FLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    f"--offload-arch={ARCH}",
+    "-munsafe-fp-atomics",
+    "-Wno-unused-result",
+    "-I",
+    str(CSRC / "kernels"),
+]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread", "-I", str(CSRC / "runtime")]
+
+
+def _key(src: Path, flags: list[str]) -> str:
+    h = hashlib.sha1()
+    h.update(" ".join(flags).encode())
+    h.update(src.read_bytes())
+    for hdr in sorted(src.parent.glob("*.h")):
+        h.update(hdr.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def _compile(cmd_base: list[str], src: Path, flags: list[str]) -> Path:
+    obj = BUILD / f"{src.stem}.{_key(src, flags)}.o"
+    if obj.exists():
+        return obj
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    cmd = cmd_base + flags + ["-c", str(src), "-o", str(obj) + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"compile failed: {src}")
+    os.replace(str(obj) + ".tmp", obj)
+    return obj
+
+
+_PROTO = None
+
+
+def extract_signatures(srcs) -> dict[str, str]:
+    """Parse ``extern "C"`` entry points ``int be_*(...)`` and map each parameter to a ctypes code:
+    pointer -> p, hipStream_t -> s, float -> f, long long/int64 -> l, int -> i."""
+    import re
+
+    sigs = {}
+    pat = re.compile(r"\bint\s+(be_[A-Za-z0-9_]+)\s*\(([^)]*)\)\s*\{", re.S)
+    for src in srcs:
+        text = Path(src).read_text()
+        for m in pat.finditer(text):
+            name, params = m.group(1), m.group(2).strip()
+            codes = []
+            if params and params != "void":
+                for prm in params.split(","):
+                    prm = " ".join(prm.split())
+                    if "*" in prm:
+                        codes.append("p")
+                    elif "hipStream_t" in prm:
+                        codes.append("s")
+                    elif prm.startswith("float") or prm.startswith("const float"):
+                        codes.append("f")
+                    elif "long long" in prm or "int64_t" in prm:
+                        codes.append("l")
+                    else:
+                        codes.append("i")
+            sigs[name] = "".join(codes)
+    return sigs
+
+
+def build_hip(jobs: int) -> Path:
+    srcs = sorted((CSRC / "kernels").glob("*.hip"))
+    if not srcs:
+        raise RuntimeError("no HIP sources")
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile([HIPCC], s, HIP_FLAGS), srcs))
+    out = OUT_DIR / "libbe_hip.so"
+    tl = _torch_lib_dir()
+    link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out) + ".tmp"] + [str(o) for o in objs]
+    if tl and Path(tl, "libamdhip64.so").exists():
+        # Resolve libamdhip64 against the runtime PyTorch ships so the process has ONE HIP runtime.
+        link += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
+    r = subprocess.run(link, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("link failed: libbe_hip.so")
+    os.replace(str(out) + ".tmp", out)
+    import json
+
+    (OUT_DIR / "hip_signatures.json").write_text(json.dumps(extract_signatures(srcs), indent=1, sort_keys=True))
+    return out
+
+
+def build_runtime(jobs: int) -> Path | None:
+    srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    if not srcs:
+        return None
+    cxx = shutil.which("g++") or "g++"
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile([cxx], s, CXX_FLAGS), srcs))
+    out = OUT_DIR / "libbe_runtime.so"
+    r = subprocess.run([cxx, "-shared", "-fPIC", "-pthread", "-o", str(out) + ".tmp"] + [str(o) for o in objs] + ["-lrt"],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("link failed: libbe_runtime.so")
+    os.replace(str(out) + ".tmp", out)
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", choices=["hip", "runtime"], default=None)
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    args = ap.parse_args(argv)
+    OUT_DIR.mkdir(parents=True, exist_ok=True)
+    if args.only in (None, "runtime"):
+        p = build_runtime(args.jobs)
+        print(f"built {p}")
+    if args.only in (None, "hip"):
+        p = build_hip(args.jobs)
+        print(f"built {p}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
