@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): Cellpose-cyto3 512x512 imgs/sec (node) + p50 latency;
+fine-tune samples/sec.
+
+``python bench.py --gpus N --steps K --warmup W`` — for N > 1 the driver launches one rank per GPU
+with ``torch.distributed.run`` (RCCL).  Each rank runs the *full* Cellpose inference pipeline on a
+batch of synthetic 512x512 2-channel uint16 images per step (percentile normalisation, 224-tile
+gather, CPnet forward on the fused HIP conv kernels, tapered blend, flow following, seed
+histogram/expansion, flow-error QC, hole filling) — nothing is skipped inside the timed region.
+Work per GPU is fixed as N grows (weak scaling: every GPU is an independent serving replica, the
+reference's scaling model — Ray Serve replicas, ``apps/model-runner/runtime_deployment.py:40-50``).
+
+After the timed inference steps, the same process measures (untimed for the headline):
+  * p50 / p95 latency of single-image requests (batch 1),
+  * fine-tune samples/s: CPnet fwd+bwd + fused AdamW on 256x256 crops with data-parallel gradient
+    all-reduce over RCCL (bucketed, overlapped with backward) — BASELINE config 3,
+and reports them as extra fields of the one JSON line rank 0 prints.
+
+The reference publishes no number for these metrics, so ``vs_baseline`` is null;
+``vs_reference_algorithm`` is the speedup over the same pipeline with the network run by PyTorch
+eager bf16 (MIOpen) — the "reference-algorithm baseline" of BASELINE.md — measured in-process.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def _dist_setup(ngpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def _barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def _max_over_ranks(v: float, world: int) -> float:
+    if world == 1:
+        return v
+    t = torch.tensor([v], device="cuda", dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_infer(args, world, rank, dev):
+    from bioengine_worker_amd.cellpose.pipeline import CellposeRunner, EvalParams, synthetic_cells
+
+    runner = CellposeRunner(device=dev, seed=0)
+    imgs = torch.from_numpy(synthetic_cells(args.batch, 512, 512, nchan=2, seed=rank)).to(dev)
+    p = EvalParams(niter=200, flow_threshold=0.4, cellprob_threshold=0.0, min_size=15)
+    for _ in range(args.warmup):
+        masks, _, _ = runner.eval(imgs, p)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        masks, flows, _ = runner.eval(imgs, p)
+    _barrier(world)
+    dt = time.perf_counter() - t0
+    dt = _max_over_ranks(dt, world)
+    extra = {"masks_per_image": float(masks.amax(dim=(1, 2)).float().mean().item()),
+             "fg_fraction": float((flows[:, 2] > 0).float().mean().item())}
+    return dt, runner, imgs, p, extra
+
+
+def bench_latency(runner, imgs, p, n=20):
+    one = imgs[:1]
+    for _ in range(3):
+        runner.eval(one, p)
+    torch.cuda.synchronize()
+    lat = []
+    for _ in range(n):
+        t = time.perf_counter()
+        runner.eval(one, p)
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - t) * 1e3)
+    lat.sort()
+    return statistics.median(lat), lat[int(0.95 * (len(lat) - 1))]
+
+
+def bench_reference_algorithm(runner, imgs, p, steps=3):
+    """Same pipeline, network replaced by PyTorch eager bf16 autocast (MIOpen convs)."""
+    from bioengine_worker_amd.cellpose.gpu import compute_masks_gpu, normalize99
+
+    net = runner.net.to(imgs.device).to(memory_format=torch.channels_last)
+    plan = runner._plan(512, 512, p)
+
+    def run():
+        x = normalize99(imgs.float())
+        tiles = plan.gather(x, runner.cin_pad)[..., : runner.nchan].permute(0, 3, 1, 2).float()
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            yt = net(tiles.contiguous(memory_format=torch.channels_last))[0]
+        y = plan.blend(yt.float().contiguous(), imgs.shape[0])
+        return compute_masks_gpu(y)
+
+    run()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    runner.net.cpu()
+    return (time.perf_counter() - t) / steps
+
+
+def bench_mask_recovery(dev, batch, steps=3):
+    """Mask recovery alone on *cell-like* flows (random-init weights give no convergent flows, so the
+    headline run under-exercises seeds/QC/fill): flows from ~150 synthetic cells per 512x512 image."""
+    from bioengine_worker_amd.cellpose.gpu import compute_masks_gpu
+    from bioengine_worker_amd.train.cellpose_train import labels_to_flows, synthetic_instances
+
+    _, labels = synthetic_instances(batch, 512, 512, ncells=150, seed=7)
+    lab = torch.from_numpy(labels).to(dev)
+    t = labels_to_flows(lab)
+    y = torch.cat([5.0 * t[:, 1:3], torch.where(lab[:, None] > 0, 5.0, -5.0)], 1).contiguous()
+    m = compute_masks_gpu(y)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m = compute_masks_gpu(y)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return dt / batch * 1e3, float(m.amax(dim=(1, 2)).float().mean().item())
+
+
+def bench_train(args, world, rank, dev):
+    from bioengine_worker_amd.train.cellpose_train import TrainConfig, synthetic_train_batch, build_trainer
+
+    cfg = TrainConfig(batch_size=args.train_batch, bsize=256, lr=1e-5, weight_decay=1e-4)
+    trainer = build_trainer(cfg, device=dev, world_size=world, rank=rank)
+    batch = synthetic_train_batch(args.train_batch, cfg.bsize, device=dev, seed=rank)
+    for _ in range(max(2, args.warmup)):
+        trainer.step(*batch)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.train_steps):
+        trainer.step(*batch)
+    _barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="512x512 images per step per GPU")
+    ap.add_argument("--train-batch", type=int, default=8, help="256x256 crops per step per GPU")
+    ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--no-extras", action="store_true", help="skip latency / train / reference-algorithm extras")
+    args = ap.parse_args()
+
+    world, rank, local = _dist_setup(args.gpus)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    from bioengine_worker_amd.ops import _native
+
+    _native.hip()  # fail loudly if the kernels are missing
+
+    dt, runner, imgs, p, extra = bench_infer(args, world, rank, dev)
+    total_imgs = args.batch * args.steps * world
+    value = total_imgs / dt
+    ms_per_step = dt / args.steps * 1e3
+    out = {
+        "metric": "cellpose_cyto3_512x512_imgs_per_sec",
+        "value": round(value, 2),
+        "unit": "img/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (512x512x2 uint16 blob images, random-init CPnet weights)",
+        "config": {
+            "model": "cellpose-cyto3 CPnet (nbase 2-32-64-128-256, style on, BN folded)",
+            "global_batch": args.batch * world,
+            "seq_len": None,
+            "image": [512, 512, 2],
+            "pipeline": "normalize99 + 224-tile/0.1-overlap + CPnet + taper blend + dynamics(niter=200) + flow QC(0.4) + fill holes(min 15)",
+            "parallelism": f"dp{world} (replica per GPU)",
+        },
+    }
+    out.update(extra)
+    if not args.no_extras:
+        try:
+            if rank == 0:
+                p50, p95 = bench_latency(runner, imgs, p)
+                out["p50_latency_ms_batch1"] = round(p50, 3)
+                out["p95_latency_ms_batch1"] = round(p95, 3)
+                ref_dt = bench_reference_algorithm(runner, imgs, p)
+                out["reference_algorithm_imgs_per_sec_per_gpu"] = round(args.batch / ref_dt, 2)
+                out["vs_reference_algorithm"] = round((value / world) / (args.batch / ref_dt), 3)
+                mr_ms, mr_n = bench_mask_recovery(dev, args.batch)
+                out["mask_recovery_ms_per_image_150cells"] = round(mr_ms, 3)
+                out["mask_recovery_masks_per_image"] = mr_n
+        except Exception as e:  # extras must never take the headline down
+            out["extras_error"] = f"latency/ref: {type(e).__name__}: {e}"
+        try:
+            tdt = bench_train(args, world, rank, dev)
+            out["finetune_samples_per_sec"] = round(args.train_batch * args.train_steps * world / tdt, 2)
+            out["finetune_config"] = {"crop": 256, "batch_per_gpu": args.train_batch, "optimizer": "fused AdamW (HIP)",
+                                      "grad_allreduce": "RCCL bucketed, overlapped" if world > 1 else "none (1 GPU)"}
+        except Exception as e:
+            out["extras_error_train"] = f"{type(e).__name__}: {e}"
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,285 @@
+"""GPU (HIP) implementation of Cellpose pre/post-processing on batches of images.
+
+Every heavy step is a kernel in ``csrc/kernels/{tiles,cellpose_dynamics,cellpose_masks}.hip``;
+torch is only used for tiny bookkeeping (sorting the seed keys, prefix sums over labels, building
+per-mask job lists).  The semantics are those of :mod:`bioengine_worker_amd.cellpose.reference`
+(the CPU oracle), which the GPU tests compare against.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import _native
+from . import reference as ref
+
+RPAD = 20
+_JOB_BYTES = 32
+LDS_DIFFUSE_BYTES = 48 * 1024
+LDS_FILL_BYTES = 32 * 1024
+
+
+def _launch_cfg(n: int):
+    return n
+
+
+# ------------------------------------------------------------------ percentiles / tiles
+
+
+def normalize99(x: torch.Tensor, lower: float = 1.0, upper: float = 99.0) -> torch.Tensor:
+    """x [B, C, H, W] -> float32 normalised per (image, channel) with np.percentile 'linear' semantics."""
+    B, C, H, W = x.shape
+    xf = x.float().reshape(B * C, H * W)
+    srt, _ = torch.sort(xf, dim=1)
+    n = H * W
+
+    def pct(q):
+        pos = q / 100.0 * (n - 1)
+        lo = int(np.floor(pos))
+        hi = min(lo + 1, n - 1)
+        frac = pos - lo
+        return srt[:, lo] * (1 - frac) + srt[:, hi] * frac
+
+    p1, p99 = pct(lower), pct(upper)
+    rng = (p99 - p1)
+    ok = rng > 1e-3
+    scale = torch.where(ok, 1.0 / torch.where(ok, rng, torch.ones_like(rng)), torch.ones_like(rng))
+    const = (srt[:, -1] - srt[:, 0]) == 0
+    out = (xf - p1[:, None]) * scale[:, None]
+    out = torch.where(const[:, None], torch.zeros_like(out), out)
+    return out.reshape(B, C, H, W)
+
+
+class TilePlan:
+    """Cellpose tiling of an (H, W) image: pad to a multiple of 16 (+8 margin), 224 tiles, 10 % overlap."""
+
+    def __init__(self, H: int, W: int, bsize: int = 224, overlap: float = 0.1, device="cpu"):
+        self.H, self.W = H, W
+        ya, yb = ref.pad_amounts(H)
+        xa, xb = ref.pad_amounts(W)
+        self.pad_y, self.pad_x = ya, xa
+        self.Hp, self.Wp = H + ya + yb, W + xa + xb
+        self.ys = ref.tile_starts(self.Hp, bsize, overlap)
+        self.xs = ref.tile_starts(self.Wp, bsize, overlap)
+        self.by, self.bx = min(bsize, self.Hp), min(bsize, self.Wp)
+        self.nt = len(self.ys) * len(self.xs)
+        m = ref.taper_mask(self.by, self.bx)
+        # the 2-D taper is separable: recover the 1-D factors from its centre row/col
+        cy, cx = self.by // 2, self.bx // 2
+        wy = m[:, cx] / np.sqrt(m[cy, cx])
+        wx = m[cy, :] / np.sqrt(m[cy, cx])
+        dev = torch.device(device)
+        self.ys_t = torch.tensor(self.ys, dtype=torch.int32, device=dev)
+        self.xs_t = torch.tensor(self.xs, dtype=torch.int32, device=dev)
+        self.wy = torch.tensor(wy, dtype=torch.float32, device=dev)
+        self.wx = torch.tensor(wx, dtype=torch.float32, device=dev)
+
+    def gather(self, img: torch.Tensor, cpad: int) -> torch.Tensor:
+        B, C, H, W = img.shape
+        out = torch.empty(B * self.nt, self.by, self.bx, cpad, dtype=torch.bfloat16, device=img.device)
+        img = img.float().contiguous()
+        _native.call("be_tiles_gather", _native.ptr(img), B, C, H, W, self.pad_y, self.pad_x, _native.ptr(self.ys_t),
+                     _native.ptr(self.xs_t), len(self.ys), len(self.xs), self.by, self.bx, cpad, _native.ptr(out),
+                     _native.stream(img.device))
+        return out
+
+    def blend(self, yt: torch.Tensor, B: int) -> torch.Tensor:
+        nout = yt.shape[1]
+        out = torch.empty(B, nout, self.H, self.W, dtype=torch.float32, device=yt.device)
+        _native.call("be_tiles_blend", _native.ptr(yt), B, nout, self.H, self.W, self.pad_y, self.pad_x,
+                     _native.ptr(self.ys_t), _native.ptr(self.xs_t), len(self.ys), len(self.xs), self.by, self.bx,
+                     _native.ptr(self.wy), _native.ptr(self.wx), _native.ptr(out), _native.stream(yt.device))
+        return out
+
+
+# ------------------------------------------------------------------ mask recovery
+
+
+def _jobs_tensor(b, lab, y0, x0, ly, lx, scratch) -> torch.Tensor:
+    """Pack MaskJob structs {int b, lab, y0, x0, ly, lx; int64 scratch} as int64 words."""
+    w0 = (b.long() & 0xFFFFFFFF) | (lab.long() << 32)
+    w1 = (y0.long() & 0xFFFFFFFF) | (x0.long() << 32)
+    w2 = (ly.long() & 0xFFFFFFFF) | (lx.long() << 32)
+    return torch.stack([w0, w1, w2, scratch.long()], 1).contiguous()
+
+
+def _split_jobs(bbox_valid, labs_b, labs_l, lds_elems_fn, lds_budget, scratch_elems_fn):
+    """Returns (small_jobs, big_jobs, scratch_size) for masks given their bboxes."""
+    y0, y1, x0, x1 = bbox_valid.unbind(1)
+    ly, lx = y1 - y0 + 1, x1 - x0 + 1
+    need = lds_elems_fn(ly, lx)
+    small = need <= lds_budget
+    dev = bbox_valid.device
+    sj = _jobs_tensor(labs_b[small], labs_l[small], y0[small], x0[small], ly[small], lx[small],
+                      torch.full((int(small.sum()),), -1, dtype=torch.long, device=dev))
+    big = ~small
+    nb = int(big.sum())
+    if nb:
+        sz = scratch_elems_fn(ly[big], lx[big])
+        off = torch.cumsum(sz, 0) - sz
+        bj = _jobs_tensor(labs_b[big], labs_l[big], y0[big], x0[big], ly[big], lx[big], off)
+        total = int(sz.sum())
+    else:
+        bj = sj[:0]
+        total = 0
+    return sj, bj, total
+
+
+def _diffuse_lds_bytes(ly, lx):
+    R = (ly + 2) * (lx + 2)
+    return 16 * R + 4 * (ly + 2 + lx + 2) + R + 16
+
+
+def _diffuse_scratch_doubles(ly, lx):
+    R = (ly + 2) * (lx + 2)
+    return 2 * R + (ly + 2 + lx + 2 + 1) // 2 + (R + 7) // 8 + 2
+
+
+def mask_bboxes(M: torch.Tensor, nlab: int) -> torch.Tensor:
+    B, H, W = M.shape
+    bbox = torch.empty(B, nlab, 4, dtype=torch.int32, device=M.device)
+    bbox[..., 0] = 2 ** 31 - 1
+    bbox[..., 1] = -1
+    bbox[..., 2] = 2 ** 31 - 1
+    bbox[..., 3] = -1
+    _native.call("be_cp_bbox", _native.ptr(M), B, H, W, nlab, _native.ptr(bbox), _native.stream(M.device))
+    return bbox
+
+
+def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: int | None = None):
+    """Heat-diffusion flows of label images M [B, H, W] int32 (labels 1..n, contiguous per image).
+
+    Returns (mu [B, 2, H, W] fp32, err_sum [B, nlab] fp32 or None, counts [B, nlab]).  When ``dp``
+    ([B, >=2, H, W] network output) is given, err_sum[b, l] = sum over mask l of |mu - dp/5|^2.
+    """
+    B, H, W = M.shape
+    dev = M.device
+    nlab = int(M.max().item()) + 1 if M.numel() else 1
+    mu = torch.zeros(B, 2, H, W, dtype=torch.float32, device=dev)
+    counts = torch.zeros(B, nlab, dtype=torch.int32, device=dev)
+    counts.view(-1).index_add_(0, (M.long() + torch.arange(B, device=dev).view(B, 1, 1) * nlab).view(-1),
+                               torch.ones(M.numel(), dtype=torch.int32, device=dev))
+    if nlab <= 1:
+        return mu, (torch.zeros(B, nlab, device=dev) if dp is not None else None), counts
+    bbox = mask_bboxes(M, nlab)
+    present = bbox[..., 1] >= 0
+    present[:, 0] = False
+    ext = (bbox[..., 1] - bbox[..., 0] + bbox[..., 3] - bbox[..., 2] + 4).clamp(min=0) * present
+    niter_img = (2 * ext.max(dim=1).values).to(torch.int32) if niter is None else torch.full((B,), niter, dtype=torch.int32, device=dev)
+    idx = present.nonzero()
+    labs_b, labs_l = idx[:, 0].int(), idx[:, 1].int()
+    bb = bbox[idx[:, 0], idx[:, 1]]
+    sj, bj, ssize = _split_jobs(bb, labs_b, labs_l, _diffuse_lds_bytes, LDS_DIFFUSE_BYTES, _diffuse_scratch_doubles)
+    L = torch.zeros(B, H, W, dtype=torch.float64, device=dev)
+    scratch = torch.empty(max(ssize, 1), dtype=torch.float64, device=dev)
+    st = _native.stream(dev)
+    Mc = M.contiguous()
+    if sj.shape[0]:
+        _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(sj), sj.shape[0], H, W, _native.ptr(niter_img),
+                     _native.ptr(scratch), _native.ptr(L), LDS_DIFFUSE_BYTES, st)
+    if bj.shape[0]:
+        _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], H, W, _native.ptr(niter_img),
+                     _native.ptr(scratch), _native.ptr(L), 0, st)
+    err = None
+    dpp = None
+    bstride = 0
+    if dp is not None:
+        dpp = dp.float().contiguous()
+        bstride = dpp.shape[1] * H * W
+        err = torch.zeros(B, nlab, dtype=torch.float32, device=dev)
+    _native.call("be_cp_flow_grad", _native.ptr(Mc), _native.ptr(L), B, H, W, _native.ptr(mu), _native.ptr(dpp),
+                 bstride, _native.ptr(err), nlab, st)
+    return mu, err, counts
+
+
+def _renumber(M: torch.Tensor, keep: torch.Tensor) -> torch.Tensor:
+    """keep [B, nlab] bool (index 0 ignored) -> M relabelled 1..k per image, dropped labels -> 0."""
+    keep = keep.clone()
+    keep[:, 0] = False
+    lut = torch.cumsum(keep.int(), dim=1) * keep.int()
+    B = M.shape[0]
+    return torch.gather(lut, 1, M.reshape(B, -1).long()).reshape(M.shape).to(torch.int32)
+
+
+def fill_holes_gpu(M: torch.Tensor, min_size: int = 15) -> torch.Tensor:
+    B, H, W = M.shape
+    dev = M.device
+    nlab = int(M.max().item()) + 1 if M.numel() else 1
+    if nlab <= 1:
+        return M.clone()
+    counts = torch.zeros(B, nlab, dtype=torch.int32, device=dev)
+    counts.view(-1).index_add_(0, (M.long() + torch.arange(B, device=dev).view(B, 1, 1) * nlab).view(-1),
+                               torch.ones(M.numel(), dtype=torch.int32, device=dev))
+    keep = counts > 0
+    if min_size > 0:
+        keep &= counts >= min_size
+    keep[:, 0] = False
+    lut = (torch.cumsum(keep.int(), dim=1) * keep.int()).to(torch.int32).contiguous()
+    bbox = mask_bboxes(M, nlab)
+    idx = keep.nonzero()
+    out = torch.zeros_like(M)
+    if idx.shape[0] == 0:
+        return out
+    bb = bbox[idx[:, 0], idx[:, 1]]
+    sj, bj, ssize = _split_jobs(bb, idx[:, 0].int(), idx[:, 1].int(), lambda ly, lx: (ly + 2) * (lx + 2),
+                                LDS_FILL_BYTES, lambda ly, lx: (ly + 2) * (lx + 2))
+    scratch = torch.empty(max(ssize, 1), dtype=torch.uint8, device=dev)
+    st = _native.stream(dev)
+    Mc = M.contiguous()
+    if sj.shape[0]:
+        _native.call("be_cp_fill_holes", _native.ptr(Mc), _native.ptr(sj), sj.shape[0], H, W, _native.ptr(lut), nlab,
+                     _native.ptr(scratch), _native.ptr(out), LDS_FILL_BYTES, st)
+    if bj.shape[0]:
+        _native.call("be_cp_fill_holes", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], H, W, _native.ptr(lut), nlab,
+                     _native.ptr(scratch), _native.ptr(out), 0, st)
+    return out
+
+
+def follow_and_label(y: torch.Tensor, niter: int = 200, cellprob_threshold: float = 0.0,
+                     max_size_fraction: float = 0.4) -> torch.Tensor:
+    """Network output y [B, 3, H, W] -> raw masks M0 [B, H, W] int32 (before QC / fill)."""
+    B, _, H, W = y.shape
+    dev = y.device
+    st = _native.stream(dev)
+    y = y.float().contiguous()
+    flow2 = torch.empty(B, H, W, 2, dtype=torch.float32, device=dev)
+    fg = torch.empty(B, H, W, dtype=torch.uint8, device=dev)
+    _native.call("be_cp_prep_flow", _native.ptr(y), B, H, W, float(cellprob_threshold), _native.ptr(flow2),
+                 _native.ptr(fg), st)
+    Hp, Wp = H + 2 * RPAD, W + 2 * RPAD
+    hist = torch.zeros(B, Hp, Wp, dtype=torch.int32, device=dev)
+    pos = torch.empty(B, H, W, dtype=torch.int32, device=dev)
+    _native.call("be_cp_follow_flows", _native.ptr(flow2), _native.ptr(fg), _native.ptr(hist), _native.ptr(pos), B, H,
+                 W, int(niter), st)
+    cap = H * W // 11 + 1
+    keys = torch.full((B, cap), torch.iinfo(torch.int64).max, dtype=torch.int64, device=dev)
+    nseeds = torch.zeros(B, dtype=torch.int32, device=dev)
+    _native.call("be_cp_seeds", _native.ptr(hist), B, Hp, Wp, _native.ptr(keys), _native.ptr(nseeds), cap, st)
+    keys_sorted, _ = torch.sort(keys, dim=1)
+    kmax = int(nseeds.max().item()) if B else 0  # host sync: sizes the expansion grid
+    kmax = min(kmax, cap)
+    M1 = torch.zeros(B, Hp, Wp, dtype=torch.int32, device=dev)
+    M0 = torch.zeros(B, H, W, dtype=torch.int32, device=dev)
+    if kmax == 0:
+        return M0
+    _native.call("be_cp_expand", _native.ptr(hist), _native.ptr(keys_sorted), _native.ptr(nseeds), B, Hp, Wp, cap, kmax,
+                 _native.ptr(M1), st)
+    nlab = kmax + 1
+    counts = torch.zeros(B, nlab, dtype=torch.int32, device=dev)
+    _native.call("be_cp_label_lookup", _native.ptr(pos), _native.ptr(M1), B, H * W, Hp * Wp, _native.ptr(M0),
+                 _native.ptr(counts), nlab, st)
+    big = H * W * max_size_fraction
+    keep = (counts > 0) & (counts <= big)
+    return _renumber(M0, keep)
+
+
+def compute_masks_gpu(y: torch.Tensor, niter: int = 200, cellprob_threshold: float = 0.0, flow_threshold: float = 0.4,
+                      min_size: int = 15, max_size_fraction: float = 0.4) -> torch.Tensor:
+    """Full Cellpose mask recovery for a batch: y [B, 3, H, W] -> masks [B, H, W] int32."""
+    M = follow_and_label(y, niter, cellprob_threshold, max_size_fraction)
+    if flow_threshold is not None and flow_threshold > 0 and int(M.max().item()) > 0:
+        _, err, counts = masks_to_flows_gpu(M, dp=y)
+        merr = err / counts.clamp(min=1).float()
+        keep = (counts > 0) & ~(merr > flow_threshold)
+        M = _renumber(M, keep)
+    return fill_holes_gpu(M, min_size)

@@ -1,0 +1,193 @@
+"""End-to-end Cellpose inference: normalise -> (rescale) -> tile -> CPnet -> blend -> masks.
+
+``CellposeRunner.eval`` mirrors the call the reference apps make on ``cellpose.models.CellposeModel``
+(``model.eval(images, diameter, flow_threshold, cellprob_threshold, niter, min_size, ...)``;
+``apps/cellpose-finetuning/main.py:4965-5052`` and ``:3559-3567``) but runs a whole *batch* of images
+through one set of kernel launches: the tiles of every image in the batch are one CPnet batch,
+blending and mask recovery are batched kernels.  This is what the continuous-batching router feeds.
+
+GPU path: HIP kernels (:mod:`.gpu`, :class:`~bioengine_worker_amd.models.cpnet.CPnetEngine`).
+CPU path: the numpy/torch oracle (:mod:`.reference`) — used by CPU tests and CPU-only workers.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..models.cpnet import CPnet, CPnetEngine
+from . import reference as ref
+
+
+@dataclass
+class EvalParams:
+    diameter: float | None = None
+    niter: int = 200
+    flow_threshold: float = 0.4
+    cellprob_threshold: float = 0.0
+    min_size: int = 15
+    max_size_fraction: float = 0.4
+    normalize: bool = True
+    tile: bool = True
+    bsize: int = 224
+    tile_overlap: float = 0.1
+    compute_masks: bool = True
+
+
+def as_batch(images, nchan: int) -> torch.Tensor:
+    """Accept [H,W], [H,W,C], [C,H,W], [B,C,H,W] numpy/torch -> float tensor [B, nchan, H, W]."""
+    x = torch.as_tensor(np.asarray(images) if not torch.is_tensor(images) else images)
+    if x.dim() == 2:
+        x = x[None, None]
+    elif x.dim() == 3:
+        # channel-last if the last dim is small and the first is not
+        if x.shape[-1] <= 4 and x.shape[0] > 4:
+            x = x.permute(2, 0, 1)
+        x = x[None]
+    x = x.float()
+    B, C, H, W = x.shape
+    if C < nchan:
+        x = torch.cat([x, torch.zeros(B, nchan - C, H, W, dtype=x.dtype)], 1)
+    elif C > nchan:
+        x = x[:, :nchan]
+    return x
+
+
+class CellposeRunner:
+    """Batched Cellpose (cyto3-style CPnet) inference on one device."""
+
+    def __init__(self, net: CPnet | None = None, device: str | torch.device = "cuda", seed: int = 0):
+        self.device = torch.device(device)
+        self.net = (net or CPnet().randomize_(seed)).eval()
+        self.nchan = self.net.nchan
+        self.diam_mean = float(self.net.diam_mean.item())
+        self.cin_pad = (self.nchan + 7) // 8 * 8
+        self.engine = CPnetEngine(self.net, self.device)
+        self._plans: dict = {}
+
+    # ---------------------------------------------------------------- network
+    def _plan(self, H, W, p: EvalParams):
+        from .gpu import TilePlan
+
+        key = (H, W, p.bsize, p.tile_overlap)
+        if key not in self._plans:
+            self._plans[key] = TilePlan(H, W, p.bsize, p.tile_overlap, device=self.device)
+        return self._plans[key]
+
+    @torch.no_grad()
+    def run_net(self, x: torch.Tensor, p: EvalParams) -> tuple[torch.Tensor, torch.Tensor]:
+        """x: normalised [B, nchan, H, W] on device -> (y [B, 3, H, W] fp32, style [B, S])."""
+        B, C, H, W = x.shape
+        if self.device.type == "cuda":
+            if p.tile:
+                plan = self._plan(H, W, p)
+                tiles = plan.gather(x, self.cin_pad)
+                yt, st = self.engine(tiles)
+                y = plan.blend(yt, B)
+                style = st.view(B, plan.nt, -1).sum(1)
+            else:
+                Hp, Wp = math.ceil(H / 8) * 8, math.ceil(W / 8) * 8
+                xin = torch.zeros(B, Hp, Wp, self.cin_pad, dtype=torch.bfloat16, device=x.device)
+                xin[:, :H, :W, :C] = x.permute(0, 2, 3, 1)
+                y, style = self.engine(xin)
+                y = y[:, :, :H, :W].contiguous()
+            style = style / torch.sqrt((style * style).sum(1, keepdim=True))
+            return y, style
+        # CPU oracle path
+        ys, styles = [], []
+        for b in range(B):
+            img = x[b].numpy()
+            if p.tile:
+                ya, yb = ref.pad_amounts(H)
+                xa, xb = ref.pad_amounts(W)
+                imgp = np.pad(img, ((0, 0), (ya, yb), (xa, xb)))
+                tiles, tys, txs = ref.make_tiles(imgp, p.bsize, p.tile_overlap)
+                tt = torch.from_numpy(tiles).float()
+                yt, st, _ = self.net(tt)
+                yf = ref.average_tiles(yt.numpy(), tys, txs, imgp.shape[1], imgp.shape[2])
+                ys.append(torch.from_numpy(yf[:, ya: ya + H, xa: xa + W].copy()))
+                styles.append(st.sum(0))
+            else:
+                yt, st, _ = self.net(x[b: b + 1])
+                ys.append(yt[0])
+                styles.append(st[0])
+        style = torch.stack(styles)
+        return torch.stack(ys), style / torch.sqrt((style * style).sum(1, keepdim=True))
+
+    # ---------------------------------------------------------------- full eval
+    @torch.no_grad()
+    def eval(self, images, p: EvalParams | None = None, **kw):
+        """Returns (masks [B, H, W] int32 tensor, flows [B, 3, H, W] fp32 tensor, styles [B, S])."""
+        p = p or EvalParams()
+        for k, v in kw.items():
+            setattr(p, k, v)
+        x = as_batch(images, self.nchan).to(self.device)
+        B, C, H, W = x.shape
+        if p.normalize:
+            x = self._normalize(x)
+        rescale = 1.0
+        if p.diameter is not None and p.diameter > 0:
+            rescale = self.diam_mean / float(p.diameter)
+        if abs(rescale - 1.0) > 1e-3:
+            Hs, Ws = max(8, int(round(H * rescale))), max(8, int(round(W * rescale)))
+            xs = F.interpolate(x, size=(Hs, Ws), mode="bilinear", align_corners=False)
+            y, style = self.run_net(xs, p)
+            y = F.interpolate(y, size=(H, W), mode="bilinear", align_corners=False)
+        else:
+            y, style = self.run_net(x, p)
+        if not p.compute_masks:
+            return None, y, style
+        masks = self.compute_masks(y, p, rescale)
+        return masks, y, style
+
+    def _normalize(self, x):
+        if self.device.type == "cuda":
+            from .gpu import normalize99
+
+            return normalize99(x)
+        return torch.stack([torch.from_numpy(ref.normalize99(x[b].numpy())) for b in range(x.shape[0])])
+
+    def compute_masks(self, y: torch.Tensor, p: EvalParams, rescale: float = 1.0) -> torch.Tensor:
+        niter = p.niter if p.niter else int(200 / max(rescale, 1e-3))
+        if self.device.type == "cuda":
+            from .gpu import compute_masks_gpu
+
+            return compute_masks_gpu(y, niter=niter, cellprob_threshold=p.cellprob_threshold,
+                                     flow_threshold=p.flow_threshold, min_size=p.min_size,
+                                     max_size_fraction=p.max_size_fraction)
+        out = []
+        for b in range(y.shape[0]):
+            yb = y[b].numpy()
+            m = ref.compute_masks(yb[:2], yb[2], niter=niter, cellprob_threshold=p.cellprob_threshold,
+                                  flow_threshold=p.flow_threshold, min_size=p.min_size,
+                                  max_size_fraction=p.max_size_fraction)
+            out.append(torch.from_numpy(m.astype(np.int32)))
+        return torch.stack(out)
+
+
+def synthetic_cells(B: int, H: int = 512, W: int = 512, nchan: int = 2, ncells: int = 150, seed: int = 0) -> np.ndarray:
+    """Synthetic fluorescence-like images [B, nchan, H, W] uint16: Gaussian blobs (cells) + nuclei + noise."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((B, nchan, H, W), np.float32)
+    yy, xx = np.mgrid[0:H, 0:W]
+    for b in range(B):
+        cy = rng.uniform(0, H, ncells)
+        cx = rng.uniform(0, W, ncells)
+        r = rng.uniform(6, 14, ncells)
+        img = np.zeros((H, W), np.float32)
+        nuc = np.zeros((H, W), np.float32)
+        for i in range(ncells):
+            y0, y1 = int(max(0, cy[i] - 3 * r[i])), int(min(H, cy[i] + 3 * r[i]))
+            x0, x1 = int(max(0, cx[i] - 3 * r[i])), int(min(W, cx[i] + 3 * r[i]))
+            d2 = (yy[y0:y1, x0:x1] - cy[i]) ** 2 + (xx[y0:y1, x0:x1] - cx[i]) ** 2
+            img[y0:y1, x0:x1] += np.exp(-d2 / (2 * r[i] ** 2))
+            nuc[y0:y1, x0:x1] += np.exp(-d2 / (2 * (0.4 * r[i]) ** 2))
+        out[b, 0] = img
+        if nchan > 1:
+            out[b, 1] = nuc
+    out += 0.05 * rng.standard_normal(out.shape).astype(np.float32)
+    out = np.clip(out, 0, None)
+    return (out / out.max() * 4000).astype(np.uint16)

@@ -1,0 +1,163 @@
+"""Data-parallel training over RCCL: flat parameter/gradient buffers + bucketed, overlapped all-reduce.
+
+The reference trains on one GPU only (``apps/cellpose-finetuning/main.py:3603`` num_gpus=1,
+batch 1 at ``:1292``).  This module is the MI355X data-parallel path (BASELINE
+config 3): one process per GPU, ``torch.distributed`` with the ``nccl`` backend (= RCCL on ROCm)
+over xGMI.
+
+Design
+------
+* **Flat buffers.**  Every trainable parameter becomes a view into ONE contiguous fp32 buffer, and
+  every ``.grad`` a view into ONE contiguous fp32 gradient buffer.  The fused AdamW kernel then
+  updates all parameters in a single launch, and gradient buckets are plain slices — no
+  pack/unpack copies around the collectives.
+* **Buckets in backward order.**  Parameters are laid out in *reverse* registration order (the
+  order autograd produces their gradients), and the flat gradient buffer is cut into buckets of
+  ``bucket_mb``.  A post-accumulate-grad hook counts arrivals; the moment a bucket is complete its
+  ``all_reduce`` is issued asynchronously, so communication of late layers overlaps the backward of
+  early layers.
+* **Sized for xGMI.**  MI355X has 7 point-to-point xGMI links (~153 GB/s each); RCCL's ring/tree
+  all-reduce is per-link bound, so per-collective latency (not NVSwitch bandwidth) decides the
+  bucket size: a handful of multi-MB buckets (default 16 MB) amortise launch/latency while still
+  overlapping.  CPnet (6.6 M params, 26 MB fp32 grads) becomes ~2 buckets.
+* **Mean folded into the optimizer.**  Buckets are summed (``ReduceOp.SUM``); the 1/world factor is
+  passed to the AdamW kernel as ``grad_scale`` instead of a separate scaling pass.
+* Optional bf16 gradient communication (``comm_dtype=torch.bfloat16``) halves bytes on the wire.
+
+Works on gloo (CPU tests, world_size 2) and RCCL (GPU) unchanged.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class FlatParams:
+    """Re-home a module's trainable parameters into flat fp32 param / grad buffers."""
+
+    def __init__(self, module: torch.nn.Module, device: torch.device | str | None = None):
+        params = [p for p in module.parameters() if p.requires_grad]
+        params = list(reversed(params))  # gradient-arrival order
+        self.params = params
+        device = torch.device(device) if device is not None else params[0].device
+        n = sum(p.numel() for p in params)
+        # pad every segment to 4 elements (16 B) so vector kernels never straddle params
+        self.offsets = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += (p.numel() + 3) // 4 * 4
+        self.numel = off
+        self.flat = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        for p, o in zip(params, self.offsets):
+            k = p.numel()
+            self.flat[o: o + k].copy_(p.detach().reshape(-1).float())
+            p.data = self.flat[o: o + k].view_as(p)
+            p.grad = self.grad[o: o + k].view_as(p)
+        self.nparams = n
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+
+class BucketedAllReduce:
+    """Overlapped gradient all-reduce over slices of a FlatParams gradient buffer."""
+
+    def __init__(self, fp: FlatParams, group=None, bucket_mb: float = 16.0, comm_dtype: torch.dtype | None = None):
+        self.fp = fp
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.comm_dtype = comm_dtype
+        cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        # bucket boundaries on parameter boundaries, in gradient-arrival order
+        self.buckets: list[tuple[int, int, list[int]]] = []
+        start, members = 0, []
+        for i, (p, o) in enumerate(zip(fp.params, fp.offsets)):
+            end = o + (p.numel() + 3) // 4 * 4
+            members.append(i)
+            if end - start >= cap:
+                self.buckets.append((start, end, members))
+                start, members = end, []
+        if members:
+            self.buckets.append((start, fp.numel, members))
+        self.param_bucket = {}
+        for bi, (_, _, mem) in enumerate(self.buckets):
+            for i in mem:
+                self.param_bucket[i] = bi
+        self.pending = [0] * len(self.buckets)
+        self.works: list = []
+        self._hooks = []
+        if self.world > 1:
+            for i, p in enumerate(fp.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.reset()
+
+    def reset(self):
+        self.pending = [len(m) for (_, _, m) in self.buckets]
+        self.works = []
+        self._bufs = []
+
+    def _make_hook(self, i: int):
+        def hook(_p):
+            bi = self.param_bucket[i]
+            self.pending[bi] -= 1
+            if self.pending[bi] == 0:
+                self._launch(bi)
+        return hook
+
+    def _launch(self, bi: int):
+        s, e, _ = self.buckets[bi]
+        view = self.fp.grad[s:e]
+        if self.comm_dtype is not None and self.comm_dtype != torch.float32:
+            buf = view.to(self.comm_dtype)
+            w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._bufs.append((view, buf))
+        else:
+            w = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.works.append(w)
+
+    def finish(self) -> float:
+        """Wait for every bucket (launching any that never filled, e.g. unused params).
+        Returns the gradient scale (1/world) the optimizer must apply."""
+        if self.world == 1:
+            return 1.0
+        for bi, n in enumerate(self.pending):
+            if n > 0:
+                self.pending[bi] = 0
+                self._launch(bi)
+        for w in self.works:
+            w.wait()
+        for view, buf in self._bufs:
+            view.copy_(buf.float())
+        self.reset()
+        return 1.0 / self.world
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def broadcast_params(fp: FlatParams, src: int = 0, group=None) -> None:
+    """Weights broadcast at replica start."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.broadcast(fp.flat, src=src, group=group)
+
+
+def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from torchrun env vars. Returns (world, rank, local_rank)."""
+    import os
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local

@@ -1,0 +1,254 @@
+"""Cellpose fine-tuning loop (single GPU or data-parallel over RCCL).
+
+Mirrors the reference training core ``train_seg_with_callbacks``
+(``apps/cellpose-finetuning/main.py:1278-1713``): AdamW (``:1451-1453``), the reference's LR
+schedule (10-epoch linear warm-up, halving tail for n_epochs > 99 / > 300, ``:1430-1445``),
+per-epoch LR (``:1479-1480``), random rotate/resize augmentation to ``bsize`` crops
+(``:1501-1503``), ``_loss_fn_seg`` (``:1514-1517``), validation at epoch 0 and every
+``validation_interval`` epochs with pixel TP/FP/FN/TN on the cell-probability channel
+(``:1554-1675``, ``:1225-1270``), batch/epoch callbacks and a cooperative stop check.
+
+MI355X specifics: augmentation is a batched HIP affine-warp kernel on device-resident training
+images; the loss is a fused fwd+bwd HIP kernel; all parameters live in one flat fp32 buffer updated
+by ONE fused AdamW launch; in DP mode gradient buckets are all-reduced over RCCL while backward is
+still running (:mod:`bioengine_worker_amd.parallel.ddp`).  Optimizer moments, step, LR-schedule
+position and RNG state are checkpointed, so resume is exact (the reference resumes weights only,
+SURVEY.md §5 "Checkpoint / resume").
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import asdict, dataclass, field
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..models.cpnet import CPnet
+from ..ops import train_ops
+from ..parallel.ddp import BucketedAllReduce, FlatParams, broadcast_params
+
+
+@dataclass
+class TrainConfig:
+    batch_size: int = 1
+    bsize: int = 256
+    lr: float = 5e-5
+    weight_decay: float = 0.1
+    n_epochs: int = 100
+    scale_range: float = 0.5
+    validation_interval: int = 10
+    min_train_masks: int = 5
+    norm: str = "batch"
+    autocast_bf16: bool = True
+    bucket_mb: float = 16.0
+    comm_bf16: bool = False
+    seed: int = 0
+
+
+def lr_schedule(learning_rate: float, n_epochs: int) -> np.ndarray:
+    """Exact replica of the reference schedule (main.py:1430-1445)."""
+    s = np.linspace(0, learning_rate, 10)
+    s = np.append(s, learning_rate * np.ones(max(0, n_epochs - 10)))
+    if n_epochs > 300:
+        s = s[:-100]
+        for _ in range(10):
+            s = np.append(s, s[-1] / 2 * np.ones(10))
+    elif n_epochs > 99:
+        s = s[:-50]
+        for _ in range(10):
+            s = np.append(s, s[-1] / 2 * np.ones(5))
+    return s
+
+
+class CellposeTrainer:
+    def __init__(self, net: CPnet, cfg: TrainConfig, device, world_size: int = 1, rank: int = 0, group=None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.world = world_size
+        self.rank = rank
+        self.net = net.to(self.device).train()
+        if self.device.type == "cuda":
+            self.net = self.net.to(memory_format=torch.channels_last)
+        self.fp = FlatParams(self.net, self.device)
+        if world_size > 1:
+            broadcast_params(self.fp, 0, group)
+        self.ar = BucketedAllReduce(self.fp, group=group, bucket_mb=cfg.bucket_mb,
+                                    comm_dtype=torch.bfloat16 if cfg.comm_bf16 else None)
+        self.m = torch.zeros_like(self.fp.flat)
+        self.v = torch.zeros_like(self.fp.flat)
+        self.step_count = 0
+        self.lr = cfg.lr
+        self.gen = torch.Generator().manual_seed(cfg.seed * 1000 + rank)
+
+    # ------------------------------------------------------------------ core step
+    def set_lr(self, lr: float):
+        self.lr = float(lr)
+
+    def augment(self, imgs: torch.Tensor, lbls: torch.Tensor, rescale=None):
+        B, C, H, W = imgs.shape
+        aff, flip, _ = train_ops.random_affine_params(B, H, W, xy=(self.cfg.bsize, self.cfg.bsize),
+                                                      scale_range=self.cfg.scale_range, rescale=rescale,
+                                                      generator=self.gen)
+        return train_ops.affine_warp(imgs, lbls, aff, flip, self.cfg.bsize, self.cfg.bsize)
+
+    def forward_loss(self, x: torch.Tensor, lbl: torch.Tensor) -> torch.Tensor:
+        if self.device.type == "cuda":
+            x = x.contiguous(memory_format=torch.channels_last)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.cfg.autocast_bf16):
+                y = self.net(x)[0]
+        else:
+            y = self.net(x)[0]
+        return train_ops.seg_loss(y, lbl)
+
+    def step(self, imgs: torch.Tensor, lbls: torch.Tensor, rescale=None) -> torch.Tensor:
+        """One optimisation step on a batch of (full-size) training images + [cellprob, flowY, flowX] labels."""
+        x, lbl = self.augment(imgs, lbls, rescale)
+        self.fp.zero_grad()
+        loss = self.forward_loss(x, lbl)
+        loss.backward()
+        gscale = self.ar.finish()
+        self.step_count += 1
+        train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
+                              weight_decay=self.cfg.weight_decay, grad_scale=gscale)
+        return loss.detach()
+
+    @torch.no_grad()
+    def validate(self, imgs: torch.Tensor, lbls: torch.Tensor) -> dict:
+        self.net.eval()
+        x, lbl = self.augment(imgs, lbls)
+        if self.device.type == "cuda":
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.cfg.autocast_bf16):
+                y = self.net(x.contiguous(memory_format=torch.channels_last))[0]
+        else:
+            y = self.net(x)[0]
+        loss = train_ops.seg_loss_ref(y.float(), lbl)
+        pred = y[:, 2].float() > 0
+        tgt = lbl[:, 0] > 0.5
+        tp = (pred & tgt).sum().item()
+        fp = (pred & ~tgt).sum().item()
+        fn = (~pred & tgt).sum().item()
+        tn = (~pred & ~tgt).sum().item()
+        self.net.train()
+        prec = tp / max(1, tp + fp)
+        rec = tp / max(1, tp + fn)
+        return {"loss": float(loss), "tp": tp, "fp": fp, "fn": fn, "tn": tn, "precision": prec, "recall": rec,
+                "f1": 2 * prec * rec / max(1e-12, prec + rec), "iou": tp / max(1, tp + fp + fn)}
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self) -> dict:
+        return {"flat": self.fp.flat.detach().cpu(), "m": self.m.cpu(), "v": self.v.cpu(), "step": self.step_count,
+                "lr": self.lr, "rng": self.gen.get_state(), "cfg": asdict(self.cfg),
+                "buffers": {k: v.cpu() for k, v in self.net.named_buffers()}}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.fp.flat.copy_(sd["flat"].to(self.device))
+        self.m.copy_(sd["m"].to(self.device))
+        self.v.copy_(sd["v"].to(self.device))
+        self.step_count = int(sd["step"])
+        self.lr = float(sd["lr"])
+        self.gen.set_state(sd["rng"])
+        bufs = dict(self.net.named_buffers())
+        for k, v in sd.get("buffers", {}).items():
+            if k in bufs:
+                bufs[k].copy_(v.to(bufs[k].device))
+
+
+def build_trainer(cfg: TrainConfig, device, world_size: int = 1, rank: int = 0, net: CPnet | None = None,
+                  group=None) -> CellposeTrainer:
+    net = net or CPnet(norm=cfg.norm).randomize_(cfg.seed)
+    return CellposeTrainer(net, cfg, device, world_size, rank, group)
+
+
+# ------------------------------------------------------------------ data
+
+def synthetic_instances(B: int, H: int, W: int, ncells: int | None = None, seed: int = 0):
+    """Synthetic instance data: images [B, 2, H, W] float32 and label maps [B, H, W] int32 (disks)."""
+    rng = np.random.default_rng(seed)
+    ncells = ncells or max(4, H * W // 2500)
+    imgs = np.zeros((B, 2, H, W), np.float32)
+    labels = np.zeros((B, H, W), np.int32)
+    yy, xx = np.mgrid[0:H, 0:W]
+    for b in range(B):
+        k = 0
+        for _ in range(ncells * 4):
+            if k >= ncells:
+                break
+            r = rng.uniform(5, 12)
+            cy, cx = rng.uniform(r, H - r), rng.uniform(r, W - r)
+            d2 = (yy - cy) ** 2 + (xx - cx) ** 2
+            m = d2 <= r * r
+            if labels[b][m].any():
+                continue
+            k += 1
+            labels[b][m] = k
+            imgs[b, 0] += np.exp(-d2 / (2 * r * r)) * m
+            imgs[b, 1] += np.exp(-d2 / (2 * (0.4 * r) ** 2))
+    imgs += 0.05 * rng.standard_normal(imgs.shape).astype(np.float32)
+    return imgs, labels
+
+
+def labels_to_flows(labels: torch.Tensor) -> torch.Tensor:
+    """Label maps [B, H, W] -> training targets [B, 3, H, W] = (labels, flowY, flowX)."""
+    if labels.is_cuda:
+        from ..cellpose.gpu import masks_to_flows_gpu
+
+        mu, _, _ = masks_to_flows_gpu(labels.int().contiguous())
+    else:
+        from ..cellpose import reference as ref
+
+        mu = torch.stack([torch.from_numpy(ref.masks_to_flows(l.numpy())) for l in labels])
+    return torch.cat([labels.float()[:, None], mu], 1)
+
+
+def synthetic_train_batch(B: int, bsize: int = 256, device="cuda", seed: int = 0):
+    """Device-resident (imgs [B, 2, S, S], lbl [B, 3, S, S]) with S = bsize + 64 source images."""
+    S = bsize + 64
+    imgs, labels = synthetic_instances(B, S, S, seed=seed)
+    dev = torch.device(device)
+    imgs_t = torch.from_numpy(imgs).to(dev)
+    lbl = labels_to_flows(torch.from_numpy(labels).to(dev))
+    return imgs_t, lbl
+
+
+def run_training(trainer: CellposeTrainer, train_imgs: torch.Tensor, train_lbls: torch.Tensor, n_epochs: int,
+                 test_imgs: torch.Tensor | None = None, test_lbls: torch.Tensor | None = None,
+                 batch_callback=None, epoch_callback=None, stop_check=None, start_epoch: int = 0) -> dict:
+    """Epoch loop with the reference's schedule, callbacks and validation cadence.
+
+    In DP mode each rank takes a disjoint shard of every epoch's permutation (global batch =
+    batch_size * world)."""
+    cfg = trainer.cfg
+    sched = lr_schedule(cfg.lr, n_epochs)
+    nimg = train_imgs.shape[0]
+    losses = np.zeros(n_epochs)
+    test_losses: list = [None] * n_epochs
+    t0 = time.time()
+    gb = cfg.batch_size * trainer.world
+    for ep in range(start_epoch, n_epochs):
+        rng = np.random.default_rng(ep)
+        perm = rng.permutation(nimg)
+        trainer.set_lr(float(sched[min(ep, len(sched) - 1)]))
+        nb = math.ceil(nimg / gb)
+        for k in range(nb):
+            sl = perm[k * gb: (k + 1) * gb]
+            mine = sl[trainer.rank::trainer.world] if trainer.world > 1 else sl
+            if len(mine) == 0:
+                mine = sl[:1]
+            idx = torch.as_tensor(mine, device=train_imgs.device)
+            loss = trainer.step(train_imgs[idx], train_lbls[idx])
+            lv = float(loss)
+            losses[ep] += lv * len(sl)
+            if batch_callback is not None:
+                batch_callback(ep + 1, k, nb, lv, time.time() - t0, None)
+            if stop_check is not None and stop_check():
+                return {"train_losses": losses[: ep + 1].tolist(), "test_losses": test_losses[: ep + 1], "stopped": True}
+        losses[ep] /= nimg
+        metrics = None
+        if test_imgs is not None and (ep == 0 or (ep + 1) % cfg.validation_interval == 0):
+            metrics = trainer.validate(test_imgs, test_lbls)
+            test_losses[ep] = metrics["loss"]
+        if epoch_callback is not None:
+            epoch_callback(ep + 1, losses[ep], test_losses[ep], time.time() - t0, metrics)
+    return {"train_losses": losses.tolist(), "test_losses": test_losses, "stopped": False}

@@ -38,20 +38,23 @@ struct MaskJob {
 };
 
 // Heat diffusion of one mask; writes L = log(1 + T) for its pixels into Lout [B, H, W].
+// The heat field spans hundreds of orders of magnitude far from the centre of large masks (T decays
+// like exp(-d^2/t)); cellpose runs it in float64 for that reason and so do we (gfx950 runs fp64 VALU
+// at full vector rate, and this kernel is latency/LDS bound anyway).
 template <bool USE_LDS>
 __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs, int H,
-                                                     int W, const int* __restrict__ niter_img, float* __restrict__ scratch,
-                                                     float* __restrict__ Lout) {
+                                                     int W, const int* __restrict__ niter_img, double* __restrict__ scratch,
+                                                     double* __restrict__ Lout) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const MaskJob J = jobs[blockIdx.x];
   const int RY = J.ly + 2, RX = J.lx + 2, R = RY * RX;
-  float* T0;
-  float* T1;
+  double* T0;
+  double* T1;
   int* hy;
   int* hx;
   unsigned char* inm;
   if (USE_LDS) {
-    T0 = reinterpret_cast<float*>(smem);
+    T0 = reinterpret_cast<double*>(smem);
     T1 = T0 + R;
     hy = reinterpret_cast<int*>(T1 + R);
     hx = hy + RY;
@@ -67,7 +70,7 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
   __shared__ int total;
   const int tid = threadIdx.x;
   const int* Mb = M + (size_t)J.b * H * W;
-  for (int e = tid; e < R; e += MT) { T0[e] = 0.f; T1[e] = 0.f; }
+  for (int e = tid; e < R; e += MT) { T0[e] = 0.0; T1[e] = 0.0; }
   for (int e = tid; e < RY; e += MT) hy[e] = 0;
   for (int e = tid; e < RX; e += MT) hx[e] = 0;
   if (tid == 0) { best = ~0ull; total = 0; }
@@ -110,37 +113,37 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
   __syncthreads();
   const int ce = (int)(best & 0xffffffffu);
   const int niter = niter_img[J.b];
-  float* cur = T0;
-  float* nxt = T1;
+  double* cur = T0;
+  double* nxt = T1;
   for (int it = 0; it < niter; ++it) {
-    if (tid == 0) cur[ce] += 1.f;
+    if (tid == 0) cur[ce] += 1.0;
     __syncthreads();
     for (int e = tid; e < R; e += MT) {
       if (!inm[e]) continue;
-      float s = 0.f;
+      double s = 0.0;
 #pragma unroll
       for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
         for (int dx = -1; dx <= 1; ++dx) {
           const int q = e + dy * RX + dx;
-          s += inm[q] ? cur[q] : 0.f;
+          s += inm[q] ? cur[q] : 0.0;
         }
-      nxt[e] = s * (1.f / 9.f);
+      nxt[e] = s * (1.0 / 9.0);
     }
     __syncthreads();
-    float* t = cur; cur = nxt; nxt = t;
+    double* t = cur; cur = nxt; nxt = t;
   }
-  float* Lb = Lout + (size_t)J.b * H * W;
+  double* Lb = Lout + (size_t)J.b * H * W;
   for (int e = tid; e < R; e += MT) {
     if (!inm[e]) continue;
     const int y = J.y0 + e / RX - 1, x = J.x0 + e % RX - 1;
-    Lb[y * W + x] = log1pf(cur[e]);
+    Lb[y * W + x] = log1p(cur[e]);
   }
 }
 
 // mu = normalised central-difference gradient of L inside masks; per-mask squared error vs dP/5.
 // dp: optional [B, 2(or 3), H, W] network output (channel stride H*W, image stride dp_bstride).
-__global__ __launch_bounds__(256) void flow_grad_kernel(const int* __restrict__ M, const float* __restrict__ L, int B, int H,
+__global__ __launch_bounds__(256) void flow_grad_kernel(const int* __restrict__ M, const double* __restrict__ L, int B, int H,
                                                         int W, float* __restrict__ mu, const float* __restrict__ dp,
                                                         long long dp_bstride, float* __restrict__ err, int nlab) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -151,14 +154,13 @@ __global__ __launch_bounds__(256) void flow_grad_kernel(const int* __restrict__ 
   const int y = p / W, x = p % W;
   float gy = 0.f, gx = 0.f;
   if (lab > 0) {
-    const float* Lb = L + (size_t)b * HW;
-    const float up = y > 0 ? Lb[p - W] : 0.f, dn = y < H - 1 ? Lb[p + W] : 0.f;
-    const float lf = x > 0 ? Lb[p - 1] : 0.f, rt = x < W - 1 ? Lb[p + 1] : 0.f;
-    gy = dn - up;
-    gx = rt - lf;
-    const float nrm = sqrtf(gy * gy + gx * gx) + 1e-30f;
-    gy /= nrm;
-    gx /= nrm;
+    const double* Lb = L + (size_t)b * HW;
+    const double up = y > 0 ? Lb[p - W] : 0.0, dn = y < H - 1 ? Lb[p + W] : 0.0;
+    const double lf = x > 0 ? Lb[p - 1] : 0.0, rt = x < W - 1 ? Lb[p + 1] : 0.0;
+    const double dgy = dn - up, dgx = rt - lf;
+    const double nrm = sqrt(dgy * dgy + dgx * dgx) + 1e-60;
+    gy = (float)(dgy / nrm);
+    gx = (float)(dgx / nrm);
     if (dp && err) {
       const float* db = dp + (size_t)b * dp_bstride;
       const float ey = gy - db[p] * 0.2f, ex = gx - db[HW + p] * 0.2f;
@@ -242,8 +244,8 @@ int be_cp_bbox(const int* M, int B, int H, int W, int nlab, int* bbox, hipStream
 }
 
 // jobs: device array of MaskJob (7 x int64-aligned fields: see struct); lds_bytes > 0 => LDS variant.
-int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, float* scratch,
-                  float* Lout, int lds_bytes, hipStream_t s) {
+int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, double* scratch,
+                  double* Lout, int lds_bytes, hipStream_t s) {
   if (njobs == 0) return 0;
   if (lds_bytes > 0)
     hipLaunchKernelGGL((diffuse_kernel<true>), dim3(njobs), dim3(MT), lds_bytes, s, M, (const MaskJob*)jobs, H, W, niter_img,
@@ -254,7 +256,7 @@ int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const
   return BE_CHECK_LAUNCH();
 }
 
-int be_cp_flow_grad(const int* M, const float* L, int B, int H, int W, float* mu, const float* dp, long long dp_bstride,
+int be_cp_flow_grad(const int* M, const double* L, int B, int H, int W, float* mu, const float* dp, long long dp_bstride,
                     float* err, int nlab, hipStream_t s) {
   const long long n = (long long)B * H * W;
   hipLaunchKernelGGL(flow_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, L, B, H, W, mu, dp, dp_bstride,
