@@ -135,6 +135,15 @@ def _diffuse_scratch_doubles(ly, lx):
     return 2 * R + (ly + 2 + lx + 2 + 1) // 2 + (R + 7) // 8 + 2
 
 
+def label_counts(M: torch.Tensor, nlab: int) -> torch.Tensor:
+    """Pixels per label [B, nlab] (label 0 not counted)."""
+    B = M.shape[0]
+    counts = torch.zeros(B, nlab, dtype=torch.int32, device=M.device)
+    Mc = M.contiguous()
+    _native.call("be_label_counts", _native.ptr(Mc), B, Mc[0].numel(), nlab, _native.ptr(counts), _native.stream(M.device))
+    return counts
+
+
 def mask_bboxes(M: torch.Tensor, nlab: int) -> torch.Tensor:
     B, H, W = M.shape
     bbox = torch.empty(B, nlab, 4, dtype=torch.int32, device=M.device)
@@ -156,9 +165,7 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
     dev = M.device
     nlab = int(M.max().item()) + 1 if M.numel() else 1
     mu = torch.zeros(B, 2, H, W, dtype=torch.float32, device=dev)
-    counts = torch.zeros(B, nlab, dtype=torch.int32, device=dev)
-    counts.view(-1).index_add_(0, (M.long() + torch.arange(B, device=dev).view(B, 1, 1) * nlab).view(-1),
-                               torch.ones(M.numel(), dtype=torch.int32, device=dev))
+    counts = label_counts(M, nlab)
     if nlab <= 1:
         return mu, (torch.zeros(B, nlab, device=dev) if dp is not None else None), counts
     bbox = mask_bboxes(M, nlab)
@@ -207,9 +214,7 @@ def fill_holes_gpu(M: torch.Tensor, min_size: int = 15) -> torch.Tensor:
     nlab = int(M.max().item()) + 1 if M.numel() else 1
     if nlab <= 1:
         return M.clone()
-    counts = torch.zeros(B, nlab, dtype=torch.int32, device=dev)
-    counts.view(-1).index_add_(0, (M.long() + torch.arange(B, device=dev).view(B, 1, 1) * nlab).view(-1),
-                               torch.ones(M.numel(), dtype=torch.int32, device=dev))
+    counts = label_counts(M, nlab)
     keep = counts > 0
     if min_size > 0:
         keep &= counts >= min_size

@@ -279,3 +279,24 @@ int be_cp_fill_holes(const int* M, const void* jobs, int njobs, int H, int W, co
 int be_cp_mask_job_bytes() { return (int)sizeof(MaskJob); }
 
 }  // extern "C"
+
+// Pixel count per label (label 0 skipped, so background never contends on one counter).
+namespace {
+__global__ __launch_bounds__(256) void label_counts_kernel(const int* __restrict__ M, long long n, int HW, int nlab,
+                                                           int* __restrict__ counts) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int lab = M[i];
+    if (lab > 0) atomicAdd(counts + (size_t)(i / HW) * nlab + lab, 1);
+  }
+}
+}  // namespace
+
+extern "C" int be_label_counts(const int* M, int B, int HW, int nlab, int* counts, hipStream_t s) {
+  const long long n = (long long)B * HW;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(label_counts_kernel, dim3(blocks), dim3(256), 0, s, M, n, HW, nlab, counts);
+  return BE_CHECK_LAUNCH();
+}

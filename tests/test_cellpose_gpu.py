@@ -81,7 +81,7 @@ def test_tiles_gather_blend_roundtrip(gpu):
     assert t.shape == (2 * plan.nt, plan.by, plan.bx, 8)
     yt = t[..., :2].permute(0, 3, 1, 2).float().contiguous()
     back = plan.blend(yt, 2)
-    assert (back - x).abs().max().item() < 1e-2  # bf16 rounding only
+    assert ((back - x).abs() <= 8e-3 * x.abs() + 1e-3).all()  # bf16 rounding only
 
 
 @pytest.mark.gpu
