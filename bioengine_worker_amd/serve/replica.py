@@ -1,0 +1,351 @@
+"""Deployment replicas: in-process asyncio replicas and one-OS-process-per-replica (GPU pinned).
+
+Replaces Ray actors hosting Serve replicas (every request crossed >= 3 process
+boundaries and pickled full ndarrays through the object store).
+
+* :class:`LocalReplica` — the user class lives in the worker process; requests are direct awaits
+  (zero copies).  Used for CPU-only deployments (entry/orchestration deployments, demo apps).
+* :class:`ProcessReplica` — the user class lives in a child Python process started with
+  ``HIP_VISIBLE_DEVICES``/``ROCR_VISIBLE_DEVICES`` set to its reserved GPU(s), so each GPU replica
+  owns its device and its HIP context.  Requests travel over a Unix-socket connection as
+  pickle-protocol-5 frames with out-of-band buffers (ndarrays are sent as raw buffers, not
+  re-encoded).  Child stdout/stderr go to a per-replica log file that status calls tail.
+
+Both expose: ``start()``, ``call(method, args, kwargs, model_id)``, ``check_health()``,
+``stop()``, ``ongoing`` (in-flight requests) and ``logs(tail)``.
+"""
+from __future__ import annotations
+
+import asyncio
+import inspect
+import itertools
+import os
+import pickle
+import secrets
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+import uuid
+from pathlib import Path
+
+from . import context as rctx
+
+STARTING, RUNNING, UNHEALTHY, STOPPING, DEAD = "STARTING", "RUNNING", "UNHEALTHY", "STOPPING", "DEAD"
+
+
+def _new_tag(app: str, dep: str) -> str:
+    return f"{app}#{dep}#{uuid.uuid4().hex[:6]}"
+
+
+async def _resolve_result(res):
+    from .tasks import ObjectRef
+
+    if inspect.isawaitable(res) and not isinstance(res, ObjectRef):
+        res = await res
+    if isinstance(res, ObjectRef):
+        res = await res
+    return res
+
+
+class ReplicaBase:
+    def __init__(self, app: str, dep: str, cls, args, kwargs, gpu_ids: list[int], env: dict | None = None):
+        self.app = app
+        self.dep = dep
+        self.cls = cls
+        self.args = args
+        self.kwargs = kwargs
+        self.gpu_ids = list(gpu_ids)
+        self.env = dict(env or {})
+        self.tag = _new_tag(app, dep)
+        self.state = STARTING
+        self.ongoing = 0
+        self.started_at = time.time()
+        self.error: str | None = None
+        self.health_failures = 0
+        self.node_id = "head"
+
+    @property
+    def replica_id(self) -> str:
+        return self.tag
+
+    def info(self) -> dict:
+        return {"replica_id": self.tag, "state": self.state, "ongoing_requests": self.ongoing,
+                "gpu_ids": self.gpu_ids, "start_time": self.started_at, "node_id": self.node_id,
+                "error": self.error, "pid": getattr(self, "pid", os.getpid())}
+
+
+class LocalReplica(ReplicaBase):
+    async def start(self):
+        rctx.install_log_capture()
+        ctx = rctx.ReplicaContext(self.app, self.dep, self.tag, None, self.gpu_ids)
+        self._ctx = ctx
+
+        def build():
+            tok = rctx.set_current(ctx)
+            old_env = {k: os.environ.get(k) for k in self.env}
+            try:
+                os.environ.update({k: str(v) for k, v in self.env.items()})
+                obj = self.cls(*self.args, **self.kwargs)
+            finally:
+                rctx.reset_current(tok)
+            return obj
+
+        try:
+            tok = rctx.set_current(ctx)
+            try:
+                self.obj = await asyncio.to_thread(build)
+            finally:
+                rctx.reset_current(tok)
+            ctx.servable_object = self.obj
+            self.state = RUNNING
+        except BaseException as e:  # noqa: BLE001
+            self.state = DEAD
+            self.error = f"{type(e).__name__}: {e}"
+            raise
+
+    async def call(self, method: str, args, kwargs, model_id: str = ""):
+        fn = getattr(self.obj, method)
+        self.ongoing += 1
+        tok = rctx.set_current(self._ctx)
+        mtok = rctx.set_model_id(model_id)
+        try:
+            if inspect.iscoroutinefunction(fn) or inspect.iscoroutinefunction(getattr(fn, "__func__", None)):
+                res = await fn(*args, **kwargs)
+            else:
+                res = await asyncio.to_thread(_run_with_ctx, self._ctx, model_id, fn, args, kwargs)
+            return await _resolve_result(res)
+        finally:
+            rctx.reset_model_id(mtok)
+            rctx.reset_current(tok)
+            self.ongoing -= 1
+
+    async def check_health(self):
+        fn = getattr(self.obj, "check_health", None)
+        if fn is None:
+            return True
+        await self.call("check_health", [], {})
+        return True
+
+    async def stop(self, timeout: float = 20.0):
+        self.state = STOPPING
+        t0 = time.time()
+        while self.ongoing > 0 and time.time() - t0 < timeout:
+            await asyncio.sleep(0.05)
+        obj = getattr(self, "obj", None)
+        if obj is not None:
+            for hook in ("__del__",):
+                pass
+            self.obj = None
+        self.state = DEAD
+
+    def logs(self, tail: int = 100) -> list[str]:
+        buf = rctx.log_buffer(self.tag)
+        return list(buf)[-tail:] if tail > 0 else list(buf)
+
+
+def _run_with_ctx(ctx, model_id, fn, args, kwargs):
+    tok = rctx.set_current(ctx)
+    mtok = rctx.set_model_id(model_id)
+    try:
+        return fn(*args, **kwargs)
+    finally:
+        rctx.reset_model_id(mtok)
+        rctx.reset_current(tok)
+
+
+# ====================================================================== process replicas
+
+
+def dumps(obj) -> list[bytes]:
+    import cloudpickle
+
+    bufs: list = []
+    head = cloudpickle.dumps(obj, protocol=5, buffer_callback=bufs.append)
+    return [head] + [bytes(b.raw()) if hasattr(b, "raw") else bytes(b) for b in bufs]
+
+
+def loads(frames: list[bytes]):
+    return pickle.loads(frames[0], buffers=frames[1:])
+
+
+def send_frames(conn, lock: threading.Lock, obj):
+    frames = dumps(obj)
+    with lock:
+        conn.send(len(frames))
+        for f in frames:
+            conn.send_bytes(f)
+
+
+def recv_frames(conn):
+    n = conn.recv()
+    frames = [conn.recv_bytes() for _ in range(n)]
+    return loads(frames)
+
+
+class ProcessReplica(ReplicaBase):
+    _ids = itertools.count(1)
+
+    def __init__(self, *a, log_dir: str | Path | None = None, python: str | None = None, **k):
+        super().__init__(*a, **k)
+        self.log_dir = Path(log_dir or tempfile.gettempdir()) / "bioengine_replicas"
+        self.log_dir.mkdir(parents=True, exist_ok=True)
+        self.log_file = self.log_dir / f"{self.tag.replace('#', '_')}.log"
+        self.python = python or sys.executable
+        self.pending: dict[int, asyncio.Future] = {}
+        self.rids = itertools.count(1)
+        self.send_lock = threading.Lock()
+        self.proc = None
+        self.conn = None
+
+    async def start(self):
+        from multiprocessing.connection import Listener
+
+        self.loop = asyncio.get_running_loop()
+        sock = str(Path(tempfile.gettempdir()) / f"be-rep-{os.getpid()}-{next(self._ids)}-{uuid.uuid4().hex[:6]}.sock")
+        key = secrets.token_bytes(16)
+        listener = Listener(sock, family="AF_UNIX", authkey=key)
+        env = dict(os.environ)
+        env.update({k: str(v) for k, v in self.env.items()})
+        if self.gpu_ids:
+            # indices are relative to the parent's visible set; the child sees exactly its GPUs
+            env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in self.gpu_ids)
+        env["BE_REPLICA_SOCK"] = sock
+        env["BE_REPLICA_KEY"] = key.hex()
+        env["BE_REPLICA_TAG"] = self.tag
+        root = str(Path(__file__).resolve().parents[2])
+        env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        logf = open(self.log_file, "ab", buffering=0)
+        self.proc = subprocess.Popen([self.python, "-u", "-m", "bioengine_worker_amd.serve.replica_worker"], env=env,
+                                     stdout=logf, stderr=subprocess.STDOUT, close_fds=True)
+        self.pid = self.proc.pid
+        logf.close()
+        try:
+            self.conn = await asyncio.wait_for(asyncio.to_thread(listener.accept), timeout=120)
+        except Exception as e:
+            self._kill()
+            self.state = DEAD
+            self.error = f"replica process failed to connect: {e}"
+            raise RuntimeError(self.error) from e
+        finally:
+            listener.close()
+            try:
+                os.unlink(sock)
+            except OSError:
+                pass
+        self._reader = threading.Thread(target=self._read_loop, daemon=True)
+        self._reader.start()
+        fut = self.loop.create_future()
+        self.pending[0] = fut
+        await asyncio.to_thread(send_frames, self.conn, self.send_lock,
+                                ("init", self.cls, self.args, self.kwargs, self.app, self.dep, self.tag, self.gpu_ids))
+        ok, err = await fut
+        if not ok:
+            self.state = DEAD
+            self.error = err
+            self._kill()
+            raise RuntimeError(f"replica {self.tag} failed to initialize: {err}")
+        self.state = RUNNING
+
+    def _read_loop(self):
+        while True:
+            try:
+                msg = recv_frames(self.conn)
+            except (EOFError, OSError):
+                break
+            except Exception as e:  # undecodable result: fail the request that produced it
+                msg = ("fatal", repr(e))
+            self.loop.call_soon_threadsafe(self._dispatch, msg)
+        self.loop.call_soon_threadsafe(self._on_exit)
+
+    def _dispatch(self, msg):
+        kind = msg[0]
+        if kind == "ready":
+            fut = self.pending.pop(0, None)
+            if fut and not fut.done():
+                fut.set_result((msg[1], msg[2]))
+        elif kind == "result":
+            _, rid, ok, val = msg
+            fut = self.pending.pop(rid, None)
+            if fut and not fut.done():
+                if ok:
+                    fut.set_result(val)
+                else:
+                    fut.set_exception(val if isinstance(val, BaseException) else RuntimeError(str(val)))
+        elif kind == "hcall":
+            _, rid, app, dep, method, args, kwargs, model_id = msg
+            asyncio.ensure_future(self._serve_hcall(rid, app, dep, method, args, kwargs, model_id))
+
+    async def _serve_hcall(self, rid, app, dep, method, args, kwargs, model_id):
+        from .controller import get_router
+
+        try:
+            val = await get_router().call(app, dep, method, args, kwargs, model_id)
+            out = ("hresult", rid, True, val)
+        except BaseException as e:  # noqa: BLE001
+            out = ("hresult", rid, False, e)
+        try:
+            await asyncio.to_thread(send_frames, self.conn, self.send_lock, out)
+        except Exception:
+            pass
+
+    def _on_exit(self):
+        if self.state not in (STOPPING, DEAD):
+            self.state = DEAD
+            self.error = self.error or f"replica process exited (code {self.proc.poll() if self.proc else None})"
+        for fut in self.pending.values():
+            if not fut.done():
+                fut.set_exception(RuntimeError(f"replica {self.tag} died: {self.error}"))
+        self.pending.clear()
+
+    async def call(self, method: str, args, kwargs, model_id: str = ""):
+        if self.state == DEAD:
+            raise RuntimeError(f"replica {self.tag} is dead: {self.error}")
+        rid = next(self.rids)
+        fut = self.loop.create_future()
+        self.pending[rid] = fut
+        self.ongoing += 1
+        try:
+            await asyncio.to_thread(send_frames, self.conn, self.send_lock, ("call", rid, method, args, kwargs, model_id))
+            return await fut
+        finally:
+            self.ongoing -= 1
+
+    async def check_health(self):
+        if self.proc is None or self.proc.poll() is not None:
+            raise RuntimeError(f"replica process is not running (exit code {self.proc.poll() if self.proc else None})")
+        await self.call("__be_check_health__", [], {})
+        return True
+
+    def _kill(self):
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+
+    async def stop(self, timeout: float = 20.0):
+        self.state = STOPPING
+        t0 = time.time()
+        while self.ongoing > 0 and time.time() - t0 < timeout:
+            await asyncio.sleep(0.05)
+        try:
+            if self.conn is not None:
+                await asyncio.to_thread(send_frames, self.conn, self.send_lock, ("stop",))
+        except Exception:
+            pass
+        if self.proc is not None:
+            try:
+                await asyncio.wait_for(asyncio.to_thread(self.proc.wait), timeout=5)
+            except asyncio.TimeoutError:
+                self._kill()
+        self.state = DEAD
+
+    def logs(self, tail: int = 100) -> list[str]:
+        try:
+            lines = self.log_file.read_text(errors="replace").splitlines()
+        except OSError:
+            return []
+        return lines[-tail:] if tail > 0 else lines

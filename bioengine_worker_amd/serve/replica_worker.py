@@ -1,0 +1,165 @@
+"""Child-process side of a :class:`~bioengine_worker_amd.serve.replica.ProcessReplica`.
+
+Started as ``python -m bioengine_worker_amd.serve.replica_worker`` with ``HIP_VISIBLE_DEVICES`` set to
+the replica's GPU(s).  Connects back to the parent over a Unix socket, instantiates the user
+deployment class, and serves requests concurrently on its own asyncio loop.  Calls on
+``DeploymentHandle`` objects made inside the replica are forwarded to the parent's router.
+"""
+from __future__ import annotations
+
+import asyncio
+import inspect
+import itertools
+import os
+import sys
+import threading
+import traceback
+
+
+class _ChildRouter:
+    def __init__(self, conn, lock, loop):
+        self.conn = conn
+        self.lock = lock
+        self.loop = loop
+        self.rids = itertools.count(1)
+        self.pending: dict[int, asyncio.Future] = {}
+
+    async def call(self, app, dep, method, args, kwargs, model_id=""):
+        from .replica import send_frames
+
+        rid = next(self.rids)
+        fut = self.loop.create_future()
+        self.pending[rid] = fut
+        await asyncio.to_thread(send_frames, self.conn, self.lock, ("hcall", rid, app, dep, method, args, kwargs, model_id))
+        return await fut
+
+
+async def _main():
+    from multiprocessing.connection import Client
+
+    from . import context as rctx
+    from . import controller as ctrl_mod
+    from .replica import _resolve_result, recv_frames, send_frames
+
+    sock = os.environ["BE_REPLICA_SOCK"]
+    key = bytes.fromhex(os.environ["BE_REPLICA_KEY"])
+    conn = Client(sock, family="AF_UNIX", authkey=key)
+    lock = threading.Lock()
+    loop = asyncio.get_running_loop()
+    router = _ChildRouter(conn, lock, loop)
+    ctrl_mod._set_child_router(router)
+    inbox: asyncio.Queue = asyncio.Queue()
+
+    def reader():
+        while True:
+            try:
+                msg = recv_frames(conn)
+            except (EOFError, OSError):
+                loop.call_soon_threadsafe(inbox.put_nowait, ("stop",))
+                return
+            except Exception as e:  # noqa: BLE001
+                print(f"replica: undecodable message: {e!r}", flush=True)
+                continue
+            loop.call_soon_threadsafe(inbox.put_nowait, msg)
+
+    threading.Thread(target=reader, daemon=True).start()
+    obj = None
+    ctx = None
+
+    async def handle_call(rid, method, args, kwargs, model_id):
+        tok = rctx.set_current(ctx)
+        mtok = rctx.set_model_id(model_id)
+        try:
+            if method == "__be_check_health__":
+                fn = getattr(obj, "check_health", None)
+                res = None
+                if fn is not None:
+                    res = fn()
+                    if inspect.isawaitable(res):
+                        res = await res
+            else:
+                fn = getattr(obj, method)
+                if inspect.iscoroutinefunction(fn):
+                    res = await fn(*args, **kwargs)
+                else:
+                    from .replica import _run_with_ctx
+
+                    res = await asyncio.to_thread(_run_with_ctx, ctx, model_id, fn, args, kwargs)
+                res = await _resolve_result(res)
+            out = ("result", rid, True, res)
+        except BaseException as e:  # noqa: BLE001
+            traceback.print_exc()
+            out = ("result", rid, False, _picklable_exc(e))
+        finally:
+            rctx.reset_model_id(mtok)
+            rctx.reset_current(tok)
+        try:
+            await asyncio.to_thread(send_frames, conn, lock, out)
+        except Exception as e:  # result not picklable
+            await asyncio.to_thread(send_frames, conn, lock, ("result", rid, False, RuntimeError(f"unpicklable result: {e}")))
+
+    while True:
+        msg = await inbox.get()
+        kind = msg[0]
+        if kind == "init":
+            _, cls, args, kwargs, app, dep, tag, gpu_ids = msg
+            ctx = rctx.ReplicaContext(app, dep, tag, None, gpu_ids)
+            tok = rctx.set_current(ctx)
+            try:
+                obj = await asyncio.to_thread(_construct, ctx, cls, args, kwargs)
+                ctx.servable_object = obj
+                await asyncio.to_thread(send_frames, conn, lock, ("ready", True, None))
+            except BaseException as e:  # noqa: BLE001
+                traceback.print_exc()
+                await asyncio.to_thread(send_frames, conn, lock, ("ready", False, f"{type(e).__name__}: {e}"))
+            finally:
+                rctx.reset_current(tok)
+        elif kind == "call":
+            _, rid, method, args, kwargs, model_id = msg
+            asyncio.ensure_future(handle_call(rid, method, args, kwargs, model_id))
+        elif kind == "hresult":
+            _, rid, ok, val = msg
+            fut = router.pending.pop(rid, None)
+            if fut is not None and not fut.done():
+                if ok:
+                    fut.set_result(val)
+                else:
+                    fut.set_exception(val if isinstance(val, BaseException) else RuntimeError(str(val)))
+        elif kind == "stop":
+            break
+    try:
+        conn.close()
+    except Exception:
+        pass
+
+
+def _construct(ctx, cls, args, kwargs):
+    from . import context as rctx
+
+    tok = rctx.set_current(ctx)
+    try:
+        return cls(*args, **kwargs)
+    finally:
+        rctx.reset_current(tok)
+
+
+def _picklable_exc(e: BaseException) -> BaseException:
+    import pickle
+
+    try:
+        pickle.dumps(e)
+        return e
+    except Exception:
+        return RuntimeError(f"{type(e).__name__}: {e}")
+
+
+def main():
+    sys.path.insert(0, os.getcwd())
+    from ..compat import install
+
+    install()
+    asyncio.run(_main())
+
+
+if __name__ == "__main__":
+    main()

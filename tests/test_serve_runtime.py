@@ -1,0 +1,222 @@
+"""Native serving runtime with the Ray-Serve-compatible API (no Ray installed)."""
+import asyncio
+import os
+import time
+
+import pytest
+
+from bioengine_worker_amd.compat import install
+
+install()
+
+from ray import serve  # noqa: E402  (the native shim)
+from ray.serve.handle import DeploymentHandle  # noqa: E402
+
+from bioengine_worker_amd.serve import controller as ctrl_mod  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def fresh_controller():
+    ctrl_mod.set_controller(None)
+    yield
+    ctrl_mod.set_controller(None)
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0})
+class Adder:
+    def __init__(self, k: int = 1):
+        self.k = k
+        self.tag = serve.get_replica_context().replica_tag
+
+    async def add(self, x):
+        return x + self.k
+
+    def sync_mul(self, x):
+        return x * self.k
+
+    @serve.multiplexed(max_num_models_per_replica=2)
+    async def get_model(self, model_id: str):
+        self.loads = getattr(self, "loads", 0) + 1
+        return f"model-{model_id}"
+
+    async def use_model(self):
+        return await self.get_model(serve.get_multiplexed_model_id())
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0})
+class Entry:
+    def __init__(self, adder: DeploymentHandle):
+        self.adder = adder
+
+    async def __call__(self, x):
+        return await self.adder.add.remote(x)
+
+    async def mux(self, mid):
+        return await self.adder.options(multiplexed_model_id=mid).use_model.remote()
+
+
+@pytest.mark.unit
+def test_compose_route_and_multiplex():
+    async def main():
+        h = await serve.run(Entry.bind(Adder.bind(5)), name="app1")
+        assert await h.remote(1) == 6
+        assert await h.mux.remote("a") == "model-a"
+        st = serve.status()
+        assert st.applications["app1"].status == "RUNNING"
+        assert set(st.applications["app1"].deployments) == {"Adder", "Entry"}
+        await serve.delete("app1")
+        assert "app1" not in serve.status().applications
+
+    asyncio.run(main())
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0}, max_ongoing_requests=1, max_queued_requests=2)
+class Slow:
+    async def work(self, t):
+        await asyncio.sleep(t)
+        return t
+
+
+@pytest.mark.unit
+def test_admission_queue_and_backpressure():
+    from ray.serve.exceptions import BackPressureError
+
+    async def main():
+        h = await serve.run(Slow.bind(), name="slow")
+        rs = [h.work.remote(0.2) for _ in range(3)]
+        await asyncio.sleep(0.05)
+        with pytest.raises(BackPressureError):
+            await h.work.remote(0.0)
+        assert await asyncio.gather(*rs) == [0.2] * 3
+        await serve.delete("slow")
+
+    asyncio.run(main())
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0}, max_ongoing_requests=64)
+class Batcher:
+    def __init__(self):
+        self.sizes = []
+
+    @serve.batch(max_batch_size=8, batch_wait_timeout_s=0.05)
+    async def infer(self, xs):
+        self.sizes.append(len(xs))
+        await asyncio.sleep(0.01)
+        return [x * 2 for x in xs]
+
+    async def sizes_seen(self):
+        return self.sizes
+
+
+@pytest.mark.unit
+def test_continuous_batching():
+    async def main():
+        h = await serve.run(Batcher.bind(), name="b")
+        out = await asyncio.gather(*[h.infer.remote(i) for i in range(20)])
+        assert out == [2 * i for i in range(20)]
+        sizes = await h.sizes_seen.remote()
+        assert sum(sizes) == 20 and max(sizes) == 8 and len(sizes) <= 4
+        await serve.delete("b")
+
+    asyncio.run(main())
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0}, max_ongoing_requests=1,
+                  autoscaling_config={"min_replicas": 1, "max_replicas": 3, "target_ongoing_requests": 1,
+                                      "upscale_delay_s": 0.0, "downscale_delay_s": 0.0})
+class Scaler:
+    async def work(self, t):
+        await asyncio.sleep(t)
+        return serve.get_replica_context().replica_tag
+
+
+@pytest.mark.unit
+def test_autoscaling_up_and_down():
+    async def main():
+        ctrl_mod.set_controller(ctrl_mod.ServeController(tick_s=0.05))
+        h = await serve.run(Scaler.bind(), name="s")
+        rs = [h.work.remote(0.6) for _ in range(6)]
+        await asyncio.sleep(0.4)
+        n_up = len(ctrl_mod.get_controller().apps["s"].deployments["Scaler"].running())
+        tags = set(await asyncio.gather(*rs))
+        assert n_up >= 2 and len(tags) >= 2
+        await asyncio.sleep(0.5)
+        assert len(ctrl_mod.get_controller().apps["s"].deployments["Scaler"].running()) == 1
+        await serve.delete("s")
+
+    asyncio.run(main())
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0}, health_check_period_s=0.1)
+class Flaky:
+    def __init__(self):
+        self.fail = False
+
+    async def set_fail(self):
+        self.fail = True
+
+    async def check_health(self):
+        if self.fail:
+            raise RuntimeError("boom")
+
+    async def tag(self):
+        return serve.get_replica_context().replica_tag
+
+
+@pytest.mark.unit
+def test_unhealthy_replica_is_replaced():
+    async def main():
+        ctrl_mod.set_controller(ctrl_mod.ServeController(tick_s=0.05))
+        h = await serve.run(Flaky.bind(), name="f")
+        t0 = await h.tag.remote()
+        await h.set_fail.remote()
+        for _ in range(60):
+            await asyncio.sleep(0.1)
+            ds = ctrl_mod.get_controller().apps["f"].deployments["Flaky"]
+            if ds.running() and ds.running()[0].tag != t0:
+                break
+        assert await h.tag.remote() != t0
+        assert ds.history and "boom" in (ds.history[-1]["error"] or "")
+        await serve.delete("f")
+
+    asyncio.run(main())
+
+
+@pytest.mark.integration
+def test_process_replica_and_handle_callback(monkeypatch):
+    monkeypatch.setenv("BIOENGINE_REPLICA_MODE", "process")
+
+    async def main():
+        h = await serve.run(Entry.bind(Adder.bind(3)), name="proc")
+        assert await h.remote(4) == 7
+        assert await h.mux.remote("z") == "model-z"
+        ds = ctrl_mod.get_controller().apps["proc"].deployments["Adder"]
+        assert ds.running()[0].pid != os.getpid()
+        await serve.delete("proc")
+
+    asyncio.run(main())
+
+
+@pytest.mark.unit
+def test_remote_tasks_thread_and_isolated():
+    import ray
+
+    @ray.remote
+    def sq(x):
+        return x * x
+
+    assert ray.get([sq.remote(i) for i in range(4)]) == [0, 1, 4, 9]
+
+    def whoami():
+        return os.getpid()
+
+    pid = ray.get(ray.remote(whoami).options(isolate=True).remote())
+    assert pid != os.getpid()
+
+    def bad():
+        raise ValueError("nope")
+
+    from ray.exceptions import RayTaskError
+
+    with pytest.raises(RayTaskError):
+        ray.get(ray.remote(bad).remote())
