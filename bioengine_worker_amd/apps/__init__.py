@@ -1,1 +1,1 @@
-
+"""App platform: manifests, builder, service bridge, lifecycle manager."""

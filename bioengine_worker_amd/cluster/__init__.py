@@ -1,1 +1,1 @@
-
+"""Cluster runtime: node agent + resource accounting, SLURM autoscaling."""

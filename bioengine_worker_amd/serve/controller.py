@@ -164,7 +164,18 @@ class DeploymentState:
         self.replicas.append(r)
         try:
             await r.start()
-        except BaseException:
+            # initial readiness probe: runs the app's lazy async_init before traffic is admitted
+            from .replica import STARTING as _ST
+
+            r.state = _ST
+            await asyncio.wait_for(r.check_health(), timeout=max(120.0, 10 * self.cfg.health_check_timeout_s))
+            r.state = RUNNING
+        except BaseException as e:
+            r.error = r.error or f"{type(e).__name__}: {e}"
+            try:
+                await r.stop(1.0)
+            except Exception:
+                pass
             self._retire(r)
             raise
         self._wake()

@@ -1,1 +1,1 @@
-
+"""The BioEngine worker service (L6) and code executor."""
