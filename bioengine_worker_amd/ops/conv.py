@@ -151,8 +151,34 @@ def fused_conv2d_ref(x, pc: PackedConv, x2=None, scale=None, shift=None, relu=Fa
     return y.to(x.dtype).contiguous()
 
 
+#: waves per workgroup (tile = 2*nw rows x 32 cols); overridable per call and per (ks, cin, cout).
+NW_POLICY: dict = {}
+DEFAULT_NW = None  # None = shape policy below; 4 / 8 forces one value (sweeps)
+
+
+def choose_nw(pc: PackedConv, H: int, W: int, inmode: str = "none", has_x2: bool = False) -> int:
+    """Measured on MI355X (tools/conv_sweep2.py, profiles/conv_sweep.md): the persistent
+    small-channel variants (tco <= 32) prefer 8 waves (more halo reuse per weight fetch); the
+    64-channel variants prefer 4 waves (two blocks/CU hide the barrier) except when the halo loader
+    does the 2x2 max-pool (8 waves amortise the 4x wider input read).  The skip-add (x2) 64-channel
+    variant only fits without spills at 4 waves."""
+    key = (pc.ks, pc.cin_pad, pc.cout, inmode)
+    if key in NW_POLICY:
+        return NW_POLICY[key]
+    if DEFAULT_NW is not None:
+        return DEFAULT_NW
+    if pc.tco <= 32:
+        return 8
+    if has_x2:
+        return 4
+    if inmode == "pool2" and pc.ks == 3:
+        return 8
+    return 4
+
+
 def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=None, relu=False, residual=None,
-                 inmode: str = "none", out_nchw_f32: bool = False, cout_valid: int | None = None) -> torch.Tensor:
+                 inmode: str = "none", out_nchw_f32: bool = False, cout_valid: int | None = None,
+                 nw: int | None = None) -> torch.Tensor:
     """Fused conv on NHWC activations.  ``x`` is [N, Hs, Ws, Cin_pad] bf16 (GPU) or any float (CPU)."""
     N, Hs, Ws, Cin = x.shape
     if inmode == "up2":
@@ -193,6 +219,6 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
         _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns, int(bool(relu)),
         _native.ptr(pc.wp), _native.ptr(pc.bias), _native.ptr(residual), _native.ptr(out),
         N, H, W, Hs, Ws, Cin, cout_store, cout_valid, pc.ks, pc.ck, pc.tco, INMODES[inmode], int(out_nchw_f32),
-        _native.stream(x.device),
+        int(nw or choose_nw(pc, H, W, inmode, x2 is not None)), _native.stream(x.device),
     )
     return out

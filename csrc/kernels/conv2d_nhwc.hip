@@ -13,10 +13,13 @@
 //  * NHWC bf16 activations, implicit GEMM on v_mfma_f32_16x16x32_bf16 with the *weights as the A
 //    operand* (rows = output channels) and pixels as B, so each lane ends with 4 consecutive
 //    output channels of one pixel -> 8-byte stores in NHWC and 64-byte rows in NCHW heads.
-//  * one workgroup = 4 waves = an 8x32 output pixel tile x TCO output channels; the input halo
-//    ((8+KS-1) x (32+KS-1) x CK channels) is staged through LDS once per Cin chunk with the
+//  * one workgroup = NW waves = a (2*NW)x32 output pixel tile x TCO output channels; the input
+//    halo ((2NW+KS-1) x (32+KS-1) x CK channels) is staged through LDS once per Cin chunk with the
 //    pre-activation (BN affine, style shift, skip add, ReLU, pool/upsample) applied in registers
 //    on the way in, so the activated tensor never exists in HBM.
+//  * software pipeline across Cin chunks: the global loads of chunk c+1 (halo + packed weights)
+//    are issued into registers right after chunk c is committed to LDS, so they are in flight
+//    while the MFMAs of chunk c run (register staging, "issue early / write late").
 //  * K ordering inside a chunk is tap-major / channel-minor (k = tap*CK + c), so a 16-byte
 //    B fragment is 8 contiguous channels of one shifted pixel; small-Cin layers (Cin=8) pack 4
 //    taps into one 32-deep MFMA step instead of padding channels to 32.
@@ -25,9 +28,7 @@
 
 namespace {
 
-constexpr int TH = 8;    // output tile rows
-constexpr int TW = 32;   // output tile cols
-constexpr int NT = 256;  // threads / block (4 waves)
+constexpr int TW = 32;  // output tile cols (two 16-pixel MFMA column tiles)
 
 struct ConvArgs {
   const bf16_t* x;       // [N, Hs, Ws, Cin]
@@ -44,139 +45,138 @@ struct ConvArgs {
   int prelu;
   int out_f32_nchw;
   int tiles_x, tiles_y;
+  int persist_blocks;  // 0 = auto
 };
 
-template <int KS, int CK, int TCO, int INMODE>
-__global__ __launch_bounds__(NT, 2) void conv2d_nhwc_kernel(ConvArgs a) {
-  constexpr int HH = TH + KS - 1;
-  constexpr int HW_ = TW + KS - 1;
-  constexpr int PSTR = CK + 8;                    // elements per pixel in LDS (16 B pad)
-  constexpr int KSTEPS = (KS * KS * CK + 31) / 32;
-  constexpr int KPL = KSTEPS * 32;
-  constexpr int WSTR = KPL + 8;                   // elements per cout row in LDS
-  constexpr int CG = CK / 8;                      // 8-channel groups per pixel
-  constexpr int NCT = TCO / 16;
+template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
+struct Cfg {
+  static constexpr int NT = NW * 64;
+  static constexpr int TH = 2 * NW;
+  static constexpr int HH = TH + KS - 1;
+  static constexpr int HW_ = TW + KS - 1;
+  static constexpr int PSTR = CK + 8;
+  static constexpr int KSTEPS = (KS * KS * CK + 31) / 32;
+  static constexpr int KPL = KSTEPS * 32;
+  static constexpr int WSTR = KPL + 8;
+  static constexpr int CG = CK / 8;
+  static constexpr int NCT = TCO / 16;
+  static constexpr int HU = HH * HW_ * CG;
+  static constexpr int HUPT = (HU + NT - 1) / NT;
+  static constexpr int WU = TCO * KPL / 8;
+  static constexpr int WUPT = (WU + NT - 1) / NT;
+  static constexpr size_t LDS = (size_t)(HH * HW_ * PSTR + TCO * WSTR) * sizeof(bf16_t);
+};
 
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* hl = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* wl = hl + HH * HW_ * PSTR;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-
-  int bid = blockIdx.x;
-  const int tiles_per_img = a.tiles_x * a.tiles_y;
-  const int n = bid / tiles_per_img;
-  const int t = bid % tiles_per_img;
-  const int ty0 = (t / a.tiles_x) * TH;
-  const int tx0 = (t % a.tiles_x) * TW;
-  const int co0 = blockIdx.y * TCO;
-
-  f32x4 acc[NCT][4];
+// Issue the global loads of one Cin chunk into registers (halo raw values + packed weights).
+template <typename C, int KS, int INMODE, bool X2>
+__device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, int tx0, int co0, int ch, int tid,
+                                            u32x4 (&hraw)[C::HUPT], u32x4 (&h2raw)[X2 ? C::HUPT : 1],
+                                            u32x4 (&wraw)[C::WUPT], bool with_weights) {
+  const int c0 = ch * (C::CG * 8);
 #pragma unroll
-  for (int i = 0; i < NCT; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const float* shift_row = a.pshift ? a.pshift + (size_t)n * a.pshift_ns : nullptr;
-
-  for (int ch = 0; ch < a.nchunk; ++ch) {
-    const int c0 = ch * CK;
-    // ---- stage activated input halo into LDS ----
-    for (int u = tid; u < HH * HW_ * CG; u += NT) {
-      const int pix = u / CG, cg = u % CG;
-      const int hy = pix / HW_, hx = pix % HW_;
-      const int gy = ty0 + hy - KS / 2, gx = tx0 + hx - KS / 2;
-      u32x4 packed = (u32x4){0u, 0u, 0u, 0u};
+  for (int i = 0; i < C::HUPT; ++i) {
+    const int u = tid + i * C::NT;
+    u32x4 r = (u32x4){0u, 0u, 0u, 0u};
+    u32x4 r2 = (u32x4){0u, 0u, 0u, 0u};
+    if (u < C::HU) {
+      const int pix = u / C::CG, cg = u % C::CG;
+      const int gy = ty0 + pix / C::HW_ - KS / 2, gx = tx0 + pix % C::HW_ - KS / 2;
       if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
         const int c = c0 + cg * 8;
-        float v[8];
         if (INMODE == 0) {
-          const u32x4 r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + gy) * a.Ws + gx) * a.Cin + c);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(r[j]); v[2 * j + 1] = hi_bf(r[j]); }
-        } else if (INMODE == 1) {  // nearest upsample x2: source is half resolution
-          const u32x4 r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * a.Cin + c);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(r[j]); v[2 * j + 1] = hi_bf(r[j]); }
-        } else {  // maxpool 2x2: source is double resolution
+          r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + gy) * a.Ws + gx) * a.Cin + c);
+        } else if (INMODE == 1) {
+          r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * a.Cin + c);
+        } else {
           const bf16_t* base = a.x + (((size_t)n * a.Hs + 2 * gy) * a.Ws + 2 * gx) * a.Cin + c;
           const u32x4 r0 = *reinterpret_cast<const u32x4*>(base);
           const u32x4 r1 = *reinterpret_cast<const u32x4*>(base + a.Cin);
-          const u32x4 r2 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin);
-          const u32x4 r3 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin + a.Cin);
+          const u32x4 q0 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin);
+          const u32x4 q1 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin + a.Cin);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[2 * j] = fmaxf(fmaxf(lo_bf(r0[j]), lo_bf(r1[j])), fmaxf(lo_bf(r2[j]), lo_bf(r3[j])));
-            v[2 * j + 1] = fmaxf(fmaxf(hi_bf(r0[j]), hi_bf(r1[j])), fmaxf(hi_bf(r2[j]), hi_bf(r3[j])));
+          for (int j = 0; j < 4; ++j) {  // max of bf16 values is exact in bf16
+            const float lo = fmaxf(fmaxf(lo_bf(r0[j]), lo_bf(r1[j])), fmaxf(lo_bf(q0[j]), lo_bf(q1[j])));
+            const float hi = fmaxf(fmaxf(hi_bf(r0[j]), hi_bf(r1[j])), fmaxf(hi_bf(q0[j]), hi_bf(q1[j])));
+            r[j] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
           }
         }
-        if (a.x2) {
-          const u32x4 r = *reinterpret_cast<const u32x4*>(a.x2 + (((size_t)n * a.H + gy) * a.W + gx) * a.Cin + c);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { v[2 * j] += lo_bf(r[j]); v[2 * j + 1] += hi_bf(r[j]); }
-        }
-        if (a.pscale) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = v[j] * a.pscale[c + j] + (shift_row ? shift_row[c + j] : 0.f);
-        } else if (shift_row) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += shift_row[c + j];
-        }
-        if (a.prelu) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) packed[j] = pack2bf(v[2 * j], v[2 * j + 1]);
-      }
-      *reinterpret_cast<u32x4*>(hl + pix * PSTR + cg * 8) = packed;
-    }
-    // ---- stage packed weights for this chunk ----
-    {
-      constexpr int WU = TCO * KPL / 8;
-      for (int u = tid; u < WU; u += NT) {
-        const int r = u / (KPL / 8), k8 = u % (KPL / 8);
-        const u32x4 wv = *reinterpret_cast<const u32x4*>(a.w + ((size_t)(co0 + r) * a.nchunk + ch) * a.KP + k8 * 8);
-        *reinterpret_cast<u32x4*>(wl + r * WSTR + k8 * 8) = wv;
+        if (X2) r2 = *reinterpret_cast<const u32x4*>(a.x2 + (((size_t)n * a.H + gy) * a.W + gx) * a.Cin + c);
       }
     }
-    __syncthreads();
-
-    // ---- MFMA main loop over the chunk's K ----
-    const int lrow = lane & 15;
-    const int kq = lane >> 4;
-#pragma unroll
-    for (int ks = 0; ks < KSTEPS; ++ks) {
-      const int g = ks * 4 + kq;
-      int tap = g / CG;
-      const int cg = g % CG;
-      if (tap >= KS * KS) tap = 0;  // zero-weight K padding: read any finite data
-      const int dy = tap / KS, dx = tap % KS;
-      bf16x8 af[NCT];
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
-        af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * WSTR + ks * 32 + kq * 8);
-      bf16x8 bfr[4];
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        const int py = 2 * wave + (pt >> 1);
-        const int px = (pt & 1) * 16 + lrow;
-        bfr[pt] = *reinterpret_cast<const bf16x8*>(hl + ((py + dy) * HW_ + (px + dx)) * PSTR + cg * 8);
-      }
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-        for (int pt = 0; pt < 4; ++pt)
-          acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr[pt], acc[ct][pt], 0, 0, 0);
-    }
-    __syncthreads();
+    hraw[i] = r;
+    if (X2) h2raw[i] = r2;
   }
+  if (!with_weights) return;
+#pragma unroll
+  for (int i = 0; i < C::WUPT; ++i) {
+    const int u = tid + i * C::NT;
+    if (u < C::WU) {
+      const int r = u / (C::KPL / 8), k8 = u % (C::KPL / 8);
+      wraw[i] = *reinterpret_cast<const u32x4*>(a.w + ((size_t)(co0 + r) * a.nchunk + ch) * a.KP + k8 * 8);
+    }
+  }
+}
 
-  // ---- epilogue: bias, residual, store ----
-  const int lrow = lane & 15;
-  const int kq = lane >> 4;
+// Apply the pre-activation to the staged registers and write the chunk into LDS.
+template <typename C, int KS, bool X2>
+__device__ __forceinline__ void commit_chunk(const ConvArgs& a, const float* shift_row, int ty0, int tx0, int ch, int tid,
+                                             const u32x4 (&hraw)[C::HUPT], const u32x4 (&h2raw)[X2 ? C::HUPT : 1],
+                                             const u32x4 (&wraw)[C::WUPT], bf16_t* hl, bf16_t* wl,
+                                             bool with_weights) {
+  const int c0 = ch * (C::CG * 8);
+#pragma unroll
+  for (int i = 0; i < C::HUPT; ++i) {
+    const int u = tid + i * C::NT;
+    if (u >= C::HU) continue;
+    const int pix = u / C::CG, cg = u % C::CG;
+    const int gy = ty0 + pix / C::HW_ - KS / 2, gx = tx0 + pix % C::HW_ - KS / 2;
+    u32x4 packed = (u32x4){0u, 0u, 0u, 0u};
+    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {  // conv zero-padding applies AFTER the activation
+      const int c = c0 + cg * 8;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(hraw[i][j]); v[2 * j + 1] = hi_bf(hraw[i][j]); }
+      if (X2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[2 * j] += lo_bf(h2raw[i][j]); v[2 * j + 1] += hi_bf(h2raw[i][j]); }
+      }
+      if (a.pscale) {
+        const float4 s0 = *reinterpret_cast<const float4*>(a.pscale + c);
+        const float4 s1 = *reinterpret_cast<const float4*>(a.pscale + c + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= sc[j];
+      }
+      if (shift_row) {
+        const float4 t0 = *reinterpret_cast<const float4*>(shift_row + c);
+        const float4 t1 = *reinterpret_cast<const float4*>(shift_row + c + 4);
+        const float sh[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += sh[j];
+      }
+      if (a.prelu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) packed[j] = pack2bf(v[2 * j], v[2 * j + 1]);
+    }
+    *reinterpret_cast<u32x4*>(hl + pix * C::PSTR + cg * 8) = packed;
+  }
+  if (!with_weights) return;
+#pragma unroll
+  for (int i = 0; i < C::WUPT; ++i) {
+    const int u = tid + i * C::NT;
+    if (u < C::WU) {
+      const int r = u / (C::KPL / 8), k8 = u % (C::KPL / 8);
+      *reinterpret_cast<u32x4*>(wl + r * C::WSTR + k8 * 8) = wraw[i];
+    }
+  }
+}
+
+template <typename C>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT][4], int n, int ty0, int tx0, int co0,
+                                         int wave, int lrow, int kq) {
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt) {
     const int py = ty0 + 2 * wave + (pt >> 1);
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(NT, 2) void conv2d_nhwc_kernel(ConvArgs a) {
     if (py >= a.H || px >= a.W) continue;
     const size_t pix = ((size_t)n * a.H + py) * a.W + px;
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
+    for (int ct = 0; ct < C::NCT; ++ct) {
       const int co = co0 + ct * 16 + kq * 4;
       float v0 = acc[ct][pt][0], v1 = acc[ct][pt][1], v2 = acc[ct][pt][2], v3 = acc[ct][pt][3];
       if (a.out_f32_nchw) {
@@ -193,14 +193,14 @@ __global__ __launch_bounds__(NT, 2) void conv2d_nhwc_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = co + i;
-          if (c < a.cout_valid) {
-            float r = vv[i] + (a.bias ? a.bias[c] : 0.f);
-            o[(((size_t)n * a.cout_valid + c) * a.H + py) * a.W + px] = r;
-          }
+          if (c < a.cout_valid) o[(((size_t)n * a.cout_valid + c) * a.H + py) * a.W + px] = vv[i] + (a.bias ? a.bias[c] : 0.f);
         }
       } else {
         if (co >= a.Cout) continue;
-        if (a.bias) { v0 += a.bias[co]; v1 += a.bias[co + 1]; v2 += a.bias[co + 2]; v3 += a.bias[co + 3]; }
+        if (a.bias) {
+          const float4 b = *reinterpret_cast<const float4*>(a.bias + co);
+          v0 += b.x; v1 += b.y; v2 += b.z; v3 += b.w;
+        }
         if (a.res) {
           const u32x2 r = *reinterpret_cast<const u32x2*>(a.res + pix * a.Cout + co);
           v0 += lo_bf(r[0]); v1 += hi_bf(r[0]); v2 += lo_bf(r[1]); v3 += hi_bf(r[1]);
@@ -214,39 +214,222 @@ __global__ __launch_bounds__(NT, 2) void conv2d_nhwc_kernel(ConvArgs a) {
   }
 }
 
-template <int KS, int CK, int TCO, int INMODE>
-int launch(const ConvArgs& a, hipStream_t s) {
-  constexpr int HH = TH + KS - 1, HW_ = TW + KS - 1, PSTR = CK + 8;
-  constexpr int KSTEPS = (KS * KS * CK + 31) / 32, WSTR = KSTEPS * 32 + 8;
-  const size_t lds = (size_t)(HH * HW_ * PSTR + TCO * WSTR) * sizeof(bf16_t);
-  dim3 grid(a.N * a.tiles_x * a.tiles_y, (a.Cout + TCO - 1) / TCO);
-  hipLaunchKernelGGL((conv2d_nhwc_kernel<KS, CK, TCO, INMODE>), grid, dim3(NT), lds, s, a);
+// Persistent over pixel tiles: block b handles tiles b, b + gridDim.x, ...; the (tile, chunk)
+// stages form one software pipeline, so the next tile's halo loads overlap this tile's MFMAs and
+// its epilogue stores.  Single-chunk layers keep their weights resident in LDS for all tiles.
+template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void conv2d_nhwc_persist(ConvArgs a) {
+  using C = Cfg<KS, CK, TCO, INMODE, X2, NW>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* hl = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* wl = hl + C::HH * C::HW_ * C::PSTR;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int lrow = lane & 15;
+  const int kq = lane >> 4;
+  const int tiles_per_img = a.tiles_x * a.tiles_y;
+  const int total = a.N * tiles_per_img;
+  const int co0 = blockIdx.y * TCO;
+  const bool resident_w = a.nchunk == 1;
+
+  int tile = blockIdx.x;
+  if (tile >= total) return;
+  int n = tile / tiles_per_img;
+  int ty0 = ((tile % tiles_per_img) / a.tiles_x) * C::TH;
+  int tx0 = ((tile % tiles_per_img) % a.tiles_x) * TW;
+  int ch = 0;
+
+  f32x4 acc[C::NCT][4];
+#pragma unroll
+  for (int i = 0; i < C::NCT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 hraw[C::HUPT];
+  u32x4 h2raw[X2 ? C::HUPT : 1];
+  u32x4 wraw[C::WUPT];
+  issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, 0, tid, hraw, h2raw, wraw, true);
+  bool first = true;
+  for (;;) {
+    const float* shift_row = a.pshift ? a.pshift + (size_t)n * a.pshift_ns : nullptr;
+    if (!first) __syncthreads();  // MFMAs of the previous stage finished reading LDS
+    commit_chunk<C, KS, X2>(a, shift_row, ty0, tx0, ch, tid, hraw, h2raw, wraw, hl, wl, first || !resident_w);
+    __syncthreads();
+    first = false;
+    // next stage (chunk ch+1 of this tile, or chunk 0 of the next tile)
+    int nch = ch + 1, ntile = tile;
+    if (nch == a.nchunk) { nch = 0; ntile += gridDim.x; }
+    // TCO=64 tiles keep 64 accumulator registers live; crossing tiles in the same block would
+    // spill, so only the <=32-channel layers (latency-bound, 1 chunk) run persistent.
+    const bool more = ntile < total;
+    int nn = n, nty0 = ty0, ntx0 = tx0;
+    if (more) {
+      nn = ntile / tiles_per_img;
+      nty0 = ((ntile % tiles_per_img) / a.tiles_x) * C::TH;
+      ntx0 = ((ntile % tiles_per_img) % a.tiles_x) * TW;
+      issue_chunk<C, KS, INMODE, X2>(a, nn, nty0, ntx0, co0, nch, tid, hraw, h2raw, wraw, !resident_w);
+    }
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+      const int g = ks * 4 + kq;
+      int tap = g / C::CG;
+      const int cg = g % C::CG;
+      if (tap >= KS * KS) tap = 0;  // zero-weight K padding: read any finite data
+      const int dy = tap / KS, dx = tap % KS;
+      bf16x8 af[C::NCT];
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct)
+        af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTR + ks * 32 + kq * 8);
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        const int py = 2 * wave + (pt >> 1);
+        const int px = (pt & 1) * 16 + lrow;
+        bfr[pt] = *reinterpret_cast<const bf16x8*>(hl + ((py + dy) * C::HW_ + (px + dx)) * C::PSTR + cg * 8);
+      }
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct)
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt)
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr[pt], acc[ct][pt], 0, 0, 0);
+    }
+    if (ch == a.nchunk - 1) {
+      epilogue<C>(a, acc, n, ty0, tx0, co0, wave, lrow, kq);
+#pragma unroll
+      for (int i = 0; i < C::NCT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    if (!more) break;
+    tile = ntile; ch = nch; n = nn; ty0 = nty0; tx0 = ntx0;
+  }
+}
+
+// One block per pixel tile (no cross-tile pipeline): the 64-output-channel variants need all
+// their registers for accumulators + the chunk prefetch, and their multi-chunk K loop already
+// overlaps loads with MFMAs.
+template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
+__global__ __launch_bounds__(NW * 64, X2 ? 1 : 2) void conv2d_nhwc_kernel(ConvArgs a) {
+  using C = Cfg<KS, CK, TCO, INMODE, X2, NW>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* hl = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* wl = hl + C::HH * C::HW_ * C::PSTR;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int lrow = lane & 15;
+  const int kq = lane >> 4;
+  const int tiles_per_img = a.tiles_x * a.tiles_y;
+  const int tile = blockIdx.x;
+  const int n = tile / tiles_per_img;
+  const int ty0 = ((tile % tiles_per_img) / a.tiles_x) * C::TH;
+  const int tx0 = ((tile % tiles_per_img) % a.tiles_x) * TW;
+  const int co0 = blockIdx.y * TCO;
+  const float* shift_row = a.pshift ? a.pshift + (size_t)n * a.pshift_ns : nullptr;
+  f32x4 acc[C::NCT][4];
+#pragma unroll
+  for (int i = 0; i < C::NCT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  u32x4 hraw[C::HUPT];
+  u32x4 h2raw[X2 ? C::HUPT : 1];
+  u32x4 wraw[C::WUPT];
+  issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, 0, tid, hraw, h2raw, wraw, true);
+  for (int ch = 0; ch < a.nchunk; ++ch) {
+    if (ch > 0) __syncthreads();
+    commit_chunk<C, KS, X2>(a, shift_row, ty0, tx0, ch, tid, hraw, h2raw, wraw, hl, wl, true);
+    __syncthreads();
+    if (ch + 1 < a.nchunk) issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, ch + 1, tid, hraw, h2raw, wraw, true);
+#pragma unroll
+    for (int ks = 0; ks < C::KSTEPS; ++ks) {
+      const int g = ks * 4 + kq;
+      int tap = g / C::CG;
+      const int cg = g % C::CG;
+      if (tap >= KS * KS) tap = 0;
+      const int dy = tap / KS, dx = tap % KS;
+      bf16x8 af[C::NCT];
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct)
+        af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTR + ks * 32 + kq * 8);
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        const int py = 2 * wave + (pt >> 1);
+        const int px = (pt & 1) * 16 + lrow;
+        bfr[pt] = *reinterpret_cast<const bf16x8*>(hl + ((py + dy) * C::HW_ + (px + dx)) * C::PSTR + cg * 8);
+      }
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct)
+#pragma unroll
+        for (int pt = 0; pt < 4; ++pt)
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr[pt], acc[ct][pt], 0, 0, 0);
+    }
+  }
+  epilogue<C>(a, acc, n, ty0, tx0, co0, wave, lrow, kq);
+}
+
+template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
+int launch(ConvArgs a, hipStream_t s) {
+  using C = Cfg<KS, CK, TCO, INMODE, X2, NW>;
+  a.tiles_x = (a.W + TW - 1) / TW;
+  a.tiles_y = (a.H + C::TH - 1) / C::TH;
+  const int tiles = a.N * a.tiles_x * a.tiles_y;
+  const int cot = (a.Cout + TCO - 1) / TCO;
+  // persistent blocks: ~4 resident workgroups per CU across the cout tiles (256 CUs)
+  if (TCO > 32) {  // non-persistent variant: one block per tile
+    hipLaunchKernelGGL((conv2d_nhwc_kernel<KS, CK, TCO, INMODE, X2, NW>), dim3(tiles, cot), dim3(C::NT), C::LDS, s, a);
+    return BE_CHECK_LAUNCH();
+  }
+  int gx = (256 * 4 * (NW == 4 ? 2 : 1)) / cot;
+  if (a.persist_blocks > 0) gx = a.persist_blocks;
+  if (gx < 1) gx = 1;
+  if (gx > tiles) gx = tiles;
+  hipLaunchKernelGGL((conv2d_nhwc_persist<KS, CK, TCO, INMODE, X2, NW>), dim3(gx, cot), dim3(C::NT), C::LDS, s, a);
   return BE_CHECK_LAUNCH();
 }
 
+template <int KS, int CK, int TCO, int INMODE, bool X2>
+int dispatch_nw(int nw, const ConvArgs& a, hipStream_t s) {
+  if (nw == 8) return launch<KS, CK, TCO, INMODE, X2, 8>(a, s);
+  return launch<KS, CK, TCO, INMODE, X2, 4>(a, s);
+}
+
 template <int KS, int CK, int TCO>
-int dispatch_inmode(int inmode, const ConvArgs& a, hipStream_t s) {
+int dispatch_mode(int inmode, bool x2, int nw, const ConvArgs& a, hipStream_t s) {
+  if (x2) {
+    if (inmode != 0) return -3;
+    return dispatch_nw<KS, CK, TCO, 0, true>(nw, a, s);
+  }
   switch (inmode) {
-    case 0: return launch<KS, CK, TCO, 0>(a, s);
-    case 1: return launch<KS, CK, TCO, 1>(a, s);
-    case 2: return launch<KS, CK, TCO, 2>(a, s);
+    case 0: return dispatch_nw<KS, CK, TCO, 0, false>(nw, a, s);
+    case 1: return dispatch_nw<KS, CK, TCO, 1, false>(nw, a, s);
+    case 2: return dispatch_nw<KS, CK, TCO, 2, false>(nw, a, s);
   }
   return -1;
 }
 
 template <int KS, int CK>
-int dispatch_tco(int tco, int inmode, const ConvArgs& a, hipStream_t s) {
+int dispatch_tco(int tco, int inmode, bool x2, int nw, const ConvArgs& a, hipStream_t s) {
   switch (tco) {
-    case 16: return dispatch_inmode<KS, CK, 16>(inmode, a, s);
-    case 32: return dispatch_inmode<KS, CK, 32>(inmode, a, s);
-    case 64: return dispatch_inmode<KS, CK, 64>(inmode, a, s);
+    case 16: return dispatch_mode<KS, CK, 16>(inmode, x2, nw, a, s);
+    case 32: return dispatch_mode<KS, CK, 32>(inmode, x2, nw, a, s);
+    case 64: return dispatch_mode<KS, CK, 64>(inmode, x2, nw, a, s);
   }
   return -2;
 }
 
 }  // namespace
 
+static int g_persist_blocks = 0;  // tuning override (0 = heuristic)
+
 extern "C" {
+
+int be_conv2d_set_persist(int blocks) {
+  g_persist_blocks = blocks;
+  return 0;
+}
 
 // Returns the K chunk length (padded) the packed weight layout must use for (ks, ck).
 int be_conv2d_packed_kp(int ks, int ck) { return ((ks * ks * ck + 31) / 32) * 32; }
@@ -254,7 +437,7 @@ int be_conv2d_packed_kp(int ks, int ck) { return ((ks * ks * ck + 31) / 32) * 32
 int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const float* pshift, int pshift_ns,
                    int prelu, const void* w, const float* bias, const void* res, void* out, int N, int H, int W,
                    int Hs, int Ws, int Cin, int Cout, int cout_valid, int ks, int ck, int tco, int inmode,
-                   int out_f32_nchw, hipStream_t stream) {
+                   int out_f32_nchw, int nw, hipStream_t stream) {
   if (Cin % ck != 0 || Cout % 4 != 0) return -10;
   if (!(ks == 1 || ks == 3)) return -11;
   ConvArgs a;
@@ -264,13 +447,14 @@ int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const flo
   a.N = N; a.H = H; a.W = W; a.Hs = Hs; a.Ws = Ws; a.Cin = Cin; a.Cout = Cout; a.cout_valid = cout_valid;
   a.nchunk = Cin / ck; a.KP = be_conv2d_packed_kp(ks, ck);
   a.out_f32_nchw = out_f32_nchw;
-  a.tiles_x = (W + TW - 1) / TW; a.tiles_y = (H + TH - 1) / TH;
+  a.persist_blocks = g_persist_blocks;
+  const bool x2p = x2 != nullptr;
   if (ks == 3) {
-    if (ck == 8) return dispatch_tco<3, 8>(tco, inmode, a, stream);
-    if (ck == 32) return dispatch_tco<3, 32>(tco, inmode, a, stream);
+    if (ck == 8) return dispatch_tco<3, 8>(tco, inmode, x2p, nw, a, stream);
+    if (ck == 32) return dispatch_tco<3, 32>(tco, inmode, x2p, nw, a, stream);
   } else {
-    if (ck == 8) return dispatch_tco<1, 8>(tco, inmode, a, stream);
-    if (ck == 32) return dispatch_tco<1, 32>(tco, inmode, a, stream);
+    if (ck == 8) return dispatch_tco<1, 8>(tco, inmode, x2p, nw, a, stream);
+    if (ck == 32) return dispatch_tco<1, 32>(tco, inmode, x2p, nw, a, stream);
   }
   return -12;
 }

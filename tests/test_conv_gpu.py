@@ -55,3 +55,28 @@ def test_fused_conv_nchw_f32_head(gpu):
                        out_nchw_f32=True, cout_valid=3).cpu()
     assert out.shape == (3, 3, 48, 64)
     assert (out - ref).abs().max().item() < 2e-2 * max(1, ref.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nw", [4, 8])
+@pytest.mark.parametrize("cin,cout,inmode,persist", [(32, 32, "none", 7), (8, 32, "none", 0), (64, 32, "up2", 13),
+                                                     (32, 16, "none", 3), (64, 64, "pool2", 0)])
+def test_fused_conv_persistent_many_tiles(gpu, nw, cin, cout, inmode, persist):
+    """Many more pixel tiles than persistent workgroups: every tile must be produced exactly once."""
+    from bioengine_worker_amd.ops import _native
+
+    torch.manual_seed(2)
+    N, H, W = 6, 96, 160
+    Hs, Ws = {"none": (H, W), "pool2": (H * 2, W * 2), "up2": (H // 2, W // 2)}[inmode]
+    x = torch.randn(N, Hs, Ws, cin).bfloat16()
+    w = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    pc = PackedConv.from_weight(w, torch.randn(cout) * 0.1)
+    shift = (0.1 * torch.randn(N, cin)).float()
+    ref = fused_conv2d_ref(x, pc, shift=shift, relu=True, inmode=inmode).float()
+    _native.call("be_conv2d_set_persist", persist)
+    try:
+        out = fused_conv2d(x.to(gpu), pc.to(gpu), shift=shift.to(gpu), relu=True, inmode=inmode, nw=nw).float().cpu()
+    finally:
+        _native.call("be_conv2d_set_persist", 0)
+    err = (out - ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
