@@ -135,6 +135,47 @@ def _diffuse_scratch_doubles(ly, lx):
     return 2 * R + (ly + 2 + lx + 2 + 1) // 2 + (R + 7) // 8 + 2
 
 
+_TILE_PARAMS: tuple | None = None
+#: "tiled" = multi-workgroup time-blocked diffusion for masks larger than LDS (default);
+#: "block" = one workgroup per mask on a global scratch slab (kept as a cross-check).
+BIG_MASK_MODE = "tiled"
+
+
+def _diffuse_big(Mc, bj, niter_img, scratch, L, st) -> None:
+    """Diffusion of masks too large for one workgroup's LDS (see diffuse_tiled_kernel)."""
+    global _TILE_PARAMS
+    B, H, W = Mc.shape
+    if BIG_MASK_MODE == "block":
+        _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], H, W, _native.ptr(niter_img),
+                     _native.ptr(scratch), _native.ptr(L), 0, st)
+        return
+    if _TILE_PARAMS is None:
+        import ctypes
+
+        buf = (ctypes.c_int * 3)()
+        _native.call("be_cp_diffuse_tile_params", ctypes.addressof(buf))
+        _TILE_PARAMS = (buf[0], buf[1], buf[2])
+    core = _TILE_PARAMS[0]
+    w2 = bj[:, 2].cpu()
+    ly, lx = (w2 & 0xFFFFFFFF), (w2 >> 32)
+    nty = (ly + 2 + core - 1) // core
+    ntx = (lx + 2 + core - 1) // core
+    per = (nty * ntx)
+    job = torch.repeat_interleave(torch.arange(bj.shape[0]), per)
+    start = torch.cumsum(per, 0) - per
+    k = torch.arange(int(per.sum())) - start[job]
+    ty = (k // ntx[job]) * core
+    tx = (k % ntx[job]) * core
+    tiles = torch.stack([job, ty, tx, torch.zeros_like(job)], 1).to(torch.int32).to(Mc.device)
+    centers = torch.empty(bj.shape[0], dtype=torch.int32, device=Mc.device)
+    ws = torch.zeros(4, dtype=torch.int32, device=Mc.device)
+    _native.call("be_cp_diffuse_tiled", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], _native.ptr(tiles),
+                 tiles.shape[0], H, W, _native.ptr(niter_img), _native.ptr(scratch), _native.ptr(L),
+                 _native.ptr(centers), _native.ptr(ws), st)
+    if int(ws[1].item()) != 0:
+        raise RuntimeError("diffuse_tiled_kernel: grid barrier timed out (workgroups not co-resident)")
+
+
 def label_counts(M: torch.Tensor, nlab: int) -> torch.Tensor:
     """Pixels per label [B, nlab] (label 0 not counted)."""
     B = M.shape[0]
@@ -185,8 +226,7 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
         _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(sj), sj.shape[0], H, W, _native.ptr(niter_img),
                      _native.ptr(scratch), _native.ptr(L), LDS_DIFFUSE_BYTES, st)
     if bj.shape[0]:
-        _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], H, W, _native.ptr(niter_img),
-                     _native.ptr(scratch), _native.ptr(L), 0, st)
+        _diffuse_big(Mc, bj, niter_img, scratch, L, st)
     err = None
     dpp = None
     bstride = 0

@@ -4,11 +4,11 @@
 // training targets, invoked at main.py:1370-1387).  Oracle: bioengine_worker_amd/cellpose/reference.py.
 //
 // MI355X mapping: one workgroup per mask.  The mask's bounding box (+1 ring) is staged in LDS
-// (membership bytes + two fp32 heat buffers), the whole Jacobi diffusion runs on-chip with one
-// barrier per half-step, and only log(1 + T) of the mask pixels goes back to HBM.  Masks whose box
-// exceeds the LDS budget run the same code on a per-mask global scratch slab (same block, so
-// __syncthreads still orders the sweeps).  Centres are exact medians from row/column histograms in
-// LDS, ties broken in raster order with a 64-bit atomicMin key.
+// (membership bytes + two fp64 heat buffers), the whole Jacobi diffusion runs on-chip with one
+// barrier per sweep, and only log(1 + T) of the mask pixels goes back to HBM.  Masks whose box
+// exceeds the LDS budget are tiled across many workgroups with time-blocked sweeps and a grid
+// barrier per block of iterations (diffuse_tiled_kernel).  Centres are exact medians from
+// row/column histograms in LDS, ties broken in raster order with a 64-bit atomicMin key.
 #include "common.h"
 
 namespace {
@@ -44,7 +44,7 @@ struct MaskJob {
 template <bool USE_LDS>
 __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs, int H,
                                                      int W, const int* __restrict__ niter_img, double* __restrict__ scratch,
-                                                     double* __restrict__ Lout) {
+                                                     double* __restrict__ Lout, int* __restrict__ centers_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const MaskJob J = jobs[blockIdx.x];
   const int RY = J.ly + 2, RX = J.lx + 2, R = RY * RX;
@@ -112,23 +112,38 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
   }
   __syncthreads();
   const int ce = (int)(best & 0xffffffffu);
+  if (centers_out) {  // big masks: the tiled multi-workgroup diffusion below runs the iterations
+    if (tid == 0) centers_out[blockIdx.x] = ce;
+    return;
+  }
   const int niter = niter_img[J.b];
+  // Column-segment register blocking: a work item is DV consecutive rows of one column; the three
+  // horizontal 3-sums it needs per row are formed once and slid down the segment, so a cell costs
+  // ~3 reads instead of 9.  Non-mask cells hold 0 in both buffers, so neighbour reads need no mask.
+  constexpr int DV = 8;
+  const int nseg = (RY - 2 + DV - 1) / DV;
+  const int nitems = (RX - 2) * nseg;
   double* cur = T0;
   double* nxt = T1;
   for (int it = 0; it < niter; ++it) {
     if (tid == 0) cur[ce] += 1.0;
     __syncthreads();
-    for (int e = tid; e < R; e += MT) {
-      if (!inm[e]) continue;
-      double s = 0.0;
-#pragma unroll
-      for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int q = e + dy * RX + dx;
-          s += inm[q] ? cur[q] : 0.0;
-        }
-      nxt[e] = s * (1.0 / 9.0);
+    for (int w = tid; w < nitems; w += MT) {
+      const int x = 1 + w % (RX - 2);
+      const int y0 = 1 + (w / (RX - 2)) * DV;
+      const int y1 = min(y0 + DV, RY - 1);
+      const double* c = cur + (y0 - 1) * RX + x;
+      double hp = c[-1] + c[0] + c[1];
+      c += RX;
+      double hc = c[-1] + c[0] + c[1];
+      for (int y = y0; y < y1; ++y) {
+        c += RX;
+        const double hn = c[-1] + c[0] + c[1];
+        const int e = y * RX + x;
+        nxt[e] = inm[e] ? (hp + hc + hn) * (1.0 / 9.0) : 0.0;
+        hp = hc;
+        hc = hn;
+      }
     }
     __syncthreads();
     double* t = cur; cur = nxt; nxt = t;
@@ -138,6 +153,135 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
     if (!inm[e]) continue;
     const int y = J.y0 + e / RX - 1, x = J.x0 + e % RX - 1;
     Lb[y * W + x] = log1p(cur[e]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Masks too large for one workgroup's LDS: the Jacobi sweep of every big mask is split into
+// DT_CORE x DT_CORE tiles, and the iterations are blocked in time — a workgroup stages its tile
+// plus a DT_K-pixel halo in LDS, runs DT_K iterations on-chip (the valid region shrinks one pixel
+// per step, so the core stays exact), and writes the core back.  Rounds are separated by a grid
+// barrier (agent-scope release/acquire counter, bounded spin), so one cooperative launch runs all
+// niter iterations of all big masks across the whole chip instead of one CU per mask.
+constexpr int DT_K = 8;
+constexpr int DT_CORE = 48;
+constexpr int DT_RG = DT_CORE + 2 * DT_K;  // 64
+constexpr int DT_LDS = 2 * DT_RG * DT_RG * 8 + DT_RG * DT_RG;
+
+__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned target, unsigned* timeout_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    int good = 1;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24) || __hip_atomic_load(timeout_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(timeout_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        good = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ok = good;
+  }
+  __syncthreads();
+  return ok != 0;
+}
+
+// tiles: int4 {job, ry0, rx0, 0} (core origin in the job's padded box coordinates).
+// bar[0] = arrival counter, bar[1] = timeout flag (both zeroed by the launcher).
+__global__ __launch_bounds__(MT) void diffuse_tiled_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs,
+                                                           int njobs, const int4* __restrict__ tiles, int ntiles, int H,
+                                                           int W, const int* __restrict__ niter_img,
+                                                           const int* __restrict__ centers, double* scratch,
+                                                           double* __restrict__ Lout, unsigned* bar) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* A = reinterpret_cast<double*>(smem);
+  double* Bf = A + DT_RG * DT_RG;
+  unsigned char* mk = reinterpret_cast<unsigned char*>(Bf + DT_RG * DT_RG);
+  const int tid = threadIdx.x;
+  int maxn = 0;
+  for (int j = 0; j < njobs; ++j) maxn = max(maxn, niter_img[jobs[j].b]);
+  const int rounds = (maxn + DT_K - 1) / DT_K;
+  for (int r = 0; r < rounds; ++r) {
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+      const int4 td = tiles[t];
+      const MaskJob J = jobs[td.x];
+      const int niter = niter_img[J.b];
+      const int r0 = r * DT_K;
+      if (r0 >= niter) continue;
+      const int steps = min(DT_K, niter - r0);
+      const bool last = r0 + steps == niter;
+      const int RY = J.ly + 2, RX = J.lx + 2, R = RY * RX;
+      double* cur = scratch + J.scratch + ((r & 1) ? R : 0);
+      double* nxt = scratch + J.scratch + ((r & 1) ? 0 : R);
+      const int oy = td.y - DT_K, ox = td.z - DT_K;  // region origin in box coordinates
+      const int* Mb = M + (size_t)J.b * H * W;
+      for (int e = tid; e < DT_RG * DT_RG; e += MT) {
+        const int ry = oy + e / DT_RG, rx = ox + e % DT_RG;
+        unsigned char m = 0;
+        double v = 0.0;
+        if (ry >= 1 && ry <= J.ly && rx >= 1 && rx <= J.lx &&
+            Mb[(J.y0 + ry - 1) * W + (J.x0 + rx - 1)] == J.lab) {
+          m = 1;
+          v = r == 0 ? 0.0 : cur[ry * RX + rx];
+        }
+        mk[e] = m;
+        A[e] = v;
+        Bf[e] = v;
+      }
+      const int ce = centers[td.x];
+      const int cy = ce / RX - oy, cx = ce % RX - ox;
+      const int cl = (cy >= 0 && cy < DT_RG && cx >= 0 && cx < DT_RG) ? cy * DT_RG + cx : -1;
+      __syncthreads();
+      double* a = A;
+      double* b = Bf;
+      // thread = one column x, rows [r0, r0 + 16): the whole region is swept every step (cells
+      // outside the shrinking valid window turn to garbage that never reaches the core).
+      const int x = tid & (DT_RG - 1);
+      const int sr0 = (tid / DT_RG) * (DT_RG * DT_RG / MT);
+      const bool xl = x > 0, xr = x < DT_RG - 1;
+      for (int s = 0; s < steps; ++s) {
+        if (tid == 0 && cl >= 0) a[cl] += 1.0;
+        __syncthreads();
+        auto hsum = [&](int r) -> double {
+          if (r < 0 || r >= DT_RG) return 0.0;
+          const double* c = a + r * DT_RG + x;
+          return (xl ? c[-1] : 0.0) + c[0] + (xr ? c[1] : 0.0);
+        };
+        double hp = hsum(sr0 - 1), hc = hsum(sr0);
+#pragma unroll 4
+        for (int i = 0; i < DT_RG * DT_RG / MT; ++i) {
+          const double hn = hsum(sr0 + i + 1);
+          const int q = (sr0 + i) * DT_RG + x;
+          b[q] = mk[q] ? (hp + hc + hn) * (1.0 / 9.0) : 0.0;
+          hp = hc;
+          hc = hn;
+        }
+        __syncthreads();
+        double* tmp = a; a = b; b = tmp;
+      }
+      double* Lb = Lout + (size_t)J.b * H * W;
+      for (int e = tid; e < DT_CORE * DT_CORE; e += MT) {
+        const int ly_ = DT_K + e / DT_CORE, lx_ = DT_K + e % DT_CORE;
+        const int ry = oy + ly_, rx = ox + lx_;
+        if (ry >= RY || rx >= RX) continue;
+        const int q = ly_ * DT_RG + lx_;
+        if (last) {
+          if (mk[q]) Lb[(J.y0 + ry - 1) * W + (J.x0 + rx - 1)] = log1p(a[q]);
+        } else {
+          nxt[ry * RX + rx] = mk[q] ? a[q] : 0.0;
+        }
+      }
+      __syncthreads();  // LDS reuse by the next tile of this round
+    }
+    if (r + 1 < rounds && !grid_barrier(bar, (unsigned)(r + 1) * gridDim.x, bar + 1)) return;
   }
 }
 
@@ -249,11 +393,54 @@ int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const
   if (njobs == 0) return 0;
   if (lds_bytes > 0)
     hipLaunchKernelGGL((diffuse_kernel<true>), dim3(njobs), dim3(MT), lds_bytes, s, M, (const MaskJob*)jobs, H, W, niter_img,
-                       scratch, Lout);
+                       scratch, Lout, nullptr);
   else
     hipLaunchKernelGGL((diffuse_kernel<false>), dim3(njobs), dim3(MT), 0, s, M, (const MaskJob*)jobs, H, W, niter_img, scratch,
-                       Lout);
+                       Lout, nullptr);
   return BE_CHECK_LAUNCH();
+}
+
+int be_cp_diffuse_tile_params(int* out3) {
+  out3[0] = DT_CORE;
+  out3[1] = DT_K;
+  out3[2] = DT_LDS;
+  return 0;
+}
+
+// Big masks, multi-workgroup: centres (one block per mask), then one cooperative launch for all
+// iterations.  tiles: int4 per tile (see diffuse_tiled_kernel); ws: >= 16 bytes of device memory
+// (barrier counter + timeout flag); centers: njobs ints.  Returns 1 if the barrier timed out.
+int be_cp_diffuse_tiled(const int* M, const void* jobs, int njobs, const void* tiles, int ntiles, int H, int W,
+                        const int* niter_img, double* scratch, double* Lout, int* centers, unsigned* ws,
+                        hipStream_t s) {
+  if (njobs == 0 || ntiles == 0) return 0;
+  hipLaunchKernelGGL((diffuse_kernel<false>), dim3(njobs), dim3(MT), 0, s, M, (const MaskJob*)jobs, H, W, niter_img,
+                     scratch, Lout, centers);
+  if (BE_CHECK_LAUNCH()) return -1;
+  static int max_grid = 0;
+  if (max_grid == 0) {
+    int dev = 0, ncu = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(diffuse_tiled_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        DT_LDS);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(diffuse_tiled_kernel), MT,
+                                                 DT_LDS);
+    max_grid = max(1, ncu * max(1, per_cu));
+  }
+  const int grid = min(ntiles, max_grid);
+  (void)hipMemsetAsync(ws, 0, 16, s);
+  const MaskJob* jp = (const MaskJob*)jobs;
+  const int4* tp = (const int4*)tiles;
+  void* args[] = {(void*)&M, (void*)&jp, (void*)&njobs, (void*)&tp, (void*)&ntiles, (void*)&H, (void*)&W,
+                  (void*)&niter_img, (void*)&centers, (void*)&scratch, (void*)&Lout, (void*)&ws};
+  hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(diffuse_tiled_kernel), dim3(grid), dim3(MT),
+                                            args, DT_LDS, s);
+  if (e != hipSuccess) {
+    fprintf(stderr, "be_cp_diffuse_tiled: cooperative launch failed: %s\n", hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
 }
 
 int be_cp_flow_grad(const int* M, const double* L, int B, int H, int W, float* mu, const float* dp, long long dp_bstride,

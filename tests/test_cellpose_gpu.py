@@ -30,15 +30,22 @@ def test_masks_to_flows_gpu_matches_reference(gpu):
 
 
 @pytest.mark.gpu
-def test_big_mask_global_scratch_path(gpu):
-    from bioengine_worker_amd.cellpose.gpu import masks_to_flows_gpu
+@pytest.mark.parametrize("mode", ["tiled", "block"])
+def test_big_mask_global_scratch_path(gpu, mode, monkeypatch):
+    from bioengine_worker_amd.cellpose import gpu as cg
 
-    M = np.zeros((200, 220), np.int32)
-    M[10:190, 10:210] = 1  # box exceeds the LDS budget -> global scratch variant
-    M[50:60, 50:60] = 2
-    mu, _, _ = masks_to_flows_gpu(torch.from_numpy(M[None]).to(gpu))
-    mref = ref.masks_to_flows(M)
-    assert np.abs(mu[0].cpu().numpy() - mref).max() < 2e-3
+    monkeypatch.setattr(cg, "BIG_MASK_MODE", mode)
+    M = np.zeros((2, 200, 220), np.int32)
+    M[0, 10:190, 10:210] = 1  # box exceeds the LDS budget -> big-mask path
+    M[0, 50:60, 50:60] = 2
+    yy, xx = np.mgrid[0:200, 0:220]
+    M[1][((yy - 100) ** 2 / 90 ** 2 + (xx - 120) ** 2 / 70 ** 2) < 1] = 1  # ellipse, ragged tile edges
+    M[1, 5:20, 5:200] = 2
+    M[1, 20:24, 30:40] = 2  # break the strip's symmetry (its centre flow is otherwise a rounding tie)
+    mu, _, _ = cg.masks_to_flows_gpu(torch.from_numpy(M).to(gpu))
+    for b in range(2):
+        mref = ref.masks_to_flows(M[b])
+        assert np.abs(mu[b].cpu().numpy() - mref).max() < 2e-3, b
 
 
 @pytest.mark.gpu
