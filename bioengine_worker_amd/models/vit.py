@@ -1,0 +1,221 @@
+"""DINOv2-compatible Vision Transformer (ViT-S/B/L/g /14) and its HIP inference engine.
+
+The cell-image-search app embeds nucleus crops with DINOv2 ViT-B/14 (reference
+``apps/cell-image-search/embedder.py:23-99``: torch.hub ``dinov2_vitb14``, fp16, batch 64, CLS token,
+L2-normalised).  Here:
+
+* :class:`ViT` — a plain PyTorch module whose parameter names match the public DINOv2 checkpoints
+  (``patch_embed.proj``, ``cls_token``, ``pos_embed``, ``blocks.{i}.norm1/attn.qkv/attn.proj/ls1.gamma/
+  norm2/mlp.fc1/mlp.fc2/ls2.gamma``, ``norm``) so a ``dinov2_vitb14_pretrain.pth`` state dict loads
+  with ``load_state_dict`` (``torch.load(..., weights_only=True)``).  Used as the fp32 reference and
+  for training.
+* :class:`ViTEngine` — the MI355X inference path: bf16 weights resident on the GPU, patch
+  embedding as one GEMM over a reshaped (not unfolded) image, hipBLASLt GEMMs for qkv/proj/MLP,
+  the fused flash-attention kernel reading q/k/v straight out of the packed qkv GEMM output,
+  LayerScale+residual fused into the next LayerNorm, bias+GELU fused into one pass.
+
+Offline there are no pretrained weights: ``ViT(...).randomize_(seed)`` gives DINOv2-style init
+(trunc-normal 0.02, LayerScale 1e-5 → we use 1.0 for a non-degenerate random network).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.transformer import add_layernorm, attention_ref, bias_gelu_, flash_attention
+
+
+@dataclass
+class ViTConfig:
+    embed_dim: int = 768
+    depth: int = 12
+    num_heads: int = 12
+    mlp_ratio: float = 4.0
+    patch_size: int = 14
+    img_size: int = 518          # DINOv2 position grid: 518 / 14 = 37 x 37
+    layerscale: bool = True
+    eps: float = 1e-6
+
+    @staticmethod
+    def dinov2(name: str = "vitb14") -> "ViTConfig":
+        table = {"vits14": (384, 12, 6), "vitb14": (768, 12, 12), "vitl14": (1024, 24, 16), "vitg14": (1536, 40, 24)}
+        d, L, h = table[name]
+        return ViTConfig(embed_dim=d, depth=L, num_heads=h)
+
+
+class _Attn(nn.Module):
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.num_heads = heads
+        self.qkv = nn.Linear(dim, 3 * dim, bias=True)
+        self.proj = nn.Linear(dim, dim, bias=True)
+
+
+class _Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+
+class _LayerScale(nn.Module):
+    def __init__(self, dim, init=1e-5):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.full((dim,), init))
+
+
+class _Block(nn.Module):
+    def __init__(self, cfg: ViTConfig):
+        super().__init__()
+        d = cfg.embed_dim
+        self.norm1 = nn.LayerNorm(d, eps=cfg.eps)
+        self.attn = _Attn(d, cfg.num_heads)
+        self.ls1 = _LayerScale(d) if cfg.layerscale else nn.Identity()
+        self.norm2 = nn.LayerNorm(d, eps=cfg.eps)
+        self.mlp = _Mlp(d, int(d * cfg.mlp_ratio))
+        self.ls2 = _LayerScale(d) if cfg.layerscale else nn.Identity()
+
+    def forward(self, x):
+        B, N, C = x.shape
+        H = self.attn.num_heads
+        qkv = self.attn.qkv(self.norm1(x)).reshape(B, N, 3, H, C // H)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        if q.dtype == torch.bfloat16:
+            a = flash_attention(q, k, v).reshape(B, N, C)
+        else:  # fp32 reference path
+            a = attention_ref(q, k, v, 1.0 / math.sqrt(C // H)).to(q.dtype).reshape(B, N, C)
+        y = self.attn.proj(a)
+        x = x + (self.ls1.gamma * y if isinstance(self.ls1, _LayerScale) else y)
+        m = self.mlp.fc2(F.gelu(self.mlp.fc1(self.norm2(x))))
+        return x + (self.ls2.gamma * m if isinstance(self.ls2, _LayerScale) else m)
+
+
+class _PatchEmbed(nn.Module):
+    def __init__(self, cfg: ViTConfig, in_chans=3):
+        super().__init__()
+        self.proj = nn.Conv2d(in_chans, cfg.embed_dim, cfg.patch_size, cfg.patch_size)
+
+
+class ViT(nn.Module):
+    def __init__(self, cfg: ViTConfig | None = None):
+        super().__init__()
+        self.cfg = cfg = cfg or ViTConfig()
+        self.patch_embed = _PatchEmbed(cfg)
+        g = cfg.img_size // cfg.patch_size
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, cfg.embed_dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, 1 + g * g, cfg.embed_dim))
+        self.blocks = nn.ModuleList([_Block(cfg) for _ in range(cfg.depth)])
+        self.norm = nn.LayerNorm(cfg.embed_dim, eps=cfg.eps)
+
+    @torch.no_grad()
+    def randomize_(self, seed: int = 0, layerscale: float = 1.0) -> "ViT":
+        gen = torch.Generator().manual_seed(seed)
+        for name, p in self.named_parameters():
+            if name.endswith("gamma"):
+                p.fill_(layerscale)
+            elif "norm" in name:
+                p.fill_(1.0 if name.endswith("weight") else 0.0)
+            elif name.endswith("bias"):
+                p.zero_()
+            else:
+                p.copy_(torch.randn(p.shape, generator=gen).clamp_(-2, 2) * 0.02)
+        return self
+
+    def interpolate_pos(self, gh: int, gw: int) -> torch.Tensor:
+        """DINOv2 bicubic interpolation of the patch position grid to (gh, gw); CLS position kept."""
+        pe = self.pos_embed
+        M = int(math.sqrt(pe.shape[1] - 1))
+        if gh == M and gw == M:
+            return pe
+        patch = pe[:, 1:].reshape(1, M, M, -1).permute(0, 3, 1, 2).float()
+        patch = F.interpolate(patch, size=(gh, gw), mode="bicubic", align_corners=False)
+        patch = patch.permute(0, 2, 3, 1).reshape(1, gh * gw, -1)
+        return torch.cat([pe[:, :1].float(), patch], 1).to(pe.dtype)
+
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        B, _, Hh, Ww = x.shape
+        p = self.cfg.patch_size
+        t = self.patch_embed.proj(x).flatten(2).transpose(1, 2)
+        t = torch.cat([self.cls_token.expand(B, -1, -1).to(t.dtype), t], 1)
+        t = t + self.interpolate_pos(Hh // p, Ww // p).to(t.dtype)
+        for blk in self.blocks:
+            t = blk(t)
+        return self.norm(t)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """CLS embedding (the torch.hub DINOv2 ``model(x)`` output)."""
+        return self.forward_features(x)[:, 0]
+
+
+class ViTEngine:
+    """bf16 HIP inference engine for a :class:`ViT` (see module docstring)."""
+
+    def __init__(self, net: ViT, device, img_size: int = 224):
+        self.device = torch.device(device)
+        self.cfg = cfg = net.cfg
+        self.p = cfg.patch_size
+        self.g = img_size // cfg.patch_size
+        self.img_size = img_size
+        bf = lambda t: t.detach().to(self.device, torch.bfloat16).contiguous()
+        f32 = lambda t: t.detach().to(self.device, torch.float32).contiguous()
+        w = net.patch_embed.proj.weight  # [D, 3, p, p]
+        self.pe_w = bf(w.reshape(w.shape[0], -1))
+        self.pe_b = bf(net.patch_embed.proj.bias)
+        with torch.no_grad():
+            pos = net.interpolate_pos(self.g, self.g)[0]
+            self.cls_pos = bf(net.cls_token[0, 0] + pos[0])
+            self.patch_pos = bf(pos[1:])
+        self.blocks = []
+        for blk in net.blocks:
+            ls = lambda m, d=cfg.embed_dim: f32(m.gamma) if isinstance(m, _LayerScale) else torch.ones(d, device=self.device)
+            self.blocks.append(dict(
+                n1w=f32(blk.norm1.weight), n1b=f32(blk.norm1.bias), qkv_w=bf(blk.attn.qkv.weight),
+                qkv_b=bf(blk.attn.qkv.bias), proj_w=bf(blk.attn.proj.weight), proj_b=bf(blk.attn.proj.bias),
+                g1=ls(blk.ls1), n2w=f32(blk.norm2.weight), n2b=f32(blk.norm2.bias),
+                fc1_w=bf(blk.mlp.fc1.weight), fc1_b=f32(blk.mlp.fc1.bias), fc2_w=bf(blk.mlp.fc2.weight),
+                fc2_b=bf(blk.mlp.fc2.bias), g2=ls(blk.ls2)))
+        self.nw, self.nb = f32(net.norm.weight), f32(net.norm.bias)
+
+    def patchify(self, x: torch.Tensor) -> torch.Tensor:
+        """[B, C, H, W] -> [B, gh*gw, C*p*p] in conv-weight order (c, ky, kx) — a reshape + one copy."""
+        B, C, H, W = x.shape
+        p = self.p
+        return (x.reshape(B, C, H // p, p, W // p, p).permute(0, 2, 4, 1, 3, 5)
+                .reshape(B, (H // p) * (W // p), C * p * p))
+
+    @torch.no_grad()
+    def features(self, x: torch.Tensor) -> torch.Tensor:
+        """x: [B, 3, S, S] float (ImageNet-normalised) -> final-norm tokens [B, 1 + g*g, D] bf16."""
+        cfg = self.cfg
+        B = x.shape[0]
+        D, Hh = cfg.embed_dim, cfg.num_heads
+        x = x.to(self.device, torch.bfloat16)
+        tok = F.linear(self.patchify(x), self.pe_w, self.pe_b) + self.patch_pos  # [B, g*g, D]
+        N = tok.shape[1] + 1
+        t = torch.empty(B, N, D, device=self.device, dtype=torch.bfloat16)
+        t[:, 0] = self.cls_pos
+        t[:, 1:] = tok
+        blocks = self.blocks
+        h = add_layernorm(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"], cfg.eps)
+        for i, b in enumerate(blocks):
+            qkv = F.linear(h, b["qkv_w"], b["qkv_b"]).view(B, N, 3, Hh, D // Hh)
+            a = flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]).view(B, N, D)
+            y = F.linear(a, b["proj_w"], b["proj_b"])
+            h2 = add_layernorm(t, y, b["g1"], b["n2w"], b["n2b"], cfg.eps)
+            m = bias_gelu_(F.linear(h2, b["fc1_w"]), b["fc1_b"])
+            m = F.linear(m, b["fc2_w"], b["fc2_b"])
+            if i + 1 < len(blocks):
+                h = add_layernorm(t, m, b["g2"], blocks[i + 1]["n1w"], blocks[i + 1]["n1b"], cfg.eps)
+            else:
+                h = add_layernorm(t, m, b["g2"], self.nw, self.nb, cfg.eps)
+        return h
+
+    @torch.no_grad()
+    def embed(self, x: torch.Tensor, normalize: bool = True) -> torch.Tensor:
+        """CLS embeddings [B, D] fp32 (L2-normalised like embedder.py:89-92)."""
+        cls = self.features(x)[:, 0].float()
+        return F.normalize(cls, dim=1, eps=1e-9) if normalize else cls

@@ -1,0 +1,302 @@
+// Fused multi-head attention forward (flash-style) for the ViT encoders: DINOv2 ViT-B/14
+// (cell-image-search embedder, SURVEY.md §2.5 K17, reference apps/cell-image-search/embedder.py:59-95)
+// and the Cellpose-SAM ViT-L/8 encoder (K8, reference apps/cellpose-finetuning/main.py:126-127),
+// including SAM's decomposed relative-position bias (attn += rel_h[q, key_row] + rel_w[q, key_col]),
+// so the N x N score matrix never exists in HBM.
+//
+// CDNA4 design (head_dim 64, bf16 in/out, fp32 online softmax):
+//  * v_mfma_f32_32x32x16_bf16 with the *keys on the rows* ("swapped" S^T = K Q^T): a lane owns one
+//    query column and 16 of every 32 keys, so the row max / row sum is lane-local plus one exchange
+//    with lane^32, and the S^T accumulator converted to bf16 IS the B operand of O^T = V^T P^T
+//    (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand") — P never touches LDS.
+//  * V^T fragments come from ds_read_b64_tr_b16 transposed reads of a row-major V tile; K and V LDS
+//    tiles are XOR-swizzled per 16-byte chunk (conflict-free transposed reads, spread b128 row reads).
+//  * K/V tiles of 64 keys are register-staged: the next tile's global loads are in flight while the
+//    current tile's MFMAs run (T14 "issue early / write late"), one LDS image per tile.
+//  * block = NW waves x 32 queries of one (batch, head); the linear block id is XCD-remapped so the
+//    blocks sharing a (batch, head)'s K/V stream run on one XCD's L2.
+#include "common.h"
+
+namespace {
+
+constexpr int HD = 64;    // head dim
+constexpr int KT = 64;    // keys per tile
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+struct AttnArgs {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  long long s_tok, s_head, s_batch;  // element strides shared by q, k, v
+  bf16_t* o;
+  long long o_tok, o_head, o_batch;
+  float* lse;          // optional [B, H, N] natural-log sum-exp of the scaled (+bias) scores
+  const float* relh;   // optional [B*H, N, Hg]
+  const float* relw;   // optional [B*H, N, Wg]
+  int Hg, Wg;
+  int B, H, N;
+  float scale;
+  int qblocks;         // ceil(N / (32 * NW))
+};
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
+// chunk swizzles (16-byte chunks, 8 per 128-byte row)
+__device__ __forceinline__ int k_off(int row, int ch) { return row * HD + ((ch ^ ((row >> 1) & 7)) << 3); }
+__device__ __forceinline__ int v_off(int row, int ch) { return row * HD + ((ch ^ (((row >> 1) & 1) << 2)) << 3); }
+
+// BIAS: 0 none, 1 generic decomposed rel-pos (per-key gathers), 2 the SAM 32-wide grid: a 32-key
+// block is exactly one grid row, so a lane's 16 key columns are fixed (rel_w in registers) and the
+// row term is one value per block.
+template <int NW, int BIAS>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int NT = NW * 64;
+  constexpr int CHUNKS = 2 * KT * (HD / 8);        // K + V tile, 16-byte chunks
+  constexpr int CPT = (CHUNKS + NT - 1) / NT;      // chunks per thread
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * HD];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int h = lane >> 5;
+  const int ql = lane & 31;
+  const int total = a.qblocks * a.B * a.H;
+  const int logical = xcd_remap(blockIdx.x, total);
+  const int bh = logical / a.qblocks;
+  const int qb = logical % a.qblocks;
+  const int b = bh / a.H, hh = bh % a.H;
+  const int q0 = qb * NW * 32 + wave * 32;
+  const int qi = q0 + ql;                 // this lane's query
+  const int qc = min(qi, a.N - 1);        // clamped for loads
+
+  const bf16_t* qbase = a.q + (long long)b * a.s_batch + (long long)hh * a.s_head;
+  const bf16_t* kbase = a.k + (long long)b * a.s_batch + (long long)hh * a.s_head;
+  const bf16_t* vbase = a.v + (long long)b * a.s_batch + (long long)hh * a.s_head;
+
+  // Q^T fragments (B operand of S^T = K Q^T): 4 k-steps of 16 head dims.
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    u32x4 r = *reinterpret_cast<const u32x4*>(qbase + (long long)qc * a.s_tok + ks * 16 + h * 8);
+    if (qi >= a.N) r = (u32x4){0u, 0u, 0u, 0u};
+    qf[ks] = *reinterpret_cast<bf16x8*>(&r);
+  }
+  const float c2 = a.scale * 1.4426950408889634f;  // scores -> log2 domain
+  const float* rh = nullptr;
+  const float* rw = nullptr;
+  float rwr[16];
+  if (BIAS) {
+    rh = a.relh + ((long long)bh * a.N + qc) * a.Hg;
+    rw = a.relw + ((long long)bh * a.N + qc) * a.Wg;
+  }
+  if (BIAS == 2) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rwr[i] = rw[8 * (i >> 2) + 4 * h + (i & 3)] * 1.4426950408889634f;
+  }
+
+  f32x16 oacc[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+
+  const int ntiles = (a.N + KT - 1) / KT;
+  u32x4 stage[CPT];
+  auto issue = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + i * NT;
+      u32x4 r = (u32x4){0u, 0u, 0u, 0u};
+      if (c < CHUNKS) {
+        const int isv = c >= CHUNKS / 2;
+        const int cc = c - isv * (CHUNKS / 2);
+        const int row = cc >> 3, ch = cc & 7;
+        const int key = t * KT + row;
+        if (key < a.N) {
+          const bf16_t* src = (isv ? vbase : kbase) + (long long)key * a.s_tok + ch * 8;
+          r = *reinterpret_cast<const u32x4*>(src);
+        }
+      }
+      stage[i] = r;
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int c = tid + i * NT;
+      if (c < CHUNKS) {
+        const int isv = c >= CHUNKS / 2;
+        const int cc = c - isv * (CHUNKS / 2);
+        const int row = cc >> 3, ch = cc & 7;
+        if (isv)
+          *reinterpret_cast<u32x4*>(Vs + v_off(row, ch)) = stage[i];
+        else
+          *reinterpret_cast<u32x4*>(Ks + k_off(row, ch)) = stage[i];
+      }
+    }
+  };
+
+  issue(0);
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();  // previous tile fully consumed
+    commit();
+    __syncthreads();
+    if (t + 1 < ntiles) issue(t + 1);
+
+    // ---- S^T = K Q^T for the two 32-key blocks
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
+      const int row = kb * 32 + ql;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(row, 2 * ks + h));
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
+      }
+    }
+    // ---- online softmax (lane = query; keys: kb*32 + 8(i>>2) + 4h + (i&3))
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float rhv = 0.f;
+      if (BIAS == 2) rhv = rh[min(2 * t + kb, a.Hg - 1)] * 1.4426950408889634f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = t * KT + kb * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+        float x = s[kb][i] * c2;
+        if (BIAS == 2) {
+          x += rhv + rwr[i];
+        } else if (BIAS == 1) {
+          const int kc = min(key, a.N - 1);
+          const int kh = kc / a.Wg, kw = kc - kh * a.Wg;
+          x += (rh[kh] + rw[kw]) * 1.4426950408889634f;
+        }
+        x = key < a.N ? x : -INFINITY;
+        s[kb][i] = x;
+        mt = fmaxf(mt, x);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(s[kb][i] - mn);
+        s[kb][i] = p;
+        rs += p;
+      }
+    l = l * alpha + rs;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        u32x4 pw;
+        pw[0] = cvt_pk_bf16(s[kb][8 * st + 0], s[kb][8 * st + 1]);
+        pw[1] = cvt_pk_bf16(s[kb][8 * st + 2], s[kb][8 * st + 3]);
+        pw[2] = cvt_pk_bf16(s[kb][8 * st + 4], s[kb][8 * st + 5]);
+        pw[3] = cvt_pk_bf16(s[kb][8 * st + 6], s[kb][8 * st + 7]);
+        const bf16x8 pf = *reinterpret_cast<bf16x8*>(&pw);
+        const int g1 = (lane >> 4) & 1;
+        const int qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int ch = db * 4 + 2 * g1 + (pp >> 1);
+          const int row0 = kb * 32 + 16 * st + 4 * h + qq;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Vs + v_off(row0, ch) + 4 * (pp & 1)));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Vs + v_off(row0 + 8, ch) + 4 * (pp & 1)));
+          bf16x8 vf;
+          vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
+          vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
+        }
+      }
+  }
+
+  // ---- epilogue: O = O^T / l  (lane = query, d = db*32 + 8(i>>2) + 4h + (i&3))
+  const float lt = l + __shfl_xor(l, 32, 64);
+  if (qi < a.N) {
+    const float inv = 1.f / lt;
+    bf16_t* ob = a.o + (long long)b * a.o_batch + (long long)hh * a.o_head + (long long)qi * a.o_tok;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 w;
+        w[0] = cvt_pk_bf16(oacc[db][4 * g + 0] * inv, oacc[db][4 * g + 1] * inv);
+        w[1] = cvt_pk_bf16(oacc[db][4 * g + 2] * inv, oacc[db][4 * g + 3] * inv);
+        *reinterpret_cast<u32x2*>(ob + db * 32 + 8 * g + 4 * h) = w;
+      }
+    if (a.lse && h == 0) a.lse[(long long)bh * a.N + qi] = (m + __log2f(lt)) * 0.6931471805599453f;
+  }
+}
+
+template <int NW>
+int launch_nw(AttnArgs a, hipStream_t s) {
+  a.qblocks = (a.N + NW * 32 - 1) / (NW * 32);
+  const int grid = a.qblocks * a.B * a.H;
+  if (a.relh && a.Wg == 32)
+    hipLaunchKernelGGL((attn_fwd_kernel<NW, 2>), dim3(grid), dim3(NW * 64), 0, s, a);
+  else if (a.relh)
+    hipLaunchKernelGGL((attn_fwd_kernel<NW, 1>), dim3(grid), dim3(NW * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<NW, 0>), dim3(grid), dim3(NW * 64), 0, s, a);
+  return BE_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+extern "C" {
+
+// q/k/v: bf16 with element strides (token, head, batch) shared by the three (e.g. a packed
+// [B, N, 3, H, 64] qkv buffer); o: bf16 with its own strides.  head_dim must be 64.
+// nw = 0 picks the waves per block (2, 3 or 4 x 32 queries) that least overpads N.
+int be_attn_fwd(const void* q, const void* k, const void* v, long long s_tok, long long s_head, long long s_batch,
+                void* o, long long o_tok, long long o_head, long long o_batch, float* lse, const float* relh,
+                const float* relw, int Hg, int Wg, int B, int H, int N, int head_dim, float scale, int nw,
+                hipStream_t stream) {
+  if (head_dim != HD) return -1;
+  if (N <= 0 || B <= 0 || H <= 0) return 0;
+  if ((relh == nullptr) != (relw == nullptr)) return -2;
+  if (relh && (Hg <= 0 || Wg <= 0 || Hg * Wg != N)) return -3;
+  AttnArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.s_tok = s_tok; a.s_head = s_head; a.s_batch = s_batch;
+  a.o = (bf16_t*)o; a.o_tok = o_tok; a.o_head = o_head; a.o_batch = o_batch;
+  a.lse = lse; a.relh = relh; a.relw = relw; a.Hg = Hg; a.Wg = Wg;
+  a.B = B; a.H = H; a.N = N; a.scale = scale;
+  if (nw == 0) {
+    const int slices = (N + 31) / 32;
+    int best = 4, waste = 1 << 30;
+    for (int c : {4, 3, 2}) {
+      const int w = ((slices + c - 1) / c) * c - slices;
+      if (w < waste) { waste = w; best = c; }
+    }
+    nw = best;
+  }
+  switch (nw) {
+    case 2: return launch_nw<2>(a, stream);
+    case 3: return launch_nw<3>(a, stream);
+    case 4: return launch_nw<4>(a, stream);
+    case 8: return launch_nw<8>(a, stream);
+  }
+  return -4;
+}
+
+}  // extern "C"
