@@ -84,9 +84,11 @@ class LocalReplica(ReplicaBase):
 
         def build():
             tok = rctx.set_current(ctx)
-            old_env = {k: os.environ.get(k) for k in self.env}
             try:
-                os.environ.update({k: str(v) for k, v in self.env.items()})
+                # in-process replicas share the worker's environment: temp-dir variables would
+                # redirect every later tempfile/AF_UNIX socket of the host process, so they are
+                # only honoured by process replicas
+                os.environ.update({k: str(v) for k, v in self.env.items() if k not in ("TMPDIR", "TEMP", "TMP")})
                 obj = self.cls(*self.args, **self.kwargs)
             finally:
                 rctx.reset_current(tok)
