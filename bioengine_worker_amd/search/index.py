@@ -1,0 +1,154 @@
+"""GPU vector index for L2-normalised embeddings (inner product = cosine).
+
+Replaces the reference's FAISS indexes (apps/cell-image-search/index_manager.py:36-182,
+SURVEY.md K20) with an HBM-resident design: MI355X holds 288 GB, i.e. ~180 M 768-d bf16 vectors,
+so exact search is one bf16 GEMM (hipBLASLt) per query batch plus a top-k, streamed over
+fixed-size chunks.  Past ``ivf_threshold`` vectors an IVF layer (spherical k-means on the GPU,
+``nlist = clamp(sqrt(N), 64, 4096)``, ``nprobe = 64`` as in the reference) restricts each query to
+its closest lists.  Storage is plain ``.npy`` + JSON (no pickles).
+
+Layout at ``<workspace>/cell_search/``: ``vectors.npy`` (fp16 [N, D]), ``index_info.json``,
+``ivf_centroids.npy`` / ``ivf_assign.npy`` (IVF only), ``metadata.parquet``, ``thumbnails.npy``.
+"""
+from __future__ import annotations
+
+import json
+import math
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+CHUNK = 1 << 20  # database rows per GEMM chunk
+
+
+class VectorIndex:
+    def __init__(self, dim: int = 768, device=None, ivf_threshold: int = 5_000_000, nprobe: int = 64):
+        self.dim = dim
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        self.vecs = torch.empty(0, dim, dtype=self.dtype, device=self.device)
+        self.ivf_threshold = ivf_threshold
+        self.nprobe = nprobe
+        self.centroids: torch.Tensor | None = None
+        self.assign: torch.Tensor | None = None
+        self.lists: list[torch.Tensor] | None = None
+
+    # ------------------------------------------------------------------ build
+    @property
+    def ntotal(self) -> int:
+        return int(self.vecs.shape[0])
+
+    @property
+    def index_type(self) -> str:
+        return f"IVFFlat-GPU(nlist={self.centroids.shape[0]})" if self.centroids is not None else "FlatIP-GPU"
+
+    def add(self, x) -> None:
+        x = torch.as_tensor(np.asarray(x, np.float32) if not torch.is_tensor(x) else x).to(self.device, self.dtype)
+        assert x.dim() == 2 and x.shape[1] == self.dim
+        self.vecs = torch.cat([self.vecs, x], 0)
+        if self.centroids is not None:
+            self._assign_new(x, self.ntotal - x.shape[0])
+        elif self.ntotal >= self.ivf_threshold:
+            self.train_ivf()
+
+    def train_ivf(self, nlist: int | None = None, iters: int = 10, seed: int = 0) -> None:
+        n = self.ntotal
+        nlist = nlist or min(4096, max(64, int(math.sqrt(n))))
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        sample = self.vecs[torch.randperm(n, generator=g)[: min(n, 256 * nlist)].to(self.device)].float()
+        cent = sample[torch.randperm(sample.shape[0], generator=g)[:nlist].to(self.device)].clone()
+        for _ in range(iters):  # spherical k-means
+            a = (sample @ cent.T).argmax(1)
+            new = torch.zeros_like(cent).index_add_(0, a, sample)
+            cnt = torch.bincount(a, minlength=nlist)
+            empty = cnt == 0
+            new[empty] = cent[empty]
+            cent = torch.nn.functional.normalize(new, dim=1)
+        self.centroids = cent.to(self.dtype)
+        self.assign = torch.empty(0, dtype=torch.int32, device=self.device)
+        self._assign_new(self.vecs, 0)
+
+    def _assign_new(self, x: torch.Tensor, base: int) -> None:
+        a = torch.cat([(x[i:i + CHUNK] @ self.centroids.T).argmax(1) for i in range(0, x.shape[0], CHUNK)]).int()
+        self.assign = torch.cat([self.assign, a])
+        order = torch.argsort(self.assign, stable=True)
+        counts = torch.bincount(self.assign.long(), minlength=self.centroids.shape[0]).tolist()
+        self.lists = list(torch.split(order, counts))
+
+    # ------------------------------------------------------------------ search
+    @torch.no_grad()
+    def search(self, q, k: int = 20):
+        """q [Q, D] -> (scores [Q, k] fp32 numpy, ids [Q, k] int64 numpy; -1 = empty slot)."""
+        q = torch.as_tensor(np.asarray(q, np.float32) if not torch.is_tensor(q) else q).to(self.device, self.dtype)
+        if q.dim() == 1:
+            q = q[None]
+        Q = q.shape[0]
+        k_eff = min(k, self.ntotal)
+        if k_eff == 0:
+            return np.full((Q, k), -np.inf, np.float32), np.full((Q, k), -1, np.int64)
+        if self.centroids is None:
+            best_s = torch.full((Q, 0), -float("inf"), device=self.device)
+            best_i = torch.empty(Q, 0, dtype=torch.long, device=self.device)
+            for i in range(0, self.ntotal, CHUNK):
+                s = (q @ self.vecs[i:i + CHUNK].T).float()
+                ts, ti = torch.topk(s, min(k_eff, s.shape[1]), dim=1)
+                best_s = torch.cat([best_s, ts], 1)
+                best_i = torch.cat([best_i, ti + i], 1)
+                best_s, j = torch.topk(best_s, min(k_eff, best_s.shape[1]), dim=1)
+                best_i = torch.gather(best_i, 1, j)
+        else:
+            probes = torch.topk((q @ self.centroids.T).float(), min(self.nprobe, self.centroids.shape[0]), dim=1).indices
+            best_s = torch.full((Q, k_eff), -float("inf"), device=self.device)
+            best_i = torch.full((Q, k_eff), -1, dtype=torch.long, device=self.device)
+            for qi in range(Q):
+                cand = torch.cat([self.lists[int(c)] for c in probes[qi].tolist()])
+                if cand.numel() == 0:
+                    continue
+                s = (self.vecs[cand] @ q[qi]).float()
+                ts, ti = torch.topk(s, min(k_eff, s.numel()))
+                best_s[qi, : ts.numel()] = ts
+                best_i[qi, : ts.numel()] = cand[ti]
+        S = np.full((Q, k), -np.inf, np.float32)
+        I = np.full((Q, k), -1, np.int64)
+        S[:, : best_s.shape[1]] = best_s.cpu().numpy()
+        I[:, : best_i.shape[1]] = best_i.cpu().numpy()
+        return S, I
+
+    def reconstruct_batch(self, ids) -> np.ndarray:
+        return self.vecs[torch.as_tensor(np.asarray(ids), device=self.device)].float().cpu().numpy()
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, out_dir) -> dict:
+        out = Path(out_dir)
+        out.mkdir(parents=True, exist_ok=True)
+        t0 = time.time()
+        np.save(out / "vectors.npy", self.vecs.float().cpu().numpy().astype(np.float16))
+        if self.centroids is not None:
+            np.save(out / "ivf_centroids.npy", self.centroids.float().cpu().numpy())
+        else:
+            (out / "ivf_centroids.npy").unlink(missing_ok=True)
+        info = {"n_cells": self.ntotal, "embed_dim": self.dim, "index_type": self.index_type,
+                "index_size_mb": round((out / "vectors.npy").stat().st_size / 2 ** 20, 3),
+                "build_seconds": round(time.time() - t0, 3),
+                "build_time_iso": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
+        (out / "index_info.json").write_text(json.dumps(info, indent=2))
+        return info
+
+    @classmethod
+    def load(cls, out_dir, device=None) -> "VectorIndex":
+        out = Path(out_dir)
+        p = out / "vectors.npy"
+        if not p.exists():
+            raise FileNotFoundError(f"No index at {p}")
+        v = np.load(p)  # allow_pickle=False
+        idx = cls(dim=v.shape[1], device=device)
+        idx.vecs = torch.from_numpy(v.astype(np.float32)).to(idx.device, idx.dtype)
+        c = out / "ivf_centroids.npy"
+        if c.exists():
+            idx.centroids = torch.from_numpy(np.load(c)).to(idx.device, idx.dtype)
+            idx.assign = torch.empty(0, dtype=torch.int32, device=idx.device)
+            idx._assign_new(idx.vecs, 0)
+        return idx

@@ -1,0 +1,81 @@
+"""cell-image-search HIP kernels vs the numpy/PIL/scipy oracle."""
+import numpy as np
+import pytest
+import torch
+
+from bioengine_worker_amd.search import reference as ref
+from bioengine_worker_amd.search.ingestion import synthetic_cell_painting
+
+
+@pytest.mark.gpu
+def test_ccl_matches_scipy(gpu):
+    from bioengine_worker_amd.search.nuclei import label_components, region_stats
+
+    rng = np.random.default_rng(0)
+    mask = rng.random((2, 300, 257)) > 0.55
+    lab = label_components(torch.from_numpy(mask).to(gpu)).cpu().numpy()
+    for b in range(2):
+        r = ref.label8(mask[b])
+        assert (lab[b] >= 0).sum() == (r > 0).sum()
+        # same partition: root labels map 1:1 onto scipy labels
+        pairs = set(zip(lab[b][r > 0].tolist(), r[r > 0].tolist()))
+        assert len(pairs) == r.max() == len({p[0] for p in pairs})
+    roots, area, cy, cx = region_stats(label_components(torch.from_numpy(mask[:1]).to(gpu)))
+    assert int(area.sum()) == int(mask[0].sum())
+
+
+@pytest.mark.gpu
+def test_nucleus_centroids_match_reference(gpu):
+    from bioengine_worker_amd.search.nuclei import extract_cell_crops, nucleus_centroids
+
+    img, _ = synthetic_cell_painting(5, size=900, n_cells=40)
+    c_ref = ref.nucleus_centroids(img, 100)
+    c_gpu = nucleus_centroids(torch.from_numpy(img).to(gpu), 100)
+    assert len(c_ref) >= 10 and c_gpu == c_ref
+    crops = extract_cell_crops(torch.from_numpy(img).to(gpu), 224, 30)
+    ref_crops = ref.extract_cell_crops(img, 224, 30)
+    assert crops.shape[0] == len(ref_crops) and np.array_equal(crops[0].cpu().numpy(), ref_crops[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,C", [((224, 224), 5), ((300, 260), 3), ((150, 100), 2), ((64, 64), 1)])
+def test_batch_to_dinov2_matches_pil(gpu, hw, C):
+    from bioengine_worker_amd.search.preprocess import batch_to_dinov2
+
+    rng = np.random.default_rng(1)
+    crops = (rng.random((3,) + hw + (C,)) * 3000).astype(np.uint16)
+    out = batch_to_dinov2(torch.from_numpy(crops).to(gpu)).float().cpu().numpy()
+    for i in range(3):
+        r = ref.to_dinov2_array(ref.to_rgb_uint8(crops[i]))
+        d = np.abs(out[i] - r)
+        # 8-bit rounding of the resample passes may differ by one level (1/255/0.225 ~ 0.0175)
+        assert d.max() < 0.04 and (d > 0.02).mean() < 0.01, (d.max(), (d > 0.02).mean())
+
+
+@pytest.mark.gpu
+def test_vector_index_gpu_matches_numpy(gpu):
+    from bioengine_worker_amd.search.index import VectorIndex
+
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(20000, 768)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    idx = VectorIndex(dim=768, device=gpu)
+    idx.add(x)
+    S, I = idx.search(x[:16], 10)
+    assert (I[:, 0] == np.arange(16)).all()
+    ref_I = np.argsort(-(x[:16] @ x.T), axis=1)[:, :10]
+    assert np.mean([len(set(a) & set(b)) / 10 for a, b in zip(I, ref_I)]) > 0.9  # bf16 storage
+
+
+@pytest.mark.gpu
+def test_ingestion_synthetic_gpu(gpu, tmp_path):
+    from bioengine_worker_amd.search.index import VectorIndex
+    from bioengine_worker_amd.search.ingestion import index_dir, run_ingestion
+
+    st = run_ingestion(str(tmp_path), "s1", dataset="synthetic", n_images=3, n_crops_per_image=20,
+                       devices=[str(gpu)])
+    assert st["status"] == "completed", st
+    idx = VectorIndex.load(index_dir(str(tmp_path)), device=gpu)
+    assert idx.ntotal == st["n_embedded"] >= 30
+    S, I = idx.search(idx.reconstruct_batch([0]), 3)
+    assert I[0, 0] == 0 and S[0, 0] > 0.99
