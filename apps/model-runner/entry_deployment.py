@@ -1,0 +1,259 @@
+"""Model runner entry deployment (CPU): model zoo search, RDF / documentation, validation,
+testing with cached reports, upload URLs and inference orchestration.
+
+API parity with the reference ``EntryDeployment`` (apps/model-runner/entry_deployment.py:1012-1990):
+search_models, get_model_rdf, get_model_documentation, validate, test, get_upload_url, infer.
+Model packages come from the on-disk :class:`ModelCache` filled from a local zoo directory
+(``BIOENGINE_MODEL_ZOO``; a demo U-Net package is written there when none is configured) or from
+the hub's ``bioimage-io`` artifact collection.  GPU work is delegated to ``RuntimeDeployment``.
+"""
+from __future__ import annotations
+
+import asyncio
+import io
+import json
+import logging
+import os
+import time
+import uuid
+from pathlib import Path
+from typing import Dict, List, Literal, Optional, Union
+
+import numpy as np
+from hypha_rpc.utils.schema import schema_method
+from pydantic import Field
+from ray import serve
+from ray.serve.handle import DeploymentHandle
+
+logger = logging.getLogger("ray.serve")
+COLLECTION = "bioimage-io/bioimage.io"
+
+
+@serve.deployment(
+    ray_actor_options={"num_cpus": 1, "num_gpus": 0, "memory": 4 * 1024 ** 3},
+    max_ongoing_requests=10,
+    max_queued_requests=30,
+    health_check_period_s=30.0,
+    health_check_timeout_s=30.0,
+)
+class EntryDeployment:
+    def __init__(self, runtime_deployment: DeploymentHandle, cache_size_in_gb: float = 50.0) -> None:
+        from bioengine_worker_amd.bioimageio.zoo import ModelCache
+
+        self.runtime_deployment = runtime_deployment
+        try:
+            self.replica_id = serve.get_replica_context().replica_tag
+        except Exception:  # noqa: BLE001
+            self.replica_id = "unknown"
+        self.model_cache = ModelCache(cache_size_in_gb=cache_size_in_gb, replica_id=self.replica_id,
+                                      fetch_remote=self._fetch_remote)
+        self.server = None
+        self.artifact_manager = None
+        self.s3 = None
+
+    async def async_init(self) -> None:
+        from bioengine_worker_amd.bioimageio.zoo import local_zoo_root
+
+        if local_zoo_root() is None:  # offline: a built-in demo zoo in the app's workdir
+            from bioengine_worker_amd.bioimageio.package import write_unet2d_package
+
+            root = Path(os.environ.get("HOME", ".")) / "model_zoo"
+            if not (root / "demo-unet2d" / "rdf.yaml").exists():
+                await asyncio.to_thread(write_unet2d_package, root / "demo-unet2d", "demo-unet2d")
+            os.environ["BIOENGINE_MODEL_ZOO"] = str(root)
+        url = os.environ.get("HYPHA_SERVER_URL")
+        if url:
+            try:
+                from hypha_rpc import connect_to_server
+
+                self.server = await connect_to_server({"server_url": url, "token": os.environ.get("HYPHA_TOKEN")})
+                self.artifact_manager = await self.server.get_service("public/artifact-manager")
+                try:
+                    self.s3 = await self.server.get_service("public/s3-storage")
+                except Exception:  # noqa: BLE001
+                    self.s3 = None
+            except Exception as e:  # noqa: BLE001
+                logger.warning("hub not reachable (%s); local model zoo only", e)
+
+    async def check_health(self) -> None:
+        return None
+
+    async def _check_runtime_available(self) -> None:
+        try:
+            await asyncio.wait_for(self.runtime_deployment.check_health.remote(), timeout=5.0)
+        except Exception as e:  # noqa: BLE001
+            raise RuntimeError("GPU runtime deployment is not available; inference, test and validate are "
+                               "unavailable until it starts.") from e
+
+    async def _fetch_remote(self, model_id: str, dest: Path, stage: bool):
+        if self.artifact_manager is None:
+            raise ValueError(f"model '{model_id}' not in the local zoo and no hub connection")
+        import httpx
+
+        aid = f"bioimage-io/{model_id}"
+        files = await self.artifact_manager.list_files(aid, stage=stage)
+        latest = 0.0
+        async with httpx.AsyncClient(timeout=300) as c:
+            for f in files:
+                name = f["name"] if isinstance(f, dict) else str(f)
+                url = await self.artifact_manager.get_file(aid, file_path=name, stage=stage)
+                r = await c.get(url)
+                r.raise_for_status()
+                p = dest / name
+                p.parent.mkdir(parents=True, exist_ok=True)
+                p.write_bytes(r.content)
+                latest = max(latest, float(f.get("last_modified", 0) or 0) if isinstance(f, dict) else 0.0)
+        return latest or time.time()
+
+    async def _load_input(self, source: str) -> np.ndarray:
+        import httpx
+
+        if source.startswith("http://") or source.startswith("https://"):
+            url = source
+        else:
+            if self.s3 is None:
+                raise FileNotFoundError(f"cannot resolve '{source}' without S3 storage")
+            url = await self.s3.generate_presigned_url(source, client_method="get_object")
+        async with httpx.AsyncClient(timeout=300) as c:
+            r = await c.get(url)
+        if r.status_code == 404:
+            raise FileNotFoundError(source)
+        r.raise_for_status()
+        data = r.content
+        if data[:6] == b"\x93NUMPY":
+            return np.load(io.BytesIO(data))
+        from PIL import Image
+
+        return np.asarray(Image.open(io.BytesIO(data)))
+
+    # ------------------------------------------------------------------ API
+    @schema_method
+    async def search_models(self, keywords: Optional[List[str]] = Field(None, description="Keywords to filter by."),
+                            limit: Optional[int] = Field(10, description="Maximum number of results."),
+                            ignore_checks: Optional[bool] = Field(False, description="Include models without a passed "
+                                                                                     "inference check.")) -> List[Dict[str, str]]:
+        """Search the model zoo (local zoo first, then the hub collection)."""
+        from bioengine_worker_amd.bioimageio.zoo import search_local
+
+        res = search_local(keywords, limit or 10)
+        if self.artifact_manager is not None and len(res) < (limit or 10):
+            try:
+                arts = await self.artifact_manager.list(parent_id=COLLECTION, filters={"type": "model"},
+                                                        keywords=keywords, limit=limit)
+                seen = {r["model_id"] for r in res}
+                for a in arts:
+                    if a["alias"] not in seen:
+                        res.append({"model_id": a["alias"], "description": a.get("manifest", {}).get("description", "")})
+            except Exception as e:  # noqa: BLE001
+                logger.info("hub search unavailable: %s", e)
+        return res[: limit or 10]
+
+    @schema_method
+    async def get_model_rdf(self, model_id: str = Field(..., description="Model id, e.g. 'demo-unet2d'."),
+                            stage: Optional[bool] = Field(False, description="Staged version.")) -> Dict:
+        """The model's RDF (rdf.yaml) as a dictionary."""
+        import yaml
+
+        lease = await self.model_cache.get_model_package(model_id, stage=stage)
+        async with lease:
+            return yaml.safe_load((lease.source / "rdf.yaml").read_text())
+
+    @schema_method
+    async def get_model_documentation(self, model_id: str = Field(..., description="Model id."),
+                                      stage: Optional[bool] = Field(False, description="Staged version.")) -> Optional[str]:
+        """Content of the RDF's ``documentation`` file (None when absent)."""
+        rdf = await self.get_model_rdf(model_id=model_id, stage=stage)
+        doc = rdf.get("documentation")
+        if not doc:
+            return None
+        lease = await self.model_cache.get_model_package(model_id, stage=stage)
+        async with lease:
+            p = lease.source / doc
+            return p.read_text() if p.exists() else None
+
+    @schema_method
+    async def validate(self, rdf_dict: Dict = Field(..., description="Complete RDF dictionary."),
+                       known_files: Optional[Dict[str, str]] = Field(None, description="file path -> sha256")) -> Dict:
+        """Format validation of an RDF (no I/O checks unless known_files is given)."""
+        from bioengine_worker_amd.bioimageio.spec import format_summary, validate_format
+
+        s = validate_format(rdf_dict, known_files)
+        return {"success": s["status"] == "valid-format", "details": format_summary(s)}
+
+    @schema_method
+    async def test(self, model_id: str = Field(..., description="Model id."),
+                   stage: Optional[bool] = Field(False, description="Staged version."),
+                   additional_requirements: Optional[List[str]] = Field(None, description="Extra packages (ignored offline)."),
+                   skip_cache: Optional[bool] = Field(False, description="Re-download and re-test."),
+                   publish_test_report: Optional[bool] = Field(False, description="Upload the report to the artifact.")) -> Dict:
+        """Run the package's test (test inputs -> outputs) on the GPU runtime; reports are cached
+        per package modification time."""
+        await self._check_runtime_available()
+        lease = await self.model_cache.get_model_package(model_id, stage=stage, skip_cache=skip_cache)
+        async with lease:
+            cache = lease.source / ".test_cache.json"
+            if cache.exists() and not skip_cache:
+                c = json.loads(cache.read_text())
+                if c.get("latest_remote_modified") == lease.latest_remote_modified:
+                    return c["report"]
+            report = await self.runtime_deployment.test.remote(rdf_path=str(lease.rdf_path),
+                                                               additional_requirements=additional_requirements)
+            cache.write_text(json.dumps({"latest_remote_modified": lease.latest_remote_modified,
+                                         "additional_requirements": additional_requirements, "report": report},
+                                        default=str))
+        if publish_test_report and self.artifact_manager is not None:
+            aid = f"bioimage-io/{model_id}"
+            try:
+                await self.artifact_manager.edit(aid, stage=True, manifest={"test_summary": {"status": report["status"]}})
+                await self.artifact_manager.commit(aid)
+            except Exception as e:  # noqa: BLE001
+                report["publish_error"] = str(e)
+        return report
+
+    @schema_method
+    async def get_upload_url(self, file_type: str = Field(".npy", description="File extension of the upload.")) -> Dict:
+        """Presigned PUT URL (1 h) for a large input; pass the returned file_path as ``infer(inputs=...)``."""
+        if self.s3 is None:
+            raise RuntimeError("S3 storage is not available on this worker")
+        fp = f"tmp/model-runner/{uuid.uuid4().hex}{file_type}"
+        url = await self.s3.generate_presigned_url(fp, client_method="put_object", expiration=3600)
+        return {"upload_url": url, "file_path": fp}
+
+    @schema_method(arbitrary_types_allowed=True)
+    async def infer(self, model_id: str = Field(..., description="Model id."),
+                    inputs: Union[np.ndarray, Dict[str, Union[np.ndarray, str]], str] = Field(..., description=(
+                        "Array, {input_id: array|url|file_path}, or a URL / uploaded file path.")),
+                    weights_format: Optional[str] = Field(None, description="pytorch_state_dict | torchscript"),
+                    device: Optional[Literal["cuda", "cpu"]] = Field(None, description="Target device."),
+                    default_blocksize_parameter: Optional[int] = Field(None, description="Tiling block size parameter."),
+                    sample_id: Optional[str] = Field("sample", description="Request id for logs."),
+                    skip_cache: Optional[bool] = Field(False, description="Re-download the package first."),
+                    return_download_url: Optional[bool] = Field(False, description="Return .npy download URLs.")) -> Dict:
+        """Run a model on the GPU runtime; returns {output_id: array (or URL)}."""
+        await self._check_runtime_available()
+        if isinstance(inputs, str):
+            inputs = await self._load_input(inputs)
+        elif isinstance(inputs, dict):
+            inputs = {k: (await self._load_input(v) if isinstance(v, str) else v) for k, v in inputs.items()}
+        lease = await self.model_cache.get_model_package(model_id, skip_cache=skip_cache)
+        async with lease:
+            result = await self.runtime_deployment.predict.remote(
+                rdf_path=str(lease.rdf_path), inputs=inputs, weights_format=weights_format, device=device,
+                default_blocksize_parameter=default_blocksize_parameter, sample_id=sample_id,
+                latest_remote_modified=lease.latest_remote_modified)
+        if return_download_url:
+            if self.s3 is None:
+                raise RuntimeError("return_download_url needs S3 storage")
+            import httpx
+
+            out = {}
+            async with httpx.AsyncClient(timeout=300) as c:
+                for k, v in result.items():
+                    fp = f"tmp/model-runner/{uuid.uuid4().hex}.npy"
+                    buf = io.BytesIO()
+                    np.save(buf, v)
+                    put = await self.s3.generate_presigned_url(fp, client_method="put_object")
+                    (await c.put(put, content=buf.getvalue())).raise_for_status()
+                    out[k] = await self.s3.generate_presigned_url(fp, client_method="get_object")
+            result = out
+        return result

@@ -1,0 +1,140 @@
+"""Self-contained bioimage.io demo model packages (offline model zoo, tests, bench).
+
+``write_unet2d_package(dir)`` writes a complete RDF 0.5 package: ``model.py`` (a 2-D U-Net with
+Conv-BN-ReLU blocks, max-pool encoder, transposed-conv decoder with skip concatenation, 1x1 head +
+sigmoid — the architecture family of the zoo's nucleus-segmentation U-Nets such as
+``affable-shark``), ``weights.pt`` (state dict, random init with non-trivial BN statistics),
+``weights_torchscript.pt``, ``test_input.npy`` / ``test_output.npy`` (computed in fp32 on CPU),
+``README.md`` and ``rdf.yaml``.
+"""
+from __future__ import annotations
+
+import importlib.util
+import textwrap
+from pathlib import Path
+
+import numpy as np
+import torch
+import yaml
+
+from .spec import sha256_file
+
+MODEL_SRC = textwrap.dedent('''
+    import torch
+    import torch.nn as nn
+
+
+    def conv_block(cin, cout):
+        return nn.Sequential(
+            nn.Conv2d(cin, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True),
+            nn.Conv2d(cout, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+
+
+    class UNet2d(nn.Module):
+        def __init__(self, in_channels=1, out_channels=2, features=(32, 64, 128, 256), final_activation="Sigmoid"):
+            super().__init__()
+            self.encoders = nn.ModuleList()
+            c = in_channels
+            for f in features[:-1]:
+                self.encoders.append(conv_block(c, f))
+                c = f
+            self.pool = nn.MaxPool2d(2)
+            self.base = conv_block(c, features[-1])
+            self.ups = nn.ModuleList()
+            self.decoders = nn.ModuleList()
+            c = features[-1]
+            for f in reversed(features[:-1]):
+                self.ups.append(nn.ConvTranspose2d(c, f, 2, stride=2))
+                self.decoders.append(conv_block(2 * f, f))
+                c = f
+            self.head = nn.Conv2d(c, out_channels, 1)
+            self.act = getattr(nn, final_activation)() if final_activation else nn.Identity()
+
+        def forward(self, x):
+            skips = []
+            for enc in self.encoders:
+                x = enc(x)
+                skips.append(x)
+                x = self.pool(x)
+            x = self.base(x)
+            for up, dec, s in zip(self.ups, self.decoders, reversed(skips)):
+                x = dec(torch.cat([s, up(x)], dim=1))
+            return self.act(self.head(x))
+''')
+
+
+def load_module(path: Path, name: str = "bioimageio_model_src"):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def write_unet2d_package(out: str | Path, model_id: str = "demo-unet2d", in_channels: int = 1, out_channels: int = 2,
+                         features=(32, 64, 128, 256), test_shape=(1, 1, 256, 256), seed: int = 0,
+                         torchscript: bool = True) -> Path:
+    out = Path(out)
+    out.mkdir(parents=True, exist_ok=True)
+    (out / "model.py").write_text(MODEL_SRC)
+    mod = load_module(out / "model.py", f"pkg_{model_id.replace('-', '_')}")
+    kwargs = {"in_channels": in_channels, "out_channels": out_channels, "features": list(features),
+              "final_activation": "Sigmoid"}
+    torch.manual_seed(seed)
+    net = mod.UNet2d(**kwargs)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+                m.running_var.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
+                m.weight.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
+                m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    net.eval()
+    torch.save(net.state_dict(), out / "weights.pt")
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:test_shape[2], 0:test_shape[3]]
+    img = rng.normal(0, 0.2, test_shape).astype(np.float32)
+    for _ in range(12):
+        cy, cx, r = rng.uniform(20, test_shape[2] - 20), rng.uniform(20, test_shape[3] - 20), rng.uniform(6, 14)
+        img[:, :, ((yy - cy) ** 2 + (xx - cx) ** 2) < r * r] += 1.0
+    img = (img * 200 + 300).astype(np.float32)
+    np.save(out / "test_input.npy", img)
+    x = torch.from_numpy(img)
+    x = (x - x.mean(dim=(2, 3), keepdim=True)) / (x.std(dim=(2, 3), keepdim=True, unbiased=False) + 1e-6)
+    with torch.no_grad():
+        y = net(x).numpy()
+    np.save(out / "test_output.npy", y)
+    weights = {"pytorch_state_dict": {
+        "source": "weights.pt", "sha256": sha256_file(out / "weights.pt"),
+        "architecture": {"source": "model.py", "sha256": sha256_file(out / "model.py"), "callable": "UNet2d",
+                         "kwargs": kwargs},
+        "pytorch_version": "2.5"}}
+    if torchscript:
+        ts = torch.jit.trace(net, x[:, :, :64, :64])
+        ts.save(str(out / "weights_torchscript.pt"))
+        weights["torchscript"] = {"source": "weights_torchscript.pt", "sha256": sha256_file(out / "weights_torchscript.pt"),
+                                  "pytorch_version": "2.5", "parent": "pytorch_state_dict"}
+    (out / "README.md").write_text(f"# {model_id}\n\nDemo 2-D U-Net (random weights) for the MI355X model runner.\n")
+    rdf = {
+        "format_version": "0.5.3", "type": "model", "id": model_id, "name": f"Demo U-Net 2D ({model_id})",
+        "description": "2-D U-Net nucleus segmentation demo package (random weights) for the bioengine-worker-amd model runner.",
+        "authors": [{"name": "bioengine-worker-amd"}], "cite": [{"text": "Ronneberger et al. U-Net", "doi": "10.1007/978-3-319-24574-4_28"}],
+        "license": "MIT", "documentation": "README.md", "tags": ["unet", "segmentation", "nuclei", "2d", "demo"],
+        "inputs": [{"id": "raw", "axes": [
+            {"type": "batch"}, {"type": "channel", "channel_names": [f"c{i}" for i in range(in_channels)]},
+            {"type": "space", "id": "y", "size": {"min": 64, "step": 16}},
+            {"type": "space", "id": "x", "size": {"min": 64, "step": 16}}],
+            "test_tensor": {"source": "test_input.npy", "sha256": sha256_file(out / "test_input.npy")},
+            "data": {"type": "float32"},
+            "preprocessing": [{"id": "zero_mean_unit_variance", "kwargs": {"axes": ["y", "x"], "eps": 1e-6}}]}],
+        "outputs": [{"id": "probabilities", "axes": [
+            {"type": "batch"}, {"type": "channel", "channel_names": [f"p{i}" for i in range(out_channels)]},
+            {"type": "space", "id": "y", "size": {"tensor_id": "raw", "axis_id": "y"}, "halo": 16},
+            {"type": "space", "id": "x", "size": {"tensor_id": "raw", "axis_id": "x"}, "halo": 16}],
+            "test_tensor": {"source": "test_output.npy", "sha256": sha256_file(out / "test_output.npy")},
+            "data": {"type": "float32"}}],
+        "weights": weights,
+        "config": {"bioimageio": {"reproducibility_tolerance": [{"relative_tolerance": 1e-3, "absolute_tolerance": 1e-4}]}},
+    }
+    (out / "rdf.yaml").write_text(yaml.safe_dump(rdf, sort_keys=False))
+    return out

@@ -1,0 +1,118 @@
+"""bioimage.io pre-/post-processing operators on (GPU) torch tensors.
+
+Operators (spec 0.4 ``name`` / 0.5 ``id``): scale_range, zero_mean_unit_variance,
+fixed_zero_mean_unit_variance, scale_linear, scale_mean_variance, sigmoid, binarize, clip,
+ensure_dtype, softmax.  ``axes`` name the *reduced* axes (e.g. "xy" / ["x", "y"]); statistics are
+computed per sample and per remaining axis, as bioimageio.core does.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+_DT = {"float32": torch.float32, "float64": torch.float64, "uint8": torch.uint8, "int8": torch.int8,
+       "uint16": torch.int32, "int16": torch.int16, "int32": torch.int32, "int64": torch.int64, "bool": torch.bool,
+       "float16": torch.float16, "uint32": torch.int64}
+
+
+def _norm_axes(axes, axis_ids: list[str]) -> list[int]:
+    if axes is None:
+        return [i for i, a in enumerate(axis_ids) if a not in ("b", "c", "i")]
+    if isinstance(axes, str):
+        axes = list(axes)
+    out = []
+    for a in axes:
+        a = {"batch": "b", "channel": "c"}.get(a, a)
+        if a in axis_ids:
+            out.append(axis_ids.index(a))
+    return out
+
+
+def _percentile(x: torch.Tensor, dims: list[int], q: float) -> torch.Tensor:
+    """np.percentile(x, q, axis=dims, keepdims=True) with linear interpolation."""
+    keep = [d for d in range(x.dim()) if d not in dims]
+    perm = keep + dims
+    xp = x.permute(perm)
+    kshape = [x.shape[d] for d in keep]
+    flat = xp.reshape(int(math.prod(kshape)) if kshape else 1, -1).float()
+    srt, _ = torch.sort(flat, dim=1)
+    n = srt.shape[1]
+    pos = q / 100.0 * (n - 1)
+    lo = int(math.floor(pos))
+    hi = min(lo + 1, n - 1)
+    fr = pos - lo
+    v = srt[:, lo] * (1 - fr) + srt[:, hi] * fr
+    shape = [x.shape[d] if d in keep else 1 for d in range(x.dim())]
+    return v.reshape(shape)
+
+
+def _per_axis(val, axis_ids, ref_axis, x):
+    t = torch.as_tensor(val, dtype=torch.float32, device=x.device)
+    if t.dim() == 0 or ref_axis is None:
+        return t
+    shape = [1] * x.dim()
+    shape[axis_ids.index(ref_axis)] = -1
+    return t.reshape(shape)
+
+
+def apply_op(x: torch.Tensor, op: dict, axis_ids: list[str], tensors: dict | None = None) -> torch.Tensor:
+    name = op.get("id") or op.get("name")
+    kw = dict(op.get("kwargs") or {})
+    eps = float(kw.get("eps", 1e-6))
+    if name == "scale_range":
+        src = x
+        if kw.get("reference_tensor") and tensors and kw["reference_tensor"] in tensors:
+            src = tensors[kw["reference_tensor"]]
+        dims = _norm_axes(kw.get("axes"), axis_ids)
+        if kw.get("mode") == "per_dataset":
+            dims = sorted(set(dims) | {axis_ids.index("b")} if "b" in axis_ids else set(dims))
+        lo = _percentile(src.float(), dims, float(kw.get("min_percentile", 0.0)))
+        hi = _percentile(src.float(), dims, float(kw.get("max_percentile", 100.0)))
+        return (x.float() - lo) / (hi - lo + eps)
+    if name in ("zero_mean_unit_variance", "fixed_zero_mean_unit_variance"):
+        if name == "fixed_zero_mean_unit_variance" or kw.get("mode") == "fixed":
+            ax = kw.get("axis")
+            mean = _per_axis(kw["mean"], axis_ids, ax if ax in axis_ids else ("c" if isinstance(kw["mean"], list) else None), x)
+            std = _per_axis(kw["std"], axis_ids, ax if ax in axis_ids else ("c" if isinstance(kw["std"], list) else None), x)
+        else:
+            dims = _norm_axes(kw.get("axes"), axis_ids)
+            xf = x.float()
+            mean = xf.mean(dim=dims, keepdim=True)
+            std = xf.std(dim=dims, keepdim=True, unbiased=False)
+        return (x.float() - mean) / (std + eps)
+    if name == "scale_linear":
+        ax = kw.get("axis") or (kw.get("axes") if isinstance(kw.get("axes"), str) and len(kw.get("axes")) == 1 else None)
+        gain = _per_axis(kw.get("gain", 1.0), axis_ids, ax if isinstance(kw.get("gain"), list) else None, x)
+        off = _per_axis(kw.get("offset", 0.0), axis_ids, ax if isinstance(kw.get("offset"), list) else None, x)
+        return x.float() * gain + off
+    if name == "scale_mean_variance":
+        ref = tensors[kw["reference_tensor"]].float()
+        dims = _norm_axes(kw.get("axes"), axis_ids)
+        xf = x.float()
+        m, s = xf.mean(dim=dims, keepdim=True), xf.std(dim=dims, keepdim=True, unbiased=False)
+        rm, rs = ref.mean(dim=dims, keepdim=True), ref.std(dim=dims, keepdim=True, unbiased=False)
+        return (xf - m) / (s + eps) * (rs + eps) + rm
+    if name == "sigmoid":
+        return torch.sigmoid(x.float())
+    if name == "softmax":
+        return torch.softmax(x.float(), dim=axis_ids.index(kw.get("axis", "c")))
+    if name == "binarize":
+        thr = kw.get("threshold", 0.5)
+        if isinstance(thr, list):
+            thr = _per_axis(thr, axis_ids, kw.get("axis", "c"), x)
+        return (x.float() > thr).float()
+    if name == "clip":
+        return x.float().clamp(kw.get("min", None), kw.get("max", None))
+    if name == "ensure_dtype":
+        dt = kw.get("dtype", "float32")
+        if dt.startswith("uint") or dt.startswith("int"):
+            return x.round().to(_DT.get(dt, torch.int64))
+        return x.to(_DT.get(dt, torch.float32))
+    raise ValueError(f"unsupported processing operator {name!r}")
+
+
+def apply_chain(x: torch.Tensor, ops: list, axis_ids: list[str], tensors: dict | None = None) -> torch.Tensor:
+    for op in ops or []:
+        x = apply_op(x, op, axis_ids, tensors)
+    return x

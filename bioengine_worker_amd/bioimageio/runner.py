@@ -1,0 +1,268 @@
+"""Prediction pipeline for bioimage.io model packages (reference: bioimageio.core
+``create_prediction_pipeline`` + ``predict_sample_with/without_blocking`` as called by
+apps/model-runner/runtime_deployment.py:187-312).
+
+MI355X specifics: pytorch_state_dict models go through :func:`convert.optimize_for_mi355x`
+(fused NHWC MFMA convs, bf16 channels-last); with blocking, tiles are cut on the GPU and pushed
+through the network in batches (``tile_batch`` tiles per forward) instead of one by one, and the
+halo-cropped tiles are written straight into the output tensor on the device.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import processing
+from .spec import TensorSpec, load_rdf, tensors, weights_entries
+
+PREFERRED_FORMATS = ("pytorch_state_dict", "torchscript")
+UNSUPPORTED = {"onnx": "onnxruntime", "tensorflow_saved_model": "tensorflow", "keras_hdf5": "tensorflow"}
+
+
+def _src(v):
+    return v.get("source") if isinstance(v, dict) else v
+
+
+def _pad(x: torch.Tensor, pads: dict, mode: str) -> torch.Tensor:
+    """pads: {dim: (before, after)} on trailing dims (torch's F.pad order: last dim first)."""
+    if not any(b or a for b, a in pads.values()):
+        return x
+    first = min(pads)
+    cfg = []
+    for d in range(x.dim() - 1, first - 1, -1):
+        b, a = pads.get(d, (0, 0))
+        cfg += [b, a]
+    if mode == "reflect" and not all(max(b, a) < x.shape[d] for d, (b, a) in pads.items()):
+        mode = "replicate"
+    if mode != "constant" and not (3 <= x.dim() <= 5 and len(cfg) // 2 <= x.dim() - 2):
+        mode = "constant"
+    return F.pad(x, cfg, mode=mode)
+
+
+class PredictionPipeline:
+    def __init__(self, source, device=None, weights_format: str | None = None, optimize: bool = True,
+                 default_blocksize_parameter: int | None = None, tile_batch: int = 8):
+        self.rdf, self.root = load_rdf(source)
+        self.inputs: list[TensorSpec] = tensors(self.rdf, "inputs")
+        self.outputs: list[TensorSpec] = tensors(self.rdf, "outputs")
+        self.device = torch.device(device) if device else (
+            torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
+        self.blocksize = default_blocksize_parameter
+        self.tile_batch = tile_batch
+        w = weights_entries(self.rdf)
+        if weights_format:
+            if weights_format not in w:
+                raise ValueError(f"weights format {weights_format!r} not available (have {list(w)})")
+            fmt = weights_format
+        else:
+            fmt = next((f for f in PREFERRED_FORMATS if f in w), None)
+            if fmt is None:
+                missing = ", ".join(f"{k} (needs {UNSUPPORTED.get(k, '?')})" for k in w)
+                raise RuntimeError(f"no supported weights format in package: {missing}")
+        if fmt in UNSUPPORTED:
+            raise RuntimeError(f"weights format {fmt} needs {UNSUPPORTED[fmt]}, which this MI355X runtime does not ship")
+        self.weights_format = fmt
+        self.optimized = False
+        self.convert_stats: dict = {}
+        self.model = self._load(fmt, w[fmt], optimize)
+
+    # ------------------------------------------------------------------ model
+    def _load(self, fmt, entry, optimize):
+        root = self.root or Path(".")
+        if fmt == "torchscript":
+            m = torch.jit.load(str(root / _src(entry)), map_location=self.device)
+            return m.eval()
+        from .package import load_module
+
+        arch = entry.get("architecture") if isinstance(entry, dict) else None
+        kwargs = dict(entry.get("kwargs") or {})
+        if isinstance(arch, str):  # 0.4: "file.py:Callable"
+            file, call = arch.split(":")
+            mod = load_module(root / file)
+            ctor = getattr(mod, call)
+        elif isinstance(arch, dict) and arch.get("source"):
+            mod = load_module(root / arch["source"])
+            ctor = getattr(mod, arch["callable"])
+            kwargs.update(arch.get("kwargs") or {})
+        elif isinstance(arch, dict) and arch.get("import_from"):
+            import importlib
+
+            ctor = getattr(importlib.import_module(arch["import_from"]), arch["callable"])
+            kwargs.update(arch.get("kwargs") or {})
+        else:
+            raise ValueError("pytorch_state_dict weights without a usable architecture")
+        net = ctor(**kwargs)
+        sd = torch.load(root / _src(entry), map_location="cpu", weights_only=True)
+        net.load_state_dict(sd)
+        net.eval()
+        if optimize and self.device.type == "cuda":
+            from .convert import optimize_for_mi355x
+
+            net, self.convert_stats = optimize_for_mi355x(net, self.device)
+            self.optimized = True
+        return net.to(self.device)
+
+    # ------------------------------------------------------------------ sizes
+    @staticmethod
+    def _valid_len(L: int, size) -> int:
+        if isinstance(size, dict) and "min" in size:
+            mn, st = int(size["min"]), int(size["step"])
+            if st == 0:
+                return mn
+            return mn + max(0, math.ceil((L - mn) / st)) * st
+        if isinstance(size, int):
+            return size
+        return L
+
+    def _as_sample(self, inputs) -> dict[str, torch.Tensor]:
+        if not isinstance(inputs, dict):
+            inputs = {self.inputs[0].id: inputs}
+        out = {}
+        for spec in self.inputs:
+            key = spec.id if spec.id in inputs else (list(inputs)[self.inputs.index(spec)] if len(inputs) > self.inputs.index(spec) else None)
+            if key is None:
+                raise ValueError(f"missing input {spec.id!r}")
+            a = inputs[key]
+            t = torch.as_tensor(np.asarray(a)) if not torch.is_tensor(a) else a
+            while t.dim() < len(spec.axes):
+                t = t[None]  # missing leading singleton axes (batch / channel)
+            if t.dim() != len(spec.axes):
+                raise ValueError(f"input {spec.id!r}: got {t.dim()} dims, model axes are {spec.axis_ids}")
+            out[spec.id] = t.to(self.device)
+        return out
+
+    # ------------------------------------------------------------------ run
+    def _forward(self, xs: list[torch.Tensor]) -> list[torch.Tensor]:
+        with torch.no_grad():
+            if self.optimized:
+                xs = [x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if x.dim() == 4 else
+                      x.to(torch.bfloat16) for x in xs]
+            y = self.model(*xs)
+        ys = list(y) if isinstance(y, (tuple, list)) else [y]
+        return [t.float() for t in ys]
+
+    def _out_len(self, spec_o: TensorSpec, ax_o, in_lens: dict) -> int:
+        s = ax_o.size
+        if isinstance(s, dict) and "tensor_id" in s:
+            L = in_lens[(s["tensor_id"], s.get("axis_id", ax_o.id))]
+            return int(L * float(s.get("scale", ax_o.scale or 1.0)) + 2 * float(s.get("offset", 0)))
+        if isinstance(s, int):
+            return s
+        return -1
+
+    def predict(self, inputs, blocksize: int | None = None) -> dict[str, np.ndarray]:
+        sample = self._as_sample(inputs)
+        proc = {}
+        for spec in self.inputs:
+            proc[spec.id] = processing.apply_chain(sample[spec.id].float(), spec.preprocessing, spec.axis_ids, sample)
+        blocksize = blocksize if blocksize is not None else self.blocksize
+        if blocksize is not None and len(self.inputs) == 1:
+            outs = self._predict_blocked(proc, int(blocksize))
+        else:
+            outs = self._predict_whole(proc)
+        result = {}
+        for spec, y in zip(self.outputs, outs):
+            y = processing.apply_chain(y, spec.postprocessing, spec.axis_ids, {**proc, **{spec.id: y}})
+            result[spec.id] = y.cpu().numpy()
+        return result
+
+    def _pad_to_valid(self, spec: TensorSpec, x: torch.Tensor):
+        pads = {}
+        for i, ax in enumerate(spec.axes):
+            if ax.type == "space":
+                L = x.shape[i]
+                pads[i] = (0, self._valid_len(L, ax.size) - L)
+        return _pad(x, pads, "reflect"), pads
+
+    def _predict_whole(self, proc: dict) -> list[torch.Tensor]:
+        xs, orig = [], {}
+        for spec in self.inputs:
+            x = proc[spec.id]
+            for i, ax in enumerate(spec.axes):
+                orig[(spec.id, ax.id)] = x.shape[i]
+            xp, _ = self._pad_to_valid(spec, x)
+            xs.append(xp)
+        ys = self._forward(xs)
+        outs = []
+        for spec_o, y in zip(self.outputs, ys):
+            sl = []
+            for i, ax in enumerate(spec_o.axes):
+                L = self._out_len(spec_o, ax, orig) if ax.type == "space" else -1
+                sl.append(slice(0, L) if L > 0 and L <= y.shape[i] else slice(None))
+            outs.append(y[tuple(sl)])
+        return outs
+
+    def _predict_blocked(self, proc: dict, n: int) -> list[torch.Tensor]:
+        """Tiled inference: tile = min + n*step per space axis; overlap = output halo."""
+        spec = self.inputs[0]
+        x = proc[spec.id]
+        sp = [i for i, a in enumerate(spec.axes) if a.type == "space"]
+        halo = {}
+        for so in self.outputs:
+            for ax in so.axes:
+                if ax.type == "space":
+                    halo[ax.id] = max(halo.get(ax.id, 0), int(ax.halo))
+        tile, step, hal = {}, {}, {}
+        for i in sp:
+            ax = spec.axes[i]
+            s = ax.size
+            L = x.shape[i]
+            t = (int(s["min"]) + n * int(s["step"])) if isinstance(s, dict) and "min" in s else L
+            t = min(t, self._valid_len(L, s))
+            h = min(halo.get(ax.id, 0), max(0, (t - 1) // 2))
+            tile[i], hal[i] = t, h
+            step[i] = max(1, t - 2 * h)
+        # pad so every tile (plus halo) lies inside the padded image
+        pads, starts = {}, {}
+        for i in sp:
+            L = x.shape[i]
+            ncore = max(1, math.ceil(L / step[i]))
+            total = (ncore - 1) * step[i] + tile[i]
+            pads[i] = (hal[i], max(0, total - L - hal[i]))
+            starts[i] = [k * step[i] for k in range(ncore)]
+        xp = _pad(x, pads, "reflect")
+        coords = list(itertools.product(*[starts[i] for i in sp]))
+        outs = None
+        batch_axis = 0 if spec.axes[0].type == "batch" else None
+        for b0 in range(0, len(coords), self.tile_batch):
+            chunk = coords[b0:b0 + self.tile_batch]
+            tiles = []
+            for c in chunk:
+                sl = [slice(None)] * x.dim()
+                for i, s0 in zip(sp, c):
+                    sl[i] = slice(s0, s0 + tile[i])
+                tiles.append(xp[tuple(sl)])
+            if batch_axis is not None:
+                B = x.shape[0]
+                tb = torch.cat(tiles, 0)
+                ys = self._forward([tb])
+                ys = [list(torch.split(y, B, 0)) for y in ys]
+            else:
+                ys = [[self._forward([t])[0] for t in tiles]]
+            if outs is None:
+                outs = []
+                for so, yl in zip(self.outputs, ys):
+                    shape = list(yl[0].shape)
+                    for i in sp:
+                        shape[i] = x.shape[i]
+                    outs.append(torch.zeros(shape, dtype=torch.float32, device=self.device))
+            for oi, yl in enumerate(ys):
+                for c, y in zip(chunk, yl):
+                    src, dst = [slice(None)] * y.dim(), [slice(None)] * y.dim()
+                    for i, s0 in zip(sp, c):
+                        L = x.shape[i]
+                        d0 = s0
+                        d1 = min(s0 + step[i], L)
+                        if d1 <= d0:
+                            src = None
+                            break
+                        src[i] = slice(hal[i], hal[i] + (d1 - d0))
+                        dst[i] = slice(d0, d1)
+                    if src is not None:
+                        outs[oi][tuple(dst)] = y[tuple(src)]
+        return outs

@@ -129,7 +129,7 @@ def _act_ref(x, x2, scale, shift, relu, inmode):
 
 
 def fused_conv2d_ref(x, pc: PackedConv, x2=None, scale=None, shift=None, relu=False, residual=None,
-                     inmode="none", out_nchw_f32=False, cout_valid=None, act_dtype=torch.bfloat16):
+                     inmode="none", out_nchw_f32=False, cout_valid=None, act_dtype=torch.bfloat16, post_relu=False):
     """PyTorch fp32 reference (and CPU path).  The activated input is rounded to ``act_dtype``
     exactly like the kernel's LDS staging, so GPU-vs-reference differences are accumulation-order only."""
     a = _act_ref(x.float(), x2, scale, shift, relu, inmode)
@@ -144,10 +144,13 @@ def fused_conv2d_ref(x, pc: PackedConv, x2=None, scale=None, shift=None, relu=Fa
         y = y + pc.bias.to(y.device).view(1, -1, 1, 1)
     if out_nchw_f32:
         cv = cout_valid or pc.cout
-        return y[:, :cv].contiguous()
+        y = y[:, :cv].contiguous()
+        return torch.relu(y) if post_relu else y
     y = y.permute(0, 2, 3, 1)
     if residual is not None:
         y = y + residual.float()
+    if post_relu:
+        y = torch.relu(y)
     return y.to(x.dtype).contiguous()
 
 
@@ -178,8 +181,9 @@ def choose_nw(pc: PackedConv, H: int, W: int, inmode: str = "none", has_x2: bool
 
 def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=None, relu=False, residual=None,
                  inmode: str = "none", out_nchw_f32: bool = False, cout_valid: int | None = None,
-                 nw: int | None = None) -> torch.Tensor:
-    """Fused conv on NHWC activations.  ``x`` is [N, Hs, Ws, Cin_pad] bf16 (GPU) or any float (CPU)."""
+                 nw: int | None = None, post_relu: bool = False) -> torch.Tensor:
+    """Fused conv on NHWC activations.  ``x`` is [N, Hs, Ws, Cin_pad] bf16 (GPU) or any float (CPU).
+    ``relu`` applies to the pre-activation input, ``post_relu`` to the output (after bias/residual)."""
     N, Hs, Ws, Cin = x.shape
     if inmode == "up2":
         H, W = Hs * 2, Ws * 2
@@ -189,7 +193,7 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
         H, W = Hs, Ws
     if not x.is_cuda:
         return fused_conv2d_ref(x, pc, x2, scale, shift, relu, residual, inmode, out_nchw_f32, cout_valid,
-                                act_dtype=torch.bfloat16 if x.dtype == torch.bfloat16 else None)
+                                act_dtype=torch.bfloat16 if x.dtype == torch.bfloat16 else None, post_relu=post_relu)
     assert x.dtype == torch.bfloat16 and x.is_contiguous(), "fused_conv2d expects contiguous NHWC bf16"
     assert Cin == pc.cin_pad, f"input channels {Cin} != packed cin {pc.cin_pad}"
     if pc.wp.device != x.device:
@@ -216,7 +220,8 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
             assert shift.shape == (N, Cin)
     _native.call(
         "be_conv2d_nhwc",
-        _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns, int(bool(relu)),
+        _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns,
+        int(bool(relu)) | (2 if post_relu else 0),
         _native.ptr(pc.wp), _native.ptr(pc.bias), _native.ptr(residual), _native.ptr(out),
         N, H, W, Hs, Ws, Cin, cout_store, cout_valid, pc.ks, pc.ck, pc.tco, INMODES[inmode], int(out_nchw_f32),
         int(nw or choose_nw(pc, H, W, inmode, x2 is not None)), _native.stream(x.device),

@@ -42,7 +42,7 @@ struct ConvArgs {
   int N, H, W, Hs, Ws, Cin, Cout, cout_valid;
   int nchunk, KP;
   int pshift_ns;
-  int prelu;
+  int prelu;           // bit 0: ReLU on the (affine) input; bit 1: ReLU on the output (after bias/residual)
   int out_f32_nchw;
   int tiles_x, tiles_y;
   int persist_blocks;  // 0 = auto
@@ -154,7 +154,7 @@ __device__ __forceinline__ void commit_chunk(const ConvArgs& a, const float* shi
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += sh[j];
       }
-      if (a.prelu) {
+      if (a.prelu & 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
       }
@@ -193,7 +193,11 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = co + i;
-          if (c < a.cout_valid) o[(((size_t)n * a.cout_valid + c) * a.H + py) * a.W + px] = vv[i] + (a.bias ? a.bias[c] : 0.f);
+          if (c < a.cout_valid) {
+            float r = vv[i] + (a.bias ? a.bias[c] : 0.f);
+            if (a.prelu & 2) r = fmaxf(r, 0.f);
+            o[(((size_t)n * a.cout_valid + c) * a.H + py) * a.W + px] = r;
+          }
         }
       } else {
         if (co >= a.Cout) continue;
@@ -204,6 +208,9 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
         if (a.res) {
           const u32x2 r = *reinterpret_cast<const u32x2*>(a.res + pix * a.Cout + co);
           v0 += lo_bf(r[0]); v1 += hi_bf(r[0]); v2 += lo_bf(r[1]); v3 += hi_bf(r[1]);
+        }
+        if (a.prelu & 2) {
+          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
         }
         u32x2 st;
         st[0] = pack2bf(v0, v1);
