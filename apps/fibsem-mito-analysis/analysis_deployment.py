@@ -1,0 +1,168 @@
+"""EM mitochondria analysis app.
+
+API parity with the reference ``MitoAnalysisDeployment``
+(apps/fibsem-mito-analysis/analysis_deployment.py:41-286): ``ping`` and ``analyze(image,
+pixel_size_nm, tile_size, overlap)`` returning labels, per-instance properties (area_um2,
+aspect_ratio, eccentricity, centroids), count, shape, model and timing — plus ``analyze_volume``
+for 3-D stacks.
+
+Where the reference is a CPU deployment that ships every 512x512 tile to the model-runner service
+through S3 (3 concurrent round trips), this deployment owns a GPU and runs the tiles in batches
+through the model-runner's in-process pipeline (fused MFMA convs), stitches with the HIP
+gather-blend kernel and post-processes on the GPU; ``model_runner_service`` switches to the
+reference's remote mode (any model-runner service on the hub).
+"""
+from __future__ import annotations
+
+import base64
+import io
+import os
+import time
+from datetime import datetime
+from pathlib import Path
+
+import numpy as np
+from hypha_rpc.utils.schema import schema_method
+from pydantic import Field
+from ray import serve
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 2, "num_gpus": 1, "memory": 8 * 1024 ** 3},
+                  max_ongoing_requests=4)
+class MitoAnalysisDeployment:
+    def __init__(self, model_id: str = "mito-unet2d", model_runner_service: str | None = None,
+                 tile_batch: int = 8, features: list | None = None) -> None:
+        self.start_time = time.time()
+        self.model_id = model_id
+        self.remote_service = model_runner_service
+        self.tile_batch = tile_batch
+        self.features = features or [32, 64, 128, 256]
+        self._pipe = None
+        self._remote = None
+
+    async def async_init(self) -> None:
+        import asyncio
+
+        if self.remote_service:
+            from hypha_rpc import connect_to_server
+
+            server = await connect_to_server({"server_url": os.environ.get("HYPHA_SERVER_URL"),
+                                              "token": os.environ.get("HYPHA_TOKEN")})
+            self._remote = await server.get_service(self.remote_service)
+            return
+        await asyncio.to_thread(self._load_local)
+
+    def _load_local(self) -> None:
+        from bioengine_worker_amd.bioimageio.package import write_unet2d_package
+        from bioengine_worker_amd.bioimageio.runner import PredictionPipeline
+        from bioengine_worker_amd.bioimageio.zoo import list_local_models
+
+        local = list_local_models().get(self.model_id)
+        if local is not None:
+            root = local["dir"]
+        else:
+            root = Path(os.environ.get("HOME", ".")) / "model_zoo" / self.model_id
+            if not (root / "rdf.yaml").exists():
+                write_unet2d_package(root, self.model_id, in_channels=1, out_channels=1, features=tuple(self.features),
+                                     test_shape=(1, 1, 128, 128), torchscript=False)
+        self._pipe = PredictionPipeline(root)
+
+    async def test_deployment(self) -> None:
+        r = await self.analyze(image=(np.random.rand(64, 64) * 255).astype(np.uint8).tolist())
+        assert r["image_shape"] == [64, 64]
+
+    async def check_health(self) -> None:
+        if self._pipe is None and self._remote is None:
+            raise RuntimeError("no inference backend")
+
+    # ------------------------------------------------------------------ inference
+    def _predict_local(self, tiles):
+        out = self._pipe.predict_tensors(tiles)
+        return next(iter(out.values()))
+
+    async def _predict_remote(self, tiles):
+        import torch
+
+        res = []
+        for t in tiles:
+            r = await self._remote.infer(model_id=self.model_id, inputs=t.cpu().numpy())
+            res.append(torch.from_numpy(np.asarray(next(iter(r.values())))).to(tiles.device))
+        return torch.cat(res)
+
+    async def _probability(self, img_norm, tile_size: int, overlap: int):
+        import asyncio
+
+        import torch
+
+        from bioengine_worker_amd.em import mito
+
+        H, W = img_norm.shape
+        if self._remote is not None:
+            # remote path: collect tiles, infer over RPC, blend on the device
+            stride = tile_size - overlap
+            ys, xs = list(range(0, H, stride)), list(range(0, W, stride))
+            padded = torch.nn.functional.pad(img_norm[None, None], (0, max(0, xs[-1] + tile_size - W), 0,
+                                                                    max(0, ys[-1] + tile_size - H)), mode="replicate")[0, 0]
+            t = torch.stack([padded[y:y + tile_size, x:x + tile_size] for y in ys for x in xs])[:, None]
+            probs = await self._predict_remote(t)
+            return mito.infer_tiled(img_norm, lambda tt, it=iter(torch.split(probs, self.tile_batch)): next(it),
+                                    tile_size, overlap, self.tile_batch)
+        if H <= tile_size and W <= tile_size:
+            return await asyncio.to_thread(lambda: self._predict_local(img_norm[None, None])[0])
+        return await asyncio.to_thread(mito.infer_tiled, img_norm, self._predict_local, tile_size, overlap, self.tile_batch)
+
+    # ------------------------------------------------------------------ API
+    @schema_method
+    async def ping(self) -> dict:
+        """Service status."""
+        return {"status": "ok", "model": self.model_id,
+                "model_runner": self.remote_service or "in-process (MI355X fused pipeline)",
+                "uptime_s": round(time.time() - self.start_time, 1), "timestamp": datetime.now().isoformat()}
+
+    @schema_method
+    async def analyze(self, image: list = Field(..., description="2D grayscale EM image (H x W nested list)."),
+                      pixel_size_nm: float = Field(5.0, description="Pixel size in nm."),
+                      tile_size: int = Field(512, description="Tile edge length for tiled inference."),
+                      overlap: int = Field(64, description="Overlap between adjacent tiles.")) -> dict:
+        """Segment mitochondria in a 2D EM image; labels + per-instance morphometrics."""
+        import asyncio
+
+        import torch
+
+        from bioengine_worker_amd.em import mito
+
+        t0 = time.time()
+        arr = np.asarray(image, dtype=np.float32)
+        if arr.ndim != 2:
+            raise ValueError(f"Expected 2-D image, got shape {arr.shape}.")
+        H, W = arr.shape
+        dev = self._pipe.device if self._pipe is not None else torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        img = mito.normalize_percentile(torch.from_numpy(arr).to(dev))
+        prob = await self._probability(img, tile_size, overlap)
+        prob = prob[0] if prob.dim() == 3 else prob
+        if dev.type == "cuda":
+            labels = await asyncio.to_thread(mito.prob_to_instances, prob)
+        else:  # CPU deployments: scipy oracle of the same pipeline
+            labels = await asyncio.to_thread(mito.prob_to_instances_cpu, prob.cpu().numpy())
+        props = await asyncio.to_thread(mito.region_properties, labels, pixel_size_nm, dev)
+        return {"labels": labels.tolist(), "properties": props, "n_mitochondria": int(labels.max()),
+                "image_shape": [H, W], "pixel_size_nm": pixel_size_nm, "model": self.model_id,
+                "processing_time_s": round(time.time() - t0, 2)}
+
+    @schema_method
+    async def analyze_volume(self, volume_npy_b64: str = Field(..., description="3-D stack as base64 .npy bytes (Z,Y,X)."),
+                             pixel_size_nm: float = Field(5.0, description="In-plane pixel size in nm."),
+                             tile_size: int = Field(512, description="Tile edge length."),
+                             overlap: int = Field(64, description="Tile overlap.")) -> dict:
+        """Slice-wise inference + 3-D connected instances (6-connectivity) with per-instance volume."""
+        import torch
+
+        from bioengine_worker_amd.em import volume as vol
+
+        vol_np = np.load(io.BytesIO(base64.b64decode(volume_npy_b64)))
+        dev = self._pipe.device if self._pipe is not None else torch.device("cpu")
+        res = vol.analyze_volume(torch.from_numpy(vol_np.astype(np.float32)).to(dev), self._predict_local, tile_size,
+                                 overlap, self.tile_batch)
+        res["pixel_size_nm"] = pixel_size_nm
+        res["model"] = self.model_id
+        return res

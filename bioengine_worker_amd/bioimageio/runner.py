@@ -156,6 +156,10 @@ class PredictionPipeline:
         return -1
 
     def predict(self, inputs, blocksize: int | None = None) -> dict[str, np.ndarray]:
+        return {k: v.cpu().numpy() for k, v in self.predict_tensors(inputs, blocksize).items()}
+
+    def predict_tensors(self, inputs, blocksize: int | None = None) -> dict[str, torch.Tensor]:
+        """Like :meth:`predict` but keeps the outputs on the device (used by in-process pipelines)."""
         sample = self._as_sample(inputs)
         proc = {}
         for spec in self.inputs:
@@ -168,7 +172,7 @@ class PredictionPipeline:
         result = {}
         for spec, y in zip(self.outputs, outs):
             y = processing.apply_chain(y, spec.postprocessing, spec.axis_ids, {**proc, **{spec.id: y}})
-            result[spec.id] = y.cpu().numpy()
+            result[spec.id] = y
         return result
 
     def _pad_to_valid(self, spec: TensorSpec, x: torch.Tensor):

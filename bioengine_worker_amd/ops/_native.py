@@ -42,7 +42,7 @@ _HIP_SIGS: dict[str, str] = {}
 
 
 def _ctype(ch):
-    return {"p": c_void_p, "i": c_int, "f": c_float, "l": c_int64, "s": c_void_p}[ch]
+    return {"p": c_void_p, "i": c_int, "f": c_float, "l": c_int64, "s": c_void_p, "d": ctypes.c_double}[ch]
 
 
 def _bind(lib, sigs):
@@ -102,8 +102,24 @@ def runtime():
             p = Path(os.environ.get("BE_RUNTIME_LIB", _HERE / "libbe_runtime.so"))
             if not p.exists():
                 raise NativeUnavailable(f"{p} not built (run `python tools/build_native.py`)")
-            _rt = ctypes.CDLL(str(p))
+            lib = ctypes.CDLL(str(p))
+            sig_file = p.parent / "runtime_signatures.json"
+            if sig_file.exists():
+                import json
+
+                _bind(lib, json.loads(sig_file.read_text()))
+            _rt = lib
     return _rt
+
+
+def rt_call(name: str, *args) -> None:
+    """Call a host-runtime (C++) entry point and raise on a non-zero status."""
+    fn = getattr(runtime(), name)
+    if fn.argtypes is not None and len(fn.argtypes) != len(args):
+        raise TypeError(f"{name}: expected {len(fn.argtypes)} args, got {len(args)}")
+    rc = fn(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
 
 
 def hip_available() -> bool:

@@ -40,7 +40,7 @@ __global__ void ccl_init(const unsigned char* __restrict__ mask, int* __restrict
 }
 
 // images are stacked [B, H, W]; labels are linear indices within each image's slab
-__global__ void ccl_merge(const unsigned char* __restrict__ mask, int* __restrict__ Lall, int B, int H, int W) {
+__global__ void ccl_merge(const unsigned char* __restrict__ mask, int* __restrict__ Lall, int B, int H, int W, int conn8) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long HW = (long long)H * W;
   if (gid >= B * HW) return;
@@ -53,8 +53,10 @@ __global__ void ccl_merge(const unsigned char* __restrict__ mask, int* __restric
   if (x > 0 && m[p - 1]) uf_unite(L, p, p - 1);
   if (y > 0) {
     if (m[p - W]) uf_unite(L, p, p - W);
-    if (x > 0 && m[p - W - 1]) uf_unite(L, p, p - W - 1);
-    if (x < W - 1 && m[p - W + 1]) uf_unite(L, p, p - W + 1);
+    if (conn8) {
+      if (x > 0 && m[p - W - 1]) uf_unite(L, p, p - W - 1);
+      if (x < W - 1 && m[p - W + 1]) uf_unite(L, p, p - W + 1);
+    }
   }
 }
 
@@ -64,6 +66,17 @@ __global__ void ccl_compress(int* __restrict__ Lall, int B, long long HW) {
   int* L = Lall + (gid / HW) * HW;
   const int p = (int)(gid % HW);
   if (L[p] >= 0) L[p] = uf_find(L, p);
+}
+
+// 3-D, 6-connectivity (face neighbours); volume < 2^31 voxels (a z-slab per rank)
+__global__ void ccl3d_merge(const unsigned char* __restrict__ m, int* __restrict__ L, int D, int H, int W) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long HW = (long long)H * W;
+  if (p >= D * HW || !m[p]) return;
+  const int z = (int)(p / HW), y = (int)((p / W) % H), x = (int)(p % W);
+  if (x > 0 && m[p - 1]) uf_unite(L, (int)p, (int)(p - 1));
+  if (y > 0 && m[p - W]) uf_unite(L, (int)p, (int)(p - W));
+  if (z > 0 && m[p - HW]) uf_unite(L, (int)p, (int)(p - HW));
 }
 
 // stats [B*HW, 3] int64: area, sum_y, sum_x indexed by root
@@ -147,13 +160,28 @@ inline unsigned nblk(long long n) { return (unsigned)((n + 255) / 256); }
 extern "C" {
 
 // mask uint8 [B, H, W] -> labels int32 [B, H, W] (root linear index within the image, -1 background)
-int be_ccl(const void* mask, int B, int H, int W, int* labels, hipStream_t s) {
+int be_ccl_conn(const void* mask, int B, int H, int W, int conn, int* labels, hipStream_t s) {
   const long long n = (long long)B * H * W;
   if (n == 0) return 0;
   hipLaunchKernelGGL(ccl_init, dim3(nblk(n)), dim3(256), 0, s, (const unsigned char*)mask, labels, n, (long long)H * W);
-  hipLaunchKernelGGL(ccl_merge, dim3(nblk(n)), dim3(256), 0, s, (const unsigned char*)mask, labels, B, H, W);
+  hipLaunchKernelGGL(ccl_merge, dim3(nblk(n)), dim3(256), 0, s, (const unsigned char*)mask, labels, B, H, W,
+                     conn == 8 ? 1 : 0);
   hipLaunchKernelGGL(ccl_compress, dim3(nblk(n)), dim3(256), 0, s, labels, B, (long long)H * W);
   return BE_CHECK_LAUNCH();
+}
+
+int be_ccl3d(const void* mask, int D, int H, int W, int* labels, hipStream_t s) {
+  const long long n = (long long)D * H * W;
+  if (n == 0) return 0;
+  if (n >= (1ll << 31)) return -1;
+  hipLaunchKernelGGL(ccl_init, dim3(nblk(n)), dim3(256), 0, s, (const unsigned char*)mask, labels, n, n);
+  hipLaunchKernelGGL(ccl3d_merge, dim3(nblk(n)), dim3(256), 0, s, (const unsigned char*)mask, labels, D, H, W);
+  hipLaunchKernelGGL(ccl_compress, dim3(nblk(n)), dim3(256), 0, s, labels, 1, n);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_ccl(const void* mask, int B, int H, int W, int* labels, hipStream_t s) {
+  return be_ccl_conn(mask, B, H, W, 8, labels, s);
 }
 
 int be_region_stats(const int* labels, int B, int H, int W, void* stats, hipStream_t s) {

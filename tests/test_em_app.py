@@ -1,0 +1,56 @@
+"""EM mitochondria app through the worker (CPU, small U-Net): analyze + analyze_volume."""
+import asyncio
+import base64
+import io
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.end_to_end
+def test_em_app_e2e(tmp_path, monkeypatch):
+    from bioengine_worker_amd.transport import connect_to_server
+    from bioengine_worker_amd.transport.hub import get_local_hub, reset_local_hubs
+    from bioengine_worker_amd.worker.worker import BioEngineWorker
+
+    monkeypatch.setenv("BIOENGINE_LOCAL_ARTIFACT_PATH", str(ROOT / "apps"))
+    monkeypatch.setenv("BIOENGINE_REPLICA_MODE", "local")
+    monkeypatch.setenv("HOME", str(tmp_path / "home"))
+    monkeypatch.delenv("BIOENGINE_MODEL_ZOO", raising=False)
+    reset_local_hubs()
+
+    async def main():
+        hub = get_local_hub("em")
+        await hub.start_http()
+        tok = hub.issue_token("admin-user", workspace="ws-admin")
+        w = BioEngineWorker(mode="single-machine", workspace_dir=tmp_path / "be", server_url="local://em", token=tok,
+                            client_id="worker1", log_file="off", head_num_cpus=4, head_num_gpus=0,
+                            monitoring_interval_seconds=0.5, data_server_url=None)
+        await w.start(blocking=False)
+        admin = await connect_to_server({"server_url": "local://em", "token": tok})
+        svc = await admin.get_service(w.full_service_id)
+        aid = await svc.deploy_app(artifact_id="em-mito-analyzer", application_id="em", disable_gpu=True,
+                                   application_kwargs={"MitoAnalysisDeployment": {"features": [8, 16, 32]}})
+        assert await w.apps_manager.wait_for(aid, timeout=240) == "RUNNING", \
+            (await svc.get_app_status(application_ids=[aid]))["message"]
+        st = await svc.get_app_status(application_ids=[aid])
+        app = await admin.get_service(st["service_ids"][0]["websocket_service_id"])
+        assert (await app.ping())["status"] == "ok"
+        rng = np.random.default_rng(0)
+        img = (rng.random((300, 340)) * 255).astype(np.uint8)
+        r = await app.analyze(image=img.tolist(), pixel_size_nm=4.0, tile_size=128, overlap=32)
+        assert r["image_shape"] == [300, 340] and len(r["labels"]) == 300
+        assert set(r["properties"]) >= {"label", "area_um2", "aspect_ratio", "eccentricity", "centroid_y", "centroid_x"}
+        assert r["n_mitochondria"] == len(r["properties"]["label"])
+        buf = io.BytesIO()
+        np.save(buf, (rng.random((4, 96, 96)) * 255).astype(np.uint8))
+        rv = await app.analyze_volume(volume_npy_b64=base64.b64encode(buf.getvalue()).decode(), tile_size=64, overlap=16)
+        assert rv["volume_shape"] == [4, 96, 96] and "instances" in rv
+        await svc.stop_worker(blocking=True)
+        await admin.disconnect()
+
+    asyncio.run(asyncio.wait_for(main(), 600))
+    reset_local_hubs()

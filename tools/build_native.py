@@ -101,6 +101,8 @@ def extract_signatures(srcs) -> dict[str, str]:
                         codes.append("s")
                     elif prm.startswith("float") or prm.startswith("const float"):
                         codes.append("f")
+                    elif prm.startswith("double"):
+                        codes.append("d")
                     elif "long long" in prm or "int64_t" in prm:
                         codes.append("l")
                     else:
@@ -146,6 +148,9 @@ def build_runtime(jobs: int) -> Path | None:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("link failed: libbe_runtime.so")
     os.replace(str(out) + ".tmp", out)
+    import json
+
+    (OUT_DIR / "runtime_signatures.json").write_text(json.dumps(extract_signatures(srcs), indent=1, sort_keys=True))
     return out
 
 
