@@ -121,6 +121,54 @@ class NodeCluster:
         self.pending_demands: list = []
         self.log = logger
         self.is_ready = False
+        self.server = None
+        self.controller = None
+
+    def attach(self, server, controller) -> None:
+        """Give the cluster the hub connection (node discovery) and the serving controller
+        (placement on remote nodes; in SLURM mode unplaceable replicas wait for a new node)."""
+        self.server = server
+        self.controller = controller
+        if self.mode == "slurm":
+            controller.wait_for_nodes_s = float(getattr(self.slurm, "node_wait_timeout", 900.0) or 900.0)
+        if self.slurm is not None:
+            self.slurm.controller = controller
+
+    async def discover_nodes(self) -> None:
+        """Track ``bioengine-node`` services (node agents) of this workspace."""
+        if self.server is None or self.controller is None or self.mode == "single-machine":
+            return
+        from ..serve.remote import RemoteNode
+
+        try:
+            infos = await self.server.list_services({"type": "bioengine-node"})
+        except Exception as e:  # noqa: BLE001
+            if self.log:
+                self.log.warning("node discovery failed: %s", e)
+            return
+        seen = set()
+        for info in infos:
+            sid = info["id"]
+            seen.add(sid)
+            node = self.controller.remote_nodes.get(sid)
+            try:
+                if node is None:
+                    svc = await self.server.get_service(sid)
+                    res = await svc.get_resources()
+                    self.controller.add_remote_node(RemoteNode(sid, svc, res))
+                    if self.log:
+                        self.log.info("node joined: %s (%d GPUs)", sid, len(res.get("gpu_ids", [])))
+                else:
+                    node.info.update(await node.service.get_resources())
+                    node.last_seen = time.time()
+            except Exception as e:  # noqa: BLE001
+                if self.log:
+                    self.log.warning("node %s unreachable: %s", sid, e)
+        for nid in list(self.controller.remote_nodes):
+            if nid not in seen:
+                self.controller.remove_remote_node(nid)
+                if self.log:
+                    self.log.info("node left: %s", nid)
 
     async def start(self):
         self.is_ready = True
@@ -151,6 +199,8 @@ class NodeCluster:
     def monitor(self) -> dict:
         nodes = {f"head-{self.hostname}": self.node_state()}
         nodes.update(self.remote_nodes)
+        if self.controller is not None:
+            nodes.update({nid: n.status() for nid, n in self.controller.remote_nodes.items()})
         cluster = {"total_cpu": 0.0, "used_cpu": 0.0, "total_gpu": 0.0, "used_gpu": 0.0}
         for n in nodes.values():
             for k in cluster:
@@ -173,6 +223,7 @@ class NodeCluster:
                 "mode": self.mode, "cluster": last["cluster"], "nodes": last["nodes"]}
 
     async def monitor_cluster(self):
+        await self.discover_nodes()
         self.monitor()
         if self.slurm is not None:
             await self.slurm.check_scaling(self.status)

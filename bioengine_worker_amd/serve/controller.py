@@ -153,14 +153,19 @@ class DeploymentState:
 
     async def add_replica(self):
         cpus, gpus, mem = self.cfg.num_cpus(), self.cfg.num_gpus(), self.cfg.memory()
-        ids = self.ctrl.resources.reserve(cpus, gpus, mem)
+        node, ids = await self.ctrl.place(cpus, gpus, mem, self)
         env = dict((self.cfg.ray_actor_options.get("runtime_env") or {}).get("env_vars") or {})
         cls = self.ctrl._replica_cls(self)
-        if self._use_process():
+        if node is not None:
+            from .remote import RemoteReplica
+
+            r = RemoteReplica(node, self.app, self.name, cls, self.args, self.kwargs, ids, env)
+        elif self._use_process():
             r = ProcessReplica(self.app, self.name, cls, self.args, self.kwargs, ids, env, log_dir=self.ctrl.log_dir)
         else:
             r = LocalReplica(self.app, self.name, cls, self.args, self.kwargs, ids, env)
         r._res = (cpus, gpus, mem, ids)
+        r._pool = node.pool if node is not None else self.ctrl.resources
         self.replicas.append(r)
         try:
             await r.start()
@@ -185,7 +190,7 @@ class DeploymentState:
         if r in self.replicas:
             self.replicas.remove(r)
         cpus, gpus, mem, ids = r._res
-        self.ctrl.resources.release(cpus, gpus, mem, ids)
+        getattr(r, "_pool", self.ctrl.resources).release(cpus, gpus, mem, ids)
         self.history.append({"replica_id": r.tag, "logs": r.logs(200), "error": r.error, "stopped_at": time.time()})
         self.history = self.history[-10:]
 
@@ -330,7 +335,7 @@ class DeploymentState:
         if desired > cur:
             self.status = "UPSCALING"
             for _ in range(desired - cur):
-                if not self.ctrl.resources.can_fit(self.cfg.num_cpus(), self.cfg.num_gpus(), self.cfg.memory()):
+                if not self.ctrl.can_place(self.cfg.num_cpus(), self.cfg.num_gpus(), self.cfg.memory()):
                     self.ctrl.pending_demands.append({"deployment": self.name, "app": self.app,
                                                       "num_cpus": self.cfg.num_cpus(), "num_gpus": self.cfg.num_gpus()})
                     break
@@ -387,9 +392,48 @@ class ServeController:
         self.log_dir = log_dir
         self.tick_s = tick_s
         self.pending_demands: list = []
+        self.remote_nodes: dict = {}          # node_id -> serve.remote.RemoteNode
+        self.wait_for_nodes_s = 0.0           # > 0 (SLURM mode): wait this long for a node to join
         self._task = None
         self._health_last: dict = {}
         self.replica_class_wrappers = []  # callables (DeploymentState, cls) -> cls
+
+    def can_place(self, cpus: float, gpus: float, mem: float) -> bool:
+        return self.resources.can_fit(cpus, gpus, mem) or any(n.pool.can_fit(cpus, gpus, mem)
+                                                               for n in self.remote_nodes.values())
+
+    async def place(self, cpus: float, gpus: float, mem: float, ds=None):
+        """Reserve resources for one replica: the head first, then remote nodes (least loaded).
+        Returns (RemoteNode | None, gpu_ids).  In SLURM mode an unplaceable replica is recorded as
+        pending demand (the autoscaler submits a worker job) and waited for."""
+        deadline = time.time() + self.wait_for_nodes_s
+        demand = None
+        while True:
+            if self.resources.can_fit(cpus, gpus, mem):
+                if demand in self.pending_demands:
+                    self.pending_demands.remove(demand)
+                return None, self.resources.reserve(cpus, gpus, mem)
+            fits = [n for n in self.remote_nodes.values() if n.pool.can_fit(cpus, gpus, mem)]
+            if fits:
+                n = min(fits, key=lambda n: (n.pool.used_gpu, n.pool.used_cpu))
+                if demand in self.pending_demands:
+                    self.pending_demands.remove(demand)
+                return n, n.pool.reserve(cpus, gpus, mem)
+            if time.time() >= deadline:
+                if demand in self.pending_demands:
+                    self.pending_demands.remove(demand)
+                return None, self.resources.reserve(cpus, gpus, mem)  # raises with the usual message
+            if demand is None:
+                demand = {"deployment": getattr(ds, "name", "?"), "app": getattr(ds, "app", "?"), "num_cpus": cpus,
+                          "num_gpus": gpus, "since": time.time()}
+                self.pending_demands.append(demand)
+            await asyncio.sleep(0.5)
+
+    def add_remote_node(self, node) -> None:
+        self.remote_nodes[node.node_id] = node
+
+    def remove_remote_node(self, node_id: str) -> None:
+        self.remote_nodes.pop(node_id, None)
 
     def _replica_cls(self, ds: DeploymentState):
         cls = ds.cls

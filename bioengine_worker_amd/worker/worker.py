@@ -52,7 +52,7 @@ class BioEngineWorker:
                  graceful_shutdown_timeout: float = 60.0, data_server_url: str | None = "auto",
                  log_file: str | None = None, debug: bool = False, head_num_cpus: float | None = None,
                  head_num_gpus: int | None = None, head_memory_in_gb: float | None = None,
-                 slurm_workers=None, **_ignored):
+                 slurm_workers=None, slurm_config: dict | None = None, **_ignored):
         self.mode = mode
         self.workspace_dir = Path(workspace_dir).expanduser().resolve()
         self.workspace_dir.mkdir(parents=True, exist_ok=True)
@@ -73,6 +73,11 @@ class BioEngineWorker:
         self.graceful_shutdown_timeout = graceful_shutdown_timeout
         self.data_server_url_param = data_server_url
         self.data_server_url: str | None = None
+        if slurm_workers is None and mode == "slurm":
+            from ..cluster.slurm import SlurmWorkers
+
+            slurm_workers = SlurmWorkers(server_url, self._token, self.workspace_dir, logger=self.log,
+                                         **(slurm_config or {}))
         self.cluster = NodeCluster(mode, head_num_cpus, head_num_gpus, head_memory_in_gb, slurm_workers=slurm_workers,
                                    logger=self.log)
         self.controller = ServeController(resources=self.cluster.resources,
@@ -116,6 +121,20 @@ class BioEngineWorker:
         self._admin_context = create_context(uid, email)
         self.full_service_id = f"{self.workspace}/{self.client_id}:{self.service_id}"
 
+    async def route_call(self, payload: bytes, context: dict | None = None) -> bytes:
+        """Node agents route DeploymentHandle calls of their replicas through the head (admin only)."""
+        import cloudpickle
+
+        from ..utils.permissions import check_permissions
+
+        check_permissions(context, self.admin_users, "route deployment calls")
+        app, dep, method, args, kwargs, model_id = cloudpickle.loads(payload)
+        try:
+            val = await self.controller.call(app, dep, method, args, kwargs, model_id)
+            return cloudpickle.dumps((True, val))
+        except BaseException as e:  # noqa: BLE001
+            return cloudpickle.dumps((False, e))
+
     async def _register_service(self):
         desc = {"slurm": "Manages BioEngine Apps and Datasets on a HPC system with SLURM autoscaling.",
                 "single-machine": "Manages BioEngine Apps and Datasets on a single machine (native MI355X runtime).",
@@ -128,6 +147,7 @@ class BioEngineWorker:
             "get_app_manifest": self.apps_manager.get_app_manifest, "delete_app": self.apps_manager.delete_app,
             "deploy_app": self.apps_manager.deploy_app, "stop_app": self.apps_manager.stop_app,
             "stop_all_apps": self.apps_manager.stop_all_apps, "get_app_status": self.apps_manager.get_app_status,
+            "route_call": self.route_call,
         }
         info = await self.server.register_service({
             "id": self.service_id, "name": self.worker_name, "type": "bioengine-worker", "description": desc,
@@ -149,6 +169,7 @@ class BioEngineWorker:
         self.start_time = time.time()
         await self.cluster.start()
         await self._connect()
+        self.cluster.attach(self.server, self.controller)
         await self._discover_data_server()
         await self.apps_manager.complete_initialization(self.server, self.admin_users, self.full_service_id,
                                                         self.server_url, self._token)
@@ -216,17 +237,24 @@ class BioEngineWorker:
                                    timeout=self.graceful_shutdown_timeout)
         except Exception as e:  # noqa: BLE001
             self.log.error(f"stopping apps during cleanup failed: {e}")
-        try:
-            if self.server is not None:
-                try:
-                    await self.server.unregister_service(self.service_id)
-                except Exception:
-                    pass
-                await self.server.disconnect()
-        except Exception:
-            pass
-        await self.cluster.stop()
+        await self.cluster.stop()  # SLURM nodes are shut down through the hub: before disconnecting
         await self.controller.shutdown()
+        if self.server is not None:
+            try:
+                await self.server.unregister_service(self.service_id)
+            except Exception:  # noqa: BLE001
+                pass
+            server = self.server
+
+            async def _disconnect():
+                # deferred so that a stop_worker(blocking=True) RPC can still deliver its reply
+                await asyncio.sleep(0.25)
+                try:
+                    await server.disconnect()
+                except Exception:  # noqa: BLE001
+                    pass
+
+            self._disconnect_task = asyncio.ensure_future(_disconnect())
         self.is_ready.clear()
 
     async def _stop(self, blocking: bool = False):
