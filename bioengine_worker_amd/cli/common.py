@@ -36,8 +36,22 @@ def fail(msg: str, hint: str = "") -> None:
     sys.exit(1)
 
 
+_OPEN: list = []
+
+
 def run(coro):
-    return asyncio.run(coro)
+    """Run a command coroutine and close every hub connection it opened in the same loop."""
+    async def wrapped():
+        try:
+            return await coro
+        finally:
+            while _OPEN:
+                srv = _OPEN.pop()
+                try:
+                    await srv.disconnect()
+                except Exception:  # noqa: BLE001
+                    pass
+    return asyncio.run(wrapped())
 
 
 def as_async(f):
@@ -73,7 +87,9 @@ async def connect(url: str, tok: str | None):
     cfg = {"server_url": url}
     if tok:
         cfg["token"] = tok
-    return await connect_to_server(cfg)
+    srv = await connect_to_server(cfg)
+    _OPEN.append(srv)
+    return srv
 
 
 async def get_service(url: str, service_id: str, tok: str | None):
