@@ -76,6 +76,17 @@ def bench_infer(args, world, rank, dev):
     dt = _max_over_ranks(dt, world)
     extra = {"masks_per_image": float(masks.amax(dim=(1, 2)).float().mean().item()),
              "fg_fraction": float((flows[:, 2] > 0).float().mean().item())}
+    if getattr(args, "trace", None) and rank == 0:  # outside the timed region
+        from bioengine_worker_amd.profiling import trace
+
+        trace.clear()
+        trace.enable(True)
+        with trace.request("bench.step", images=args.batch):
+            runner.eval(imgs, p)
+        torch.cuda.synchronize()
+        trace.export(args.trace)
+        extra["trace_summary"] = trace.summary()
+        trace.enable(False)
     return dt, runner, imgs, p, extra
 
 
@@ -165,6 +176,8 @@ def main():
     ap.add_argument("--train-batch", type=int, default=8, help="256x256 crops per step per GPU")
     ap.add_argument("--train-steps", type=int, default=10)
     ap.add_argument("--no-extras", action="store_true", help="skip latency / train / reference-algorithm extras")
+    ap.add_argument("--trace", default=None, metavar="PATH",
+                    help="after the timed steps, run one more traced step and write a Chrome trace (rank 0)")
     args = ap.parse_args()
 
     world, rank, local = _dist_setup(args.gpus)

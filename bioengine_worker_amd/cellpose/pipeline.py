@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from ..models.cpnet import CPnet, CPnetEngine
+from ..profiling import trace
 from . import reference as ref
 
 
@@ -84,9 +85,12 @@ class CellposeRunner:
         if self.device.type == "cuda":
             if p.tile:
                 plan = self._plan(H, W, p)
-                tiles = plan.gather(x, self.cin_pad)
-                yt, st = self.engine(tiles)
-                y = plan.blend(yt, B)
+                with trace.span("cellpose.tiles_gather", cuda=True, tiles=B * plan.nt):
+                    tiles = plan.gather(x, self.cin_pad)
+                with trace.span("cellpose.cpnet", cuda=True, tiles=B * plan.nt):
+                    yt, st = self.engine(tiles)
+                with trace.span("cellpose.blend", cuda=True):
+                    y = plan.blend(yt, B)
                 style = st.view(B, plan.nt, -1).sum(1)
             else:
                 Hp, Wp = math.ceil(H / 8) * 8, math.ceil(W / 8) * 8
@@ -127,7 +131,8 @@ class CellposeRunner:
         x = as_batch(images, self.nchan).to(self.device)
         B, C, H, W = x.shape
         if p.normalize:
-            x = self._normalize(x)
+            with trace.span("cellpose.normalize99", cuda=True, images=B):
+                x = self._normalize(x)
         rescale = 1.0
         if p.diameter is not None and p.diameter > 0:
             rescale = self.diam_mean / float(p.diameter)
@@ -140,7 +145,8 @@ class CellposeRunner:
             y, style = self.run_net(x, p)
         if not p.compute_masks:
             return None, y, style
-        masks = self.compute_masks(y, p, rescale)
+        with trace.span("cellpose.masks", cuda=True, images=B):
+            masks = self.compute_masks(y, p, rescale)
         return masks, y, style
 
     def _normalize(self, x):

@@ -269,11 +269,15 @@ class DeploymentState:
         return await w.fut
 
     async def call(self, method, args, kwargs, model_id=""):
-        r = await self.acquire()
+        from ..profiling import trace
+
+        with trace.span("router.admission", cat="router", deployment=self.name):
+            r = await self.acquire()
         t0 = time.perf_counter()
         try:
             r.ongoing -= 1  # replica.call() tracks its own in-flight count
-            return await r.call(method, args, kwargs, model_id)
+            with trace.span(f"replica.{method}", cat="replica", deployment=self.name, replica=r.tag):
+                return await r.call(method, args, kwargs, model_id)
         finally:
             self.requests_total += 1
             self.latency.append(time.perf_counter() - t0)

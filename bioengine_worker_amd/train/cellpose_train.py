@@ -104,14 +104,21 @@ class CellposeTrainer:
 
     def step(self, imgs: torch.Tensor, lbls: torch.Tensor, rescale=None) -> torch.Tensor:
         """One optimisation step on a batch of (full-size) training images + [cellprob, flowY, flowX] labels."""
-        x, lbl = self.augment(imgs, lbls, rescale)
+        from ..profiling import trace
+
+        with trace.span("train.augment", cuda=True):
+            x, lbl = self.augment(imgs, lbls, rescale)
         self.fp.zero_grad()
-        loss = self.forward_loss(x, lbl)
-        loss.backward()
-        gscale = self.ar.finish()
+        with trace.span("train.forward_loss", cuda=True):
+            loss = self.forward_loss(x, lbl)
+        with trace.span("train.backward", cuda=True):
+            loss.backward()
+        with trace.span("train.grad_allreduce_finish", cuda=True):
+            gscale = self.ar.finish()
         self.step_count += 1
-        train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
-                              weight_decay=self.cfg.weight_decay, grad_scale=gscale)
+        with trace.span("train.adamw", cuda=True):
+            train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
+                                  weight_decay=self.cfg.weight_decay, grad_scale=gscale)
         return loss.detach()
 
     @torch.no_grad()
