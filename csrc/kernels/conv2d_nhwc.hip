@@ -23,8 +23,17 @@
 //  * K ordering inside a chunk is tap-major / channel-minor (k = tap*CK + c), so a 16-byte
 //    B fragment is 8 contiguous channels of one shifted pixel; small-Cin layers (Cin=8) pack 4
 //    taps into one 32-deep MFMA step instead of padding channels to 32.
-//  * pixel stride in LDS is padded by 16 B to break the power-of-two bank pattern of ds_read_b128.
+//  * LDS layouts are bank-conflict-free for ds_read_b128 (lane groups {0-3,12-15,20-27},
+//    {4-11,16-19,28-31}, ...): rows (pixels / output channels) are 64 B (or 64 B mod 256 B) apart
+//    unpadded and the 16-byte K chunks are XOR-swizzled by bit 2 of the row index
+//    (chunk ^ 2*((row>>2)&1)), so every 16-lane group hits 16 distinct 4-bank slots for any
+//    halo shift (dy, dx).  The padded layout of the previous version measured ~4 conflict cycles
+//    per LDS instruction (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS, profiles/conv_pmc_r1.csv).
 #include "common.h"
+
+#ifndef CONV_SCHED_BARRIER
+#define CONV_SCHED_BARRIER 0
+#endif
 
 namespace {
 
@@ -54,25 +63,46 @@ struct Cfg {
   static constexpr int TH = 2 * NW;
   static constexpr int HH = TH + KS - 1;
   static constexpr int HW_ = TW + KS - 1;
-  static constexpr int PSTR = CK + 8;
+  static constexpr bool HSWZ = (CK == 32);  // 4 chunks per pixel -> swizzled, unpadded
+  static constexpr int PSTR = HSWZ ? CK : CK + 8;
   static constexpr int KSTEPS = (KS * KS * CK + 31) / 32;
   static constexpr int KPL = KSTEPS * 32;
-  static constexpr int WSTR = KPL + 8;
+  static constexpr int WSTR = KPL;  // KPL/2 dwords == 16 or 48 (mod 64) for every (KS, CK) used
   static constexpr int CG = CK / 8;
   static constexpr int NCT = TCO / 16;
   static constexpr int HU = HH * HW_ * CG;
   static constexpr int HUPT = (HU + NT - 1) / NT;
   static constexpr int WU = TCO * KPL / 8;
   static constexpr int WUPT = (WU + NT - 1) / NT;
+  static_assert(NT % CG == 0, "a thread's halo channel group must not change across units");
+  static_assert((KPL / 2) % 64 == 16 || (KPL / 2) % 64 == 48, "weight rows must be 64 B apart mod 256 B");
   static constexpr size_t LDS = (size_t)(HH * HW_ * PSTR + TCO * WSTR) * sizeof(bf16_t);
 };
+
+template <typename C>
+__device__ __forceinline__ int hoff(int pix, int cg) {
+  return pix * C::PSTR + (C::HSWZ ? (cg ^ (((pix >> 2) & 1) << 1)) : cg) * 8;
+}
+__device__ __forceinline__ int woff(int wstr, int r, int kc) { return r * wstr + (kc ^ (((r >> 2) & 1) << 1)) * 8; }
 
 // Issue the global loads of one Cin chunk into registers (halo raw values + packed weights).
 template <typename C, int KS, int INMODE, bool X2>
 __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, int tx0, int co0, int ch, int tid,
                                             u32x4 (&hraw)[C::HUPT], u32x4 (&h2raw)[X2 ? C::HUPT : 1],
-                                            u32x4 (&wraw)[C::WUPT], bool with_weights) {
+                                            u32x4 (&wraw)[C::WUPT], float4 (&aff)[4], bool with_weights) {
   const int c0 = ch * (C::CG * 8);
+  {  // this thread's 8 channels are the same for every halo unit (NT % CG == 0): prefetch the affine
+    const int c = c0 + (tid % C::CG) * 8;
+    if (a.pscale) {
+      aff[0] = *reinterpret_cast<const float4*>(a.pscale + c);
+      aff[1] = *reinterpret_cast<const float4*>(a.pscale + c + 4);
+    }
+    if (a.pshift) {
+      const float* sr = a.pshift + (size_t)n * a.pshift_ns + c;
+      aff[2] = *reinterpret_cast<const float4*>(sr);
+      aff[3] = *reinterpret_cast<const float4*>(sr + 4);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < C::HUPT; ++i) {
     const int u = tid + i * C::NT;
@@ -119,11 +149,12 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
 
 // Apply the pre-activation to the staged registers and write the chunk into LDS.
 template <typename C, int KS, bool X2>
-__device__ __forceinline__ void commit_chunk(const ConvArgs& a, const float* shift_row, int ty0, int tx0, int ch, int tid,
+__device__ __forceinline__ void commit_chunk(const ConvArgs& a, int ty0, int tx0, int tid,
                                              const u32x4 (&hraw)[C::HUPT], const u32x4 (&h2raw)[X2 ? C::HUPT : 1],
-                                             const u32x4 (&wraw)[C::WUPT], bf16_t* hl, bf16_t* wl,
+                                             const u32x4 (&wraw)[C::WUPT], const float4 (&aff)[4], bf16_t* hl, bf16_t* wl,
                                              bool with_weights) {
-  const int c0 = ch * (C::CG * 8);
+  const float sc[8] = {aff[0].x, aff[0].y, aff[0].z, aff[0].w, aff[1].x, aff[1].y, aff[1].z, aff[1].w};
+  const float sh[8] = {aff[2].x, aff[2].y, aff[2].z, aff[2].w, aff[3].x, aff[3].y, aff[3].z, aff[3].w};
 #pragma unroll
   for (int i = 0; i < C::HUPT; ++i) {
     const int u = tid + i * C::NT;
@@ -132,7 +163,6 @@ __device__ __forceinline__ void commit_chunk(const ConvArgs& a, const float* shi
     const int gy = ty0 + pix / C::HW_ - KS / 2, gx = tx0 + pix % C::HW_ - KS / 2;
     u32x4 packed = (u32x4){0u, 0u, 0u, 0u};
     if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {  // conv zero-padding applies AFTER the activation
-      const int c = c0 + cg * 8;
       float v[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(hraw[i][j]); v[2 * j + 1] = hi_bf(hraw[i][j]); }
@@ -140,20 +170,8 @@ __device__ __forceinline__ void commit_chunk(const ConvArgs& a, const float* shi
 #pragma unroll
         for (int j = 0; j < 4; ++j) { v[2 * j] += lo_bf(h2raw[i][j]); v[2 * j + 1] += hi_bf(h2raw[i][j]); }
       }
-      if (a.pscale) {
-        const float4 s0 = *reinterpret_cast<const float4*>(a.pscale + c);
-        const float4 s1 = *reinterpret_cast<const float4*>(a.pscale + c + 4);
-        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= sc[j];
-      }
-      if (shift_row) {
-        const float4 t0 = *reinterpret_cast<const float4*>(shift_row + c);
-        const float4 t1 = *reinterpret_cast<const float4*>(shift_row + c + 4);
-        const float sh[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] += sh[j];
-      }
+      for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
       if (a.prelu & 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
@@ -161,7 +179,7 @@ __device__ __forceinline__ void commit_chunk(const ConvArgs& a, const float* shi
 #pragma unroll
       for (int j = 0; j < 4; ++j) packed[j] = pack2bf(v[2 * j], v[2 * j + 1]);
     }
-    *reinterpret_cast<u32x4*>(hl + pix * C::PSTR + cg * 8) = packed;
+    *reinterpret_cast<u32x4*>(hl + hoff<C>(pix, cg)) = packed;
   }
   if (!with_weights) return;
 #pragma unroll
@@ -169,14 +187,112 @@ __device__ __forceinline__ void commit_chunk(const ConvArgs& a, const float* shi
     const int u = tid + i * C::NT;
     if (u < C::WU) {
       const int r = u / (C::KPL / 8), k8 = u % (C::KPL / 8);
-      *reinterpret_cast<u32x4*>(wl + r * C::WSTR + k8 * 8) = wraw[i];
+      *reinterpret_cast<u32x4*>(wl + woff(C::WSTR, r, k8)) = wraw[i];
     }
   }
 }
 
+// K loop of one staged chunk.  Fragments of step ks+1 are read while the MFMAs of step ks run
+// (explicit register double buffer); the scheduling barrier keeps the compiler from hoisting every
+// step's ds_reads to the top, which cost ~100 VGPRs (and the occupancy) in the fully unrolled loop.
+template <typename C, int KS>
+__device__ __forceinline__ void load_frags(int ks, const bf16_t* hl, const bf16_t* wl, int wave, int lrow, int kq,
+                                           bf16x8 (&af)[C::NCT], bf16x8 (&bfr)[4]) {
+  const int g = ks * 4 + kq;
+  int tap = g / C::CG;
+  const int cg = g % C::CG;
+  if (tap >= KS * KS) tap = 0;  // zero-weight K padding: read any finite data
+  const int dy = tap / KS, dx = tap % KS;
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct)
+    af[ct] = *reinterpret_cast<const bf16x8*>(wl + woff(C::WSTR, ct * 16 + lrow, ks * 4 + kq));
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int py = 2 * wave + (pt >> 1);
+    const int px = (pt & 1) * 16 + lrow;
+    bfr[pt] = *reinterpret_cast<const bf16x8*>(hl + hoff<C>((py + dy) * C::HW_ + (px + dx), cg));
+  }
+}
+
+template <typename C, int KS>
+__device__ __forceinline__ void mma_chunk(f32x4 (&acc)[C::NCT][4], const bf16_t* hl, const bf16_t* wl, int wave,
+                                          int lrow, int kq) {
+  bf16x8 af[2][C::NCT], bfr[2][4];
+  load_frags<C, KS>(0, hl, wl, wave, lrow, kq, af[0], bfr[0]);
+#pragma unroll
+  for (int ks = 0; ks < C::KSTEPS; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < C::KSTEPS) load_frags<C, KS>(ks + 1, hl, wl, wave, lrow, kq, af[cur ^ 1], bfr[cur ^ 1]);
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct)
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+        acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bfr[cur][pt], acc[ct][pt], 0, 0, 0);
+#if CONV_SCHED_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+}
+
 template <typename C>
-__device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT][4], int n, int ty0, int tx0, int co0,
-                                         int wave, int lrow, int kq) {
+__device__ __forceinline__ void load_bias(const ConvArgs& a, int co0, int kq, float4 (&bias)[C::NCT]) {
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct) {
+    const int co = co0 + ct * 16 + kq * 4;
+    bias[ct] = (a.bias && !a.out_f32_nchw && co < a.Cout) ? *reinterpret_cast<const float4*>(a.bias + co)
+                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// All global loads (residual) are issued before the first store: out may alias nothing, but the
+// compiler cannot know that, and a load->wait->store chain per fragment serialises 8-16 memory
+// latencies per tile (measured: ~45% of wave cycles in SQ_WAIT_ANY before this ordering).
+template <typename C>
+__device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT][4], const float4 (&bias)[C::NCT],
+                                         int n, int ty0, int tx0, int co0, int wave, int lrow, int kq) {
+  if (a.out_f32_nchw) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int py = ty0 + 2 * wave + (pt >> 1);
+      const int px = tx0 + (pt & 1) * 16 + lrow;
+      if (py >= a.H || px >= a.W) continue;
+      float* o = reinterpret_cast<float*>(a.out);
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = co0 + ct * 16 + kq * 4 + i;
+          if (c < a.cout_valid) {
+            float r = acc[ct][pt][i] + (a.bias ? a.bias[c] : 0.f);
+            if (a.prelu & 2) r = fmaxf(r, 0.f);
+            o[(((size_t)n * a.cout_valid + c) * a.H + py) * a.W + px] = r;
+          }
+        }
+      }
+    }
+    return;
+  }
+  u32x2 rv[4][C::NCT];
+  if (a.res) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int py = ty0 + 2 * wave + (pt >> 1);
+      const int px = tx0 + (pt & 1) * 16 + lrow;
+      const bool ok = py < a.H && px < a.W;
+      const size_t pix = ((size_t)n * a.H + py) * a.W + px;
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) {
+        const int co = co0 + ct * 16 + kq * 4;
+        rv[pt][ct] = (ok && co < a.Cout) ? *reinterpret_cast<const u32x2*>(a.res + pix * a.Cout + co) : (u32x2){0u, 0u};
+      }
+    }
+  } else {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) rv[pt][ct] = (u32x2){0u, 0u};
+  }
+  const bool post = a.prelu & 2;
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt) {
     const int py = ty0 + 2 * wave + (pt >> 1);
@@ -186,37 +302,18 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
 #pragma unroll
     for (int ct = 0; ct < C::NCT; ++ct) {
       const int co = co0 + ct * 16 + kq * 4;
-      float v0 = acc[ct][pt][0], v1 = acc[ct][pt][1], v2 = acc[ct][pt][2], v3 = acc[ct][pt][3];
-      if (a.out_f32_nchw) {
-        float* o = reinterpret_cast<float*>(a.out);
-        const float vv[4] = {v0, v1, v2, v3};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = co + i;
-          if (c < a.cout_valid) {
-            float r = vv[i] + (a.bias ? a.bias[c] : 0.f);
-            if (a.prelu & 2) r = fmaxf(r, 0.f);
-            o[(((size_t)n * a.cout_valid + c) * a.H + py) * a.W + px] = r;
-          }
-        }
-      } else {
-        if (co >= a.Cout) continue;
-        if (a.bias) {
-          const float4 b = *reinterpret_cast<const float4*>(a.bias + co);
-          v0 += b.x; v1 += b.y; v2 += b.z; v3 += b.w;
-        }
-        if (a.res) {
-          const u32x2 r = *reinterpret_cast<const u32x2*>(a.res + pix * a.Cout + co);
-          v0 += lo_bf(r[0]); v1 += hi_bf(r[0]); v2 += lo_bf(r[1]); v3 += hi_bf(r[1]);
-        }
-        if (a.prelu & 2) {
-          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-        }
-        u32x2 st;
-        st[0] = pack2bf(v0, v1);
-        st[1] = pack2bf(v2, v3);
-        *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + pix * a.Cout + co) = st;
+      if (co >= a.Cout) continue;
+      float v0 = acc[ct][pt][0] + bias[ct].x + lo_bf(rv[pt][ct][0]);
+      float v1 = acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]);
+      float v2 = acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]);
+      float v3 = acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]);
+      if (post) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
       }
+      u32x2 st;
+      st[0] = pack2bf(v0, v1);
+      st[1] = pack2bf(v2, v3);
+      *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + pix * a.Cout + co) = st;
     }
   }
 }
@@ -225,7 +322,10 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
 // stages form one software pipeline, so the next tile's halo loads overlap this tile's MFMAs and
 // its epilogue stores.  Single-chunk layers keep their weights resident in LDS for all tiles.
 template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void conv2d_nhwc_persist(ConvArgs a) {
+#ifndef CONV_PERSIST_WPE
+#define CONV_PERSIST_WPE 2
+#endif
+__global__ __launch_bounds__(NW * 64, CONV_PERSIST_WPE) void conv2d_nhwc_persist(ConvArgs a) {
   using C = Cfg<KS, CK, TCO, INMODE, X2, NW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* hl = reinterpret_cast<bf16_t*>(smem);
@@ -257,12 +357,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2d_nhwc_persist(ConvArgs a) {
   u32x4 hraw[C::HUPT];
   u32x4 h2raw[X2 ? C::HUPT : 1];
   u32x4 wraw[C::WUPT];
-  issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, 0, tid, hraw, h2raw, wraw, true);
+  float4 aff[4] = {make_float4(1.f, 1.f, 1.f, 1.f), make_float4(1.f, 1.f, 1.f, 1.f), make_float4(0.f, 0.f, 0.f, 0.f),
+                   make_float4(0.f, 0.f, 0.f, 0.f)};
+  float4 bias[C::NCT];
+  load_bias<C>(a, co0, kq, bias);
+  issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, 0, tid, hraw, h2raw, wraw, aff, true);
   bool first = true;
   for (;;) {
-    const float* shift_row = a.pshift ? a.pshift + (size_t)n * a.pshift_ns : nullptr;
     if (!first) __syncthreads();  // MFMAs of the previous stage finished reading LDS
-    commit_chunk<C, KS, X2>(a, shift_row, ty0, tx0, ch, tid, hraw, h2raw, wraw, hl, wl, first || !resident_w);
+    commit_chunk<C, KS, X2>(a, ty0, tx0, tid, hraw, h2raw, wraw, aff, hl, wl, first || !resident_w);
     __syncthreads();
     first = false;
     // next stage (chunk ch+1 of this tile, or chunk 0 of the next tile)
@@ -276,34 +379,11 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2d_nhwc_persist(ConvArgs a) {
       nn = ntile / tiles_per_img;
       nty0 = ((ntile % tiles_per_img) / a.tiles_x) * C::TH;
       ntx0 = ((ntile % tiles_per_img) % a.tiles_x) * TW;
-      issue_chunk<C, KS, INMODE, X2>(a, nn, nty0, ntx0, co0, nch, tid, hraw, h2raw, wraw, !resident_w);
+      issue_chunk<C, KS, INMODE, X2>(a, nn, nty0, ntx0, co0, nch, tid, hraw, h2raw, wraw, aff, !resident_w);
     }
-#pragma unroll
-    for (int ks = 0; ks < C::KSTEPS; ++ks) {
-      const int g = ks * 4 + kq;
-      int tap = g / C::CG;
-      const int cg = g % C::CG;
-      if (tap >= KS * KS) tap = 0;  // zero-weight K padding: read any finite data
-      const int dy = tap / KS, dx = tap % KS;
-      bf16x8 af[C::NCT];
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct)
-        af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTR + ks * 32 + kq * 8);
-      bf16x8 bfr[4];
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        const int py = 2 * wave + (pt >> 1);
-        const int px = (pt & 1) * 16 + lrow;
-        bfr[pt] = *reinterpret_cast<const bf16x8*>(hl + ((py + dy) * C::HW_ + (px + dx)) * C::PSTR + cg * 8);
-      }
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct)
-#pragma unroll
-        for (int pt = 0; pt < 4; ++pt)
-          acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr[pt], acc[ct][pt], 0, 0, 0);
-    }
+    mma_chunk<C, KS>(acc, hl, wl, wave, lrow, kq);
     if (ch == a.nchunk - 1) {
-      epilogue<C>(a, acc, n, ty0, tx0, co0, wave, lrow, kq);
+      epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq);
 #pragma unroll
       for (int i = 0; i < C::NCT; ++i)
 #pragma unroll
@@ -318,7 +398,10 @@ __global__ __launch_bounds__(NW * 64, 2) void conv2d_nhwc_persist(ConvArgs a) {
 // their registers for accumulators + the chunk prefetch, and their multi-chunk K loop already
 // overlaps loads with MFMAs.
 template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
-__global__ __launch_bounds__(NW * 64, X2 ? 1 : 2) void conv2d_nhwc_kernel(ConvArgs a) {
+#ifndef CONV_KERNEL_WPE
+#define CONV_KERNEL_WPE 2
+#endif
+__global__ __launch_bounds__(NW * 64, X2 ? 1 : CONV_KERNEL_WPE) void conv2d_nhwc_kernel(ConvArgs a) {
   using C = Cfg<KS, CK, TCO, INMODE, X2, NW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* hl = reinterpret_cast<bf16_t*>(smem);
@@ -334,7 +417,6 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : 2) void conv2d_nhwc_kernel(ConvAr
   const int ty0 = ((tile % tiles_per_img) / a.tiles_x) * C::TH;
   const int tx0 = ((tile % tiles_per_img) % a.tiles_x) * TW;
   const int co0 = blockIdx.y * TCO;
-  const float* shift_row = a.pshift ? a.pshift + (size_t)n * a.pshift_ns : nullptr;
   f32x4 acc[C::NCT][4];
 #pragma unroll
   for (int i = 0; i < C::NCT; ++i)
@@ -343,38 +425,20 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : 2) void conv2d_nhwc_kernel(ConvAr
   u32x4 hraw[C::HUPT];
   u32x4 h2raw[X2 ? C::HUPT : 1];
   u32x4 wraw[C::WUPT];
-  issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, 0, tid, hraw, h2raw, wraw, true);
+  float4 aff[4] = {make_float4(1.f, 1.f, 1.f, 1.f), make_float4(1.f, 1.f, 1.f, 1.f), make_float4(0.f, 0.f, 0.f, 0.f),
+                   make_float4(0.f, 0.f, 0.f, 0.f)};
+  issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, 0, tid, hraw, h2raw, wraw, aff, true);
   for (int ch = 0; ch < a.nchunk; ++ch) {
     if (ch > 0) __syncthreads();
-    commit_chunk<C, KS, X2>(a, shift_row, ty0, tx0, ch, tid, hraw, h2raw, wraw, hl, wl, true);
+    commit_chunk<C, KS, X2>(a, ty0, tx0, tid, hraw, h2raw, wraw, aff, hl, wl, true);
     __syncthreads();
-    if (ch + 1 < a.nchunk) issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, ch + 1, tid, hraw, h2raw, wraw, true);
-#pragma unroll
-    for (int ks = 0; ks < C::KSTEPS; ++ks) {
-      const int g = ks * 4 + kq;
-      int tap = g / C::CG;
-      const int cg = g % C::CG;
-      if (tap >= KS * KS) tap = 0;
-      const int dy = tap / KS, dx = tap % KS;
-      bf16x8 af[C::NCT];
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct)
-        af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTR + ks * 32 + kq * 8);
-      bf16x8 bfr[4];
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) {
-        const int py = 2 * wave + (pt >> 1);
-        const int px = (pt & 1) * 16 + lrow;
-        bfr[pt] = *reinterpret_cast<const bf16x8*>(hl + ((py + dy) * C::HW_ + (px + dx)) * C::PSTR + cg * 8);
-      }
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct)
-#pragma unroll
-        for (int pt = 0; pt < 4; ++pt)
-          acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr[pt], acc[ct][pt], 0, 0, 0);
-    }
+    if (ch + 1 < a.nchunk)
+      issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, ch + 1, tid, hraw, h2raw, wraw, aff, true);
+    mma_chunk<C, KS>(acc, hl, wl, wave, lrow, kq);
   }
-  epilogue<C>(a, acc, n, ty0, tx0, co0, wave, lrow, kq);
+  float4 bias[C::NCT];
+  load_bias<C>(a, co0, kq, bias);
+  epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq);
 }
 
 template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
@@ -385,16 +449,17 @@ int launch(ConvArgs a, hipStream_t s) {
   const int tiles = a.N * a.tiles_x * a.tiles_y;
   const int cot = (a.Cout + TCO - 1) / TCO;
   // persistent blocks: ~4 resident workgroups per CU across the cout tiles (256 CUs)
-  if (TCO > 32) {  // non-persistent variant: one block per tile
+  if constexpr (TCO > 32) {  // non-persistent variant: one block per tile
     hipLaunchKernelGGL((conv2d_nhwc_kernel<KS, CK, TCO, INMODE, X2, NW>), dim3(tiles, cot), dim3(C::NT), C::LDS, s, a);
     return BE_CHECK_LAUNCH();
-  }
+  } else {
   int gx = (256 * 4 * (NW == 4 ? 2 : 1)) / cot;
   if (a.persist_blocks > 0) gx = a.persist_blocks;
   if (gx < 1) gx = 1;
   if (gx > tiles) gx = tiles;
   hipLaunchKernelGGL((conv2d_nhwc_persist<KS, CK, TCO, INMODE, X2, NW>), dim3(gx, cot), dim3(C::NT), C::LDS, s, a);
   return BE_CHECK_LAUNCH();
+  }
 }
 
 template <int KS, int CK, int TCO, int INMODE, bool X2>

@@ -111,13 +111,24 @@ def extract_signatures(srcs) -> dict[str, str]:
     return sigs
 
 
-def build_hip(jobs: int) -> Path:
+def build_hip(jobs: int, variant: str | None = None, vsrc: str | None = None, vflags: list[str] | None = None) -> Path:
+    """``variant``: build ``_native/variants/<variant>/libbe_hip.so`` with ``vflags`` added to the
+    sources whose stem contains ``vsrc`` (kernel tuning experiments; load with BE_HIP_LIB=...)."""
     srcs = sorted((CSRC / "kernels").glob("*.hip"))
     if not srcs:
         raise RuntimeError("no HIP sources")
+
+    def flags_for(src):
+        if variant and vsrc and vsrc in src.stem:
+            return HIP_FLAGS + list(vflags or [])
+        return HIP_FLAGS
+
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile([HIPCC], s, HIP_FLAGS), srcs))
+        objs = list(ex.map(lambda s: _compile([HIPCC], s, flags_for(s)), srcs))
     out = OUT_DIR / "libbe_hip.so"
+    if variant:
+        out = OUT_DIR / "variants" / variant / "libbe_hip.so"
+        out.parent.mkdir(parents=True, exist_ok=True)
     tl = _torch_lib_dir()
     link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out) + ".tmp"] + [str(o) for o in objs]
     if tl and Path(tl, "libamdhip64.so").exists():
@@ -130,7 +141,7 @@ def build_hip(jobs: int) -> Path:
     os.replace(str(out) + ".tmp", out)
     import json
 
-    (OUT_DIR / "hip_signatures.json").write_text(json.dumps(extract_signatures(srcs), indent=1, sort_keys=True))
+    (out.parent / "hip_signatures.json").write_text(json.dumps(extract_signatures(srcs), indent=1, sort_keys=True))
     return out
 
 
@@ -158,7 +169,13 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", choices=["hip", "runtime"], default=None)
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--variant", default=None, help="tuning variant name (writes _native/variants/NAME)")
+    ap.add_argument("--vsrc", default=None, help="source stem substring the variant flags apply to")
+    ap.add_argument("--vflags", default="", help="extra hipcc flags of the variant, e.g. '-DCONV_X=1'")
     args = ap.parse_args(argv)
+    if args.variant:
+        print(f"built {build_hip(args.jobs, args.variant, args.vsrc, args.vflags.split())}")
+        return 0
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     if args.only in (None, "runtime"):
         p = build_runtime(args.jobs)
