@@ -20,16 +20,23 @@ typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  // round-to-nearest-even, NaN preserved
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)0x7fc0;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+// fp32 -> bf16 round-to-nearest-even (NaN stays NaN): one v_cvt_pk_bf16_f32 on gfx950 for a pair.
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+// ReLU of two packed bf16 values as one v_pk_max_i16: a negative bf16 (sign bit set) is a negative
+// int16, so max(.., 0) zeroes it and leaves non-negative values bit-exact.
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t w) {
+  const s16x2_t z = {0, 0};
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, w), z));
 }
 
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }

@@ -24,11 +24,13 @@
 //    B fragment is 8 contiguous channels of one shifted pixel; small-Cin layers (Cin=8) pack 4
 //    taps into one 32-deep MFMA step instead of padding channels to 32.
 //  * LDS layouts are bank-conflict-free for ds_read_b128 (lane groups {0-3,12-15,20-27},
-//    {4-11,16-19,28-31}, ...): rows (pixels / output channels) are 64 B (or 64 B mod 256 B) apart
-//    unpadded and the 16-byte K chunks are XOR-swizzled by bit 2 of the row index
-//    (chunk ^ 2*((row>>2)&1)), so every 16-lane group hits 16 distinct 4-bank slots for any
-//    halo shift (dy, dx).  The padded layout of the previous version measured ~4 conflict cycles
-//    per LDS instruction (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS, profiles/conv_pmc_r1.csv).
+//    {4-11,16-19,28-31}, ...; MI355X_MICROARCH.md §LDS): a fragment read is 16 rows (pixels or
+//    output channels) x 4 K-chunks of 16 B, and a row stride of 8 (mod 64) dwords + 16 B chunks
+//    maps every lane group onto 64 distinct banks for ANY row offset (halo shift dy, dx) — so the
+//    layout stays linear (pixel stride CK+16 bf16, weight stride KPL+16) and the compiler folds
+//    the tap offsets into ds_read immediates instead of holding ~50 swizzled addresses in VGPRs.
+//    The previous +8 padding measured ~4 conflict cycles per LDS instruction
+//    (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS; profiles/conv_pmc_swizzled.txt shows 0 after the fix).
 #include "common.h"
 
 #ifndef CONV_SCHED_BARRIER
@@ -63,11 +65,10 @@ struct Cfg {
   static constexpr int TH = 2 * NW;
   static constexpr int HH = TH + KS - 1;
   static constexpr int HW_ = TW + KS - 1;
-  static constexpr bool HSWZ = (CK == 32);  // 4 chunks per pixel -> swizzled, unpadded
-  static constexpr int PSTR = HSWZ ? CK : CK + 8;
+  static constexpr int PSTR = CK == 8 ? 24 : CK + 16;  // dwords/pixel = 8 (mod 64) for CK=32; CK=8: 12
   static constexpr int KSTEPS = (KS * KS * CK + 31) / 32;
   static constexpr int KPL = KSTEPS * 32;
-  static constexpr int WSTR = KPL;  // KPL/2 dwords == 16 or 48 (mod 64) for every (KS, CK) used
+  static constexpr int WSTR = KPL + 16;
   static constexpr int CG = CK / 8;
   static constexpr int NCT = TCO / 16;
   static constexpr int HU = HH * HW_ * CG;
@@ -75,15 +76,14 @@ struct Cfg {
   static constexpr int WU = TCO * KPL / 8;
   static constexpr int WUPT = (WU + NT - 1) / NT;
   static_assert(NT % CG == 0, "a thread's halo channel group must not change across units");
-  static_assert((KPL / 2) % 64 == 16 || (KPL / 2) % 64 == 48, "weight rows must be 64 B apart mod 256 B");
+  static_assert((WSTR / 2) % 16 == 8, "weight row stride must be 8 (mod 16) dwords");
+  static_assert(CK == 8 || (PSTR / 2) % 16 == 8, "pixel stride must be 8 (mod 16) dwords");
   static constexpr size_t LDS = (size_t)(HH * HW_ * PSTR + TCO * WSTR) * sizeof(bf16_t);
 };
 
 template <typename C>
-__device__ __forceinline__ int hoff(int pix, int cg) {
-  return pix * C::PSTR + (C::HSWZ ? (cg ^ (((pix >> 2) & 1) << 1)) : cg) * 8;
-}
-__device__ __forceinline__ int woff(int wstr, int r, int kc) { return r * wstr + (kc ^ (((r >> 2) & 1) << 1)) * 8; }
+__device__ __forceinline__ int hoff(int pix, int cg) { return pix * C::PSTR + cg * 8; }
+__device__ __forceinline__ int woff(int wstr, int r, int kc) { return r * wstr + kc * 8; }
 
 // Issue the global loads of one Cin chunk into registers (halo raw values + packed weights).
 template <typename C, int KS, int INMODE, bool X2>
@@ -172,12 +172,12 @@ __device__ __forceinline__ void commit_chunk(const ConvArgs& a, int ty0, int tx0
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
-      if (a.prelu & 1) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
-      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) packed[j] = pack2bf(v[2 * j], v[2 * j + 1]);
+      if (a.prelu & 1) {  // ReLU commutes with the (monotone, sign-preserving) bf16 rounding
+#pragma unroll
+        for (int j = 0; j < 4; ++j) packed[j] = relu_bf16x2(packed[j]);
+      }
     }
     *reinterpret_cast<u32x4*>(hl + hoff<C>(pix, cg)) = packed;
   }
@@ -307,12 +307,13 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
       float v1 = acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]);
       float v2 = acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]);
       float v3 = acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]);
-      if (post) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
       u32x2 st;
       st[0] = pack2bf(v0, v1);
       st[1] = pack2bf(v2, v3);
+      if (post) {
+        st[0] = relu_bf16x2(st[0]);
+        st[1] = relu_bf16x2(st[1]);
+      }
       *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + pix * a.Cout + co) = st;
     }
   }
