@@ -33,6 +33,11 @@
 //    (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS; profiles/conv_pmc_swizzled.txt shows 0 after the fix).
 #include "common.h"
 
+// Tuning experiments only (tools/build_native.py --variant): 1 = no halo loads, 2 = no output
+// stores, 3 = no MFMAs.  0 in every shipped build.
+#ifndef CONV_EXP
+#define CONV_EXP 0
+#endif
 #ifndef CONV_SCHED_BARRIER
 #define CONV_SCHED_BARRIER 0
 #endif
@@ -78,7 +83,12 @@ struct Cfg {
   static_assert(NT % CG == 0, "a thread's halo channel group must not change across units");
   static_assert((WSTR / 2) % 16 == 8, "weight row stride must be 8 (mod 16) dwords");
   static_assert(CK == 8 || (PSTR / 2) % 16 == 8, "pixel stride must be 8 (mod 16) dwords");
-  static constexpr size_t LDS = (size_t)(HH * HW_ * PSTR + TCO * WSTR) * sizeof(bf16_t);
+  // Output staging (coalesced 16-byte stores): each wave's 2 x 32 pixels x TCO bf16, placed over
+  // the halo region once the MFMAs are done with it.  Chunk swizzle shift: see stage_off().
+  static constexpr int OUT_WAVE = 2 * TW * TCO;  // bf16 elements per wave
+  static constexpr int OSH = TCO == 16 ? 2 : (TCO == 32 ? 1 : 0);
+  static constexpr int HREG = HH * HW_ * PSTR > NW * OUT_WAVE ? HH * HW_ * PSTR : NW * OUT_WAVE;
+  static constexpr size_t LDS = (size_t)(HREG + TCO * WSTR) * sizeof(bf16_t);
 };
 
 template <typename C>
@@ -108,7 +118,7 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
     const int u = tid + i * C::NT;
     u32x4 r = (u32x4){0u, 0u, 0u, 0u};
     u32x4 r2 = (u32x4){0u, 0u, 0u, 0u};
-    if (u < C::HU) {
+    if (CONV_EXP != 1 && u < C::HU) {
       const int pix = u / C::CG, cg = u % C::CG;
       const int gy = ty0 + pix / C::HW_ - KS / 2, gx = tx0 + pix % C::HW_ - KS / 2;
       if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
@@ -133,6 +143,7 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
         if (X2) r2 = *reinterpret_cast<const u32x4*>(a.x2 + (((size_t)n * a.H + gy) * a.W + gx) * a.Cin + c);
       }
     }
+    if (CONV_EXP == 1) r = (u32x4){(uint32_t)u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u};
     hraw[i] = r;
     if (X2) h2raw[i] = r2;
   }
@@ -227,7 +238,11 @@ __device__ __forceinline__ void mma_chunk(f32x4 (&acc)[C::NCT][4], const bf16_t*
     for (int ct = 0; ct < C::NCT; ++ct)
 #pragma unroll
       for (int pt = 0; pt < 4; ++pt)
-        acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bfr[cur][pt], acc[ct][pt], 0, 0, 0);
+        if constexpr (CONV_EXP == 3) {
+          acc[ct][pt][0] += __builtin_bit_cast(float, (int)(af[cur][ct][0] ^ bfr[cur][pt][1]));
+        } else {
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bfr[cur][pt], acc[ct][pt], 0, 0, 0);
+        }
 #if CONV_SCHED_BARRIER
     __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -247,9 +262,19 @@ __device__ __forceinline__ void load_bias(const ConvArgs& a, int co0, int kq, fl
 // All global loads (residual) are issued before the first store: out may alias nothing, but the
 // compiler cannot know that, and a load->wait->store chain per fragment serialises 8-16 memory
 // latencies per tile (measured: ~45% of wave cycles in SQ_WAIT_ANY before this ordering).
+// Staging layout: pixel-major, TCO bf16 per pixel, 16-byte chunks XOR-swizzled by pixel bits so
+// both the 8-byte fragment writes (16 pixels x one channel quad per lane group: 2-way at most) and
+// the 16-byte row reads (conflict-free) spread over the banks.
+template <typename C>
+__device__ __forceinline__ int stage_off(int p, int co) {
+  constexpr int CPP = C::NCT * 2;  // 16-byte chunks per pixel
+  return p * (C::NCT * 16) + ((co >> 3) ^ ((p >> C::OSH) & (CPP - 1))) * 8 + (co & 7);
+}
+
 template <typename C>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT][4], const float4 (&bias)[C::NCT],
-                                         int n, int ty0, int tx0, int co0, int wave, int lrow, int kq) {
+                                         int n, int ty0, int tx0, int co0, int wave, int lrow, int kq,
+                                         bf16_t* stage) {
   if (a.out_f32_nchw) {
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
@@ -293,6 +318,41 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
       for (int ct = 0; ct < C::NCT; ++ct) rv[pt][ct] = (u32x2){0u, 0u};
   }
   const bool post = a.prelu & 2;
+  if (stage != nullptr) {  // Cout % 8 == 0: stage the wave's 2x32xTCO tile, then full-row 16-byte stores
+    bf16_t* ws = stage + wave * C::OUT_WAVE;
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int p = (pt >> 1) * TW + (pt & 1) * 16 + lrow;
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) {
+        const int col = ct * 16 + kq * 4;
+        u32x2 st;
+        st[0] = pack2bf(acc[ct][pt][0] + bias[ct].x + lo_bf(rv[pt][ct][0]), acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]));
+        st[1] = pack2bf(acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]), acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]));
+        if (post) {
+          st[0] = relu_bf16x2(st[0]);
+          st[1] = relu_bf16x2(st[1]);
+        }
+        *reinterpret_cast<u32x2*>(ws + stage_off<C>(p, col)) = st;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int CPP = C::NCT * 2;
+    const int lane = lrow + 16 * kq;
+#pragma unroll
+    for (int it = 0; it < 2 * TW * CPP / 64; ++it) {
+      const int q = it * 64 + lane;
+      const int p = q / CPP, c = q % CPP;
+      const int py = ty0 + 2 * wave + p / TW, px = tx0 + p % TW;
+      const int co = co0 + c * 8;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(ws + stage_off<C>(p, c * 8));
+      if (py < a.H && px < a.W && co < a.Cout)
+        *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(a.out) + (((size_t)n * a.H + py) * a.W + px) * a.Cout + co) = v;
+    }
+    return;
+  }
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt) {
     const int py = ty0 + 2 * wave + (pt >> 1);
@@ -314,7 +374,8 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
         st[0] = relu_bf16x2(st[0]);
         st[1] = relu_bf16x2(st[1]);
       }
-      *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + pix * a.Cout + co) = st;
+      if (CONV_EXP != 2 || a.cout_valid == -12345)
+        *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(a.out) + pix * a.Cout + co) = st;
     }
   }
 }
@@ -330,7 +391,7 @@ __global__ __launch_bounds__(NW * 64, CONV_PERSIST_WPE) void conv2d_nhwc_persist
   using C = Cfg<KS, CK, TCO, INMODE, X2, NW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* hl = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* wl = hl + C::HH * C::HW_ * C::PSTR;
+  bf16_t* wl = hl + C::HREG;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -341,6 +402,7 @@ __global__ __launch_bounds__(NW * 64, CONV_PERSIST_WPE) void conv2d_nhwc_persist
   const int total = a.N * tiles_per_img;
   const int co0 = blockIdx.y * TCO;
   const bool resident_w = a.nchunk == 1;
+  const bool staged = !a.out_f32_nchw && (a.Cout & 7) == 0;
 
   int tile = blockIdx.x;
   if (tile >= total) return;
@@ -384,7 +446,12 @@ __global__ __launch_bounds__(NW * 64, CONV_PERSIST_WPE) void conv2d_nhwc_persist
     }
     mma_chunk<C, KS>(acc, hl, wl, wave, lrow, kq);
     if (ch == a.nchunk - 1) {
-      epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq);
+      bf16_t* stage = nullptr;
+      if (staged) {
+        __syncthreads();  // every wave is done reading the halo the staging area overlays
+        stage = hl;
+      }
+      epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq, stage);
 #pragma unroll
       for (int i = 0; i < C::NCT; ++i)
 #pragma unroll
@@ -406,7 +473,7 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : CONV_KERNEL_WPE) void conv2d_nhwc
   using C = Cfg<KS, CK, TCO, INMODE, X2, NW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* hl = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* wl = hl + C::HH * C::HW_ * C::PSTR;
+  bf16_t* wl = hl + C::HREG;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -439,7 +506,12 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : CONV_KERNEL_WPE) void conv2d_nhwc
   }
   float4 bias[C::NCT];
   load_bias<C>(a, co0, kq, bias);
-  epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq);
+  bf16_t* stage = nullptr;
+  if (!a.out_f32_nchw && (a.Cout & 7) == 0) {
+    __syncthreads();
+    stage = hl;
+  }
+  epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq, stage);
 }
 
 template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
