@@ -135,6 +135,25 @@ def _diffuse_scratch_doubles(ly, lx):
     return 2 * R + (ly + 2 + lx + 2 + 1) // 2 + (R + 7) // 8 + 2
 
 
+#: (LDS bytes, threads) buckets of the one-workgroup-per-mask diffusion: a block reserves only its
+#: bucket's LDS, so small masks run many blocks per CU (one 48 KiB reservation per mask allowed 3).
+DIFFUSE_BUCKETS = ((6 * 1024, 64), (12 * 1024, 128), (24 * 1024, 256), (LDS_DIFFUSE_BYTES, 256))
+
+
+def _diffuse_small(Mc, sj, niter_img, L, st) -> None:
+    B, H, W = Mc.shape
+    w2 = sj[:, 2]
+    need = _diffuse_lds_bytes(w2 & 0xFFFFFFFF, w2 >> 32)
+    lo = 0
+    for cap, threads in DIFFUSE_BUCKETS:
+        sel = (need > lo) & (need <= cap)
+        lo = cap
+        jobs = sj[sel].contiguous()
+        if jobs.shape[0]:
+            _native.call("be_cp_diffuse_nt", _native.ptr(Mc), _native.ptr(jobs), jobs.shape[0], H, W,
+                         _native.ptr(niter_img), _native.ptr(L), cap, threads, st)
+
+
 _TILE_PARAMS: tuple | None = None
 #: "tiled" = multi-workgroup time-blocked diffusion for masks larger than LDS (default);
 #: "block" = one workgroup per mask on a global scratch slab (kept as a cross-check).
@@ -223,8 +242,7 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
     st = _native.stream(dev)
     Mc = M.contiguous()
     if sj.shape[0]:
-        _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(sj), sj.shape[0], H, W, _native.ptr(niter_img),
-                     _native.ptr(scratch), _native.ptr(L), LDS_DIFFUSE_BYTES, st)
+        _diffuse_small(Mc, sj, niter_img, L, st)
     if bj.shape[0]:
         _diffuse_big(Mc, bj, niter_img, scratch, L, st)
     err = None

@@ -41,7 +41,7 @@ struct MaskJob {
 // The heat field spans hundreds of orders of magnitude far from the centre of large masks (T decays
 // like exp(-d^2/t)); cellpose runs it in float64 for that reason and so do we (gfx950 runs fp64 VALU
 // at full vector rate, and this kernel is latency/LDS bound anyway).
-template <bool USE_LDS>
+template <bool USE_LDS, int MT = 256>
 __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs, int H,
                                                      int W, const int* __restrict__ niter_img, double* __restrict__ scratch,
                                                      double* __restrict__ Lout, int* __restrict__ centers_out) {
@@ -163,8 +163,11 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
 // per step, so the core stays exact), and writes the core back.  Rounds are separated by a grid
 // barrier (agent-scope release/acquire counter, bounded spin), so one cooperative launch runs all
 // niter iterations of all big masks across the whole chip instead of one CU per mask.
-constexpr int DT_K = 8;
-constexpr int DT_CORE = 48;
+#ifndef CP_DT_K
+#define CP_DT_K 16
+#endif
+constexpr int DT_K = CP_DT_K;
+constexpr int DT_CORE = 64 - 2 * DT_K;
 constexpr int DT_RG = DT_CORE + 2 * DT_K;  // 64
 constexpr int DT_LDS = 2 * DT_RG * DT_RG * 8 + DT_RG * DT_RG;
 
@@ -397,6 +400,32 @@ int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const
   else
     hipLaunchKernelGGL((diffuse_kernel<false>), dim3(njobs), dim3(MT), 0, s, M, (const MaskJob*)jobs, H, W, niter_img, scratch,
                        Lout, nullptr);
+  return BE_CHECK_LAUNCH();
+}
+
+// LDS variant with a block size matched to the masks (the launcher buckets small masks by their
+// LDS need, so a 20x20 mask no longer reserves the 48 KiB of the largest one — 3 blocks/CU — and
+// runs one wave instead of four mostly idle ones).
+int be_cp_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, double* Lout,
+                     int lds_bytes, int threads, hipStream_t s) {
+  if (njobs == 0) return 0;
+  if (lds_bytes <= 0) return -1;
+  switch (threads) {
+    case 64:
+      hipLaunchKernelGGL((diffuse_kernel<true, 64>), dim3(njobs), dim3(64), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
+                         niter_img, nullptr, Lout, nullptr);
+      break;
+    case 128:
+      hipLaunchKernelGGL((diffuse_kernel<true, 128>), dim3(njobs), dim3(128), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
+                         niter_img, nullptr, Lout, nullptr);
+      break;
+    case 256:
+      hipLaunchKernelGGL((diffuse_kernel<true, 256>), dim3(njobs), dim3(256), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
+                         niter_img, nullptr, Lout, nullptr);
+      break;
+    default:
+      return -2;
+  }
   return BE_CHECK_LAUNCH();
 }
 
