@@ -8,6 +8,8 @@ per-mask job lists).  The semantics are those of :mod:`bioengine_worker_amd.cell
 from __future__ import annotations
 
 import numpy as np
+import os
+
 import torch
 
 from ..ops import _native
@@ -15,7 +17,7 @@ from . import reference as ref
 
 RPAD = 20
 _JOB_BYTES = 32
-LDS_DIFFUSE_BYTES = 48 * 1024
+LDS_DIFFUSE_BYTES = 156 * 1024  # one mask per CU up to ~95 x 95 boxes; larger ones run tiled
 LDS_FILL_BYTES = 32 * 1024
 
 
@@ -137,13 +139,21 @@ def _diffuse_scratch_doubles(ly, lx):
 
 #: (LDS bytes, threads) buckets of the one-workgroup-per-mask diffusion: a block reserves only its
 #: bucket's LDS, so small masks run many blocks per CU (one 48 KiB reservation per mask allowed 3).
-DIFFUSE_BUCKETS = ((6 * 1024, 64), (12 * 1024, 128), (24 * 1024, 256), (LDS_DIFFUSE_BYTES, 256))
+DIFFUSE_BUCKETS = ((6 * 1024, 64), (12 * 1024, 128), (24 * 1024, 256), (48 * 1024, 256), (80 * 1024, 512),
+                   (LDS_DIFFUSE_BYTES, 512))
+
+
+_DEBUG_STATS = os.environ.get("BIOENGINE_MASK_STATS", "0") == "1"
 
 
 def _diffuse_small(Mc, sj, niter_img, L, st) -> None:
     B, H, W = Mc.shape
     w2 = sj[:, 2]
     need = _diffuse_lds_bytes(w2 & 0xFFFFFFFF, w2 >> 32)
+    if _DEBUG_STATS:
+        print(f"[diffuse_small] masks={sj.shape[0]} mean_area_box={float(((w2 & 0xFFFFFFFF) * (w2 >> 32)).float().mean()):.0f} "
+              f"buckets={[int(((need > a) & (need <= b[0])).sum()) for a, b in zip((0,) + tuple(c for c, _ in DIFFUSE_BUCKETS), DIFFUSE_BUCKETS)]}",
+              flush=True)
     lo = 0
     for cap, threads in DIFFUSE_BUCKETS:
         sel = (need > lo) & (need <= cap)
@@ -186,6 +196,9 @@ def _diffuse_big(Mc, bj, niter_img, scratch, L, st) -> None:
     ty = (k // ntx[job]) * core
     tx = (k % ntx[job]) * core
     tiles = torch.stack([job, ty, tx, torch.zeros_like(job)], 1).to(torch.int32).to(Mc.device)
+    if _DEBUG_STATS:
+        print(f"[diffuse_big] masks={bj.shape[0]} tiles={tiles.shape[0]} box_ly={ly.tolist()} box_lx={lx.tolist()} "
+              f"niter={niter_img.tolist()}", flush=True)
     centers = torch.empty(bj.shape[0], dtype=torch.int32, device=Mc.device)
     ws = torch.zeros(4, dtype=torch.int32, device=Mc.device)
     _native.call("be_cp_diffuse_tiled", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], _native.ptr(tiles),

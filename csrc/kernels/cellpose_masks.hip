@@ -423,10 +423,25 @@ int be_cp_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, co
       hipLaunchKernelGGL((diffuse_kernel<true, 256>), dim3(njobs), dim3(256), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
                          niter_img, nullptr, Lout, nullptr);
       break;
+    case 512: {
+      static int attr_set = 0;
+      if (!attr_set) {  // > 64 KiB of dynamic LDS (up to the 160 KiB of a CU) needs the opt-in
+        const hipError_t ae = hipFuncSetAttribute(reinterpret_cast<const void*>(diffuse_kernel<true, 512>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+        if (ae != hipSuccess) fprintf(stderr, "be_cp_diffuse_nt: hipFuncSetAttribute(%d): %s\n", lds_bytes, hipGetErrorString(ae));
+        attr_set = 1;
+      }
+      hipLaunchKernelGGL((diffuse_kernel<true, 512>), dim3(njobs), dim3(512), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
+                         niter_img, nullptr, Lout, nullptr);
+      break;
+    }
     default:
       return -2;
   }
-  return BE_CHECK_LAUNCH();
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    fprintf(stderr, "be_cp_diffuse_nt(njobs=%d, lds=%d, threads=%d): %s\n", njobs, lds_bytes, threads, hipGetErrorString(e));
+  return (int)e;
 }
 
 int be_cp_diffuse_tile_params(int* out3) {

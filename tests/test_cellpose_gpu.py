@@ -30,6 +30,25 @@ def test_masks_to_flows_gpu_matches_reference(gpu):
 
 
 @pytest.mark.gpu
+def test_masks_to_flows_every_lds_bucket(gpu):
+    """One mask per LDS bucket of the one-workgroup path (64/128/256/512-thread blocks, up to
+    ~95 x 95 boxes in a single CU's LDS), each against the numpy oracle."""
+    from bioengine_worker_amd.cellpose import gpu as cg
+
+    M = np.zeros((1, 260, 260), np.int32)
+    yy, xx = np.mgrid[0:260, 0:260]
+    for lab, (cy, cx, r) in enumerate([(12, 12, 8), (40, 40, 12), (80, 30, 17), (40, 100, 24), (130, 60, 30),
+                                       (160, 180, 44)], start=1):
+        # off-grid centres: no mirror symmetry, so no exact-zero gradient ties between fp orders
+        M[0][(yy - cy - 0.37) ** 2 + ((xx - cx - 0.21) * 1.1) ** 2 < r * r] = lab
+    w = cg._diffuse_lds_bytes(torch.tensor([90]), torch.tensor([80]))
+    assert int(w) <= cg.LDS_DIFFUSE_BYTES
+    mu, _, _ = cg.masks_to_flows_gpu(torch.from_numpy(M).to(gpu))
+    mref = ref.masks_to_flows(M[0])
+    assert np.abs(mu[0].cpu().numpy() - mref).max() < 2e-3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["tiled", "block"])
 def test_big_mask_global_scratch_path(gpu, mode, monkeypatch):
     from bioengine_worker_amd.cellpose import gpu as cg
