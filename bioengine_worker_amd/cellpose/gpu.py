@@ -8,6 +8,7 @@ per-mask job lists).  The semantics are those of :mod:`bioengine_worker_amd.cell
 from __future__ import annotations
 
 import numpy as np
+import ctypes
 import os
 
 import torch
@@ -146,22 +147,59 @@ DIFFUSE_BUCKETS = ((6 * 1024, 64), (12 * 1024, 128), (24 * 1024, 256), (48 * 102
 _DEBUG_STATS = os.environ.get("BIOENGINE_MASK_STATS", "0") == "1"
 
 
-def _diffuse_small(Mc, sj, niter_img, L, st) -> None:
-    B, H, W = Mc.shape
+_SIDE_STREAMS: dict = {}
+#: LDS buckets run on their own HIP streams so their launch tails (a few CUs finishing the
+#: largest masks of a bucket) overlap the next bucket instead of idling the rest of the chip.
+N_SIDE_STREAMS = 3
+
+
+def _side_streams(dev):
+    key = (dev.type, dev.index)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = [torch.cuda.Stream(dev) for _ in range(N_SIDE_STREAMS)]
+    return _SIDE_STREAMS[key]
+
+
+def _bucket_small(sj):
+    """Split the one-workgroup diffusion jobs into LDS buckets (host sync happens here, before any
+    diffusion kernel is queued)."""
     w2 = sj[:, 2]
     need = _diffuse_lds_bytes(w2 & 0xFFFFFFFF, w2 >> 32)
     if _DEBUG_STATS:
         print(f"[diffuse_small] masks={sj.shape[0]} mean_area_box={float(((w2 & 0xFFFFFFFF) * (w2 >> 32)).float().mean()):.0f} "
               f"buckets={[int(((need > a) & (need <= b[0])).sum()) for a, b in zip((0,) + tuple(c for c, _ in DIFFUSE_BUCKETS), DIFFUSE_BUCKETS)]}",
               flush=True)
+    out = []
     lo = 0
-    for cap, threads in DIFFUSE_BUCKETS:
-        sel = (need > lo) & (need <= cap)
+    for i, (cap, threads) in enumerate(DIFFUSE_BUCKETS):
+        jobs = sj[(need > lo) & (need <= cap)].contiguous()
         lo = cap
-        jobs = sj[sel].contiguous()
         if jobs.shape[0]:
-            _native.call("be_cp_diffuse_nt", _native.ptr(Mc), _native.ptr(jobs), jobs.shape[0], H, W,
-                         _native.ptr(niter_img), _native.ptr(L), cap, threads, st)
+            out.append((i, cap, threads, jobs))
+    return out[::-1]  # largest masks first: they set the critical path
+
+
+def _diffuse_small(Mc, buckets, niter_img, L, st) -> None:
+    B, H, W = Mc.shape
+    concurrent = Mc.is_cuda and N_SIDE_STREAMS > 0
+    if concurrent:
+        main = torch.cuda.current_stream(Mc.device)
+        sides = _side_streams(Mc.device)
+        for sd in sides:
+            sd.wait_stream(main)
+    for i, cap, threads, jobs in buckets:
+        if concurrent:
+            sd = sides[i % len(sides)]
+            for t in (jobs, Mc, niter_img, L):
+                t.record_stream(sd)
+            sptr = ctypes.c_void_p(sd.cuda_stream)
+        else:
+            sptr = st
+        _native.call("be_cp_diffuse_nt", _native.ptr(Mc), _native.ptr(jobs), jobs.shape[0], H, W,
+                     _native.ptr(niter_img), _native.ptr(L), cap, threads, sptr)
+    if concurrent:
+        for sd in sides:
+            main.wait_stream(sd)
 
 
 _TILE_PARAMS: tuple | None = None
@@ -177,7 +215,7 @@ def _diffuse_big(Mc, bj, niter_img, scratch, L, st) -> None:
     if BIG_MASK_MODE == "block":
         _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], H, W, _native.ptr(niter_img),
                      _native.ptr(scratch), _native.ptr(L), 0, st)
-        return
+        return None
     if _TILE_PARAMS is None:
         import ctypes
 
@@ -204,7 +242,11 @@ def _diffuse_big(Mc, bj, niter_img, scratch, L, st) -> None:
     _native.call("be_cp_diffuse_tiled", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], _native.ptr(tiles),
                  tiles.shape[0], H, W, _native.ptr(niter_img), _native.ptr(scratch), _native.ptr(L),
                  _native.ptr(centers), _native.ptr(ws), st)
-    if int(ws[1].item()) != 0:
+    return ws  # ws[1] != 0 <=> the grid barrier timed out; checked by the caller after queuing the rest
+
+
+def _check_tiled(ws) -> None:
+    if ws is not None and int(ws[1].item()) != 0:
         raise RuntimeError("diffuse_tiled_kernel: grid barrier timed out (workgroups not co-resident)")
 
 
@@ -254,10 +296,12 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
     scratch = torch.empty(max(ssize, 1), dtype=torch.float64, device=dev)
     st = _native.stream(dev)
     Mc = M.contiguous()
-    if sj.shape[0]:
-        _diffuse_small(Mc, sj, niter_img, L, st)
-    if bj.shape[0]:
-        _diffuse_big(Mc, bj, niter_img, scratch, L, st)
+    buckets = _bucket_small(sj) if sj.shape[0] else []
+    ws = None
+    if bj.shape[0]:  # first: its cooperative grid must be co-resident, so it goes in on an idle device
+        ws = _diffuse_big(Mc, bj, niter_img, scratch, L, st)
+    if buckets:
+        _diffuse_small(Mc, buckets, niter_img, L, st)
     err = None
     dpp = None
     bstride = 0
@@ -267,6 +311,7 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
         err = torch.zeros(B, nlab, dtype=torch.float32, device=dev)
     _native.call("be_cp_flow_grad", _native.ptr(Mc), _native.ptr(L), B, H, W, _native.ptr(mu), _native.ptr(dpp),
                  bstride, _native.ptr(err), nlab, st)
+    _check_tiled(ws)
     return mu, err, counts
 
 
