@@ -64,7 +64,8 @@ def bench_infer(args, world, rank, dev):
 
     runner = CellposeRunner(device=dev, seed=0)
     imgs = torch.from_numpy(synthetic_cells(args.batch, 512, 512, nchan=2, seed=rank)).to(dev)
-    p = EvalParams(niter=200, flow_threshold=0.4, cellprob_threshold=0.0, min_size=15)
+    p = EvalParams(niter=200, flow_threshold=0.4, cellprob_threshold=0.0, min_size=15,
+                   pipeline_chunks=getattr(args, "chunks", 1))
     for _ in range(args.warmup):
         masks, _, _ = runner.eval(imgs, p)
     _barrier(world)
@@ -175,6 +176,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="512x512 images per step per GPU")
     ap.add_argument("--train-batch", type=int, default=8, help="256x256 crops per step per GPU")
     ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--chunks", type=int, default=1, help="micro-batches of the two-stream net/mask pipeline")
     ap.add_argument("--no-extras", action="store_true", help="skip latency / train / reference-algorithm extras")
     ap.add_argument("--trace", default=None, metavar="PATH",
                     help="after the timed steps, run one more traced step and write a Chrome trace (rank 0)")

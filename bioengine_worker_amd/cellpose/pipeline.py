@@ -36,6 +36,11 @@ class EvalParams:
     bsize: int = 224
     tile_overlap: float = 0.1
     compute_masks: bool = True
+    #: GPU: split a batch into this many micro-batches and run mask recovery of micro-batch i on a
+    #: second HIP stream while the network runs micro-batch i+1 (the mask stage is a chain of
+    #: latency-bound kernels and host syncs that leaves most CUs idle on its own).
+    pipeline_chunks: int = 1  # measured: 2 -> -9 %, 4 -> -18 % (latency-bound mask stages run once per chunk)
+    pipeline_min_chunk: int = 4
 
 
 def as_batch(images, nchan: int) -> torch.Tensor:
@@ -130,6 +135,13 @@ class CellposeRunner:
             setattr(p, k, v)
         x = as_batch(images, self.nchan).to(self.device)
         B, C, H, W = x.shape
+        nch = min(p.pipeline_chunks, B // max(1, p.pipeline_min_chunk))
+        if self.device.type == "cuda" and p.compute_masks and nch >= 2:
+            return self._eval_pipelined(x, p, nch)
+        return self._eval_one(x, p)
+
+    def _eval_one(self, x, p: EvalParams):
+        B, C, H, W = x.shape
         if p.normalize:
             with trace.span("cellpose.normalize99", cuda=True, images=B):
                 x = self._normalize(x)
@@ -148,6 +160,58 @@ class CellposeRunner:
         with trace.span("cellpose.masks", cuda=True, images=B):
             masks = self.compute_masks(y, p, rescale)
         return masks, y, style
+
+    def _net_stage(self, x, p: EvalParams):
+        B, C, H, W = x.shape
+        if p.normalize:
+            with trace.span("cellpose.normalize99", cuda=True, images=B):
+                x = self._normalize(x)
+        rescale = 1.0
+        if p.diameter is not None and p.diameter > 0:
+            rescale = self.diam_mean / float(p.diameter)
+        if abs(rescale - 1.0) > 1e-3:
+            Hs, Ws = max(8, int(round(H * rescale))), max(8, int(round(W * rescale)))
+            xs = F.interpolate(x, size=(Hs, Ws), mode="bilinear", align_corners=False)
+            y, style = self.run_net(xs, p)
+            y = F.interpolate(y, size=(H, W), mode="bilinear", align_corners=False)
+        else:
+            y, style = self.run_net(x, p)
+        return y, style, rescale
+
+    def _eval_pipelined(self, x, p: EvalParams, nch: int):
+        """Two-stream software pipeline over micro-batches: net(i+1) on the current stream is queued
+        before mask recovery of micro-batch i (which syncs the host on its own stream) starts."""
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_mask_stream", None) is None:
+            self._mask_stream = torch.cuda.Stream(self.device)
+        side = self._mask_stream
+        parts = x.tensor_split(nch)
+        ys, styles, masks = [], [], []
+        pending = None
+
+        def finish(item):
+            y, rescale, ev = item
+            with torch.cuda.stream(side):
+                side.wait_event(ev)
+                y.record_stream(side)
+                with trace.span("cellpose.masks", cuda=True, images=y.shape[0]):
+                    m = self.compute_masks(y, p, rescale)
+            masks.append(m)
+
+        for part in parts:
+            y, style, rescale = self._net_stage(part, p)
+            ys.append(y)
+            styles.append(style)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            if pending is not None:
+                finish(pending)
+            pending = (y, rescale, ev)
+        finish(pending)
+        main.wait_stream(side)
+        for m in masks:
+            m.record_stream(main)
+        return torch.cat(masks), torch.cat(ys), torch.cat(styles)
 
     def _normalize(self, x):
         if self.device.type == "cuda":
