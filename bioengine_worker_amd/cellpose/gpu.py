@@ -147,6 +147,9 @@ DIFFUSE_BUCKETS = ((6 * 1024, 64), (12 * 1024, 128), (24 * 1024, 256), (48 * 102
 _DEBUG_STATS = os.environ.get("BIOENGINE_MASK_STATS", "0") == "1"
 
 
+#: flow-following launch: XCD-ordered + block-compacted (default) or the plain pixel-per-lane one
+FOLLOW_FLOWS_ENTRY = os.environ.get("BIOENGINE_FOLLOW_ENTRY", "be_cp_follow_flows_xcd")
+
 _SIDE_STREAMS: dict = {}
 #: LDS buckets run on their own HIP streams so their launch tails (a few CUs finishing the
 #: largest masks of a bucket) overlap the next bucket instead of idling the rest of the chip.
@@ -370,7 +373,7 @@ def follow_and_label(y: torch.Tensor, niter: int = 200, cellprob_threshold: floa
     Hp, Wp = H + 2 * RPAD, W + 2 * RPAD
     hist = torch.zeros(B, Hp, Wp, dtype=torch.int32, device=dev)
     pos = torch.empty(B, H, W, dtype=torch.int32, device=dev)
-    _native.call("be_cp_follow_flows", _native.ptr(flow2), _native.ptr(fg), _native.ptr(hist), _native.ptr(pos), B, H,
+    _native.call(FOLLOW_FLOWS_ENTRY, _native.ptr(flow2), _native.ptr(fg), _native.ptr(hist), _native.ptr(pos), B, H,
                  W, int(niter), st)
     cap = H * W // 11 + 1
     keys = torch.full((B, cap), torch.iinfo(torch.int64).max, dtype=torch.int64, device=dev)

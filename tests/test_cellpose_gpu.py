@@ -119,3 +119,22 @@ def test_runner_end_to_end(gpu):
     masks, flows, styles = r.eval(imgs)
     assert masks.shape == (2, 256, 256) and flows.shape == (2, 3, 256, 256) and styles.shape == (2, 256)
     assert torch.isfinite(flows).all()
+
+
+@pytest.mark.gpu
+def test_follow_flows_launch_variants_identical(gpu, monkeypatch):
+    """The XCD-ordered, block-compacted flow-following launch gives bit-identical masks to the plain
+    pixel-per-lane launch (same per-pixel float sequence, order-independent histogram atomics)."""
+    from bioengine_worker_amd.cellpose import gpu as cg
+
+    ys = []
+    for s in range(3):
+        M = disk_labels(128, 160, 10, seed=40 + s)
+        dP, cp = flows_from_labels(M)
+        ys.append(np.concatenate([dP, cp[None]], 0))
+    y = torch.from_numpy(np.stack(ys)).to(gpu)
+    outs = []
+    for entry in ("be_cp_follow_flows", "be_cp_follow_flows_xcd"):
+        monkeypatch.setattr(cg, "FOLLOW_FLOWS_ENTRY", entry)
+        outs.append(cg.compute_masks_gpu(y).cpu())
+    assert torch.equal(outs[0], outs[1])
