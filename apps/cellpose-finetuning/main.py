@@ -112,37 +112,17 @@ def to_chw(img: np.ndarray, nchan: int = 2) -> np.ndarray:
     return a[:nchan]
 
 
-def clahe(img: np.ndarray, clip: float = 3.0, tiles: int = 16) -> np.ndarray:
-    """Contrast-limited adaptive histogram equalisation (grayscale, bilinear LUT blend)."""
-    g = np.asarray(img, np.float32)
-    if g.ndim == 3:
-        g = g.mean(0) if g.shape[0] <= 4 else g.mean(-1)
-    lo, hi = float(g.min()), float(g.max())
-    u8 = np.zeros(g.shape, np.uint8) if hi <= lo else ((g - lo) / (hi - lo) * 255).astype(np.uint8)
-    H, W = u8.shape
-    th, tw = max(1, H // tiles), max(1, W // tiles)
-    ny, nx = (H + th - 1) // th, (W + tw - 1) // tw
-    luts = np.zeros((ny, nx, 256), np.float32)
-    for i in range(ny):
-        for j in range(nx):
-            t = u8[i * th:(i + 1) * th, j * tw:(j + 1) * tw]
-            h = np.bincount(t.ravel(), minlength=256).astype(np.float32)
-            lim = max(1.0, clip * t.size / 256)
-            excess = np.clip(h - lim, 0, None).sum()
-            h = np.minimum(h, lim) + excess / 256
-            c = np.cumsum(h)
-            luts[i, j] = (c - c[0]) / max(1.0, c[-1] - c[0]) * 255
-    cy = (np.arange(H) + 0.5) / th - 0.5
-    cx = (np.arange(W) + 0.5) / tw - 0.5
-    y0 = np.clip(np.floor(cy).astype(int), 0, ny - 1)
-    x0 = np.clip(np.floor(cx).astype(int), 0, nx - 1)
-    y1, x1 = np.clip(y0 + 1, 0, ny - 1), np.clip(x0 + 1, 0, nx - 1)
-    wy = np.clip(cy - y0, 0, 1)[:, None]
-    wx = np.clip(cx - x0, 0, 1)[None, :]
-    v = u8
-    out = ((1 - wy) * (1 - wx) * luts[y0[:, None], x0[None, :], v] + (1 - wy) * wx * luts[y0[:, None], x1[None, :], v]
-           + wy * (1 - wx) * luts[y1[:, None], x0[None, :], v] + wy * wx * luts[y1[:, None], x1[None, :], v])
-    return out.astype(np.float32)
+def clahe(img: np.ndarray, clip: float = 3.0, tiles: int = 16, device=None) -> np.ndarray:
+    """Reference CLAHE pre-processing (grayscale uint8, cv2-style CLAHE 3.0 / 16x16 tiles; main.py:273-308).
+    Runs the HIP kernel when ``device`` is a GPU, the numpy oracle otherwise."""
+    import torch
+
+    from bioengine_worker_amd.ops.clahe import clahe_u8, to_gray_u8
+
+    g = torch.from_numpy(to_gray_u8(img))
+    if device is not None and torch.device(device).type == "cuda":
+        g = g.to(device)
+    return clahe_u8(g, clip, (tiles, tiles)).cpu().numpy()
 
 
 def encode_png_b64(mask: np.ndarray) -> str:
@@ -284,7 +264,7 @@ class CellposeFinetune:
         else:
             raise ValueError("Provide input_arrays or artifact + image_paths")
         if enable_clahe:
-            images = [clahe(im) for im in images]
+            images = [clahe(im, device=self._device()) for im in images]
         prm = {"diameter": diameter, "flow_threshold": flow_threshold, "cellprob_threshold": cellprob_threshold,
                "niter": niter or 200}
         chw = [to_chw(im) for im in images]
@@ -379,10 +359,31 @@ class CellposeFinetune:
             if out.get("stopped"):
                 write_status(sid, status_type="stopped", message="Training session stopped by user.")
             else:
+                if test_imgs:
+                    write_status(sid, message="Computing instance metrics on the test images")
+                    try:
+                        write_status(sid, instance_metrics=self._instance_metrics(trainer.net, test_imgs, test_labs, dev))
+                    except Exception as e:  # noqa: BLE001 — metrics are best-effort, as in the reference
+                        log.warning("session %s: could not compute instance metrics: %s", sid, e)
                 write_status(sid, status_type="completed", message="Training completed", model_modified=True)
         except Exception as e:  # noqa: BLE001
             log.exception("training failed")
             write_status(sid, status_type="failed", message=f"{type(e).__name__}: {e}")
+
+    @staticmethod
+    def _instance_metrics(net, test_imgs, test_labs, dev) -> dict:
+        """Full Cellpose eval of the fine-tuned net on every test image, then image-mean AP at IoU
+        0.5 / 0.75 / 0.9 (reference main.py:1977-2029, cellpose metrics.average_precision)."""
+        from bioengine_worker_amd.cellpose.metrics import instance_metrics
+        from bioengine_worker_amd.cellpose.pipeline import CellposeRunner
+
+        net.eval()
+        runner = CellposeRunner(net=net, device=dev)
+        preds = []
+        for img in test_imgs:
+            masks, _, _ = runner.eval(np.asarray(img)[None])
+            preds.append(masks[0].cpu())
+        return instance_metrics([np.asarray(l, np.int32) for l in test_labs], [p.numpy() for p in preds])
 
     async def _launch(self, sid: str, imgs, labs, test_imgs, test_labs, params: dict, resume=None):
         ex = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"train-{sid[:8]}")
@@ -404,6 +405,8 @@ class CellposeFinetune:
         test_annotations: list | None = Field(None, description="Validation label paths."),
         train_arrays: list | None = Field(None, description="Training images as arrays (instead of an artifact)."),
         label_arrays: list | None = Field(None, description="Instance label arrays for train_arrays."),
+        test_arrays: list | None = Field(None, description="Validation images as arrays (instead of test_images)."),
+        test_label_arrays: list | None = Field(None, description="Instance label arrays for test_arrays."),
         model: str = Field("cyto3", description="Initial model (built-in name or session id)."),
         n_epochs: int = Field(10, description="Epochs."),
         learning_rate: float = Field(1e-6, description="AdamW learning rate."),
@@ -420,8 +423,10 @@ class CellposeFinetune:
         test_imgs, test_labs = [], []
         if test_images and test_annotations and artifact:
             test_imgs, test_labs = await self._load_training_data(artifact, test_images, test_annotations, None, None)
+        elif test_arrays and test_label_arrays:
+            test_imgs, test_labs = await self._load_training_data(None, None, None, test_arrays, test_label_arrays)
         if enable_clahe:
-            imgs = [to_chw(clahe(i)) for i in imgs]
+            imgs = [to_chw(clahe(i, device=self._device())) for i in imgs]
         sid = f"{datetime.now().strftime('%Y-%m-%d-%H%M%S')}-{uuid.uuid4().hex[:8]}"
         uid = (context or {}).get("user", {}).get("id")
         params = {"model": model, "n_epochs": n_epochs, "learning_rate": learning_rate, "weight_decay": weight_decay,

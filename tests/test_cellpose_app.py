@@ -70,11 +70,13 @@ def test_cellpose_app_infer_train_restart_export(env):
         ims, labs = synthetic_instances(3, 128, 128, seed=1)
         r = await app.start_training(train_arrays=[i for i in ims], label_arrays=[l for l in labs], n_epochs=2,
                                      batch_size=2, min_train_masks=1, learning_rate=1e-4, validation_interval=1,
-                                     label="unit")
+                                     label="unit", test_arrays=[ims[0]], test_label_arrays=[labs[0]])
         sid = r["session_id"]
         st = await _wait_status(app, sid)
         assert st["status_type"] == "completed", st
         assert len(st["train_losses"]) == 2 and all(np.isfinite(st["train_losses"]))
+        im = st["instance_metrics"]  # reference InstanceMetrics: AP@0.5/0.75/0.9 + label counts
+        assert set(im) == {"ap_0_5", "ap_0_75", "ap_0_9", "n_true", "n_pred"} and im["n_true"] == int(labs[0].max())
         sessions = await app.list_training_sessions(labels=["unit"])
         assert sid in sessions
 
