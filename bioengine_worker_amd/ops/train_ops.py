@@ -73,6 +73,18 @@ class _SegLoss(torch.autograd.Function):
         return grad * go.to(grad.dtype), None
 
 
+def seg_loss_and_grad(y: torch.Tensor, lbl: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """(loss, dLoss/dy) in one fused HIP launch (the autograd-free training engine's loss)."""
+    B, _, H, W = y.shape
+    yc = y.contiguous()
+    lc = lbl.float().contiguous()
+    loss = torch.zeros(1, device=y.device, dtype=torch.float32)
+    grad = torch.empty_like(yc)
+    _native.call("be_seg_loss", _native.ptr(yc), int(yc.dtype == torch.bfloat16), _native.ptr(lc), B, H * W,
+                 _native.ptr(loss), _native.ptr(grad), _native.stream(y.device))
+    return loss[0], grad
+
+
 def seg_loss(y: torch.Tensor, lbl: torch.Tensor) -> torch.Tensor:
     """Cellpose ``_loss_fn_seg``: MSE(y[:, :2], 5*lbl[:, 1:3])/2 + BCEWithLogits(y[:, 2], lbl[:, 0] > .5)."""
     if y.is_cuda:

@@ -88,6 +88,7 @@ class BucketedAllReduce:
         self.pending = [0] * len(self.buckets)
         self.works: list = []
         self._hooks = []
+        self._index = {id(p): i for i, p in enumerate(fp.params)}
         if self.world > 1:
             for i, p in enumerate(fp.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -97,6 +98,18 @@ class BucketedAllReduce:
         self.pending = [len(m) for (_, _, m) in self.buckets]
         self.works = []
         self._bufs = []
+
+    def mark_ready(self, params) -> None:
+        """Explicit readiness for engines that write gradients without autograd
+        (:class:`~bioengine_worker_amd.train.cpnet_engine.CPnetTrainEngine`): the moment the last
+        parameter of a bucket is reported, that bucket's all-reduce is issued."""
+        if self.world == 1:
+            return
+        for p in params:
+            bi = self.param_bucket[self._index[id(p)]]
+            self.pending[bi] -= 1
+            if self.pending[bi] == 0:
+                self._launch(bi)
 
     def _make_hook(self, i: int):
         def hook(_p):

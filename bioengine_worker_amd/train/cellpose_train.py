@@ -45,6 +45,9 @@ class TrainConfig:
     bucket_mb: float = 16.0
     comm_bf16: bool = False
     seed: int = 0
+    # "hip": hand-written fwd/bwd engine (train/cpnet_engine.py); "autograd": PyTorch autograd + MIOpen;
+    # "auto": hip on GPU for BatchNorm nets, autograd otherwise
+    engine: str = "auto"
 
 
 def lr_schedule(learning_rate: float, n_epochs: int) -> np.ndarray:
@@ -81,6 +84,11 @@ class CellposeTrainer:
         self.step_count = 0
         self.lr = cfg.lr
         self.gen = torch.Generator().manual_seed(cfg.seed * 1000 + rank)
+        eng = cfg.engine
+        if eng == "auto":
+            eng = "hip" if (self.device.type == "cuda" and cfg.norm == "batch") else "autograd"
+        self.engine_kind = eng
+        self._eng = None
 
     # ------------------------------------------------------------------ core step
     def set_lr(self, lr: float):
@@ -108,6 +116,8 @@ class CellposeTrainer:
 
         with trace.span("train.augment", cuda=True):
             x, lbl = self.augment(imgs, lbls, rescale)
+        if self.engine_kind == "hip":
+            return self._step_engine(x, lbl)
         self.fp.zero_grad()
         with trace.span("train.forward_loss", cuda=True):
             loss = self.forward_loss(x, lbl)
@@ -120,6 +130,27 @@ class CellposeTrainer:
             train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
                                   weight_decay=self.cfg.weight_decay, grad_scale=gscale)
         return loss.detach()
+
+    def _engine(self, B: int, S: int):
+        from .cpnet_engine import CPnetTrainEngine
+
+        if self._eng is None or (self._eng.B, self._eng.S) != (B, S):
+            self._eng = CPnetTrainEngine(self.net, self.fp, B, S, self.device)
+        return self._eng
+
+    def _step_engine(self, x: torch.Tensor, lbl: torch.Tensor) -> torch.Tensor:
+        from ..profiling import trace
+
+        eng = self._engine(x.shape[0], x.shape[-1])
+        with trace.span("train.fwd_bwd_engine", cuda=True):
+            loss = eng.loss_and_backward(x, lbl, on_params_ready=self.ar.mark_ready if self.world > 1 else None)
+        with trace.span("train.grad_allreduce_finish", cuda=True):
+            gscale = self.ar.finish()
+        self.step_count += 1
+        with trace.span("train.adamw", cuda=True):
+            train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
+                                  weight_decay=self.cfg.weight_decay, grad_scale=gscale)
+        return loss
 
     @torch.no_grad()
     def validate(self, imgs: torch.Tensor, lbls: torch.Tensor) -> dict:

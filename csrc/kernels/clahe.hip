@@ -12,6 +12,11 @@
 // needs come from L2 (a 16x16 grid of 256-byte LUTs is 64 KiB per image).
 #include "common.h"
 
+// HIP contracts a*b + c into FMAs by default and __fmul_rn / __fadd_rn are plain operators, so bit
+// parity with OpenCV's separately rounded fp32 blend needs contraction off: tools/build_native.py
+// compiles this file with -ffp-contract=off (the pragma alone is not honoured by hipcc's default).
+#pragma clang fp contract(off)
+
 namespace {
 
 __device__ __forceinline__ int reflect101(int i, int n) {

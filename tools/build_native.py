@@ -51,6 +51,9 @@ HIP_FLAGS = [
     "-I",
     str(CSRC / "kernels"),
 ]
+# Per-source extra flags.  clahe: OpenCV bit parity needs separately rounded fp32 products; hipcc's
+# default contraction fuses them into FMAs even under `#pragma clang fp contract(off)`.
+PER_SOURCE_FLAGS = {"clahe": ["-ffp-contract=off"]}
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread", "-I", str(CSRC / "runtime")]
 
 
@@ -119,9 +122,10 @@ def build_hip(jobs: int, variant: str | None = None, vsrc: str | None = None, vf
         raise RuntimeError("no HIP sources")
 
     def flags_for(src):
+        base = HIP_FLAGS + PER_SOURCE_FLAGS.get(src.stem, [])
         if variant and vsrc and vsrc in src.stem:
-            return HIP_FLAGS + list(vflags or [])
-        return HIP_FLAGS
+            return base + list(vflags or [])
+        return base
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile([HIPCC], s, flags_for(s)), srcs))
