@@ -1,4 +1,8 @@
-"""Composition entry: the extra deployments are bound to __init__ params named after their files."""
+"""Composition entry: the extra deployments are bound to __init__ params named after their files.
+
+Service API of the reference composition demo (apps/composition-demo/entry_deployment.py:53-131):
+``status``, ``process_text`` (runtime A), ``analyze_numbers`` (runtime B), ``time_operations``
+(runtime C), ``run_all`` (all three concurrently); plus ``process`` (one fan-out call)."""
 import asyncio
 import time
 
@@ -24,6 +28,31 @@ class EntryDeployment:
         a, b, c = await asyncio.gather(self.runtime_a.get_status.remote(), self.runtime_b.get_status.remote(),
                                        self.runtime_c.get_status.remote())
         return {"entry_uptime": time.time() - self.start_time, "runtime_a": a, "runtime_b": b, "runtime_c": c}
+
+    @schema_method
+    async def process_text(self, text: str = Field(..., description="Text to process")) -> dict:
+        """Text operations through runtime A: word/char counts, reversed, upper/lower/title case."""
+        return await self.runtime_a.process_text.remote(text)
+
+    @schema_method
+    async def analyze_numbers(self, values: list = Field(..., description="List of numbers to analyze")) -> dict:
+        """Statistics through runtime B (numpy): mean, std, min, max, sum, count, sorted."""
+        return await self.runtime_b.analyze.remote(values)
+
+    @schema_method
+    async def time_operations(self, count: int = Field(5, description="Number of timestamps to generate")) -> dict:
+        """Time-based string operations through runtime C."""
+        return await self.runtime_c.time_ops.remote(count)
+
+    @schema_method
+    async def run_all(self, text: str = Field("hello bioengine", description="Text input for runtime A"),
+                      values: list = Field(None, description="Numbers for runtime B (default [1, 2, 3, 4, 5])"),
+                      count: int = Field(3, description="Count for runtime C")) -> dict:
+        """All three runtimes concurrently, results combined."""
+        values = [1, 2, 3, 4, 5] if values is None else values
+        a, b, c = await asyncio.gather(self.runtime_a.process_text.remote(text), self.runtime_b.analyze.remote(values),
+                                       self.runtime_c.time_ops.remote(count))
+        return {"text_result": a, "data_result": b, "time_result": c}
 
     @schema_method
     async def process(self, text: str = Field(..., description="Text"), numbers: list = Field(..., description="Numbers"),

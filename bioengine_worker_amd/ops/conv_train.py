@@ -60,6 +60,9 @@ def _store(dst: torch.Tensor, val: torch.Tensor, acc: bool) -> None:
 
 # ------------------------------------------------------------------ BatchNorm (train) site
 
+#: floats of the per-block partial scratch of the GPU BN reductions (~2k blocks x 4 x 256 channels)
+SCRATCH_FLOATS = 2048 * 4 * 256
+
 @dataclass
 class BnUnit:
     """One BatchNorm2d feeding one conv: its parameters (views into the flat fp32 master), running
@@ -82,12 +85,16 @@ class BnSite:
     ``stat`` is a slice of an arena the engine zeroes once per step; ``ticket`` two int32 counters."""
 
     def __init__(self, N: int, C: int, c_valid: int, units: list[BnUnit], stat: torch.Tensor, ticket: torch.Tensor,
-                 eps: float = 1e-5, momentum: float = 0.05):
+                 eps: float = 1e-5, momentum: float = 0.05, scratch: torch.Tensor | None = None):
         assert 1 <= len(units) <= 2
         self.N, self.C, self.c_valid = N, C, c_valid
         self.units = units
         self.stat = stat
         self.ticket = ticket
+        # per-block partial sums of the GPU reductions; may be shared by every site of an engine
+        if scratch is None and stat.is_cuda:
+            scratch = torch.empty(SCRATCH_FLOATS, device=stat.device, dtype=torch.float32)
+        self.scratch = scratch
         self.eps, self.momentum = eps, momentum
         assert stat.numel() >= self.stat_numel(N, C)
 
@@ -136,7 +143,8 @@ class BnSite:
         conv = [P(a) if (a is None or isinstance(a, torch.Tensor)) else a for a in args]
         _native.call("be_bn_train", which, P(x), P(x2), P(feat), N, Hs, Ws, H, W, C, self.c_valid, INMODES[inmode],
                      len(self.units), float(self.eps), float(self.momentum), P(self.stat), P(self.ticket), *conv,
-                     P(dfeat), P(dx), int(dx_acc), P(dx2), int(dx2_acc), _native.stream(x.device))
+                     P(dfeat), P(dx), int(dx_acc), P(dx2), int(dx2_acc), P(self.scratch), self.scratch.numel(),
+                     _native.stream(x.device))
 
     # -------------------------------------------------------------- forward statistics
     def stats(self, x: torch.Tensor, inmode: str = "none", x2: torch.Tensor | None = None,
@@ -295,7 +303,8 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, *, ks: int, cin_valid: int, co
     """dw[co, ci, ky, kx] = sum_{n,y,x} dy[n, y, x, co] * act(x)[n, y+ky-k/2, x+kx-k/2, ci]; db = sum dy.
 
     ``x`` NHWC [N, Hs, Ws, Cin] (pre-transform, pre-BN), ``dy`` NHWC [N, H, W, Cy >= cout_valid].
-    ``dw``/``db`` are written (not accumulated), e.g. views into the flat fp32 gradient buffer."""
+    On GPU ``dw``/``db`` are ACCUMULATED into (split-K partials are atomically added: zero them first,
+    e.g. the engine zeroes the flat gradient buffer once per step); the CPU path overwrites."""
     N, Hs, Ws, Cin = x.shape
     H, W = _out_hw(Hs, Ws, inmode)
     if not x.is_cuda:

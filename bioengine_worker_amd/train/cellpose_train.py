@@ -48,6 +48,9 @@ class TrainConfig:
     # "hip": hand-written fwd/bwd engine (train/cpnet_engine.py); "autograd": PyTorch autograd + MIOpen;
     # "auto": hip on GPU for BatchNorm nets, autograd otherwise
     engine: str = "auto"
+    # capture the engine's forward+backward (~250 launches) in one HIP graph (single GPU; the
+    # augment's host-side random affine and the AdamW step with its per-step scalars stay outside)
+    graph: bool = True
 
 
 def lr_schedule(learning_rate: float, n_epochs: int) -> np.ndarray:
@@ -89,6 +92,8 @@ class CellposeTrainer:
             eng = "hip" if (self.device.type == "cuda" and cfg.norm == "batch") else "autograd"
         self.engine_kind = eng
         self._eng = None
+        self._graph = None
+        self._graph_io = None
 
     # ------------------------------------------------------------------ core step
     def set_lr(self, lr: float):
@@ -143,7 +148,10 @@ class CellposeTrainer:
 
         eng = self._engine(x.shape[0], x.shape[-1])
         with trace.span("train.fwd_bwd_engine", cuda=True):
-            loss = eng.loss_and_backward(x, lbl, on_params_ready=self.ar.mark_ready if self.world > 1 else None)
+            if self.cfg.graph and self.world == 1 and self.device.type == "cuda":
+                loss = self._graph_step(eng, x, lbl)
+            else:
+                loss = eng.loss_and_backward(x, lbl, on_params_ready=self.ar.mark_ready if self.world > 1 else None)
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
@@ -151,6 +159,27 @@ class CellposeTrainer:
             train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
                                   weight_decay=self.cfg.weight_decay, grad_scale=gscale)
         return loss
+
+    def _graph_step(self, eng, x: torch.Tensor, lbl: torch.Tensor) -> torch.Tensor:
+        """Replay the captured fwd+bwd on static input buffers (captured on first use per shape)."""
+        key = (tuple(x.shape), tuple(lbl.shape), x.dtype)
+        if self._graph is None or self._graph_io[0] != key:
+            xs, ls = x.clone(), lbl.clone()
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):  # warm-up on a side stream (allocator + lazy state), as torch requires
+                for _ in range(2):
+                    eng.loss_and_backward(xs, ls)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = eng.loss_and_backward(xs, ls)
+            self._graph, self._graph_io = g, (key, xs, ls, out)
+        _, xs, ls, out = self._graph_io
+        xs.copy_(x)
+        ls.copy_(lbl)
+        self._graph.replay()
+        return out.clone()
 
     @torch.no_grad()
     def validate(self, imgs: torch.Tensor, lbls: torch.Tensor) -> dict:

@@ -173,6 +173,7 @@ class CPnetTrainEngine:
         f32 = torch.float32
         # ---- BN workspaces (one arena, zeroed once per step) + prologue affines
         sizes = [ct.BnSite.stat_numel(B, s.C) for s in self._sites]
+        self._bn_scratch = torch.empty(ct.SCRATCH_FLOATS, device=d, dtype=f32) if self.cuda else None
         tot = sum(sizes) + 2 * len(self._sites) + 64
         self._ws_arena = torch.zeros(tot, device=d, dtype=f32)
         off = 0
@@ -182,7 +183,7 @@ class CPnetTrainEngine:
                 u.scale = torch.zeros(s.C, device=d, dtype=f32)
                 u.shift = torch.zeros(B, s.C, device=d, dtype=f32)
             s.bn = ct.BnSite(B, s.C, s.c_valid, s.units, self._ws_arena[off: off + n], tickets[2 * i: 2 * i + 2],
-                             momentum=self.momentum)
+                             momentum=self.momentum, scratch=self._bn_scratch)
             off += n
         # ---- packed weights: one bf16 arena + descriptor table (repacked from the fp32 master each step)
         descs, arena_off, max_e = [], 0, 0
@@ -329,6 +330,8 @@ class CPnetTrainEngine:
         act = self._act
         self._g = {}
         B = self.B
+        if self.cuda:  # wgrad split-K reductions accumulate into the flat gradient
+            self.fp.grad.zero_()
         ready = on_params_ready or (lambda ps: None)
         # ---- head: 1x1 conv 32 -> nout, BN + ReLU on its input
         g8 = convops_to_nhwc(dy_nchw, 8, self.act_dtype)

@@ -30,6 +30,7 @@
 // The data gradient (dgrad) of a stride-1 'same' conv is itself a forward conv of dOut with the
 // spatially flipped, in/out-transposed weights, so it runs on be_conv2d_nhwc unchanged.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -77,6 +78,11 @@ __device__ __forceinline__ void unpack8(const u32x4 r, float (&v)[8]) {
   for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(r[j]); v[2 * j + 1] = hi_bf(r[j]); }
 }
 
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 // ============================================================================================
 // Weight-gradient kernel
 // ============================================================================================
@@ -87,7 +93,7 @@ struct WgArgs {
   const float* pscale;  // [Cin] (null = 1)
   const float* pshift;  // [N?, Cin] (null = 0)
   const bf16_t* dy;     // dOut [N, H, W, Cy] (Cy % 8 == 0)
-  float* ws;            // partials [splits][cout_valid][KS*KS][Cin]
+  float* ws;            // partials [splits][cout_valid][Cin][KS*KS] (torch weight layout per split)
   float* wsb;           // optional dbias partials [splits][cout_valid]
   int N, H, W, Hs, Ws, Cin, Cy, cout_valid;
   int pshift_ns, relu;
@@ -113,6 +119,7 @@ struct WCfg {
   static constexpr int LDS_X = HP * SX, LDS_Y = TH * TW * SY;
   static constexpr size_t LDS = (size_t)(LDS_X + LDS_Y) * sizeof(bf16_t);
   static_assert(NCO % WCO == 0 && NCI % WCI == 0, "wave tiling");
+  static_assert(NT % CG == 0, "fixed halo channel group per thread");
   static_assert(((SX / 2) % 16) == 8 && ((SY / 2) % 16) == 8, "conflict-free transposed reads");
 };
 
@@ -159,6 +166,21 @@ __device__ __forceinline__ void wg_commit(const WgArgs& a, int t, int ci0, int t
   const int per_img = a.tiles_x * a.tiles_y;
   const int n = t / per_img, rem = t % per_img;
   const int ty0 = (rem / a.tiles_x) * C::TH, tx0 = (rem % a.tiles_x) * C::TW;
+  // a thread's halo channel group is fixed (NT % CG == 0): its 8 affine pairs are loaded once per tile
+  float sc[8], sh[8];
+  {
+    const int c = ci0 + (tid % C::CG) * 8;
+    if (a.pscale) ld8(a.pscale + c, sc);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sc[j] = 1.f;
+    }
+    if (a.pshift) ld8(a.pshift + (size_t)n * a.pshift_ns + c, sh);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sh[j] = 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < C::HUPT; ++i) {
     const int u = tid + i * C::NT;
@@ -175,13 +197,8 @@ __device__ __forceinline__ void wg_commit(const WgArgs& a, int t, int ci0, int t
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += w[j];
       }
-      const int c = ci0 + cg * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float sc = a.pscale ? a.pscale[c + j] : 1.f;
-        const float sh = a.pshift ? a.pshift[(size_t)n * a.pshift_ns + c + j] : 0.f;
-        v[j] = fmaf(v[j], sc, sh);
-      }
+      for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) packed[j] = pack2bf(v[2 * j], v[2 * j + 1]);
       if (a.relu) {
@@ -282,7 +299,7 @@ __global__ __launch_bounds__(((TCO / 16) / WCO) * ((CK >= 16 ? CK / 16 : 1) / WC
         if (ci >= a.Cin || (CK == 8 && ci_l >= 8)) continue;
 #pragma unroll
         for (int tp = 0; tp < C::NTAP; ++tp)
-          a.ws[(((size_t)split * a.cout_valid + co) * C::NTAP + tp) * a.Cin + ci] = acc[i][j][tp][e];
+          a.ws[(((size_t)split * a.cout_valid + co) * a.Cin + ci) * C::NTAP + tp] = acc[i][j][tp][e];
       }
       if (do_bias && ci_l == 0) a.wsb[(size_t)split * a.cout_valid + co] = accb[i][e];
     }
@@ -299,7 +316,7 @@ int wgrad_launch(WgArgs a, hipStream_t s) {
 
 template <int KS, int CK, int TCO, int INMODE, bool X2>
 int wgrad_wco(WgArgs a, hipStream_t s) {
-  if constexpr (TCO >= 32) return wgrad_launch<KS, CK, TCO, INMODE, X2, 2, 1>(a, s);
+  if constexpr (TCO >= 64) return wgrad_launch<KS, CK, TCO, INMODE, X2, 2, 1>(a, s);
   else return wgrad_launch<KS, CK, TCO, INMODE, X2, 1, 1>(a, s);
 }
 
@@ -327,25 +344,36 @@ int wgrad_tco(int tco, int inmode, bool x2, WgArgs a, hipStream_t s) {
   return -3;
 }
 
-// Sum the split-K partials.  Threads walk the partial layout [co][tap][ci] (coalesced across every
-// split's slab) and scatter into the torch [co][ci][tap] gradient.
+// Tunables (environment overrides read once, for sweeps): BE_WG_REDUCE_THREADS = threads of the wgrad
+// split reduction, BE_BN_BLOCKS = target blocks of the BN statistics / reduction kernels.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+// Sum the split-K partials into the (pre-zeroed) torch-layout gradient.  The partials already use the
+// weight layout [co][ci][tap], so thread t owns element t: every split's slab is read coalesced and the
+// final atomicAdd of a wave covers 256 contiguous bytes.  Grid.y splits the split dimension into
+// chunks (sized by the host so that ~256k threads run), each chunk adding its sum atomically.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, const float* __restrict__ wsb,
                                                            int splits, int cout, int ntap, int cin_ld, int cin,
                                                            float* __restrict__ dw, float* __restrict__ db) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  const int nw = cout * ntap * cin_ld;
-  if (idx < nw) {
-    const int ci = idx % cin_ld, tp = (idx / cin_ld) % ntap, co = idx / (cin_ld * ntap);
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int nw = cout * cin_ld * ntap;
+  const int spc = (splits + gridDim.y - 1) / gridDim.y;
+  const int s0 = blockIdx.y * spc, s1 = min(splits, s0 + spc);
+  if (e < nw) {
+    const int tp = e % ntap, ci = (e / ntap) % cin_ld, co = e / (ntap * cin_ld);
     if (ci >= cin) return;
-    const size_t stride = (size_t)nw;
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[idx + k * stride];
-    dw[((size_t)co * cin + ci) * ntap + tp] = s;
-  } else if (db != nullptr && idx < nw + cout) {
-    const int co = idx - nw;
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += wsb[(size_t)k * cout + co];
-    db[co] = s;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int k = s0; k < s1; ++k) acc += ws[(size_t)k * nw + e];
+    atomicAdd(dw + ((size_t)co * cin + ci) * ntap + tp, acc);
+  } else if (db != nullptr && e < nw + cout) {
+    const int co = e - nw;
+    float acc = 0.f;
+    for (int k = s0; k < s1; ++k) acc += wsb[(size_t)k * cout + co];
+    atomicAdd(db + co, acc);
   }
 }
 
@@ -377,6 +405,8 @@ struct BnArgs {
   BnUnits u;
   float* dfeat;      // backward: [N, C]
   int per_block;     // pixels per block
+  float* scratch;    // per-block partials [N][nb][NACC][C] (shared scratch, plain stores)
+  int nb;            // blocks per image of the partial kernel
 };
 
 __device__ __forceinline__ float* st_sum(const BnArgs& a) { return a.stat; }
@@ -401,11 +431,13 @@ __device__ __forceinline__ void load_v8(const BnArgs& a, int n, int pix, int c, 
   }
 }
 
-// Block-level reduction of per-thread 8-channel partials (NACC arrays) -> atomicAdd into dst[k][n*C + c].
-// Lanes l and l ^ o (o a multiple of C/8) hold the same channel group, so a shuffle butterfly over
-// those offsets reduces a wave; the 4 waves meet in LDS ([4][NACC][256] staging: C <= 256).
+// Block-level reduction of per-thread 8-channel partials (NACC arrays) -> this block's slot of the
+// partial scratch.  Lanes l and l ^ o (o a multiple of C/8) hold the same channel group, so a shuffle
+// butterfly over those offsets reduces a wave; the 4 waves meet in LDS ([4][NACC][256]: C <= 256).
+// Plain stores to a per-block slot: same-address atomics from every block serialised in one L2
+// channel (measured ~50 ns per block).
 template <int NACC>
-__device__ __forceinline__ void block_reduce_atomic(const BnArgs& a, int n, float (&acc)[NACC][8], float* const* dst) {
+__device__ __forceinline__ void block_reduce_store(const BnArgs& a, int n, float (&acc)[NACC][8]) {
   __shared__ float red[4][NACC][256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, C8 = a.C / 8;
   for (int o = C8; o < 64; o <<= 1) {
@@ -421,10 +453,37 @@ __device__ __forceinline__ void block_reduce_atomic(const BnArgs& a, int n, floa
       for (int j = 0; j < 8; ++j) red[wave][k][lane * 8 + j] = acc[k][j];
   }
   __syncthreads();
+  float* slot = a.scratch + ((size_t)n * a.nb + blockIdx.x) * NACC * a.C;
   for (int c = tid; c < a.C; c += 256) {
 #pragma unroll
-    for (int k = 0; k < NACC; ++k)
-      atomicAdd(dst[k] + (size_t)n * a.C + c, red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c]);
+    for (int k = 0; k < NACC; ++k) slot[k * a.C + c] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+  }
+}
+
+// Sum image n's nb block partials into dst[k][n*C + c] (block per image; 256 / C lane groups).
+template <int NACC>
+__device__ __forceinline__ void image_reduce(const BnArgs& a, int n, float* const* dst) {
+  __shared__ float red2[NACC][256];
+  const int tid = threadIdx.x, G = 256 / a.C, c = tid % a.C, g = tid / a.C;
+  float s[NACC];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) s[k] = 0.f;
+  const float* base = a.scratch + (size_t)n * a.nb * NACC * a.C;
+#pragma unroll 8
+  for (int b = g; b < a.nb; b += G) {
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) s[k] += base[((size_t)b * NACC + k) * a.C + c];
+  }
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) red2[k][tid] = s[k];
+  __syncthreads();
+  if (g == 0) {
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) {
+      float t = 0.f;
+      for (int q = 0; q < G; ++q) t += red2[k][q * a.C + c];
+      dst[k][(size_t)n * a.C + c] = t;
+    }
   }
 }
 
@@ -451,6 +510,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(BnArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) { acc[0][j] = 0.f; acc[1][j] = 0.f; }
   if (pl < PL) {
+#pragma unroll 4
     for (int pix = p0 + pl; pix < p1; pix += PL) {
       float v[8];
       load_v8<INMODE, X2>(a, n, pix, cg * 8, v);
@@ -458,13 +518,20 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(BnArgs a) {
       for (int j = 0; j < 8; ++j) { acc[0][j] += v[j]; acc[1][j] = fmaf(v[j], v[j], acc[1][j]); }
     }
   }
+  block_reduce_store<2>(a, n, acc);
+}
+
+// Grid = N blocks: per-image sums, then the last block finalises batch mean / var over N*H*W of
+// u = v + feat[n] into the conv-prologue affine of every unit.
+__global__ __launch_bounds__(256) void bn_stats_fin_kernel(BnArgs a) {
+  const int tid = threadIdx.x, HW = a.H * a.W;
   float* dst[2] = {st_sum(a), st_sq(a)};
-  block_reduce_atomic<2>(a, n, acc, dst);
+  image_reduce<2>(a, blockIdx.x, dst);
   if (!last_block(a.ticket)) return;
-  // ---- finalise (one block): batch mean / var over N*H*W of u = v + feat[n]
   const float cnt = (float)a.N * (float)HW;
   for (int c = tid; c < a.C; c += 256) {
     float s1 = 0.f, q = 0.f;
+#pragma unroll 8
     for (int m = 0; m < a.N; ++m) {
       const float s = ld_acq(st_sum(a) + (size_t)m * a.C + c), sq = ld_acq(st_sq(a) + (size_t)m * a.C + c);
       const float f = a.feat ? a.feat[(size_t)m * a.C + c] : 0.f;
@@ -481,7 +548,8 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(BnArgs a) {
       const float sc = valid ? a.u.gamma[k][c] * rstd : 0.f;
       const float be = valid ? a.u.beta[k][c] : 0.f;
       a.u.scale[k][c] = sc;
-      for (int m = 0; m < a.N; ++m) {
+  #pragma unroll 8
+    for (int m = 0; m < a.N; ++m) {
         const float f = a.feat ? a.feat[(size_t)m * a.C + c] : 0.f;
         a.u.shift[k][(size_t)m * a.C + c] = valid ? (f - mean) * sc + be : 0.f;
       }
@@ -519,6 +587,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
         sh[k][j] = a.u.shift[k][(size_t)n * a.C + c0 + j];
       }
     }
+#pragma unroll 2
     for (int pix = p0 + pl; pix < p1; pix += PL) {
       float v[8];
       load_v8<INMODE, X2>(a, n, pix, c0, v);
@@ -537,10 +606,16 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
       }
     }
   }
+  block_reduce_store<2 * NU>(a, n, acc);
+}
+
+template <int NU>
+__global__ __launch_bounds__(256) void bn_bwd_fin_kernel(BnArgs a) {
+  const int tid = threadIdx.x, HW = a.H * a.W;
   float* dst[2 * NU];
 #pragma unroll
   for (int k = 0; k < NU; ++k) { dst[2 * k] = st_sdy(a, k); dst[2 * k + 1] = st_sdyx(a, k); }
-  block_reduce_atomic<2 * NU>(a, n, acc, dst);
+  image_reduce<2 * NU>(a, blockIdx.x, dst);
   if (!last_block(a.ticket + 1)) return;
   const float cnt = (float)a.N * (float)HW;
   for (int c = tid; c < a.C; c += 256) {
@@ -548,7 +623,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
     float b0 = 0.f, b1 = 0.f;
     for (int k = 0; k < NU; ++k) {
       float sdy = 0.f, sdyx = 0.f;
-      for (int m = 0; m < a.N; ++m) {
+  #pragma unroll 8
+    for (int m = 0; m < a.N; ++m) {
         sdy += ld_acq(st_sdy(a, k) + (size_t)m * a.C + c);
         sdyx += ld_acq(st_sdyx(a, k) + (size_t)m * a.C + c);
       }
@@ -564,7 +640,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
     st_b1(a)[c] = b1;
     if (a.dfeat) {  // dfeat[n, c] = sum_hw du = s * sum_hw dy + HW * B0 + B1 * sum_hw xhat   (NU == 1)
       const float mean = st_mean(a)[c], rstd = st_rstd(a)[c], s = a.u.scale[0][c];
-      for (int m = 0; m < a.N; ++m) {
+  #pragma unroll 8
+    for (int m = 0; m < a.N; ++m) {
         const float f = a.feat ? a.feat[(size_t)m * a.C + c] : 0.f;
         const float sx = (ld_acq(st_sum(a) + (size_t)m * a.C + c) + (float)HW * (f - mean)) * rstd;
         const float sdy = ld_acq(st_sdy(a, 0) + (size_t)m * a.C + c);
@@ -595,11 +672,6 @@ __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8], bool acc)
 #pragma unroll
   for (int j = 0; j < 4; ++j) o[j] = pack2bf(w[2 * j], w[2 * j + 1]);
   *reinterpret_cast<u32x4*>(p) = o;
-}
-
-__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
-  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
 // Per-thread backward coefficients of its 8 channels (a thread's channel group never changes in the
@@ -741,13 +813,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnArgs a, ApplyOut o)
 template <int INMODE, bool X2>
 int bn_dispatch_x2(int which, BnArgs a, ApplyOut o, hipStream_t s) {
   const int HW = a.H * a.W;
-  const int nb = (HW + a.per_block - 1) / a.per_block;
+  const int nb = a.nb;
   dim3 grid(nb, a.N);
   if (which == 0) {
     hipLaunchKernelGGL((bn_stats_kernel<INMODE, X2>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(bn_stats_fin_kernel, dim3(a.N), dim3(256), 0, s, a);
   } else if (which == 1) {
-    if (a.nunits == 2) hipLaunchKernelGGL((bn_bwd_reduce_kernel<INMODE, X2, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<INMODE, X2, 1>), grid, dim3(256), 0, s, a);
+    if (a.nunits == 2) {
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<INMODE, X2, 2>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL(bn_bwd_fin_kernel<2>, dim3(a.N), dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<INMODE, X2, 1>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL(bn_bwd_fin_kernel<1>, dim3(a.N), dim3(256), 0, s, a);
+    }
   } else {
     const int PH = INMODE == 1 ? a.Hs : a.H, PW = INMODE == 1 ? a.Ws : a.W;
     const long long total = (long long)a.N * PH * PW * (a.C / 8);
@@ -831,9 +909,15 @@ int be_conv_wgrad(const void* x, const void* x2, const float* pscale, const floa
   else if (ks == 1) rc = Cin == 8 ? wgrad_tco<1, 8>(tco, inmode, x2 != nullptr, a, s) : wgrad_tco<1, 32>(tco, inmode, x2 != nullptr, a, s);
   else return -4;
   if (rc) return rc;
-  const int nw = cout_valid * ks * ks * Cin + (db ? cout_valid : 0);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((nw + 255) / 256), dim3(256), 0, s, ws, a.wsb, a.splits, cout_valid,
-                     ks * ks, Cin, cin_valid, dw, db);
+  // dw / db must be zero on entry (the engine zeroes the flat gradient buffer once per step)
+  const int ne = cout_valid * ks * ks * Cin + (db ? cout_valid : 0);
+  static const int target = env_int("BE_WG_REDUCE_THREADS", 262144);
+  int nch = (target + ne - 1) / ne;
+  nch = nch < 1 ? 1 : (nch > 64 ? 64 : nch);
+  nch = nch > a.splits ? a.splits : nch;
+  dim3 rgrid((ne + 255) / 256, nch);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, rgrid, dim3(256), 0, s, ws, a.wsb, a.splits, cout_valid, ks * ks, Cin,
+                     cin_valid, dw, db);
   return BE_CHECK_LAUNCH();
 }
 
@@ -845,7 +929,8 @@ int be_bn_train(int which, const void* x, const void* x2, const float* feat, int
                 const void* dact0, float* dgamma0, float* dbeta0,
                 const float* gamma1, const float* beta1, float* scale1, float* shift1, float* rm1, float* rv1, int relu1,
                 const void* dact1, float* dgamma1, float* dbeta1,
-                float* dfeat, void* dx, int dx_acc, void* dx2, int dx2_acc, hipStream_t s) {
+                float* dfeat, void* dx, int dx_acc, void* dx2, int dx2_acc, float* scratch, int scratch_floats,
+                hipStream_t s) {
   BnArgs a;
   a.x = (const bf16_t*)x; a.x2 = (const bf16_t*)x2; a.feat = feat;
   a.N = N; a.Hs = Hs; a.Ws = Ws; a.H = H; a.W = W; a.C = C; a.c_valid = c_valid; a.inmode = inmode;
@@ -859,9 +944,21 @@ int be_bn_train(int which, const void* x, const void* x2, const float* feat, int
   a.dfeat = dfeat;
   // ~4 blocks per CU over the whole tensor, at least 64 pixels per block
   const long long HW = (long long)H * W;
-  const long long want = (512 + N - 1) / N;
+  static const int bn_blocks = env_int("BE_BN_BLOCKS", 512);
+  const long long want = (bn_blocks + N - 1) / N;
   long long pb = (HW + want - 1) / want;
-  a.per_block = (int)(pb < 256 ? 256 : pb);
+  pb = pb < 256 ? 256 : pb;
+  // the partial scratch holds N * nb * NACC * C floats (NACC <= 4)
+  long long nb = (HW + pb - 1) / pb;
+  const long long cap = scratch_floats / ((long long)N * 4 * C);
+  if (cap < 1) return -5;
+  if (nb > cap) {
+    nb = cap;
+    pb = (HW + nb - 1) / nb;
+  }
+  a.per_block = (int)pb;
+  a.nb = (int)((HW + pb - 1) / pb);
+  a.scratch = scratch;
   ApplyOut o;
   o.dx = (bf16_t*)dx; o.dx2 = (bf16_t*)dx2; o.dx_acc = dx_acc; o.dx2_acc = dx2_acc;
   return bn_dispatch(which, a, o, s);

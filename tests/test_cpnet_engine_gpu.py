@@ -35,8 +35,8 @@ def test_wgrad_kernel(gpu, ks, cin, cin_valid, cy, cout_valid, inmode, use_x2, H
     scale = (1 + 0.2 * torch.randn(cin, device=gpu)).float()
     shift = (0.3 * torch.randn(N, cin, device=gpu)).float()
     dy = torch.randn(N, H, H, cy, device=gpu).to(torch.bfloat16)
-    dw = torch.empty(cout_valid, cin_valid, ks, ks, device=gpu)
-    db = torch.empty(cout_valid, device=gpu)
+    dw = torch.zeros(cout_valid, cin_valid, ks, ks, device=gpu)
+    db = torch.zeros(cout_valid, device=gpu)
     ct.conv_wgrad(x, dy, ks=ks, cin_valid=cin_valid, cout_valid=cout_valid, dw=dw, db=db, inmode=inmode, x2=x2,
                   scale=scale, shift=shift, relu=True)
     dw_ref = torch.empty(cout_valid, cin_valid, ks, ks)
