@@ -106,3 +106,21 @@ def test_pyproject_entry_points_resolve():
     from bioengine_worker_amd import __version__
 
     assert meta["project"]["version"] == __version__
+
+
+def test_every_app_frontend_entry_exists():
+    """Each app that declares a frontend (manifest ``frontend_entry``) ships it; the reference has one
+    per app (apps/*/frontend/index.html)."""
+    import yaml
+    from pathlib import Path
+
+    apps = Path(__file__).resolve().parent.parent / "apps"
+    with_fe = 0
+    for m in apps.glob("*/manifest.yaml"):
+        man = yaml.safe_load(m.read_text())
+        fe = man.get("frontend_entry")
+        if fe:
+            with_fe += 1
+            page = (m.parent / fe).read_text()
+            assert "ws_service_id" in page and "connectToServer" in page, m.parent.name
+    assert with_fe >= 5

@@ -84,6 +84,14 @@ def test_worker_status_and_apps(env):
         comp = await admin.get_service((await svc.get_app_status(application_ids=[aid]))["service_ids"][0]["websocket_service_id"])
         out = await comp.process(text="hello world", numbers=[1, 2, 3], delay=0.0)
         assert out["text"]["upper"] == "HELLO WORLD" and out["stats"]["mean"] == 2.0
+        # reference composition API (apps/composition-demo/entry_deployment.py:53-131)
+        allr = await comp.run_all(text="a b c", values=[2, 4], count=2)
+        assert allr["text_result"]["word_count"] == 3 and allr["data_result"]["sum"] == 6.0
+        assert len(allr["time_result"]["timestamps"]) == 2
+        assert (await comp.analyze_numbers(values=[1, 3]))["mean"] == 2.0
+        assert (await comp.process_text(text="ab"))["reversed"] == "ba"
+        assert (await comp.time_operations(count=1))["count"] == 1
+        assert set((await comp.status())) == {"entry_uptime", "runtime_a", "runtime_b", "runtime_c"}
         cs = await svc.get_app_status(application_ids=[aid])
         assert set(cs["deployments"]) == {"EntryDeployment", "RuntimeA", "RuntimeB", "RuntimeC"}
         assert cs["application_env_vars"]["RuntimeA"] == {"PLAIN": "1", "SECRET": "*****"}
