@@ -531,6 +531,9 @@ class CellposeFinetune:
         if st.get("user_id") and uid and st["user_id"] != uid:
             raise PermissionError(f"Session '{sid}' belongs to another user")
         t = self.tasks.get(sid)
+        if t is not None and not t.done() and st.get("status_type") in ("completed", "failed", "stopped"):
+            # the final status is written before the task returns: let it finish its teardown
+            await asyncio.wait([t], timeout=30)
         if t is not None and not t.done():
             (sessions_root() / sid / "stop").touch()
             raise RuntimeError("session is running; it has been asked to stop, retry the deletion when stopped")
