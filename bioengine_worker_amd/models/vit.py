@@ -13,6 +13,8 @@ L2-normalised).  Here:
   embedding as one GEMM over a reshaped (not unfolded) image, hipBLASLt GEMMs for qkv/proj/MLP,
   the fused flash-attention kernel reading q/k/v straight out of the packed qkv GEMM output,
   LayerScale+residual fused into the next LayerNorm, bias+GELU fused into one pass.
+  ``precision="fp8"`` runs qkv/proj/fc1/fc2 as e4m3 GEMMs on the block-scaled MFMA
+  (``ops/fp8.py``: per-channel weight scales, per-token activation scales, bias/GELU in the epilogue).
 
 Offline there are no pretrained weights: ``ViT(...).randomize_(seed)`` gives DINOv2-style init
 (trunc-normal 0.02, LayerScale 1e-5 → we use 1.0 for a non-degenerate random network).
@@ -26,6 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.fp8 import Fp8Linear, add_layernorm_fp8, quantize_rows
 from ..ops.transformer import add_layernorm, attention_ref, bias_gelu_, flash_attention
 
 
@@ -154,7 +157,10 @@ class ViT(nn.Module):
 class ViTEngine:
     """bf16 HIP inference engine for a :class:`ViT` (see module docstring)."""
 
-    def __init__(self, net: ViT, device, img_size: int = 224):
+    def __init__(self, net: ViT, device, img_size: int = 224, precision: str = "bf16", fp8_gemm: str = "hipblaslt"):
+        if precision not in ("bf16", "fp8"):
+            raise ValueError(f"precision must be 'bf16' or 'fp8', got {precision!r}")
+        self.precision = precision
         self.device = torch.device(device)
         self.cfg = cfg = net.cfg
         self.p = cfg.patch_size
@@ -179,6 +185,11 @@ class ViTEngine:
                 fc1_w=bf(blk.mlp.fc1.weight), fc1_b=f32(blk.mlp.fc1.bias), fc2_w=bf(blk.mlp.fc2.weight),
                 fc2_b=bf(blk.mlp.fc2.bias), g2=ls(blk.ls2)))
         self.nw, self.nb = f32(net.norm.weight), f32(net.norm.bias)
+        if precision == "fp8":
+            # e4m3 weights with per-output-channel scales; the bf16 copies are dropped
+            for b in self.blocks:
+                for name in ("qkv", "proj", "fc1", "fc2"):
+                    b[name + "_q"] = Fp8Linear(b.pop(name + "_w"), b.pop(name + "_b"), gemm=fp8_gemm)
 
     def patchify(self, x: torch.Tensor) -> torch.Tensor:
         """[B, C, H, W] -> [B, gh*gw, C*p*p] in conv-weight order (c, ky, kx) — a reshape + one copy."""
@@ -200,6 +211,9 @@ class ViTEngine:
         t[:, 0] = self.cls_pos
         t[:, 1:] = tok
         blocks = self.blocks
+        fp8 = self.precision == "fp8"
+        if fp8:
+            return self._blocks_fp8(t, B, N)
         h = add_layernorm(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"], cfg.eps)
         for i, b in enumerate(blocks):
             qkv = F.linear(h, b["qkv_w"], b["qkv_b"]).view(B, N, 3, Hh, D // Hh)
@@ -213,6 +227,23 @@ class ViTEngine:
             else:
                 h = add_layernorm(t, m, b["g2"], self.nw, self.nb, cfg.eps)
         return h
+
+    def _blocks_fp8(self, t: torch.Tensor, B: int, N: int) -> torch.Tensor:
+        """fp8 encoder blocks: LayerNorms emit e4m3 + per-token scales straight into the qkv / fc1
+        GEMMs; the attention output is re-quantised per token for proj, and fc1's output goes through
+        GELU + per-token quantisation in one pass for fc2."""
+        cfg, blocks = self.cfg, self.blocks
+        D, Hh = cfg.embed_dim, cfg.num_heads
+        hq = add_layernorm_fp8(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"], cfg.eps)
+        for i, b in enumerate(blocks):
+            qkv = b["qkv_q"](hq).view(B, N, 3, Hh, D // Hh)
+            a = flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]).view(B, N, D)
+            y = b["proj_q"](a)
+            h2q = add_layernorm_fp8(t, y, b["g1"], b["n2w"], b["n2b"], cfg.eps)
+            m = b["fc2_q"](quantize_rows(b["fc1_q"](h2q), gelu=True))
+            if i + 1 < len(blocks):
+                hq = add_layernorm_fp8(t, m, b["g2"], blocks[i + 1]["n1w"], blocks[i + 1]["n1b"], cfg.eps)
+        return add_layernorm(t, m, blocks[-1]["g2"], self.nw, self.nb, cfg.eps)
 
     @torch.no_grad()
     def embed(self, x: torch.Tensor, normalize: bool = True) -> torch.Tensor:

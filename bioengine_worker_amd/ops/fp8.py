@@ -1,0 +1,158 @@
+"""FP8 (OCP e4m3fn) linear layers on the CDNA4 block-scaled MFMA (``csrc/kernels/gemm_fp8.hip``).
+
+The reference embeds cells with DINOv2 ViT-B/14 in fp16 on CUDA (``apps/cell-image-search/
+embedder.py:35-57``; ~500 img/s/A100, ``README.md:122``).  On MI355X the embedding GEMMs run in fp8:
+
+* weights are quantised once per output channel (``sw[n] = amax_k |W[n,k]| / 448``);
+* activations are quantised per token on the fly (``sx[m] = amax_k |x[m,k]| / 448``,
+  ``be_quant_fp8_rows``);
+* ``be_gemm_fp8`` multiplies the e4m3 operands on ``v_mfma_scale_f32_16x16x128_f8f6f4`` (unit block
+  scales, 2x the bf16 MFMA rate) and applies ``sx * sw``, the bias and optionally GELU in its fp32
+  epilogue, writing bf16;
+* the fp8 activations come from fused producers: ``add_layernorm_fp8`` (residual + LayerNorm ->
+  e4m3 + scale) and ``quantize_rows(x, gelu=True)`` (fc1 output -> GELU -> e4m3 + scale), so
+  quantisation adds no pass over HBM of its own.
+
+Measured on MI355X (``profiles/fp8_gemm_bench.jsonl``) hipBLASLt's row-wise-scaled fp8 GEMM beats
+``be_gemm_fp8`` on the ViT-B shapes, so :class:`Fp8Linear` runs the plain GEMMs there by default
+(``gemm="hipblaslt"``) and keeps the HIP kernel selectable (``gemm="hip"``).
+
+CPU tensors run the PyTorch reference of the same math (``torch.float8_e4m3fn`` round-to-nearest-even
+quantisation, fp32 accumulation) — the oracle the GPU numerics tests compare against.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+
+FP8_MAX = 448.0
+FP8_DTYPE = torch.float8_e4m3fn
+
+
+def _row_scale(x: torch.Tensor) -> torch.Tensor:
+    return x.float().abs().amax(dim=-1).clamp_min(1e-12) / FP8_MAX
+
+
+def quantize_rows_ref(x: torch.Tensor, gelu: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
+    """[..., K] -> (e4m3fn [..., K], fp32 scale [...]) with per-row amax scaling (PyTorch math).
+    ``gelu``: quantise the bf16-rounded exact GELU of x instead."""
+    if gelu:
+        x = F.gelu(x.float()).to(torch.bfloat16)
+    s = _row_scale(x)
+    q = (x.float() / s[..., None]).clamp(-FP8_MAX, FP8_MAX).to(FP8_DTYPE)
+    return q, s
+
+
+def quantize_weight(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-output-channel quantisation of a [N, K] weight (done once, at model load)."""
+    return quantize_rows_ref(w.detach())
+
+
+def quantize_rows(x: torch.Tensor, gelu: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
+    """Dynamic per-token quantisation of a bf16 [..., K] activation (optionally of GELU(x), fused)."""
+    if not x.is_cuda:
+        return quantize_rows_ref(x, gelu)
+    K = x.shape[-1]
+    assert x.dtype == torch.bfloat16 and x.is_contiguous() and K % 8 == 0 and K <= 4096, (x.dtype, x.shape)
+    rows = x.numel() // K
+    q = torch.empty(x.shape, dtype=FP8_DTYPE, device=x.device)
+    s = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+    _native.call("be_quant_fp8_rows", _native.ptr(x), _native.ptr(q), _native.ptr(s), rows, K,
+                 int(bool(gelu)), _native.stream(x.device))
+    return q, s
+
+
+def linear_fp8_ref(xq, sx, wq, sw, bias=None, gelu: bool = False) -> torch.Tensor:
+    y = torch.matmul(xq.float(), wq.float().t()) * sx.float()[..., None] * sw.float()
+    if bias is not None:
+        y = y + bias.float()
+    if gelu:
+        y = F.gelu(y)
+    return y.to(torch.bfloat16)
+
+
+def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor,
+               bias: torch.Tensor | None = None, gelu: bool = False, tile_cfg: int = 0) -> torch.Tensor:
+    """``epi(xq . wq^T * sx * sw + bias)`` -> bf16 [..., N]; xq e4m3fn [..., K], wq e4m3fn [N, K].
+
+    ``tile_cfg`` picks the kernel's block tile (0 = by shape; 1 = 128x128, 2 = 256x128, 3 = 128x256,
+    4 = 256x256) — exposed for the tile sweep in ``tools/fp8_bench.py``."""
+    if not xq.is_cuda:
+        return linear_fp8_ref(xq, sx, wq, sw, bias, gelu)
+    K = xq.shape[-1]
+    N = wq.shape[0]
+    M = xq.numel() // K
+    assert xq.dtype == FP8_DTYPE and wq.dtype == FP8_DTYPE and wq.shape[1] == K
+    assert K % 128 == 0 and N % 4 == 0, "fp8 GEMM needs K % 128 == 0 and N % 4 == 0"
+    assert xq.is_contiguous() and wq.is_contiguous() and sx.numel() == M and sw.numel() == N
+    y = torch.empty(*xq.shape[:-1], N, dtype=torch.bfloat16, device=xq.device)
+    b = bias.float().contiguous() if bias is not None else None
+    _native.call("be_gemm_fp8", _native.ptr(xq), _native.ptr(wq), _native.ptr(sx.contiguous()),
+                 _native.ptr(sw.float().contiguous()), _native.ptr(b), _native.ptr(y), M, N, K, int(bool(gelu)),
+                 int(tile_cfg), _native.stream(xq.device))
+    return y
+
+
+def add_layernorm_fp8(x: torch.Tensor, y: torch.Tensor | None, gamma: torch.Tensor | None, w: torch.Tensor,
+                      b: torch.Tensor, eps: float = 1e-6) -> tuple[torch.Tensor, torch.Tensor]:
+    """``x <- x + gamma * y`` (in place) and returns ``quantize_rows(LN(x) * w + b)`` — the fused
+    residual + LayerNorm of ``transformer.add_layernorm`` emitting the fp8 GEMM's input directly."""
+    if not x.is_cuda:
+        from .transformer import add_layernorm
+
+        return quantize_rows_ref(add_layernorm(x, y, gamma, w, b, eps).float())
+    C = x.shape[-1]
+    rows = x.numel() // C
+    assert x.dtype == torch.bfloat16 and x.is_contiguous()
+    if y is not None:
+        assert y.shape == x.shape and y.dtype == torch.bfloat16
+        y = y.contiguous()
+    q = torch.empty(x.shape, dtype=FP8_DTYPE, device=x.device)
+    s = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+    g = gamma.float().contiguous() if gamma is not None else None
+    _native.call("be_add_layernorm_fp8", _native.ptr(x), _native.ptr(y), _native.ptr(g),
+                 _native.ptr(w.float().contiguous()), _native.ptr(b.float().contiguous()), _native.ptr(q),
+                 _native.ptr(s), rows, C, float(eps), 1, _native.stream(x.device))
+    return q, s
+
+
+def linear_fp8_hipblaslt(xq: torch.Tensor, sx: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor,
+                         bias: torch.Tensor | None = None) -> torch.Tensor:
+    """The same row-wise-scaled fp8 GEMM as :func:`linear_fp8` (no GELU) through hipBLASLt
+    (``torch._scaled_mm`` with per-token / per-channel scale vectors)."""
+    K = xq.shape[-1]
+    x2 = xq.reshape(-1, K)
+    y = torch._scaled_mm(x2, wq.t(), scale_a=sx.reshape(-1, 1).float(), scale_b=sw.reshape(1, -1).float(),
+                         bias=None if bias is None else bias.to(torch.bfloat16), out_dtype=torch.bfloat16)
+    return y.view(*xq.shape[:-1], wq.shape[0])
+
+
+class Fp8Linear:
+    """A frozen linear layer holding e4m3 weights + per-channel scales (inference only).
+
+    ``gemm`` picks the GEMM for GPU tensors: ``"hipblaslt"`` (plain row-wise-scaled library GEMM;
+    measured faster on the ViT-B shapes, ``profiles/fp8_gemm_bench.jsonl``) or ``"hip"`` (our
+    ``be_gemm_fp8``, which also fuses GELU into its epilogue).  No silent fallback between them."""
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor | None = None, gemm: str = "hipblaslt"):
+        if gemm not in ("hipblaslt", "hip"):
+            raise ValueError(f"gemm must be 'hipblaslt' or 'hip', got {gemm!r}")
+        self.gemm = gemm
+        self.wq, self.sw = quantize_weight(weight)
+        self.bias = None if bias is None else bias.detach().float().contiguous()
+
+    def to(self, device) -> "Fp8Linear":
+        self.wq, self.sw = self.wq.to(device), self.sw.to(device)
+        if self.bias is not None:
+            self.bias = self.bias.to(device)
+        return self
+
+    def __call__(self, x, gelu: bool = False) -> torch.Tensor:
+        """x: bf16 activations, or an already-quantised ``(xq, sx)`` pair (``add_layernorm_fp8``)."""
+        xq, sx = x if isinstance(x, tuple) else quantize_rows(x)
+        if xq.is_cuda and self.gemm == "hipblaslt":
+            y = linear_fp8_hipblaslt(xq, sx, self.wq, self.sw, self.bias)
+            return F.gelu(y) if gelu else y
+        return linear_fp8(xq, sx, self.wq, self.sw, self.bias, gelu)

@@ -1,0 +1,264 @@
+// FP8 (OCP e4m3fn) GEMM on the CDNA4 block-scaled MFMA, for the ViT linear layers of the
+// cell-image-search embedder (DINOv2 ViT-B/14, reference apps/cell-image-search/embedder.py:35-57,
+// SURVEY.md §2.5 K8; BASELINE.json config "ViT-B embedding extraction, CDNA4 fp8 MFMA").
+//
+//   Y[M,N] (bf16) = epi( (Xq[M,K] . Wq[N,K]^T) * sx[m] * sw[n] + bias[n] )
+//
+// * Xq: activations quantised per row (token) with sx[m] = amax_k|x[m,k]| / 448 by
+//   be_quant_fp8_rows below; Wq: weights quantised per output channel once at load time.
+// * The matrix core is v_mfma_scale_f32_16x16x128_f8f6f4 with e4m3 operands and unit E8M0 block
+//   scales (0x7f = 2^0): K = 128 per instruction at twice the bf16 MFMA rate.  The per-row /
+//   per-column dequantisation scales are applied once in the fp32 epilogue, not per k-block.
+// * Tiles: 128x128 (4 waves), 256x128 / 128x256 (8 waves, 64x64 per wave = 4x4 MFMA tiles) or
+//   256x256 (8 waves, 128x64 per wave), K-step 128; chosen by shape so the grid fills 256 CUs while
+//   the bigger tiles halve the L2->LDS bytes per FLOP.  Both operands are staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR
+//   round trip) into two LDS buffers; the LDS image is linear per wave-instruction and the 16-byte
+//   chunk index of each 128-byte row is XOR-swizzled with (row & 7) on the SOURCE address and on
+//   the ds_read address (cdna_hip_programming.md §5.4 rule 21), so the 16 rows a fragment read
+//   touches fall on distinct bank groups.
+// * The next K-tile's DMA stays in flight across the barrier (raw s_barrier + counted vmcnt),
+//   overlapping the current tile's 16 MFMAs per wave.
+// * The MFMA's "A" operand is the weight tile and "B" the activation tile, so the accumulator of
+//   each lane holds 4 consecutive output channels of one token: the epilogue writes 8-byte packed
+//   bf16 runs along N (the row-major output's contiguous axis).
+// * Block -> tile mapping is XCD-aware (common.h xcd_remap): consecutive tiles of one M-panel run
+//   on one XCD and share its L2 copy of the activation panel.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+constexpr int BK = 128;                         // k-bytes (= e4m3 elements) per K-step
+constexpr int E8M0_ONE = 0x7f7f7f7f;            // block scale 2^0 in every byte
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// s_waitcnt immediate (gfx9 encoding) waiting for vmcnt <= n only: vmcnt[3:0] | expcnt[6:4]=7 |
+// lgkmcnt[11:8]=15 | vmcnt[5:4] at [15:14].
+constexpr int waitcnt_vm(int n) { return (n & 0xf) | (0x7 << 4) | (0xf << 8) | ((n >> 4) << 14); }
+
+// Stage one R x 128-byte tile (rows r0.., k-bytes k0..) of a [rows, ld] fp8 matrix into LDS.
+// Each wave-instruction writes 8 rows (1 KiB, lane-linear); row groups go round-robin over waves.
+template <int R, int NW>
+__device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ g, long long ld, int r0, int rmax, int k0,
+                                           uint8_t* lds_tile, int wave, int lane) {
+  const int rin = lane >> 3;
+  const int chunk = (lane & 7) ^ rin;  // inverse swizzle on the source (involution)
+#pragma unroll
+  for (int j = 0; j < R / 8 / NW; ++j) {
+    const int grp = j * NW + wave;
+    int gr = r0 + grp * 8 + rin;
+    gr = gr < rmax ? gr : rmax - 1;  // clamp ragged edges to a valid row; results are masked at store
+    const uint8_t* src = g + (long long)gr * ld + k0 + chunk * 16;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + grp * 1024), 16, 0, 0);
+  }
+}
+
+// Fragment of a 16x128 (rows x k-bytes) slab for v_mfma_scale_f32_16x16x128_f8f6f4:
+// lane l holds row (l & 15), k-bytes [32*(l>>4), +32) as two swizzled 16-byte chunks.
+__device__ __forceinline__ i32x8 read_frag(const uint8_t* lds_tile, int row, int lane) {
+  const int c0 = 2 * (lane >> 4);
+  const int sw = row & 7;
+  const uint8_t* base = lds_tile + row * 128;
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(base + ((c0 ^ sw) << 4));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(base + (((c0 + 1) ^ sw) << 4));
+  i32x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// Block tile BM x BN = (WAVES_M * 16 * TM) x (WAVES_N * 16 * TN); each wave owns TM x TN MFMA tiles.
+template <int TM, int TN, int WAVES_M, int WAVES_N, int EPI>  // EPI 0: scale + bias, 1: + GELU(erf)
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
+    const uint8_t* __restrict__ X, const uint8_t* __restrict__ W, const float* __restrict__ sx,
+    const float* __restrict__ sw, const float* __restrict__ bias, bf16_t* __restrict__ Y, int M, int N, int K,
+    int tiles_n) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int BM = WAVES_M * 16 * TM, BN = WAVES_N * 16 * TN;
+  constexpr int XB = BM * BK, BUF = (BM + BN) * BK;
+  constexpr int LOADS = (BM + BN) / 8 / NW;  // glds per thread per K-step
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "row groups must split evenly over waves");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];  // the only LDS object (rule 4a)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int wm = (wave / WAVES_N) * 16 * TM, wn = (wave % WAVES_N) * 16 * TN;
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage_tile<BM, NW>(X, K, m0, M, 0, smem, wave, lane);
+  stage_tile<BN, NW>(W, K, n0, N, 0, smem + XB, wave, lane);
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint8_t* buf = smem + (kt & 1) * BUF;
+    if (kt + 1 < nk) {
+      uint8_t* nxt = smem + ((kt + 1) & 1) * BUF;
+      stage_tile<BM, NW>(X, K, m0, M, (kt + 1) * BK, nxt, wave, lane);
+      stage_tile<BN, NW>(W, K, n0, N, (kt + 1) * BK, nxt + XB, wave, lane);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(LOADS));  // tile kt landed; tile kt+1 stays in flight
+    } else {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    const uint8_t* xt = buf;
+    const uint8_t* wt = buf + XB;
+    i32x8 bx[TM];
+#pragma unroll
+    for (int b = 0; b < TM; ++b) bx[b] = read_frag(xt, wm + b * 16 + (lane & 15), lane);
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const i32x8 aw = read_frag(wt, wn + a * 16 + (lane & 15), lane);
+#pragma unroll
+      for (int b = 0; b < TM; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(aw, bx[b], acc[a][b], 0, 0, 0, E8M0_ONE, 0,
+                                                                     E8M0_ONE);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // WAR: the next iteration restages the buffer read here
+  }
+
+  // epilogue: acc[a][b][i] = C[m = wm + 16b + (lane&15)][n = wn + 16a + 4(lane>>4) + i]
+#pragma unroll
+  for (int b = 0; b < TM; ++b) {
+    const int m = m0 + wm + b * 16 + (lane & 15);
+    if (m >= M) continue;
+    const float s_m = sx[m];
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const int n = n0 + wn + a * 16 + 4 * (lane >> 4);
+      if (n >= N) continue;
+      const float4 swv = *reinterpret_cast<const float4*>(sw + n);
+      float4 bv = {0.f, 0.f, 0.f, 0.f};
+      if (bias) bv = *reinterpret_cast<const float4*>(bias + n);
+      float v0 = acc[a][b][0] * s_m * swv.x + bv.x;
+      float v1 = acc[a][b][1] * s_m * swv.y + bv.y;
+      float v2 = acc[a][b][2] * s_m * swv.z + bv.z;
+      float v3 = acc[a][b][3] * s_m * swv.w + bv.w;
+      if (EPI == 1) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3); }
+      u32x2 o;
+      o[0] = pack2bf(v0, v1);
+      o[1] = pack2bf(v2, v3);
+      *reinterpret_cast<u32x2*>(Y + (long long)m * N + n) = o;
+    }
+  }
+}
+
+template <int TM, int TN, int WAVES_M, int WAVES_N>
+int launch_gemm(const void* xq, const void* wq, const float* sx, const float* sw, const float* bias, void* y, int M,
+                int N, int K, int epi, hipStream_t s) {
+  constexpr int BM = WAVES_M * 16 * TM, BN = WAVES_N * 16 * TN;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const dim3 grid((unsigned)(tiles_m * tiles_n)), block(64 * WAVES_M * WAVES_N);
+  if (epi == 1)
+    hipLaunchKernelGGL((gemm_fp8_kernel<TM, TN, WAVES_M, WAVES_N, 1>), grid, block, 0, s, (const uint8_t*)xq,
+                       (const uint8_t*)wq, sx, sw, bias, (bf16_t*)y, M, N, K, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_fp8_kernel<TM, TN, WAVES_M, WAVES_N, 0>), grid, block, 0, s, (const uint8_t*)xq,
+                       (const uint8_t*)wq, sx, sw, bias, (bf16_t*)y, M, N, K, tiles_n);
+  return BE_CHECK_LAUNCH();
+}
+
+// Per-row dynamic quantisation bf16 -> e4m3fn: scale[m] = max(amax_k |x[m,k]|, tiny) / 448.
+// One wave per row; the row stays in registers between the amax and the conversion.  GELU: apply the
+// exact (erf) GELU first — the MLP's fc1 output becomes fc2's fp8 input in one pass over HBM.
+template <int NV, bool GELU>
+__global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restrict__ x, uint8_t* __restrict__ q,
+                                                         float* __restrict__ scale, long long rows, int K) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16_t* xr = x + row * K;
+  u32x4 v[NV];
+  float amax = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < K) {
+      v[k] = *reinterpret_cast<const u32x4*>(xr + c);
+      if (GELU) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[k][j] = pack2bf(gelu_erf(lo_bf(v[k][j])), gelu_erf(hi_bf(v[k][j])));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fmaxf(fabsf(lo_bf(v[k][j])), fabsf(hi_bf(v[k][j]))));
+    }
+  }
+  amax = wave_max(amax);
+  const float s = fmaxf(amax, 1e-12f) * (1.f / 448.f);
+  const float inv = 448.f / fmaxf(amax, 1e-12f);
+  if (lane == 0) scale[row] = s;
+  uint8_t* qr = q + row * K;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < K) {
+      u32x2 o;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(lo_bf(v[k][2 * h]) * inv, -448.f), 448.f),
+                                                fminf(fmaxf(hi_bf(v[k][2 * h]) * inv, -448.f), 448.f), 0, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(lo_bf(v[k][2 * h + 1]) * inv, -448.f), 448.f),
+                                            fminf(fmaxf(hi_bf(v[k][2 * h + 1]) * inv, -448.f), 448.f), w, true);
+        o[h] = (uint32_t)w;
+      }
+      *reinterpret_cast<u32x2*>(qr + c) = o;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Y[M,N] bf16 = epi(Xq[M,K] e4m3 . Wq[N,K]^T e4m3 * sx[M] * sw[N] + bias[N]); epi 0 = none, 1 = GELU.
+// K % 128 == 0, N % 4 == 0; any M.  cfg selects the block tile (0 = by shape):
+//   1: 128x128 (4 waves, 64x64 each)   2: 256x128 (8 waves)   3: 128x256 (8 waves)
+//   4: 256x256 (8 waves, 128x64 each)
+int be_gemm_fp8(const void* xq, const void* wq, const float* sx, const float* sw, const float* bias, void* y, int M,
+                int N, int K, int epi, int cfg, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 4 != 0) return -1;
+  if (cfg == 0) {  // measured (profiles/fp8_gemm_bench.jsonl): 256x256 only pays for long K on a full grid
+    const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+    cfg = (K >= 2048 && t256 >= 256) ? 4 : 1;
+  }
+  switch (cfg) {
+    case 1: return launch_gemm<4, 4, 2, 2>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
+    case 2: return launch_gemm<4, 4, 4, 2>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
+    case 3: return launch_gemm<4, 4, 2, 4>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
+    case 4: return launch_gemm<8, 4, 2, 4>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
+    default: return -2;
+  }
+}
+
+// x bf16 [rows, K] -> q e4m3fn [rows, K] + scale float [rows]; K % 8 == 0, K <= 4096.
+// gelu != 0: quantise GELU(x) (bf16-rounded, like a bf16 GELU pass) instead of x.
+int be_quant_fp8_rows(const void* x, void* q, float* scale, long long rows, int K, int gelu, hipStream_t s) {
+  if (K % 8 != 0 || K > 64 * 8 * 8) return -1;
+  const int nv = (K / 8 + 63) / 64;
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+#define QR(NV)                                                                                                 \
+  case NV:                                                                                                     \
+    if (gelu)                                                                                                  \
+      hipLaunchKernelGGL((quant_rows_kernel<NV, true>), grid, block, 0, s, (const bf16_t*)x, (uint8_t*)q, scale, \
+                         rows, K);                                                                             \
+    else                                                                                                       \
+      hipLaunchKernelGGL((quant_rows_kernel<NV, false>), grid, block, 0, s, (const bf16_t*)x, (uint8_t*)q,       \
+                         scale, rows, K);                                                                      \
+    break;
+  switch (nv) {
+    QR(1) QR(2) QR(3) QR(4) QR(5) QR(6) QR(7) QR(8)
+    default: return -1;
+  }
+#undef QR
+  return BE_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -26,12 +26,22 @@ __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
   *reinterpret_cast<u32x4*>(p) = r;
 }
 
-template <int NV>
+// Q8: instead of bf16 `out`, write the normalised row as e4m3fn (q8) with its per-row dequantisation
+// scale (qscale = amax / 448) — the input format of the fp8 GEMM (gemm_fp8.hip), so the GEMM's
+// activation quantisation costs no extra pass over HBM.
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(a, -448.f), 448.f), fminf(fmaxf(b, -448.f), 448.f), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(c, -448.f), 448.f), fminf(fmaxf(d, -448.f), 448.f), w, true);
+  return (uint32_t)w;
+}
+
+template <int NV, bool Q8 = false>
 __global__ __launch_bounds__(256) void add_ln_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
                                                      const float* __restrict__ gamma, const float* __restrict__ w,
                                                      const float* __restrict__ bias, bf16_t* __restrict__ out,
                                                      float* __restrict__ stats, long long rows, int C, float eps,
-                                                     int write_x) {
+                                                     int write_x, uint8_t* __restrict__ q8,
+                                                     float* __restrict__ qscale) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -80,7 +90,8 @@ __global__ __launch_bounds__(256) void add_ln_kernel(bf16_t* __restrict__ x, con
   }
   const float rstd = rsqrtf(wave_sum(q) / C + eps);
   if (stats && lane == 0) { stats[2 * row] = mean; stats[2 * row + 1] = rstd; }
-  if (!out) return;
+  if (!Q8 && !out) return;
+  float amax = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (k * 64 + lane) * 8;
@@ -94,7 +105,27 @@ __global__ __launch_bounds__(256) void add_ln_kernel(bf16_t* __restrict__ x, con
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * ww[j] + bb[j];
-      store8(out + row * C + c, o);
+      if (Q8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { v[k][j] = o[j]; amax = fmaxf(amax, fabsf(o[j])); }
+      } else {
+        store8(out + row * C + c, o);
+      }
+    }
+  }
+  if (Q8) {
+    amax = fmaxf(wave_max(amax), 1e-12f);
+    const float inv = 448.f / amax;
+    if (lane == 0) qscale[row] = amax * (1.f / 448.f);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < C) {
+        u32x2 o;
+        o[0] = pack4_fp8(v[k][0] * inv, v[k][1] * inv, v[k][2] * inv, v[k][3] * inv);
+        o[1] = pack4_fp8(v[k][4] * inv, v[k][5] * inv, v[k][6] * inv, v[k][7] * inv);
+        *reinterpret_cast<u32x2*>(q8 + row * C + c) = o;
+      }
     }
   }
 }
@@ -134,14 +165,33 @@ int be_add_layernorm(void* x, const void* y, const float* gamma, const float* w,
   const dim3 grid((unsigned)((rows + 3) / 4));
   switch (nv) {
     case 1: hipLaunchKernelGGL(add_ln_kernel<1>, grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)y, gamma, w, b,
-                               (bf16_t*)out, stats, rows, C, eps, write_x); break;
+                               (bf16_t*)out, stats, rows, C, eps, write_x, nullptr, nullptr); break;
     case 2: hipLaunchKernelGGL(add_ln_kernel<2>, grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)y, gamma, w, b,
-                               (bf16_t*)out, stats, rows, C, eps, write_x); break;
+                               (bf16_t*)out, stats, rows, C, eps, write_x, nullptr, nullptr); break;
     case 3: hipLaunchKernelGGL(add_ln_kernel<3>, grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)y, gamma, w, b,
-                               (bf16_t*)out, stats, rows, C, eps, write_x); break;
+                               (bf16_t*)out, stats, rows, C, eps, write_x, nullptr, nullptr); break;
     default: hipLaunchKernelGGL(add_ln_kernel<4>, grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)y, gamma, w, b,
-                                (bf16_t*)out, stats, rows, C, eps, write_x); break;
+                                (bf16_t*)out, stats, rows, C, eps, write_x, nullptr, nullptr); break;
   }
+  return BE_CHECK_LAUNCH();
+}
+
+// As be_add_layernorm, but the normalised output is e4m3fn q8 [rows, C] + qscale [rows] (fp8 GEMM input).
+int be_add_layernorm_fp8(void* x, const void* y, const float* gamma, const float* w, const float* b, void* q8,
+                         float* qscale, long long rows, int C, float eps, int write_x, hipStream_t s) {
+  if (C % 8 != 0 || C > 64 * 8 * MAXV || !w || !b || !q8 || !qscale) return -1;
+  const int nv = (C / 8 + 63) / 64;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+#define LNQ(NV)                                                                                                \
+  case NV:                                                                                                     \
+    hipLaunchKernelGGL((add_ln_kernel<NV, true>), grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)y, gamma, w, \
+                       b, (bf16_t*)nullptr, (float*)nullptr, rows, C, eps, write_x, (uint8_t*)q8, qscale);       \
+    break;
+  switch (nv) {
+    LNQ(1) LNQ(2) LNQ(3) LNQ(4)
+    default: return -1;
+  }
+#undef LNQ
   return BE_CHECK_LAUNCH();
 }
 

@@ -1,0 +1,140 @@
+"""FP8 (e4m3fn) linear path: the HIP block-scaled-MFMA GEMM and per-token quantiser against plain
+PyTorch fp32 references, and the fp8 ViT engine against the fp32 DINOv2 module."""
+import pytest
+import torch
+
+from bioengine_worker_amd.models.vit import ViT, ViTConfig, ViTEngine
+from bioengine_worker_amd.ops.fp8 import (FP8_DTYPE, Fp8Linear, add_layernorm_fp8, linear_fp8, linear_fp8_ref,
+                                          quantize_rows, quantize_rows_ref)
+from bioengine_worker_amd.ops.transformer import add_layernorm_ref
+
+
+def test_quantize_rows_ref_roundtrip():
+    x = torch.randn(5, 256) * torch.logspace(-3, 2, 5)[:, None]
+    q, s = quantize_rows_ref(x)
+    assert q.dtype == FP8_DTYPE and s.shape == (5,)
+    assert q.float().abs().amax(1).sub(448).abs().max() < 1e-3  # every row uses the full e4m3 range
+    rel = ((q.float() * s[:, None] - x).abs() / x.abs().amax(1, keepdim=True)).max()
+    assert rel < 2 ** -4  # 3 mantissa bits
+
+
+def test_fp8_linear_cpu_close_to_fp32():
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(96, 256, generator=g) * 0.05
+    b = torch.randn(96, generator=g)
+    x = torch.randn(33, 256, generator=g).bfloat16()
+    lin = Fp8Linear(w, b)
+    y = lin(x, gelu=True).float()
+    ref = torch.nn.functional.gelu(x.float() @ w.t() + b)
+    err = (y - ref).abs().max() / ref.abs().max()
+    assert err < 0.05, err
+
+
+def test_vit_engine_fp8_cpu_embedding_close():
+    cfg = ViTConfig(embed_dim=128, depth=2, num_heads=2, img_size=70)
+    net = ViT(cfg).randomize_(0).eval()
+    x = torch.randn(2, 3, 56, 56)
+    ref = net(x)
+    out = ViTEngine(net, "cpu", img_size=56, precision="fp8").embed(x, normalize=False)
+    cos = torch.nn.functional.cosine_similarity(out, ref.float(), dim=1)
+    assert cos.min() > 0.98, cos
+    with pytest.raises(ValueError):
+        ViTEngine(net, "cpu", img_size=56, precision="fp4")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [128, 768, 3072])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_quantize_rows_hip_matches_reference(gpu, K, gelu):
+    x = (torch.randn(77, K) * torch.rand(77, 1) * 10).bfloat16()
+    qr, sr = quantize_rows_ref(x, gelu)
+    q, s = quantize_rows(x.to(gpu), gelu)
+    torch.testing.assert_close(s.cpu(), sr, rtol=1e-6, atol=0)
+    # x * (448/amax) vs x / (amax/448): at most one e4m3 step apart, on a handful of elements
+    d = (q.cpu().float() - qr.float()).abs()
+    step = qr.float().abs().clamp_min(2 ** -6) * 2 ** -3
+    assert (d <= step + 1e-6).all()
+    assert (d > 0).float().mean() < 0.01
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (16448, 2304, 768), (300, 768, 3072), (1, 3072, 768),
+                                   (129, 260, 256)])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_gemm_fp8_matches_reference(gpu, M, N, K, gelu):
+    g = torch.Generator().manual_seed(M + N + K)
+    # asymmetric operands (cdna_hip_programming.md §3: catches transposed C-writes)
+    x = (torch.randn(M, K, generator=g) + torch.arange(K) / K).bfloat16()
+    w = torch.randn(N, K, generator=g) * 0.03 + torch.arange(N)[:, None] / (10 * N)
+    bias = torch.randn(N, generator=g)
+    lin = Fp8Linear(w, bias)
+    xq, sx = quantize_rows_ref(x)
+    ref = linear_fp8_ref(xq, sx, lin.wq, lin.sw, lin.bias, gelu).float()
+    lin.to(gpu)
+    y = linear_fp8(xq.to(gpu), sx.to(gpu), lin.wq, lin.sw, lin.bias, gelu).float().cpu()
+    err = (y - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile_cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(1000, 640, 384), (257, 256, 128)])
+def test_gemm_fp8_tile_configs(gpu, tile_cfg, M, N, K):
+    g = torch.Generator().manual_seed(tile_cfg)
+    x = (torch.randn(M, K, generator=g) + torch.arange(K) / K).bfloat16()
+    w = torch.randn(N, K, generator=g) * 0.03 + torch.arange(N)[:, None] / (10 * N)
+    lin = Fp8Linear(w, torch.randn(N, generator=g))
+    xq, sx = quantize_rows_ref(x)
+    ref = linear_fp8_ref(xq, sx, lin.wq, lin.sw, lin.bias).float()
+    lin.to(gpu)
+    y = linear_fp8(xq.to(gpu), sx.to(gpu), lin.wq, lin.sw, lin.bias, tile_cfg=tile_cfg).float().cpu()
+    assert (y - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [768, 1024])
+def test_add_layernorm_fp8_matches_reference(gpu, C):
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(300, C, generator=g).bfloat16()
+    y = torch.randn(300, C, generator=g).bfloat16()
+    gamma, w, b = (torch.randn(C, generator=g) for _ in range(3))
+    xn_ref, out_ref = add_layernorm_ref(x, y, gamma, w, b, 1e-6)
+    xg = x.to(gpu)
+    q, s = add_layernorm_fp8(xg, y.to(gpu), gamma.to(gpu), w.to(gpu), b.to(gpu), 1e-6)
+    torch.testing.assert_close(xg.cpu(), xn_ref)  # residual stream updated in place
+    deq = q.cpu().float() * s.cpu()[:, None]
+    scale = out_ref.float().abs().amax(1, keepdim=True)
+    assert ((deq - out_ref.float()).abs() / scale).max() < 2 ** -4
+
+
+@pytest.mark.gpu
+def test_gemm_fp8_identity_exact(gpu):
+    # A = I with an asymmetric B and unit scales: every output element is one exact product
+    K, N = 256, 64
+    xq = torch.eye(K)[:100].to(FP8_DTYPE)
+    w = torch.arange(N * K).reshape(N, K).remainder(13).float() - 6
+    ones_m, ones_n = torch.ones(100), torch.ones(N)
+    y = linear_fp8(xq.to(gpu), ones_m.to(gpu), w.to(FP8_DTYPE).to(gpu), ones_n.to(gpu)).float().cpu()
+    torch.testing.assert_close(y, w.t()[:100], rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gemm", ["hip", "hipblaslt"])
+def test_fp8_linear_backends_agree(gpu, gemm):
+    g = torch.Generator().manual_seed(3)
+    w, b = torch.randn(768, 768, generator=g) * 0.03, torch.randn(768, generator=g)
+    x = torch.randn(2, 257, 768, generator=g).bfloat16()
+    ref = Fp8Linear(w, b)(x).float()  # CPU reference
+    y = Fp8Linear(w, b, gemm=gemm).to(gpu)(x.to(gpu)).float().cpu()
+    assert y.shape == (2, 257, 768)
+    assert (y - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 2e-2
+
+
+@pytest.mark.gpu
+def test_vit_engine_fp8_gpu_embedding_close(gpu):
+    net = ViT(ViTConfig.dinov2("vitb14")).randomize_(0).eval()
+    x = torch.randn(4, 3, 224, 224)
+    ref = ViTEngine(net, gpu).embed(x.to(gpu))
+    out = ViTEngine(net, gpu, precision="fp8").embed(x.to(gpu))
+    cos = torch.nn.functional.cosine_similarity(out, ref, dim=1)
+    assert cos.min() > 0.99, cos
