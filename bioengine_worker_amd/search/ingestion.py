@@ -237,8 +237,11 @@ class EmbedWorker:
         return torch.cat(embs), np.concatenate(thumbs)
 
 
-def default_engine_factory(device, model: str = "vitb14"):
-    """DINOv2 engine; ``model`` = vits14/vitb14/vitl14/vitg14, or ``tiny-test`` (2 blocks, for CPU tests)."""
+def default_engine_factory(device, model: str = "vitb14", precision: str | None = None):
+    """DINOv2 engine; ``model`` = vits14/vitb14/vitl14/vitg14, or ``tiny-test`` (2 blocks, for CPU tests).
+
+    ``precision``: ``"fp8"`` (default on GPU: e4m3 GEMMs, cosine >= 0.99 to bf16, 1.11x faster —
+    profiles/README.md) or ``"bf16"``; ``BIOENGINE_EMBED_PRECISION`` overrides the default."""
     from ..models.vit import ViT, ViTConfig, ViTEngine
 
     weights = os.environ.get("BIOENGINE_DINOV2_WEIGHTS")
@@ -249,7 +252,10 @@ def default_engine_factory(device, model: str = "vitb14"):
         net.load_state_dict(sd, strict=False)
     else:
         net.randomize_(0)
-    return ViTEngine(net.eval(), device)
+    if precision is None:
+        precision = os.environ.get("BIOENGINE_EMBED_PRECISION") or (
+            "fp8" if torch.device(device).type == "cuda" else "bf16")
+    return ViTEngine(net.eval(), device, precision=precision)
 
 
 def run_ingestion(workspace_dir: str, session_id: str, dataset: str = "synthetic", n_images: int = 8,
