@@ -63,6 +63,65 @@ MODEL_SRC = textwrap.dedent('''
 ''')
 
 
+MODEL3D_SRC = textwrap.dedent('''
+    import torch
+    import torch.nn as nn
+
+
+    def conv_block(cin, cout):
+        return nn.Sequential(
+            nn.Conv3d(cin, cout, 3, padding=1), nn.BatchNorm3d(cout), nn.ReLU(inplace=True),
+            nn.Conv3d(cout, cout, 3, padding=1), nn.BatchNorm3d(cout), nn.ReLU(inplace=True))
+
+
+    class UNet3d(nn.Module):
+        """3-D U-Net (PlantSeg / 3D-UNet family): Conv3d-BN-ReLU pairs, 2x max-pool, transposed-conv
+        decoder with skip concatenation, 1x1x1 head + sigmoid."""
+
+        def __init__(self, in_channels=1, out_channels=1, features=(16, 32, 64, 128), final_activation="Sigmoid"):
+            super().__init__()
+            self.encoders = nn.ModuleList()
+            c = in_channels
+            for f in features[:-1]:
+                self.encoders.append(conv_block(c, f))
+                c = f
+            self.pool = nn.MaxPool3d(2)
+            self.base = conv_block(c, features[-1])
+            self.ups = nn.ModuleList()
+            self.decoders = nn.ModuleList()
+            c = features[-1]
+            for f in reversed(features[:-1]):
+                self.ups.append(nn.ConvTranspose3d(c, f, 2, stride=2))
+                self.decoders.append(conv_block(2 * f, f))
+                c = f
+            self.head = nn.Conv3d(c, out_channels, 1)
+            self.act = getattr(nn, final_activation)() if final_activation else nn.Identity()
+
+        def forward(self, x):
+            skips = []
+            for enc in self.encoders:
+                x = enc(x)
+                skips.append(x)
+                x = self.pool(x)
+            x = self.base(x)
+            for up, dec, s in zip(self.ups, self.decoders, reversed(skips)):
+                x = dec(torch.cat([s, up(x)], dim=1))
+            return self.act(self.head(x))
+''')
+
+
+def _randomize_bn(net: torch.nn.Module, seed: int) -> None:
+    """Non-trivial eval statistics so BN folding is exercised."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, (torch.nn.BatchNorm2d, torch.nn.BatchNorm3d)):
+                m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+                m.running_var.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
+                m.weight.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
+                m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+
+
 def load_module(path: Path, name: str = "bioimageio_model_src"):
     spec = importlib.util.spec_from_file_location(name, path)
     mod = importlib.util.module_from_spec(spec)
@@ -81,14 +140,7 @@ def write_unet2d_package(out: str | Path, model_id: str = "demo-unet2d", in_chan
               "final_activation": "Sigmoid"}
     torch.manual_seed(seed)
     net = mod.UNet2d(**kwargs)
-    g = torch.Generator().manual_seed(seed)
-    with torch.no_grad():
-        for m in net.modules():
-            if isinstance(m, torch.nn.BatchNorm2d):
-                m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
-                m.running_var.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
-                m.weight.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
-                m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    _randomize_bn(net, seed)
     net.eval()
     torch.save(net.state_dict(), out / "weights.pt")
     rng = np.random.default_rng(seed)
@@ -134,6 +186,65 @@ def write_unet2d_package(out: str | Path, model_id: str = "demo-unet2d", in_chan
             "test_tensor": {"source": "test_output.npy", "sha256": sha256_file(out / "test_output.npy")},
             "data": {"type": "float32"}}],
         "weights": weights,
+        "config": {"bioimageio": {"reproducibility_tolerance": [{"relative_tolerance": 1e-3, "absolute_tolerance": 1e-4}]}},
+    }
+    (out / "rdf.yaml").write_text(yaml.safe_dump(rdf, sort_keys=False))
+    return out
+
+
+def write_unet3d_package(out: str | Path, model_id: str = "demo-unet3d", in_channels: int = 1, out_channels: int = 1,
+                         features=(16, 32, 64, 128), test_shape=(1, 1, 32, 64, 64), seed: int = 0) -> Path:
+    """RDF 0.5 package of a 3-D U-Net (axes b, c, z, y, x) — the 3-D model-runner / volume path."""
+    out = Path(out)
+    out.mkdir(parents=True, exist_ok=True)
+    (out / "model.py").write_text(MODEL3D_SRC)
+    mod = load_module(out / "model.py", f"pkg3d_{model_id.replace('-', '_')}")
+    kwargs = {"in_channels": in_channels, "out_channels": out_channels, "features": list(features),
+              "final_activation": "Sigmoid"}
+    torch.manual_seed(seed)
+    net = mod.UNet3d(**kwargs)
+    _randomize_bn(net, seed)
+    net.eval()
+    torch.save(net.state_dict(), out / "weights.pt")
+    rng = np.random.default_rng(seed)
+    zz, yy, xx = np.mgrid[0:test_shape[2], 0:test_shape[3], 0:test_shape[4]]
+    img = rng.normal(0, 0.2, test_shape).astype(np.float32)
+    for _ in range(10):
+        c = [rng.uniform(4, n - 4) for n in test_shape[2:]]
+        r = rng.uniform(3, 8)
+        img[:, :, ((zz - c[0]) ** 2 + (yy - c[1]) ** 2 + (xx - c[2]) ** 2) < r * r] += 1.0
+    img = (img * 200 + 300).astype(np.float32)
+    np.save(out / "test_input.npy", img)
+    x = torch.from_numpy(img)
+    x = (x - x.mean(dim=(2, 3, 4), keepdim=True)) / (x.std(dim=(2, 3, 4), keepdim=True, unbiased=False) + 1e-6)
+    with torch.no_grad():
+        y = net(x).numpy()
+    np.save(out / "test_output.npy", y)
+    (out / "README.md").write_text(f"# {model_id}\n\nDemo 3-D U-Net (random weights) for the MI355X model runner.\n")
+    space = lambda a: {"type": "space", "id": a, "size": {"min": 16, "step": 8}}  # noqa: E731
+    same = lambda a: {"type": "space", "id": a, "size": {"tensor_id": "raw", "axis_id": a}, "halo": 4}  # noqa: E731
+    rdf = {
+        "format_version": "0.5.3", "type": "model", "id": model_id, "name": f"Demo U-Net 3D ({model_id})",
+        "description": "3-D U-Net volume segmentation demo package (random weights) for the bioengine-worker-amd model runner.",
+        "authors": [{"name": "bioengine-worker-amd"}],
+        "cite": [{"text": "Cicek et al. 3D U-Net", "doi": "10.1007/978-3-319-46723-8_49"}],
+        "license": "MIT", "documentation": "README.md", "tags": ["unet", "segmentation", "3d", "demo"],
+        "inputs": [{"id": "raw", "axes": [
+            {"type": "batch"}, {"type": "channel", "channel_names": [f"c{i}" for i in range(in_channels)]},
+            space("z"), space("y"), space("x")],
+            "test_tensor": {"source": "test_input.npy", "sha256": sha256_file(out / "test_input.npy")},
+            "data": {"type": "float32"},
+            "preprocessing": [{"id": "zero_mean_unit_variance", "kwargs": {"axes": ["z", "y", "x"], "eps": 1e-6}}]}],
+        "outputs": [{"id": "probabilities", "axes": [
+            {"type": "batch"}, {"type": "channel", "channel_names": [f"p{i}" for i in range(out_channels)]},
+            same("z"), same("y"), same("x")],
+            "test_tensor": {"source": "test_output.npy", "sha256": sha256_file(out / "test_output.npy")},
+            "data": {"type": "float32"}}],
+        "weights": {"pytorch_state_dict": {
+            "source": "weights.pt", "sha256": sha256_file(out / "weights.pt"),
+            "architecture": {"source": "model.py", "sha256": sha256_file(out / "model.py"), "callable": "UNet3d",
+                             "kwargs": kwargs},
+            "pytorch_version": "2.5"}},
         "config": {"bioimageio": {"reproducibility_tolerance": [{"relative_tolerance": 1e-3, "absolute_tolerance": 1e-4}]}},
     }
     (out / "rdf.yaml").write_text(yaml.safe_dump(rdf, sort_keys=False))

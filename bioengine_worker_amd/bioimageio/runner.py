@@ -140,7 +140,8 @@ class PredictionPipeline:
     def _forward(self, xs: list[torch.Tensor]) -> list[torch.Tensor]:
         with torch.no_grad():
             if self.optimized:
-                xs = [x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last) if x.dim() == 4 else
+                fmt = {4: torch.channels_last, 5: torch.channels_last_3d}
+                xs = [x.to(torch.bfloat16).contiguous(memory_format=fmt[x.dim()]) if x.dim() in fmt else
                       x.to(torch.bfloat16) for x in xs]
             y = self.model(*xs)
         ys = list(y) if isinstance(y, (tuple, list)) else [y]

@@ -129,7 +129,8 @@ def _act_ref(x, x2, scale, shift, relu, inmode):
 
 
 def fused_conv2d_ref(x, pc: PackedConv, x2=None, scale=None, shift=None, relu=False, residual=None,
-                     inmode="none", out_nchw_f32=False, cout_valid=None, act_dtype=torch.bfloat16, post_relu=False):
+                     inmode="none", out_nchw_f32=False, cout_valid=None, act_dtype=torch.bfloat16, post_relu=False,
+                     no_bias=False):
     """PyTorch fp32 reference (and CPU path).  The activated input is rounded to ``act_dtype``
     exactly like the kernel's LDS staging, so GPU-vs-reference differences are accumulation-order only."""
     a = _act_ref(x.float(), x2, scale, shift, relu, inmode)
@@ -140,7 +141,7 @@ def fused_conv2d_ref(x, pc: PackedConv, x2=None, scale=None, shift=None, relu=Fa
         w = F.pad(w, (0, 0, 0, 0, 0, a.shape[1] - w.shape[1]))
     wq = w.to(torch.bfloat16).float() if act_dtype is not None else w
     y = F.conv2d(a, wq, None, padding=pc.ks // 2)
-    if pc.bias is not None:
+    if pc.bias is not None and not no_bias:
         y = y + pc.bias.to(y.device).view(1, -1, 1, 1)
     if out_nchw_f32:
         cv = cout_valid or pc.cout
@@ -181,9 +182,13 @@ def choose_nw(pc: PackedConv, H: int, W: int, inmode: str = "none", has_x2: bool
 
 def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=None, relu=False, residual=None,
                  inmode: str = "none", out_nchw_f32: bool = False, cout_valid: int | None = None,
-                 nw: int | None = None, post_relu: bool = False) -> torch.Tensor:
+                 nw: int | None = None, post_relu: bool = False, out: torch.Tensor | None = None,
+                 no_bias: bool = False) -> torch.Tensor:
     """Fused conv on NHWC activations.  ``x`` is [N, Hs, Ws, Cin_pad] bf16 (GPU) or any float (CPU).
-    ``relu`` applies to the pre-activation input, ``post_relu`` to the output (after bias/residual)."""
+    ``relu`` applies to the pre-activation input, ``post_relu`` to the output (after bias/residual).
+    ``out`` (bf16 NHWC, contiguous) receives the result in place of a new tensor; it may be the
+    ``residual`` itself (every output element reads its residual before it is stored).
+    ``no_bias`` skips ``pc.bias`` (partial sums of a depth-decomposed 3-D conv)."""
     N, Hs, Ws, Cin = x.shape
     if inmode == "up2":
         H, W = Hs * 2, Ws * 2
@@ -192,19 +197,28 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
     else:
         H, W = Hs, Ws
     if not x.is_cuda:
-        return fused_conv2d_ref(x, pc, x2, scale, shift, relu, residual, inmode, out_nchw_f32, cout_valid,
-                                act_dtype=torch.bfloat16 if x.dtype == torch.bfloat16 else None, post_relu=post_relu)
+        y = fused_conv2d_ref(x, pc, x2, scale, shift, relu, residual, inmode, out_nchw_f32, cout_valid,
+                             act_dtype=torch.bfloat16 if x.dtype == torch.bfloat16 else None, post_relu=post_relu,
+                             no_bias=no_bias)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
     assert x.dtype == torch.bfloat16 and x.is_contiguous(), "fused_conv2d expects contiguous NHWC bf16"
     assert Cin == pc.cin_pad, f"input channels {Cin} != packed cin {pc.cin_pad}"
     if pc.wp.device != x.device:
         pc.to(x.device)
     cout_valid = cout_valid or pc.cout
     if out_nchw_f32:
+        assert out is None
         out = torch.empty(N, cout_valid, H, W, device=x.device, dtype=torch.float32)
         cout_store = pc.cout_pad
     else:
         assert pc.cout % 4 == 0
-        out = torch.empty(N, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
+        if out is None:
+            out = torch.empty(N, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
+        else:
+            assert out.shape == (N, H, W, pc.cout) and out.dtype == torch.bfloat16 and out.is_contiguous()
         cout_store = pc.cout
     if x2 is not None:
         assert x2.shape == (N, H, W, Cin) and x2.dtype == torch.bfloat16 and x2.is_contiguous()
@@ -222,7 +236,7 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
         "be_conv2d_nhwc",
         _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns,
         int(bool(relu)) | (2 if post_relu else 0),
-        _native.ptr(pc.wp), _native.ptr(pc.bias), _native.ptr(residual), _native.ptr(out),
+        _native.ptr(pc.wp), _native.ptr(None if no_bias else pc.bias), _native.ptr(residual), _native.ptr(out),
         N, H, W, Hs, Ws, Cin, cout_store, cout_valid, pc.ks, pc.ck, pc.tco, INMODES[inmode], int(out_nchw_f32),
         int(nw or choose_nw(pc, H, W, inmode, x2 is not None)), _native.stream(x.device),
     )
