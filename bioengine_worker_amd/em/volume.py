@@ -68,27 +68,66 @@ def slice_probabilities(vol: torch.Tensor, predict, tile: int = 512, overlap: in
 
 
 def _union_find_pairs(pairs: np.ndarray, n: int) -> np.ndarray:
-    parent = np.arange(n)
+    """Connected components of the label-adjacency graph: root (smallest member) per label 0..n-1."""
+    if len(pairs) == 0:
+        return np.arange(n)
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
 
-    def find(a):
-        while parent[a] != a:
-            parent[a] = parent[parent[a]]
-            a = parent[a]
-        return a
+    g = coo_matrix((np.ones(len(pairs), np.int8), (pairs[:, 0], pairs[:, 1])), shape=(n, n))
+    _, comp = connected_components(g, directed=False)
+    first = np.full(comp.max() + 1, n, np.int64)
+    np.minimum.at(first, comp, np.arange(n))
+    return first[comp]
 
-    for a, b in pairs:
-        ra, rb = find(a), find(b)
-        if ra != rb:
-            parent[max(ra, rb)] = min(ra, rb)
-    return np.array([find(i) for i in range(n)])
+
+def _face_pairs(a: torch.Tensor, b: torch.Tensor) -> np.ndarray:
+    both = (a > 0) & (b > 0)
+    if not bool(both.any()):
+        return np.zeros((0, 2), np.int64)
+    pr = torch.stack([a[both], b[both]], 1).long()
+    return torch.unique(pr, dim=0).cpu().numpy()
+
+
+#: largest z-chunk the int32 union-find CCL kernel labels in one launch (voxel index < 2^31)
+MAX_CCL_VOXELS = 2 ** 31 - 1
+
+
+def label_local(mask: torch.Tensor, max_voxels: int = MAX_CCL_VOXELS) -> tuple[torch.Tensor, int]:
+    """Instance labels 1..n of a [Z, Y, X] mask of any size: z-chunks of < 2^31 voxels are labelled by
+    the HIP CCL and chunks touching across a z-face are merged (labels in raster order of first voxel)."""
+    Z, Y, X = mask.shape
+    cz = max(1, min(Z, max_voxels // max(1, Y * X)))
+    if cz >= Z:
+        return mito.compact_labels(ccl3d(mask).to(mask.device))
+    out = torch.empty(mask.shape, dtype=torch.int32, device=mask.device)
+    n = 0
+    pairs = []
+    for z0 in range(0, Z, cz):
+        z1 = min(Z, z0 + cz)
+        lab, k = mito.compact_labels(ccl3d(mask[z0:z1]).to(mask.device))
+        out[z0:z1] = torch.where(lab > 0, lab + n, lab)
+        if z0 > 0:
+            pairs.append(_face_pairs(out[z0 - 1], out[z0]))
+        n += k
+    pr = np.concatenate(pairs) if pairs else np.zeros((0, 2), np.int64)
+    if len(pr) == 0:
+        return out, n
+    root = _union_find_pairs(pr, n + 1)
+    uniq, dense = np.unique(root[1:], return_inverse=True)
+    table = torch.zeros(n + 1, dtype=torch.int32, device=mask.device)
+    table[1:] = torch.from_numpy((dense + 1).astype(np.int32)).to(mask.device)
+    for z0 in range(0, Z, cz):  # relabel chunk-wise (no full-volume int64 temporaries)
+        z1 = min(Z, z0 + cz)
+        out[z0:z1] = table[out[z0:z1].long()]
+    return out, int(len(uniq))
 
 
 def label_sharded(mask_slab: torch.Tensor, group=None) -> tuple[torch.Tensor, int]:
     """Globally consistent instance labels (1..N) for z-slab ``mask_slab`` of this rank."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    roots = ccl3d(mask_slab).to(mask_slab.device)
-    local, n_local = mito.compact_labels(roots)  # 1..n_local in slab raster order
+    local, n_local = label_local(mask_slab)  # 1..n_local in slab raster order
     if world == 1:
         return local, n_local
     dev = mask_slab.device
@@ -97,45 +136,42 @@ def label_sharded(mask_slab: torch.Tensor, group=None) -> tuple[torch.Tensor, in
     dist.all_gather(all_counts, counts, group=group)
     offs = np.concatenate([[0], np.cumsum([int(c) for c in all_counts])])
     glob = torch.where(local > 0, local + int(offs[rank]), local)
-    Y, X = mask_slab.shape[1:]
     faces = torch.stack([glob[0], glob[-1]]).to(torch.int64)
     gathered = [torch.zeros_like(faces) for _ in range(world)]
     dist.all_gather(gathered, faces, group=group)
     n_total = int(offs[-1])
     table = torch.zeros(n_total + 1, dtype=torch.int64, device=dev)
     if rank == 0:
-        pairs = []
-        for r in range(world - 1):
-            a, b = gathered[r][1].cpu().numpy(), gathered[r + 1][0].cpu().numpy()
-            both = (a > 0) & (b > 0)
-            if both.any():
-                pairs.append(np.unique(np.stack([a[both], b[both]], 1), axis=0))
+        pairs = [_face_pairs(gathered[r][1], gathered[r + 1][0]) for r in range(world - 1)]
         pr = np.concatenate(pairs) if pairs else np.zeros((0, 2), np.int64)
         rootmap = _union_find_pairs(pr, n_total + 1)
         # renumber roots 1..N in order of first appearance (global raster order)
         uniq, dense = np.unique(rootmap[1:], return_inverse=True)
         table[1:] = torch.from_numpy(dense + 1).to(dev)
     dist.broadcast(table, src=0, group=group)
-    out = table[glob.long()].to(torch.int32)
+    table32 = table.to(torch.int32)
+    out = torch.empty_like(glob)
+    cz = max(1, (1 << 28) // max(1, glob[0].numel()))
+    for z0 in range(0, glob.shape[0], cz):
+        out[z0:z0 + cz] = table32[glob[z0:z0 + cz].long()]
     return out, int(table.max())
 
 
 def instance_stats(labels: torch.Tensor, n: int, z_offset: int = 0, group=None) -> dict:
-    """Per-instance voxel count and centroid (z, y, x), all-reduced across ranks."""
+    """Per-instance voxel count and centroid (z, y, x), all-reduced across ranks (z-chunked, so a
+    multi-GB label slab never materialises full-size index temporaries)."""
     dev = labels.device
-    l = labels.reshape(-1).long()
-    fg = l > 0
     Z, Y, X = labels.shape
-    idx = torch.nonzero(fg).squeeze(1)
-    zz = (idx // (Y * X)).double() + z_offset
-    yy = ((idx // X) % Y).double()
-    xx = (idx % X).double()
     acc = torch.zeros(4, n + 1, dtype=torch.float64, device=dev)
-    lab = l[idx]
-    acc[0].index_add_(0, lab, torch.ones_like(zz))
-    acc[1].index_add_(0, lab, zz)
-    acc[2].index_add_(0, lab, yy)
-    acc[3].index_add_(0, lab, xx)
+    cz = max(1, (1 << 27) // max(1, Y * X))
+    for z0 in range(0, Z, cz):
+        l = labels[z0:z0 + cz].reshape(-1).long()
+        idx = torch.nonzero(l > 0).squeeze(1)
+        lab = l[idx]
+        acc[0].index_add_(0, lab, torch.ones(idx.numel(), dtype=torch.float64, device=dev))
+        acc[1].index_add_(0, lab, (idx // (Y * X)).double() + (z0 + z_offset))
+        acc[2].index_add_(0, lab, ((idx // X) % Y).double())
+        acc[3].index_add_(0, lab, (idx % X).double())
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(acc, group=group)
     acc = acc.cpu().numpy()
