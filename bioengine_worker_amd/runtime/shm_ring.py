@@ -1,0 +1,126 @@
+"""Python face of the C++ shared-memory SPSC ring (``csrc/runtime/shm_ring.cpp``).
+
+The serving runtime pairs every process replica with two rings (router -> replica and
+replica -> router).  Request/response *headers* (pickle protocol 5) still travel over the replica's
+Unix socket, while the out-of-band buffers — the ndarrays / tensors of images, volumes and masks —
+are published into the ring as one atomic multi-frame message, so a 64 MiB volume crosses the
+process boundary as one memcpy in and one memcpy out instead of socket chunking through the
+kernel.  Replaces the Ray object store between the reference's proxy, entry and runtime
+deployments (reference ``bioengine/apps/proxy_deployment.py:522-554``,
+``apps/model-runner/entry_deployment.py`` → ``runtime_deployment.py`` handle calls).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import uuid
+
+import numpy as np
+
+from ..ops import _native
+
+EAGAIN_TIMEOUT, TOO_LARGE, CLOSED = -2, -3, -4
+
+
+class RingClosed(RuntimeError):
+    pass
+
+
+def _addr(buf) -> int:
+    """Address of a (possibly read-only) contiguous buffer without copying it."""
+    a = np.frombuffer(buf, dtype=np.uint8)
+    return a.ctypes.data if a.size else 0
+
+
+class ShmRing:
+    """One direction of a bulk-data channel.  ``create`` on the owning side, ``open`` on the peer;
+    exactly one thread writes and one thread reads."""
+
+    def __init__(self, handle: int, name: str, owner: bool):
+        self._h = ctypes.c_void_p(handle)
+        self.name = name
+        self.owner = owner
+        self._rt = _native.runtime()
+
+    @classmethod
+    def create(cls, capacity: int = 256 << 20, name: str | None = None) -> "ShmRing":
+        name = name or f"/be-ring-{os.getpid()}-{uuid.uuid4().hex[:10]}"
+        h = ctypes.c_void_p()
+        rc = _native.runtime().be_rt_ring_create(name.encode(), int(capacity), ctypes.byref(h))
+        if rc != 0:
+            raise OSError(-rc, f"shm ring create {name}: {os.strerror(-rc)}")
+        return cls(h.value, name, True)
+
+    @classmethod
+    def open(cls, name: str) -> "ShmRing":
+        h = ctypes.c_void_p()
+        rc = _native.runtime().be_rt_ring_open(name.encode(), ctypes.byref(h))
+        if rc != 0:
+            raise OSError(-rc, f"shm ring open {name}: {os.strerror(-rc)}")
+        return cls(h.value, name, False)
+
+    # ------------------------------------------------------------------ producer
+    @property
+    def capacity(self) -> int:
+        return self.stats()["capacity"]
+
+    def fits(self, lens) -> bool:
+        return sum(8 + ((int(n) + 7) & ~7) for n in lens) <= self.capacity
+
+    def write(self, bufs, timeout_s: float | None = 60.0) -> None:
+        """Publish ``bufs`` (bytes-like objects) as one message; blocks while the ring is full."""
+        n = len(bufs)
+        ptrs = (ctypes.c_void_p * max(1, n))(*[_addr(b) for b in bufs])
+        lens = (ctypes.c_int64 * max(1, n))(*[memoryview(b).nbytes for b in bufs])
+        rc = self._rt.be_rt_ring_write(self._h, ptrs, lens, n, -1 if timeout_s is None else int(timeout_s * 1e6))
+        if rc == TOO_LARGE:
+            raise ValueError(f"message of {sum(lens[:n])} bytes exceeds ring capacity {self.capacity}")
+        if rc == EAGAIN_TIMEOUT:
+            raise TimeoutError(f"shm ring {self.name} full for {timeout_s}s")
+        if rc == CLOSED:
+            raise RingClosed(self.name)
+        if rc != 0:
+            raise OSError(-rc, f"shm ring write: {os.strerror(-rc)}")
+
+    # ------------------------------------------------------------------ consumer
+    def read(self, timeout_s: float | None = 60.0) -> bytearray:
+        """Next frame's payload as a fresh (writable) bytearray."""
+        n = ctypes.c_int64()
+        rc = self._rt.be_rt_ring_next_len(self._h, ctypes.byref(n), -1 if timeout_s is None else int(timeout_s * 1e6))
+        if rc == EAGAIN_TIMEOUT:
+            raise TimeoutError(f"shm ring {self.name} empty for {timeout_s}s")
+        if rc == CLOSED:
+            raise RingClosed(self.name)
+        if rc != 0:
+            raise OSError(-rc, f"shm ring wait: {os.strerror(-rc)}")
+        out = bytearray(n.value)
+        dst = (ctypes.c_char * len(out)).from_buffer(out) if out else None
+        rc = self._rt.be_rt_ring_read(self._h, dst, n.value)
+        if rc != 0:
+            raise OSError(-rc, "shm ring read")
+        return out
+
+    # ------------------------------------------------------------------ lifecycle
+    def stats(self) -> dict:
+        o = (ctypes.c_int64 * 5)()
+        self._rt.be_rt_ring_stats(self._h, o)
+        return {"capacity": o[0], "queued_bytes": o[1], "frames": o[2], "bytes": o[3], "closed": bool(o[4])}
+
+    def unlink(self) -> None:
+        """Remove the name (mappings stay valid); call once both sides have opened it."""
+        self._rt.be_rt_ring_unlink(self.name.encode())
+
+    def shutdown(self) -> None:
+        if self._h:
+            self._rt.be_rt_ring_shutdown(self._h)
+
+    def close(self) -> None:
+        if self._h:
+            self._rt.be_rt_ring_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass

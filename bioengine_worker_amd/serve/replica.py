@@ -160,30 +160,54 @@ def _run_with_ctx(ctx, model_id, fn, args, kwargs):
 # ====================================================================== process replicas
 
 
-def dumps(obj) -> list[bytes]:
+def dumps(obj) -> list:
+    """Pickle-5 header + the out-of-band buffers as zero-copy memoryviews."""
     import cloudpickle
 
     bufs: list = []
     head = cloudpickle.dumps(obj, protocol=5, buffer_callback=bufs.append)
-    return [head] + [bytes(b.raw()) if hasattr(b, "raw") else bytes(b) for b in bufs]
+    return [head] + [b.raw() if hasattr(b, "raw") else memoryview(b) for b in bufs]
 
 
-def loads(frames: list[bytes]):
+def loads(frames: list):
     return pickle.loads(frames[0], buffers=frames[1:])
 
 
-def send_frames(conn, lock: threading.Lock, obj):
+#: out-of-band payloads at least this large travel through the shared-memory ring
+RING_MIN_BYTES = 2 << 20
+
+
+def send_frames(conn, lock: threading.Lock, obj, ring=None):
+    """Send ``obj``; with a ``ring`` (:class:`~bioengine_worker_amd.runtime.shm_ring.ShmRing`) the
+    out-of-band buffers go through shared memory and only the pickle header crosses the socket.
+    Ring write and socket send happen under the same lock, so both lanes stay in message order."""
     frames = dumps(obj)
+    bufs = frames[1:]
     with lock:
+        if ring is not None and bufs:
+            lens = [b.nbytes for b in bufs]
+            if sum(lens) >= RING_MIN_BYTES and ring.fits(lens):
+                ring.write(bufs)
+                conn.send(("ring", len(frames)))
+                conn.send_bytes(frames[0])
+                return
         conn.send(len(frames))
         for f in frames:
             conn.send_bytes(f)
 
 
-def recv_frames(conn):
+def recv_frames(conn, ring=None):
     n = conn.recv()
+    if isinstance(n, tuple):  # ("ring", n_frames): header on the socket, buffers in the ring
+        head = conn.recv_bytes()
+        return loads([head] + [ring.read() for _ in range(n[1] - 1)])
     frames = [conn.recv_bytes() for _ in range(n)]
     return loads(frames)
+
+
+def ring_capacity() -> int:
+    """Per-direction ring size (``BE_REPLICA_RING_MB``, default 128; 0 disables the rings)."""
+    return int(float(os.environ.get("BE_REPLICA_RING_MB", "128")) * (1 << 20))
 
 
 class ProcessReplica(ReplicaBase):
@@ -200,6 +224,28 @@ class ProcessReplica(ReplicaBase):
         self.send_lock = threading.Lock()
         self.proc = None
         self.conn = None
+        self.tx = self.rx = None  # shared-memory bulk lanes (router->replica, replica->router)
+
+    def _make_rings(self, env: dict) -> None:
+        cap = ring_capacity()
+        if cap <= 0:
+            return
+        try:
+            from ..runtime.shm_ring import ShmRing
+
+            self.tx, self.rx = ShmRing.create(cap), ShmRing.create(cap)
+        except Exception:  # runtime library unavailable or /dev/shm exhausted: socket-only
+            self._drop_rings()
+            return
+        env["BE_REPLICA_RING_RX"] = self.tx.name  # the child's receive lane is our transmit lane
+        env["BE_REPLICA_RING_TX"] = self.rx.name
+
+    def _drop_rings(self) -> None:
+        for r in (self.tx, self.rx):
+            if r is not None:
+                r.unlink()
+                r.shutdown()
+        self.tx = self.rx = None
 
     async def start(self):
         from multiprocessing.connection import Listener
@@ -216,6 +262,7 @@ class ProcessReplica(ReplicaBase):
         env["BE_REPLICA_SOCK"] = sock
         env["BE_REPLICA_KEY"] = key.hex()
         env["BE_REPLICA_TAG"] = self.tag
+        self._make_rings(env)
         root = str(Path(__file__).resolve().parents[2])
         env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         logf = open(self.log_file, "ab", buffering=0)
@@ -227,6 +274,7 @@ class ProcessReplica(ReplicaBase):
             self.conn = await asyncio.wait_for(asyncio.to_thread(listener.accept), timeout=120)
         except Exception as e:
             self._kill()
+            self._drop_rings()
             self.state = DEAD
             self.error = f"replica process failed to connect: {e}"
             raise RuntimeError(self.error) from e
@@ -236,12 +284,16 @@ class ProcessReplica(ReplicaBase):
                 os.unlink(sock)
             except OSError:
                 pass
+        for r in (self.tx, self.rx):  # the child opened both before connecting: drop the names
+            if r is not None:
+                r.unlink()
         self._reader = threading.Thread(target=self._read_loop, daemon=True)
         self._reader.start()
         fut = self.loop.create_future()
         self.pending[0] = fut
         await asyncio.to_thread(send_frames, self.conn, self.send_lock,
-                                ("init", self.cls, self.args, self.kwargs, self.app, self.dep, self.tag, self.gpu_ids))
+                                ("init", self.cls, self.args, self.kwargs, self.app, self.dep, self.tag, self.gpu_ids),
+                                self.tx)
         ok, err = await fut
         if not ok:
             self.state = DEAD
@@ -253,7 +305,7 @@ class ProcessReplica(ReplicaBase):
     def _read_loop(self):
         while True:
             try:
-                msg = recv_frames(self.conn)
+                msg = recv_frames(self.conn, self.rx)
             except (EOFError, OSError):
                 break
             except Exception as e:  # undecodable result: fail the request that produced it
@@ -288,7 +340,7 @@ class ProcessReplica(ReplicaBase):
         except BaseException as e:  # noqa: BLE001
             out = ("hresult", rid, False, e)
         try:
-            await asyncio.to_thread(send_frames, self.conn, self.send_lock, out)
+            await asyncio.to_thread(send_frames, self.conn, self.send_lock, out, self.tx)
         except Exception:
             pass
 
@@ -300,6 +352,9 @@ class ProcessReplica(ReplicaBase):
             if not fut.done():
                 fut.set_exception(RuntimeError(f"replica {self.tag} died: {self.error}"))
         self.pending.clear()
+        for r in (self.tx, self.rx):  # release a sender blocked on a ring the dead child no longer drains
+            if r is not None:
+                r.shutdown()
 
     async def call(self, method: str, args, kwargs, model_id: str = ""):
         if self.state == DEAD:
@@ -309,7 +364,8 @@ class ProcessReplica(ReplicaBase):
         self.pending[rid] = fut
         self.ongoing += 1
         try:
-            await asyncio.to_thread(send_frames, self.conn, self.send_lock, ("call", rid, method, args, kwargs, model_id))
+            await asyncio.to_thread(send_frames, self.conn, self.send_lock, ("call", rid, method, args, kwargs, model_id),
+                                    self.tx)
             return await fut
         finally:
             self.ongoing -= 1

@@ -17,8 +17,9 @@ import traceback
 
 
 class _ChildRouter:
-    def __init__(self, conn, lock, loop):
+    def __init__(self, conn, lock, loop, ring=None):
         self.conn = conn
+        self.ring = ring
         self.lock = lock
         self.loop = loop
         self.rids = itertools.count(1)
@@ -30,7 +31,8 @@ class _ChildRouter:
         rid = next(self.rids)
         fut = self.loop.create_future()
         self.pending[rid] = fut
-        await asyncio.to_thread(send_frames, self.conn, self.lock, ("hcall", rid, app, dep, method, args, kwargs, model_id))
+        await asyncio.to_thread(send_frames, self.conn, self.lock, ("hcall", rid, app, dep, method, args, kwargs, model_id),
+                                self.ring)
         return await fut
 
 
@@ -43,17 +45,22 @@ async def _main():
 
     sock = os.environ["BE_REPLICA_SOCK"]
     key = bytes.fromhex(os.environ["BE_REPLICA_KEY"])
+    rx = tx = None
+    if os.environ.get("BE_REPLICA_RING_RX"):  # open both lanes before connecting (parent unlinks after)
+        from ..runtime.shm_ring import ShmRing
+
+        rx, tx = ShmRing.open(os.environ["BE_REPLICA_RING_RX"]), ShmRing.open(os.environ["BE_REPLICA_RING_TX"])
     conn = Client(sock, family="AF_UNIX", authkey=key)
     lock = threading.Lock()
     loop = asyncio.get_running_loop()
-    router = _ChildRouter(conn, lock, loop)
+    router = _ChildRouter(conn, lock, loop, tx)
     ctrl_mod._set_child_router(router)
     inbox: asyncio.Queue = asyncio.Queue()
 
     def reader():
         while True:
             try:
-                msg = recv_frames(conn)
+                msg = recv_frames(conn, rx)
             except (EOFError, OSError):
                 loop.call_soon_threadsafe(inbox.put_nowait, ("stop",))
                 return
@@ -94,9 +101,9 @@ async def _main():
             rctx.reset_model_id(mtok)
             rctx.reset_current(tok)
         try:
-            await asyncio.to_thread(send_frames, conn, lock, out)
+            await asyncio.to_thread(send_frames, conn, lock, out, tx)
         except Exception as e:  # result not picklable
-            await asyncio.to_thread(send_frames, conn, lock, ("result", rid, False, RuntimeError(f"unpicklable result: {e}")))
+            await asyncio.to_thread(send_frames, conn, lock, ("result", rid, False, RuntimeError(f"unpicklable result: {e}")), tx)
 
     while True:
         msg = await inbox.get()

@@ -1,0 +1,69 @@
+"""Native host runtime (csrc/runtime): sanitizer builds + the shared-memory ring's Python face.
+
+* ASan+UBSan and TSan builds of every runtime source with the C++ self-test driver
+  (``tools/sanitize_runtime.py``; SURVEY.md §5 race detection / sanitizers).
+* ``ShmRing`` across two Python processes (spawned child opens the ring by name, echoes frames back
+  through a second ring).
+"""
+import multiprocessing as mp
+import os
+import shutil
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+@pytest.mark.parametrize("mode", ["asan", "tsan"])
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_runtime_sanitizers(mode, capsys):
+    import sanitize_runtime
+
+    rc = sanitize_runtime.run(mode)
+    out = capsys.readouterr().out
+    assert rc == 0, out
+    assert "runtime selftest ok" in out
+
+
+def _echo(rx_name, tx_name, n):
+    sys.path.insert(0, ROOT)
+    from bioengine_worker_amd.runtime.shm_ring import ShmRing
+
+    rx, tx = ShmRing.open(rx_name), ShmRing.open(tx_name)
+    for _ in range(n):
+        a = rx.read(timeout_s=30)
+        b = rx.read(timeout_s=30)
+        tx.write([b, a])  # swap the two frames of each message
+
+
+def test_shm_ring_cross_process():
+    from bioengine_worker_amd.runtime.shm_ring import RingClosed, ShmRing
+
+    a2b, b2a = ShmRing.create(1 << 20), ShmRing.create(1 << 20)
+    p = mp.get_context("spawn").Process(target=_echo, args=(a2b.name, b2a.name, 50))
+    p.start()
+    rng = np.random.default_rng(0)
+    try:
+        for i in range(50):
+            x = rng.integers(0, 255, size=int(rng.integers(0, 300_000)), dtype=np.uint8)
+            y = rng.integers(0, 255, size=17 * i, dtype=np.uint8)
+            a2b.write([x, memoryview(y)])
+            assert bytes(b2a.read(timeout_s=30)) == y.tobytes()
+            assert bytes(b2a.read(timeout_s=30)) == x.tobytes()
+    finally:
+        p.join(30)
+        a2b.unlink()
+        b2a.unlink()
+    assert p.exitcode == 0
+    st = a2b.stats()
+    assert st["frames"] == 100 and st["queued_bytes"] == 0
+    with pytest.raises(ValueError):
+        a2b.write([np.zeros(2 << 20, np.uint8)])
+    with pytest.raises(TimeoutError):
+        a2b.read(timeout_s=0.01)
+    a2b.shutdown()
+    with pytest.raises(RingClosed):
+        a2b.write([b"x"])

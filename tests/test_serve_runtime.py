@@ -220,3 +220,50 @@ def test_remote_tasks_thread_and_isolated():
 
     with pytest.raises(RayTaskError):
         ray.get(ray.remote(bad).remote())
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0})
+class Volume:
+    async def scale(self, arr, k):
+        return arr * k, {"sum": float(arr.sum())}
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0})
+class VolumeEntry:
+    def __init__(self, volume: DeploymentHandle):
+        self.volume = volume
+
+    async def __call__(self, arr):
+        return await self.volume.scale.remote(arr, 2)
+
+
+@pytest.mark.unit
+def test_process_replica_bulk_data_through_shm_rings(monkeypatch):
+    """ndarray payloads above RING_MIN_BYTES cross router<->replica through the C++ shared-memory
+    rings (both directions, nested handle calls too); the ring names are unlinked once the child
+    has mapped them, so nothing is left in /dev/shm."""
+    import numpy as np
+
+    monkeypatch.setenv("BIOENGINE_REPLICA_MODE", "process")
+    monkeypatch.setenv("BE_REPLICA_RING_MB", "16")
+    before = {f for f in os.listdir("/dev/shm") if f.startswith("be-ring-")}
+
+    async def main():
+        h = await serve.run(VolumeEntry.bind(Volume.bind()), name="vol")
+        rng = np.random.default_rng(0)
+        for shape in [(16, 16), (32, 256, 256), (3, 1000, 1000)]:  # socket-only, ring, > ring (fallback)
+            a = rng.standard_normal(shape).astype(np.float32)
+            out, st = await h.remote(a)
+            np.testing.assert_array_equal(out, a * 2)
+            assert st["sum"] == pytest.approx(float(a.sum()), rel=1e-5)
+        dss = ctrl_mod.get_controller().apps["vol"].deployments
+        frames = 0
+        for ds in dss.values():
+            r = ds.running()[0]
+            assert r.tx is not None and r.rx is not None
+            frames += r.tx.stats()["frames"] + r.rx.stats()["frames"]
+        assert frames >= 4  # request + result of the 8 MiB call, on both hops
+        assert not ({f for f in os.listdir("/dev/shm") if f.startswith("be-ring-")} - before)
+        await serve.delete("vol")
+
+    asyncio.run(main())

@@ -3,9 +3,10 @@
 
 * ``libbe_hip.so``     — every ``csrc/kernels/*.hip`` compiled with ``hipcc --offload-arch=gfx950``
   (CDNA4 only; no other targets, no CUDA, no hipify).
-* ``libbe_runtime.so`` — the host runtime in ``csrc/runtime/*.cpp`` (request batcher, shared-memory
-  ring, tile planner, CPU mask post-processing) compiled with g++; it has no GPU dependency so it
-  also runs in CPU-only CI.
+* ``libbe_runtime.so`` — the host runtime in ``csrc/runtime/*.cpp`` (cross-process shared-memory
+  SPSC ring used as the router <-> replica bulk-data lane, serial EM post-processing: priority-flood
+  watershed and peak spacing) compiled with g++; it has no GPU dependency so it also runs in
+  CPU-only CI.  ``tools/sanitize_runtime.py`` builds the same sources under ASan/UBSan and TSan.
 
 Objects are cached under ``build/`` keyed by source mtime + flags, so rebuilding after editing one
 kernel recompiles only that file.  Usage: ``python tools/build_native.py [--only hip|runtime] [-j N]``.
