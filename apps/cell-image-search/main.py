@@ -283,6 +283,10 @@ class CellImageSearch:
             exc = t.exception()
             if exc:
                 st["status"], st["message"] = "failed", str(exc)
+        elif t is not None and not t.done() and st.get("status") == "completed":
+            # the worker thread wrote "completed"; the new index is still being loaded into this
+            # replica — report completion only once search can see it
+            st["status"], st["message"] = "building_index", "Loading the new index"
         return st
 
     @schema_method

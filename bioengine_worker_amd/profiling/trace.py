@@ -26,6 +26,8 @@ import threading
 import time
 from typing import Any
 
+from ..runtime import faults as _faults
+
 _enabled = os.environ.get("BIOENGINE_TRACE", "0") not in ("0", "", "false")
 _events: list[dict] = []
 _gpu_pending: list = []
@@ -72,6 +74,7 @@ def request(name: str = "request", **args):
 
 @contextlib.contextmanager
 def span(name: str, cat: str = "stage", cuda: bool = False, **args):
+    _faults.point(name)  # stage boundary: deadline check + fault-injection hook (runtime/faults.py)
     if not _enabled:
         yield
         return

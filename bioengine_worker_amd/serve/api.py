@@ -43,6 +43,9 @@ class DeploymentConfig:
     logging_config: Any = None
     placement_group_bundles: Any = None
     max_replicas_per_node: int | None = None
+    #: per-request deadline enforced by the router (bioengine extension; None -> env
+    #: ``BIOENGINE_REQUEST_TIMEOUT_S`` or no deadline).  See ``runtime/faults.py``.
+    request_timeout_s: float | None = None
 
     def num_cpus(self) -> float:
         return float(self.ray_actor_options.get("num_cpus", 1) or 0)

@@ -28,6 +28,7 @@ from dataclasses import dataclass, field
 
 from .api import Application, DeploymentConfig
 from .handle import DeploymentHandle
+from ..runtime import faults
 from .replica import DEAD, RUNNING, STARTING, STOPPING, LocalReplica, ProcessReplica
 
 
@@ -139,6 +140,7 @@ class DeploymentState:
         self.restarts = 0
         self.history: list[dict] = []  # dead replicas (for logs of previous replicas)
         self.requests_total = 0
+        self.deadline_exceeded = 0
         self.latency = collections.deque(maxlen=2048)
         self._stopping = False
 
@@ -266,9 +268,41 @@ class DeploymentState:
             raise DeploymentUnavailableError(f"deployment '{self.name}' has no running replicas")
         w = _Waiter(asyncio.get_running_loop().create_future())
         self.waiters.append(w)
-        return await w.fut
+        try:
+            return await w.fut
+        except asyncio.CancelledError:  # deadline / caller gave up while queued
+            try:
+                self.waiters.remove(w)
+            except ValueError:
+                pass
+            if w.fut.done() and not w.fut.cancelled():  # a slot was reserved for us: hand it on
+                w.fut.result().ongoing -= 1
+                self._wake()
+            raise
+
+    def request_timeout(self) -> float | None:
+        t = self.cfg.request_timeout_s
+        if t is None and os.environ.get("BIOENGINE_REQUEST_TIMEOUT_S"):
+            t = float(os.environ["BIOENGINE_REQUEST_TIMEOUT_S"])
+        return t if t and t > 0 else None
 
     async def call(self, method, args, kwargs, model_id=""):
+        """Route one request: admission (queue for a free replica slot), then the replica call,
+        both bounded by the request deadline (the caller's, tightened by ``request_timeout_s``)."""
+        with faults.deadline_scope(self.request_timeout()) as deadline:
+            if deadline is None:
+                return await self._call(method, args, kwargs, model_id)
+            left = deadline - time.time()
+            try:
+                if left <= 0:
+                    raise asyncio.TimeoutError
+                return await asyncio.wait_for(self._call(method, args, kwargs, model_id), left)
+            except asyncio.TimeoutError:
+                self.deadline_exceeded += 1
+                raise faults.DeadlineExceeded(
+                    f"request {self.name}.{method} exceeded its deadline") from None
+
+    async def _call(self, method, args, kwargs, model_id=""):
         from ..profiling import trace
 
         with trace.span("router.admission", cat="router", deployment=self.name):
@@ -360,7 +394,7 @@ class DeploymentState:
         counts = collections.Counter(r.state for r in self.replicas)
         return {"status": self.status, "message": self.message, "replica_states": dict(counts),
                 "replicas": [r.info() for r in self.replicas], "target_replicas": self.target,
-                "ongoing_requests": self.ongoing, "requests_total": self.requests_total,
+                "ongoing_requests": self.ongoing, "requests_total": self.requests_total, "deadline_exceeded": self.deadline_exceeded,
                 "latency_ms": _pcts(self.latency)}
 
 

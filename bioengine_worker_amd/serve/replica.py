@@ -30,6 +30,7 @@ import time
 import uuid
 from pathlib import Path
 
+from ..runtime import faults
 from . import context as rctx
 
 STARTING, RUNNING, UNHEALTHY, STOPPING, DEAD = "STARTING", "RUNNING", "UNHEALTHY", "STOPPING", "DEAD"
@@ -65,6 +66,7 @@ class ReplicaBase:
         self.error: str | None = None
         self.health_failures = 0
         self.node_id = "head"
+        self.inflight = faults.InflightTable()  # watchdog: calls and their deadlines
 
     @property
     def replica_id(self) -> str:
@@ -113,17 +115,32 @@ class LocalReplica(ReplicaBase):
         tok = rctx.set_current(self._ctx)
         mtok = rctx.set_model_id(model_id)
         try:
-            if inspect.iscoroutinefunction(fn) or inspect.iscoroutinefunction(getattr(fn, "__func__", None)):
-                res = await fn(*args, **kwargs)
-            else:
-                res = await asyncio.to_thread(_run_with_ctx, self._ctx, model_id, fn, args, kwargs)
-            return await _resolve_result(res)
+            faults.point(f"replica_entry.{method}")
+            return await self._invoke(fn, method, model_id, args, kwargs)
         finally:
             rctx.reset_model_id(mtok)
             rctx.reset_current(tok)
             self.ongoing -= 1
 
+    async def _invoke(self, fn, method, model_id, args, kwargs):
+        if inspect.iscoroutinefunction(fn) or inspect.iscoroutinefunction(getattr(fn, "__func__", None)):
+            res = await fn(*args, **kwargs)  # cancelled at the deadline
+        else:
+            # a thread cannot be cancelled: the thread itself holds the watchdog entry, so a call
+            # still running after the router gave up on it keeps counting as wedged
+            deadline = faults.current_deadline()
+
+            def tracked(*a, **k):
+                with self.inflight.track(method, deadline):
+                    return fn(*a, **k)
+
+            res = await asyncio.to_thread(_run_with_ctx, self._ctx, model_id, tracked, args, kwargs)
+        return await _resolve_result(res)
+
     async def check_health(self):
+        self.inflight.check()
+        if self.gpu_ids:
+            await asyncio.to_thread(builtin_gpu_check)
         fn = getattr(self.obj, "check_health", None)
         if fn is None:
             return True
@@ -145,6 +162,16 @@ class LocalReplica(ReplicaBase):
     def logs(self, tail: int = 100) -> list[str]:
         buf = rctx.log_buffer(self.tag)
         return list(buf)[-tail:] if tail > 0 else list(buf)
+
+
+def builtin_gpu_check(timeout_s: float | None = None) -> None:
+    """GPU-hang watchdog of the replica health check: a tiny kernel on a private stream must finish
+    within ``BIOENGINE_GPU_PROBE_TIMEOUT_S``.  Only probes a process that already initialised HIP
+    (never brings up a GPU context in a CPU-only replica)."""
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_available() or not torch.cuda.is_initialized():
+        return
+    faults.gpu_probe(timeout_s=timeout_s or float(os.environ.get("BIOENGINE_GPU_PROBE_TIMEOUT_S", "10")))
 
 
 def _run_with_ctx(ctx, model_id, fn, args, kwargs):
@@ -328,14 +355,15 @@ class ProcessReplica(ReplicaBase):
                 else:
                     fut.set_exception(val if isinstance(val, BaseException) else RuntimeError(str(val)))
         elif kind == "hcall":
-            _, rid, app, dep, method, args, kwargs, model_id = msg
-            asyncio.ensure_future(self._serve_hcall(rid, app, dep, method, args, kwargs, model_id))
+            _, rid, app, dep, method, args, kwargs, model_id, deadline = msg
+            asyncio.ensure_future(self._serve_hcall(rid, app, dep, method, args, kwargs, model_id, deadline))
 
-    async def _serve_hcall(self, rid, app, dep, method, args, kwargs, model_id):
+    async def _serve_hcall(self, rid, app, dep, method, args, kwargs, model_id, deadline=None):
         from .controller import get_router
 
         try:
-            val = await get_router().call(app, dep, method, args, kwargs, model_id)
+            with faults.deadline_scope(deadline=deadline):
+                val = await get_router().call(app, dep, method, args, kwargs, model_id)
             out = ("hresult", rid, True, val)
         except BaseException as e:  # noqa: BLE001
             out = ("hresult", rid, False, e)
@@ -364,15 +392,17 @@ class ProcessReplica(ReplicaBase):
         self.pending[rid] = fut
         self.ongoing += 1
         try:
-            await asyncio.to_thread(send_frames, self.conn, self.send_lock, ("call", rid, method, args, kwargs, model_id),
-                                    self.tx)
-            return await fut
+            with self.inflight.track(method, faults.current_deadline()):
+                await asyncio.to_thread(send_frames, self.conn, self.send_lock,
+                                        ("call", rid, method, args, kwargs, model_id, faults.current_deadline()), self.tx)
+                return await fut
         finally:
             self.ongoing -= 1
 
     async def check_health(self):
         if self.proc is None or self.proc.poll() is not None:
             raise RuntimeError(f"replica process is not running (exit code {self.proc.poll() if self.proc else None})")
+        self.inflight.check()
         await self.call("__be_check_health__", [], {})
         return True
 

@@ -26,12 +26,14 @@ class _ChildRouter:
         self.pending: dict[int, asyncio.Future] = {}
 
     async def call(self, app, dep, method, args, kwargs, model_id=""):
+        from ..runtime import faults as _faults
         from .replica import send_frames
 
         rid = next(self.rids)
         fut = self.loop.create_future()
         self.pending[rid] = fut
-        await asyncio.to_thread(send_frames, self.conn, self.lock, ("hcall", rid, app, dep, method, args, kwargs, model_id),
+        await asyncio.to_thread(send_frames, self.conn, self.lock, ("hcall", rid, app, dep, method, args, kwargs, model_id,
+                                                                    _faults.current_deadline()),
                                 self.ring)
         return await fut
 
@@ -73,11 +75,24 @@ async def _main():
     obj = None
     ctx = None
 
-    async def handle_call(rid, method, args, kwargs, model_id):
+    from ..runtime import faults
+    from .replica import builtin_gpu_check
+
+    inflight = faults.InflightTable()
+
+    async def handle_call(rid, method, args, kwargs, model_id, deadline=None):
+        # never cancelled in the child: the entry stays until the user code returns
+        with faults.deadline_scope(deadline=deadline):
+            with inflight.track(method, deadline):
+                await _handle_call(rid, method, args, kwargs, model_id)
+
+    async def _handle_call(rid, method, args, kwargs, model_id):
         tok = rctx.set_current(ctx)
         mtok = rctx.set_model_id(model_id)
         try:
             if method == "__be_check_health__":
+                inflight.check()  # a call wedged past its deadline fails the replica
+                await asyncio.to_thread(builtin_gpu_check)  # GPU-hang watchdog
                 fn = getattr(obj, "check_health", None)
                 res = None
                 if fn is not None:
@@ -85,6 +100,7 @@ async def _main():
                     if inspect.isawaitable(res):
                         res = await res
             else:
+                faults.point(f"replica_entry.{method}")
                 fn = getattr(obj, method)
                 if inspect.iscoroutinefunction(fn):
                     res = await fn(*args, **kwargs)
@@ -122,8 +138,8 @@ async def _main():
             finally:
                 rctx.reset_current(tok)
         elif kind == "call":
-            _, rid, method, args, kwargs, model_id = msg
-            asyncio.ensure_future(handle_call(rid, method, args, kwargs, model_id))
+            _, rid, method, args, kwargs, model_id, deadline = msg
+            asyncio.ensure_future(handle_call(rid, method, args, kwargs, model_id, deadline))
         elif kind == "hresult":
             _, rid, ok, val = msg
             fut = router.pending.pop(rid, None)

@@ -246,7 +246,6 @@ def test_process_replica_bulk_data_through_shm_rings(monkeypatch):
 
     monkeypatch.setenv("BIOENGINE_REPLICA_MODE", "process")
     monkeypatch.setenv("BE_REPLICA_RING_MB", "16")
-    before = {f for f in os.listdir("/dev/shm") if f.startswith("be-ring-")}
 
     async def main():
         h = await serve.run(VolumeEntry.bind(Volume.bind()), name="vol")
@@ -261,9 +260,9 @@ def test_process_replica_bulk_data_through_shm_rings(monkeypatch):
         for ds in dss.values():
             r = ds.running()[0]
             assert r.tx is not None and r.rx is not None
+            assert not os.path.exists("/dev/shm" + r.tx.name) and not os.path.exists("/dev/shm" + r.rx.name)
             frames += r.tx.stats()["frames"] + r.rx.stats()["frames"]
         assert frames >= 4  # request + result of the 8 MiB call, on both hops
-        assert not ({f for f in os.listdir("/dev/shm") if f.startswith("be-ring-")} - before)
         await serve.delete("vol")
 
     asyncio.run(main())
