@@ -203,6 +203,24 @@ class CellposeTrainer:
         return {"loss": float(loss), "tp": tp, "fp": fp, "fn": fn, "tn": tn, "precision": prec, "recall": rec,
                 "f1": 2 * prec * rec / max(1e-12, prec + rec), "iou": tp / max(1, tp + fp + fn)}
 
+    def rebind(self, world_size: int, rank: int, group=None) -> None:
+        """Adopt a new data-parallel world (elastic shrink, ``parallel/elastic.py``): rebuild the
+        bucketed all-reduce for the new group and make every rank's weights, AdamW moments and BN
+        buffers identical to the new rank 0's."""
+        self.ar.remove()
+        self.world, self.rank = int(world_size), int(rank)
+        self.fp.zero_grad()
+        self.ar = BucketedAllReduce(self.fp, group=group, bucket_mb=self.cfg.bucket_mb,
+                                    comm_dtype=torch.bfloat16 if self.cfg.comm_bf16 else None)
+        self._graph = self._graph_io = None
+        if self.world > 1:
+            broadcast_params(self.fp, 0, group)
+            for t in [self.m, self.v] + [b for b in self.net.buffers() if b.is_floating_point()]:
+                dist.broadcast(t, src=0, group=group)
+            st = torch.tensor([self.step_count], dtype=torch.int64, device=self.fp.flat.device)
+            dist.broadcast(st, src=0, group=group)
+            self.step_count = int(st.item())
+
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:
         return {"flat": self.fp.flat.detach().cpu(), "m": self.m.cpu(), "v": self.v.cpu(), "step": self.step_count,
