@@ -51,6 +51,10 @@ class TrainConfig:
     # capture the engine's forward+backward (~250 launches) in one HIP graph (single GPU; the
     # augment's host-side random affine and the AdamW step with its per-step scalars stay outside)
     graph: bool = True
+    # data-parallel with the HIP engine: True = replay the captured fwd+bwd graph, then all-reduce
+    # every bucket (launch-free backward, no comm overlap); False = eager backward with each bucket's
+    # all-reduce issued the moment its gradients are written (overlap, ~500 individual launches)
+    ddp_graph: bool = True
 
 
 def lr_schedule(learning_rate: float, n_epochs: int) -> np.ndarray:
@@ -148,8 +152,8 @@ class CellposeTrainer:
 
         eng = self._engine(x.shape[0], x.shape[-1])
         with trace.span("train.fwd_bwd_engine", cuda=True):
-            if self.cfg.graph and self.world == 1 and self.device.type == "cuda":
-                loss = self._graph_step(eng, x, lbl)
+            if self.cfg.graph and self.device.type == "cuda" and (self.world == 1 or self.cfg.ddp_graph):
+                loss = self._graph_step(eng, x, lbl)  # ar.finish() then all-reduces every bucket
             else:
                 loss = eng.loss_and_backward(x, lbl, on_params_ready=self.ar.mark_ready if self.world > 1 else None)
         with trace.span("train.grad_allreduce_finish", cuda=True):

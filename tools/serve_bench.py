@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""End-to-end serving benchmark: Cellpose inference requests through the whole worker stack.
+
+client --(hub RPC)--> app service --> router (admission, deadlines) --> GPU-pinned process replica
+(shared-memory ring for the image/mask payloads) --> ``@serve.batch`` continuous batching -->
+HIP CPnet + dynamics + masks --> back.
+
+Each client sends ONE 512x512 2-channel image per request (the reference's cellpose service handles
+one request at a time per replica, ``apps/cellpose-finetuning/main.py:3616-3623``); C clients run
+closed-loop.  Reports img/s and p50/p95/p99 request latency per concurrency level.
+Usage: ``python tools/serve_bench.py [--size 512] [--concurrency 1,8,32] [--seconds 10] [--gpus 1]``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+
+async def main_async(a) -> list[dict]:
+    from bioengine_worker_amd.cellpose.pipeline import synthetic_cells
+    from bioengine_worker_amd.transport import connect_to_server
+    from bioengine_worker_amd.transport.hub import get_local_hub
+    from bioengine_worker_amd.worker.worker import BioEngineWorker
+
+    os.environ.setdefault("BIOENGINE_LOCAL_ARTIFACT_PATH", str(ROOT / "apps"))
+    os.environ.setdefault("BIOENGINE_REPLICA_MODE", a.replica_mode)
+    tmp = Path(tempfile.mkdtemp(prefix="serve-bench-"))
+    os.environ["HOME"] = str(tmp / "home")
+    hub = get_local_hub("sbench")
+    await hub.start_http()
+    tok = hub.issue_token("admin-user", workspace="ws-admin")
+    w = BioEngineWorker(mode="single-machine", workspace_dir=tmp / "be", server_url="local://sbench", token=tok,
+                        client_id="worker1", log_file="off", head_num_cpus=8, head_num_gpus=a.gpus,
+                        monitoring_interval_seconds=5, data_server_url=None)
+    await w.start(blocking=False)
+    admin = await connect_to_server({"server_url": "local://sbench", "token": tok})
+    svc = await admin.get_service(w.full_service_id)
+    aid = await svc.deploy_app(artifact_id="cellpose-finetuning", application_id="cpbench", disable_gpu=a.gpus == 0)
+    st = await w.apps_manager.wait_for(aid, timeout=600)
+    assert st == "RUNNING", (await svc.get_app_status(application_ids=[aid]))["message"]
+    s = await svc.get_app_status(application_ids=[aid])
+    app = await admin.get_service(s["service_ids"][0]["websocket_service_id"])
+    imgs = [synthetic_cells(1, a.size, a.size, ncells=60, seed=i)[0] for i in range(16)]
+    for i in range(3):  # warm-up: model build, kernels, graph pass, batch shapes
+        await asyncio.gather(*[app.infer(input_arrays=[imgs[j % 16]]) for j in range(8)])
+    results = []
+    for conc in a.concurrency:
+        lat: list[float] = []
+        stop = time.perf_counter() + a.seconds
+
+        async def client(cid):
+            k = cid
+            while time.perf_counter() < stop:
+                t = time.perf_counter()
+                out = await app.infer(input_arrays=[imgs[k % 16]])
+                lat.append(time.perf_counter() - t)
+                assert out[0]["output"].shape == (a.size, a.size)
+                k += conc
+
+        t0 = time.perf_counter()
+        await asyncio.gather(*[client(c) for c in range(conc)])
+        dt = time.perf_counter() - t0
+        ms = np.array(lat) * 1e3
+        r = {"concurrency": conc, "requests": len(lat), "imgs_per_s": round(len(lat) / dt, 1),
+             "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
+             "p99_ms": round(float(np.percentile(ms, 99)), 2), "image": [a.size, a.size, 2], "gpus": a.gpus,
+             "replica_mode": os.environ["BIOENGINE_REPLICA_MODE"]}
+        results.append(r)
+        print(json.dumps(r), flush=True)
+    st = await svc.get_app_status(application_ids=[aid])
+    print(json.dumps({"router": {k: v.get("latency_ms") for k, v in st.get("deployments", {}).items()}}), flush=True)
+    await svc.stop_app(application_id=aid)
+    await w._cleanup()
+    return results
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--concurrency", default="1,8,32")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--replica-mode", default="process", choices=["process", "local"])
+    a = ap.parse_args()
+    a.concurrency = [int(c) for c in a.concurrency.split(",")]
+    asyncio.run(main_async(a))
+
+
+if __name__ == "__main__":
+    main()
