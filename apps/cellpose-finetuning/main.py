@@ -106,10 +106,11 @@ def to_chw(img: np.ndarray, nchan: int = 2) -> np.ndarray:
         a = a[None]
     elif a.ndim == 3 and a.shape[-1] <= 4 and a.shape[0] > 4:
         a = np.moveaxis(a, -1, 0)
-    a = a.astype(np.float32)
+    if a.dtype not in (np.uint8, np.uint16, np.float16, np.float32):
+        a = a.astype(np.float32)  # integer/float samples keep their width: the GPU converts
     if a.shape[0] < nchan:
-        a = np.concatenate([a, np.zeros((nchan - a.shape[0],) + a.shape[1:], np.float32)], 0)
-    return a[:nchan]
+        a = np.concatenate([a, np.zeros((nchan - a.shape[0],) + a.shape[1:], a.dtype)], 0)
+    return np.ascontiguousarray(a[:nchan])
 
 
 def clahe(img: np.ndarray, clip: float = 3.0, tiles: int = 16, device=None) -> np.ndarray:
@@ -137,8 +138,8 @@ def encode_png_b64(mask: np.ndarray) -> str:
 
 @serve.deployment(
     ray_actor_options={"num_gpus": 1, "num_cpus": 4, "memory": 12 * 1024 ** 3},
-    max_ongoing_requests=16,
-    max_queued_requests=64,
+    max_ongoing_requests=64,  # >= 2 full continuous batches in flight at the replica
+    max_queued_requests=256,
     health_check_period_s=30.0,
     health_check_timeout_s=60.0,
     graceful_shutdown_timeout_s=300.0,
@@ -197,27 +198,35 @@ class CellposeFinetune:
         assert out[0]["output"].shape == (128, 128)
 
     # ------------------------------------------------------------------ inference (continuous batching)
-    @serve.batch(max_batch_size=16, batch_wait_timeout_s=0.005)
+    @serve.batch(max_batch_size=32, batch_wait_timeout_s=0.005)
     async def _segment_batch(self, reqs: list) -> list:
-        """reqs: [(model_id, image CHW float32, params dict)] -> [(masks, flows)]."""
+        """reqs: [(model_id, image CHW, params dict, want_flows)] -> [(masks, flows | None)]."""
+        from bioengine_worker_amd.profiling import trace
+
         out = [None] * len(reqs)
         groups: dict = {}
-        for i, (mid, img, prm) in enumerate(reqs):
-            key = (mid, img.shape, tuple(sorted(prm.items())))
+        for i, (mid, img, prm, want_flows) in enumerate(reqs):
+            key = (mid, img.shape, img.dtype.str, tuple(sorted(prm.items())))
             groups.setdefault(key, []).append(i)
-        for (mid, shape, prm_items), idxs in groups.items():
+        for (mid, shape, _, prm_items), idxs in groups.items():
             runner = await self._runner(mid)
-            batch = np.stack([reqs[i][1] for i in idxs])
+            with trace.span("app.stack", images=len(idxs)):
+                batch = np.stack([reqs[i][1] for i in idxs])
             prm = dict(prm_items)
+            flows_needed = any(reqs[i][3] for i in idxs)
 
             def run():
                 with self._gpu_lock:
-                    m, f, _ = runner.eval(batch, **prm)
-                    return m.cpu().numpy(), f.cpu().numpy()
+                    with trace.span("app.eval", images=len(idxs)):
+                        m, f, _ = runner.eval(batch, **prm)
+                    with trace.span("app.d2h", images=len(idxs)):
+                        m = m.cpu()
+                        f = f.cpu().numpy() if flows_needed else None  # 12 B/pixel D2H only on request
+                return m.numpy(), f
 
             masks, flows = await asyncio.to_thread(run)
             for j, i in enumerate(idxs):
-                out[i] = (masks[j], flows[j])
+                out[i] = (masks[j], flows[j] if flows is not None and reqs[i][3] else None)
         return out
 
     async def _fetch_artifact_files(self, artifact: str, paths: list[str]) -> list[np.ndarray]:
@@ -268,7 +277,8 @@ class CellposeFinetune:
         prm = {"diameter": diameter, "flow_threshold": flow_threshold, "cellprob_threshold": cellprob_threshold,
                "niter": niter or 200}
         chw = [to_chw(im) for im in images]
-        res = await asyncio.gather(*[self._segment_batch((model or self.default_model, c, prm)) for c in chw])
+        res = await asyncio.gather(*[self._segment_batch((model or self.default_model, c, prm, bool(return_flows)))
+                                     for c in chw])
         out = []
         for name, (m, f) in zip(names, res):
             item = {"input_path": name, "output": encode_png_b64(m) if json_safe else m.astype(np.int32)}
@@ -593,3 +603,11 @@ class CellposeFinetune:
     async def debug_task_info(self) -> dict:
         """Background training tasks and their state."""
         return {sid: {"done": t.done(), "cancelled": t.cancelled()} for sid, t in self.tasks.items()}
+
+    @schema_method
+    async def get_batch_stats(self) -> dict:
+        """Continuous-batching statistics of inference on this replica (batch-size histogram,
+        mean queue wait) — observability extension, not in the reference."""
+        from bioengine_worker_amd.serve.batching import batch_stats
+
+        return batch_stats(self, "_segment_batch") or {}

@@ -170,4 +170,5 @@ def summary() -> dict[str, dict]:
 
 
 if os.environ.get("BIOENGINE_TRACE_FILE"):
-    atexit.register(lambda: export(os.environ["BIOENGINE_TRACE_FILE"]))
+    # "{pid}" in the path gives every process (router, replicas) its own file
+    atexit.register(lambda: export(os.environ["BIOENGINE_TRACE_FILE"].replace("{pid}", str(os.getpid()))))

@@ -31,12 +31,32 @@ class _BatchQueue:
         self.inflight = 0
         self.task = asyncio.get_running_loop().create_task(self._loop())
         self.stats = {"batches": 0, "requests": 0, "hist": collections.Counter(), "wait_s": 0.0}
+        self.gap_ewma = float("inf")  # smoothed inter-arrival time (s)
+        self.last_batch = 1
+        self._last_arrival = None
 
     def submit(self, args, kwargs) -> asyncio.Future:
         fut = asyncio.get_running_loop().create_future()
-        self.queue.append((args, kwargs, fut, time.perf_counter()))
+        now = time.perf_counter()
+        if self._last_arrival is not None:
+            gap = now - self._last_arrival
+            self.gap_ewma = gap if self.gap_ewma == float("inf") else 0.8 * self.gap_ewma + 0.2 * gap
+        self._last_arrival = now
+        self.queue.append((args, kwargs, fut, now))
         self.event.set()
         return fut
+
+    def fill_target(self) -> int:
+        """How many requests an idle device waits for (at most ``batch_wait_timeout_s``).
+
+        * Requests arriving faster than half the timeout (open-loop load): a full batch.
+        * Otherwise the previous batch's size: clients whose results just went out are on their way
+          back (closed loop), so forming a batch from the one request that slipped in meanwhile
+          would alternate 1-image and N-image batches.
+        * A lone client (previous batch of 1, slow arrivals) never waits."""
+        if self.gap_ewma < 0.5 * self.timeout:
+            return self.max_batch_size
+        return min(self.max_batch_size, self.last_batch)
 
     async def _loop(self):
         while True:
@@ -45,9 +65,10 @@ class _BatchQueue:
                 await self.event.wait()
             await self.sem.acquire()
             # Device idle and queue short: give stragglers a bounded window to join.
-            if self.inflight == 0 and len(self.queue) < self.max_batch_size and self.timeout > 0:
+            target = self.fill_target()
+            if self.inflight == 0 and len(self.queue) < target and self.timeout > 0:
                 deadline = time.perf_counter() + self.timeout
-                while len(self.queue) < self.max_batch_size:
+                while len(self.queue) < target:
                     rem = deadline - time.perf_counter()
                     if rem <= 0:
                         break
@@ -63,6 +84,7 @@ class _BatchQueue:
                 self.sem.release()
                 continue
             self.inflight += 1
+            self.last_batch = len(items)
             asyncio.get_running_loop().create_task(self._run(items))
 
     async def _run(self, items):

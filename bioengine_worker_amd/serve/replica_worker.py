@@ -45,6 +45,9 @@ async def _main():
     from . import controller as ctrl_mod
     from .replica import _resolve_result, recv_frames, send_frames
 
+    # GPU replicas run their device work on worker threads that hold the GIL between launches; a
+    # 0.5 ms switch interval (default 5 ms) keeps the request reader and event loop responsive
+    sys.setswitchinterval(float(os.environ.get("BE_REPLICA_SWITCH_INTERVAL_S", "0.0005")))
     sock = os.environ["BE_REPLICA_SOCK"]
     key = bytes.fromhex(os.environ["BE_REPLICA_KEY"])
     rx = tx = None

@@ -138,3 +138,33 @@ def test_follow_flows_launch_variants_identical(gpu, monkeypatch):
         monkeypatch.setattr(cg, "FOLLOW_FLOWS_ENTRY", entry)
         outs.append(cg.compute_masks_gpu(y).cpu())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,kind", [((3, 2, 37, 53), "float"), ((4, 2, 128, 128), "uint16"),
+                                        ((2, 1, 64, 64), "const"), ((32, 2, 512, 512), "uint16"),
+                                        ((2, 3, 100, 101), "neg")])
+def test_normalize99_radix_select_matches_sort_and_numpy(gpu, shape, kind):
+    """HIP radix-select percentile normalisation == the sort formulation == np.percentile oracle."""
+    from bioengine_worker_amd.cellpose.gpu import normalize99, normalize99_sort
+
+    g = torch.Generator().manual_seed(0)
+    if kind == "uint16":  # microscopy-like: many ties, a dominant background mode
+        x = (torch.rand(shape, generator=g) ** 4 * 4000).round()
+    elif kind == "const":
+        x = torch.full(shape, 7.0)
+        x[1] = torch.rand(shape[1:], generator=g)
+    elif kind == "neg":
+        x = torch.randn(shape, generator=g) * 100
+    else:
+        x = torch.rand(shape, generator=g)
+    xd = x.to(gpu)
+    a = normalize99(xd)
+    b = normalize99_sort(xd)
+    torch.testing.assert_close(a, b, rtol=0, atol=1e-6)
+    if kind != "const":
+        xn = x[0, 0].numpy().astype(np.float64)
+        p1, p99 = np.percentile(xn, 1), np.percentile(xn, 99)
+        np.testing.assert_allclose(a[0, 0].cpu().numpy(), (xn - p1) / (p99 - p1), rtol=1e-4, atol=1e-4)
+    normalize99(xd)  # second call reuses the (self-clearing) workspace
+    torch.testing.assert_close(normalize99(xd), b, rtol=0, atol=1e-6)

@@ -46,7 +46,10 @@ async def main_async(a) -> list[dict]:
     await w.start(blocking=False)
     admin = await connect_to_server({"server_url": "local://sbench", "token": tok})
     svc = await admin.get_service(w.full_service_id)
-    aid = await svc.deploy_app(artifact_id="cellpose-finetuning", application_id="cpbench", disable_gpu=a.gpus == 0)
+    # deploy_app's max_ongoing_requests (the app proxy's cap, default 10 as in the reference) bounds
+    # how many requests can reach the replica's batcher at once
+    aid = await svc.deploy_app(artifact_id="cellpose-finetuning", application_id="cpbench", disable_gpu=a.gpus == 0,
+                               max_ongoing_requests=a.max_ongoing)
     st = await w.apps_manager.wait_for(aid, timeout=600)
     assert st == "RUNNING", (await svc.get_app_status(application_ids=[aid]))["message"]
     s = await svc.get_app_status(application_ids=[aid])
@@ -68,9 +71,23 @@ async def main_async(a) -> list[dict]:
                 assert out[0]["output"].shape == (a.size, a.size)
                 k += conc
 
+        prof = None
+        if a.profile and conc == max(a.concurrency):
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         await asyncio.gather(*[client(c) for c in range(conc)])
         dt = time.perf_counter() - t0
+        if prof is not None:
+            import io
+            import pstats
+
+            prof.disable()
+            buf = io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+            Path(a.profile).write_text(buf.getvalue())
         ms = np.array(lat) * 1e3
         r = {"concurrency": conc, "requests": len(lat), "imgs_per_s": round(len(lat) / dt, 1),
              "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
@@ -80,6 +97,10 @@ async def main_async(a) -> list[dict]:
         print(json.dumps(r), flush=True)
     st = await svc.get_app_status(application_ids=[aid])
     print(json.dumps({"router": {k: v.get("latency_ms") for k, v in st.get("deployments", {}).items()}}), flush=True)
+    try:
+        print(json.dumps({"batching": await app.get_batch_stats()}), flush=True)
+    except Exception:  # noqa: BLE001
+        pass
     await svc.stop_app(application_id=aid)
     await w._cleanup()
     return results
@@ -92,6 +113,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--replica-mode", default="process", choices=["process", "local"])
+    ap.add_argument("--max-ongoing", type=int, default=64, help="deploy_app max_ongoing_requests")
+    ap.add_argument("--profile", default=None, metavar="PATH",
+                    help="cProfile the worker-side event loop during the highest-concurrency phase")
     a = ap.parse_args()
     a.concurrency = [int(c) for c in a.concurrency.split(",")]
     asyncio.run(main_async(a))
