@@ -121,7 +121,8 @@ def bench_reference_algorithm(runner, imgs, p, steps=3):
         y = plan.blend(yt.float().contiguous(), imgs.shape[0])
         return compute_masks_gpu(y)
 
-    run()
+    for _ in range(3):  # MIOpen picks/compiles its conv solutions on the first calls of a fresh box
+        run()
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(steps):
