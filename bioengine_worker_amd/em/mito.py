@@ -36,6 +36,16 @@ def normalize_percentile(img: torch.Tensor, p1: float = 1.0, p99: float = 99.0) 
     return ((img.float() - lo) / (hi - lo + 1e-6)).clamp(0, 1)
 
 
+def tile_stack(img: torch.Tensor, tile: int = 512, overlap: int = 64) -> torch.Tensor:
+    """The [T, 1, tile, tile] tiles :func:`infer_tiled` feeds its model for ``img`` [H, W], in order."""
+    H, W = img.shape
+    stride = tile - overlap
+    ys, xs = list(range(0, H, stride)), list(range(0, W, stride))
+    padded = torch.nn.functional.pad(img[None, None].float(), (0, max(0, xs[-1] + tile - W), 0, max(0, ys[-1] + tile - H)),
+                                     mode="reflect" if (xs[-1] + tile - W < W and ys[-1] + tile - H < H) else "replicate")[0, 0]
+    return torch.stack([padded[y:y + tile, x:x + tile] for y in ys for x in xs])[:, None]
+
+
 def infer_tiled(img: torch.Tensor, predict: Callable[[torch.Tensor], torch.Tensor], tile: int = 512,
                 overlap: int = 64, batch: int = 8) -> torch.Tensor:
     """img [H, W] (GPU) -> blended prediction [C, H, W].  ``predict`` maps [T, 1, tile, tile] ->

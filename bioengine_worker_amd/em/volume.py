@@ -56,14 +56,37 @@ def ccl3d(mask: torch.Tensor) -> torch.Tensor:
 
 
 def slice_probabilities(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 64, batch: int = 8) -> torch.Tensor:
-    """[Z, Y, X] normalised volume -> foreground probability [Z, Y, X] (slice-wise 2-D model)."""
+    """[Z, Y, X] normalised volume -> foreground probability [Z, Y, X] (slice-wise 2-D model).
+
+    Small slices are predicted ``batch`` slices per call; large slices go through the tiled path
+    with the tiles of several slices in one call (the model sees ``batch`` tiles at a time whatever
+    the slice size, so a 2048² slice's 25 tiles do not run as 4 under-filled batches)."""
     out = torch.empty(vol.shape, dtype=torch.float32, device=vol.device)
     Z, Y, X = vol.shape
-    for z in range(Z):
-        if Y <= tile and X <= tile:
-            out[z] = predict(vol[z][None, None])[0, 0]
-        else:
-            out[z] = mito.infer_tiled(vol[z], predict, tile, overlap, batch)[0]
+    if Y <= tile and X <= tile:
+        for z0 in range(0, Z, batch):
+            out[z0:z0 + batch] = predict(vol[z0:z0 + batch][:, None])[:, 0]
+        return out
+    stride = tile - overlap
+    per_slice = len(range(0, Y, stride)) * len(range(0, X, stride))
+    k = max(1, batch // per_slice)  # slices whose tiles fill one model batch
+    pending: list = []  # tile predictions computed for the current group of slices
+
+    def pooled(t):
+        if not pending:
+            outs = []
+            for i in range(0, cur.shape[0], batch):
+                outs.append(predict(cur[i:i + batch]).float())
+            pending.extend(torch.cat(outs).split(per_slice))
+        return pending.pop(0)
+
+    for z0 in range(0, Z, k):
+        zs = list(range(z0, min(Z, z0 + k)))
+        tiles = [mito.tile_stack(vol[z], tile, overlap) for z in zs]
+        cur = torch.cat(tiles)
+        pending.clear()
+        for z in zs:
+            out[z] = mito.infer_tiled(vol[z], pooled, tile, overlap, per_slice)[0]
     return out
 
 
@@ -157,6 +180,28 @@ def label_sharded(mask_slab: torch.Tensor, group=None) -> tuple[torch.Tensor, in
     return out, int(table.max())
 
 
+def gather_slabs(x: torch.Tensor, group=None) -> torch.Tensor:
+    """All-gather z-slabs of possibly different depths into the full [Z, ...] volume on every rank
+    (one ``all_gather_into_tensor`` of max-depth-padded slabs — RCCL over xGMI on the GPU node)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return x
+    world = dist.get_world_size(group)
+    depth = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    depths = [torch.zeros_like(depth) for _ in range(world)]
+    dist.all_gather(depths, depth, group=group)
+    depths = [int(d) for d in depths]
+    zmax = max(depths)
+    buf = torch.zeros((zmax,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    buf[: x.shape[0]] = x
+    if x.dtype == torch.bool:  # collectives move bytes: ship the mask as uint8
+        buf = buf.to(torch.uint8)
+    full = torch.empty((world * zmax,) + tuple(x.shape[1:]), dtype=buf.dtype, device=x.device)
+    dist.all_gather_into_tensor(full, buf, group=group)
+    parts = [full[r * zmax: r * zmax + depths[r]] for r in range(world)]
+    out = torch.cat(parts)
+    return out.bool() if x.dtype == torch.bool else out
+
+
 def instance_stats(labels: torch.Tensor, n: int, z_offset: int = 0, group=None) -> dict:
     """Per-instance voxel count and centroid (z, y, x), all-reduced across ranks (z-chunked, so a
     multi-GB label slab never materialises full-size index temporaries)."""
@@ -176,17 +221,29 @@ def instance_stats(labels: torch.Tensor, n: int, z_offset: int = 0, group=None) 
         dist.all_reduce(acc, group=group)
     acc = acc.cpu().numpy()
     c = np.maximum(acc[0, 1:], 1)
-    return {"label": list(range(1, n + 1)), "voxels": acc[0, 1:].astype(np.int64).tolist(),
-            "centroid_z": (acc[1, 1:] / c).tolist(), "centroid_y": (acc[2, 1:] / c).tolist(),
-            "centroid_x": (acc[3, 1:] / c).tolist()}
+    return {"label": np.arange(1, n + 1), "voxels": acc[0, 1:].astype(np.int64),
+            "centroid_z": acc[1, 1:] / c, "centroid_y": acc[2, 1:] / c, "centroid_x": acc[3, 1:] / c}
 
 
 def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 64, batch: int = 8,
                    threshold: float = 0.5, min_voxels: int = 300, group=None, gather_labels: bool = False,
-                   z_offset: int = 0) -> dict:
+                   z_offset: int = 0, gather: str | None = None, timings: bool = False) -> dict:
     """Single-process (or per-rank) 3-D analysis.  With a process group, ``vol`` is this rank's
-    z-slab and results are globally consistent."""
+    z-slab and results are globally consistent.  ``gather="mask"`` / ``"labels"`` all-gathers the
+    stitched foreground mask (uint8) / global instance labels of the whole volume onto every rank
+    (``out["mask"]`` / ``out["labels_full"]``, device tensors); ``gather_labels`` returns this
+    rank's slab labels as numpy."""
+    import time
+
     from ..search.preprocess import percentiles
+
+    marks = [("start", time.perf_counter())]
+
+    def mark(name):
+        if timings:
+            if vol.is_cuda:
+                torch.cuda.synchronize(vol.device)
+            marks.append((name, time.perf_counter()))
 
     v = vol.float()
     sample = v.reshape(1, -1)[:, :: max(1, v.numel() // 4_000_000)]
@@ -197,13 +254,25 @@ def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 6
         pr /= dist.get_world_size(group)
         p1, p99 = pr[0], pr[1]
     vn = ((v - p1) / (p99 - p1 + 1e-6)).clamp(0, 1)
+    mark("normalize")
     prob = slice_probabilities(vn, predict, tile, overlap, batch)
+    mark("inference")
     mask = prob > threshold
+    del prob, vn, v
     labels, n = label_sharded(mask, group)
+    mark("label")
     stats = instance_stats(labels, n, z_offset, group)
-    keep = np.array(stats["voxels"]) >= min_voxels
+    keep = stats["voxels"] >= min_voxels
     out = {"n_instances": int(keep.sum()), "n_components": n, "volume_shape": list(vol.shape),
-           "instances": {k: [x for x, kk in zip(vv, keep) if kk] for k, vv in stats.items()}}
+           "instances": {k: vv[keep].tolist() for k, vv in stats.items()}}
+    mark("stats")
     if gather_labels:
         out["labels"] = labels.cpu().numpy()
+    if gather == "mask":
+        out["mask"] = gather_slabs(mask, group)
+    elif gather == "labels":
+        out["labels_full"] = gather_slabs(labels, group)
+    mark("gather")
+    if timings:
+        out["timings_s"] = {b[0]: round(b[1] - a[1], 4) for a, b in zip(marks, marks[1:])}
     return out

@@ -31,6 +31,12 @@ def _worker(rank, world, port, q):
     z0, z1 = slab_bounds(v.shape[0], rank, world)
     lab, n = label_sharded(torch.from_numpy(v[z0:z1]))
     st = instance_stats(lab, n, z0)
+    from bioengine_worker_amd.em.volume import gather_slabs
+
+    full_mask = gather_slabs(torch.from_numpy(v[z0:z1]))  # uneven slabs for world 3
+    full_lab = gather_slabs(lab)
+    assert full_mask.dtype == torch.bool and torch.equal(full_mask, torch.from_numpy(v))
+    assert full_lab.shape == v.shape
     q.put((rank, z0, lab.numpy(), n, st["voxels"]))
     dist.destroy_process_group()
 
@@ -74,3 +80,22 @@ def test_label_local_z_chunked_matches_whole(chunk_planes):
     ref, n_ref = ndimage.label(v, structure=ndimage.generate_binary_structure(3, 1))
     assert n_whole == n_chunked == n_ref
     assert torch.equal(whole, chunked)
+
+
+def test_slice_probabilities_pools_tiles_across_slices():
+    """Tiles of several slices share one model call; the result equals slice-by-slice inference."""
+    from bioengine_worker_amd.em import mito
+    from bioengine_worker_amd.em.volume import slice_probabilities
+
+    torch.manual_seed(0)
+    vol = torch.rand(5, 90, 70)
+    calls = []
+
+    def predict(t):
+        calls.append(t.shape[0])
+        return torch.sigmoid(t * 3 - 1 + t.mean(dim=(2, 3), keepdim=True) * 0)
+
+    pooled = slice_probabilities(vol, predict, tile=32, overlap=8, batch=40)
+    ref = torch.stack([mito.infer_tiled(vol[z], predict, 32, 8, 4)[0] for z in range(5)])
+    torch.testing.assert_close(pooled, ref)
+    assert calls[0] == 36  # 12 tiles per slice: three slices' tiles in one call (batch 40)
