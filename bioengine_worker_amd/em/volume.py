@@ -210,13 +210,23 @@ def instance_stats(labels: torch.Tensor, n: int, z_offset: int = 0, group=None) 
     acc = torch.zeros(4, n + 1, dtype=torch.float64, device=dev)
     cz = max(1, (1 << 27) // max(1, Y * X))
     for z0 in range(0, Z, cz):
-        l = labels[z0:z0 + cz].reshape(-1).long()
+        l = labels[z0:z0 + cz].reshape(-1)
         idx = torch.nonzero(l > 0).squeeze(1)
-        lab = l[idx]
-        acc[0].index_add_(0, lab, torch.ones(idx.numel(), dtype=torch.float64, device=dev))
-        acc[1].index_add_(0, lab, (idx // (Y * X)).double() + (z0 + z_offset))
-        acc[2].index_add_(0, lab, ((idx // X) % Y).double())
-        acc[3].index_add_(0, lab, (idx % X).double())
+        if idx.numel() == 0:
+            continue
+        # Segmented sums after a radix sort of the labels instead of index_add_: a large instance
+        # sends millions of fp64 atomics to ONE address (a CAS storm that stalls for minutes on a
+        # percolating mask); sorted runs reduce with one int64 cumsum per coordinate, exactly.
+        lab, perm = torch.sort(l[idx].to(torch.int32))
+        idx = idx[perm]
+        uniq, counts = torch.unique_consecutive(lab, return_counts=True)
+        ends = torch.cumsum(counts, 0) - 1
+        u = uniq.long()
+        acc[0].index_add_(0, u, counts.double())
+        for k, coord in ((1, idx // (Y * X) + z0 + z_offset), (2, (idx // X) % Y), (3, idx % X)):
+            cs = torch.cumsum(coord, 0)
+            seg = cs[ends] - torch.cat([cs.new_zeros(1), cs[ends[:-1]]])
+            acc[k].index_add_(0, u, seg.double())
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(acc, group=group)
     acc = acc.cpu().numpy()

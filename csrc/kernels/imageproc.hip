@@ -13,11 +13,29 @@
 
 namespace {
 
-__device__ __forceinline__ int uf_find(const int* L, int x) {
+// Find with path halving.  Concurrent halving stores only ever replace a parent by one of its
+// ancestors, and a link they overwrite (an atomicMin that landed on a node which had just stopped
+// being a root) is re-established by uf_unite's retry on the returned old value, so the forest stays
+// a valid union-find; without it, chains through one giant component (a noisy probability mask)
+// make every find O(n) and the merge effectively quadratic.
+__device__ __forceinline__ int uf_find_ro(const int* L, int x) {
   int p = L[x];
   while (p != x) {
     x = p;
     p = L[x];
+  }
+  return x;
+}
+
+// (merge phase only: the compress pass uses the read-only find, or its final root stores would
+// race with other threads' halving stores)
+__device__ __forceinline__ int uf_find(int* L, int x) {
+  int p = L[x];
+  while (p != x) {
+    const int gp = L[p];
+    if (gp != p) L[x] = gp;
+    x = p;
+    p = gp;
   }
   return x;
 }
@@ -65,7 +83,7 @@ __global__ void ccl_compress(int* __restrict__ Lall, int B, long long HW) {
   if (gid >= B * HW) return;
   int* L = Lall + (gid / HW) * HW;
   const int p = (int)(gid % HW);
-  if (L[p] >= 0) L[p] = uf_find(L, p);
+  if (L[p] >= 0) L[p] = uf_find_ro(L, p);
 }
 
 // 3-D, 6-connectivity (face neighbours); volume < 2^31 voxels (a z-slab per rank)

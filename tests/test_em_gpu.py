@@ -73,3 +73,21 @@ def test_ccl3d_gpu_matches_scipy(gpu):
     got = ccl3d(torch.from_numpy(m).to(gpu)).cpu().numpy()
     ref = ccl3d(torch.from_numpy(m)).numpy()
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_ccl3d_giant_noisy_component_matches_scipy(gpu):
+    """A 50 %-density random mask percolates into one huge component: the union-find must stay fast
+    (path halving) and exact vs scipy's 6-connected labelling (roots = first voxel in raster order)."""
+    import time
+
+    from bioengine_worker_amd.em.volume import ccl3d
+
+    rng = np.random.default_rng(0)
+    m = rng.random((24, 256, 256)) < 0.5
+    t = time.perf_counter()
+    got = ccl3d(torch.from_numpy(m).to(gpu)).cpu()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t < 10
+    ref = ccl3d(torch.from_numpy(m))  # scipy oracle, same root convention
+    assert torch.equal(got, ref)

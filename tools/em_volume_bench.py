@@ -38,6 +38,10 @@ def synthetic_slab(z0: int, z1: int, Y: int, X: int, dev, seed: int = 0) -> torc
 
 
 def main():
+    if os.environ.get("BE_DUMP_STACKS"):  # periodic stack dumps to find where a long run spends its time
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["BE_DUMP_STACKS"]), repeat=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--z", type=int, default=256, help="total volume depth (split across ranks)")
     ap.add_argument("--yx", type=int, default=2048)
