@@ -4,14 +4,17 @@ The reference has no multi-GPU training at all (SURVEY.md §2.7, §5 "Failure de
 communicator abort + re-init on rank failure (elastic shrink to N-1 GPUs for DP)" is a new-build
 item).  Design, one process per GPU as everywhere else:
 
-* **Control store.**  A ``TCPStore`` hosted by the launching rank (original rank 0) separate from
-  the process-group rendezvous; every generation of the process group rendezvouses under its own
-  ``PrefixStore("pg<gen>")`` so a re-init never sees stale keys.
-* **Heartbeats.**  Each rank writes ``hb/<id>`` (wall time) every ``heartbeat_s`` from a daemon
-  thread.  A monitor in the same thread watches the current members; when one goes stale while a
-  collective may be blocked on it, the communicator is *aborted* (RCCL ``abort`` through
-  ``_abort_process_group``) so the blocked ``wait()`` raises instead of hanging for the PG timeout.
-  Gloo fails fast on its own (peer socket closed).
+* **Control store.**  A ``TCPStore`` hosted OUTSIDE the training ranks -- by the launcher (the
+  gang launcher in ``serve/gang.py`` or a test parent, via :class:`ControlStore`) -- so any rank,
+  original rank 0 included, can die without taking the store with it.  Every generation of the
+  process group rendezvouses under its own ``PrefixStore("pg<gen>")`` so a re-init never sees
+  stale keys.  (``host_store=True`` keeps the old single-host mode for ad-hoc runs.)
+* **Heartbeats.**  Each rank increments a counter ``hb/<id>`` every ``heartbeat_s`` from a daemon
+  thread.  Observers never compare clocks across hosts: each remembers, on its OWN monotonic
+  clock, when it last saw a member's counter change, and a member is stale when its counter has
+  not moved for ``stale_s``.  When a current member goes stale while a collective may be blocked
+  on it, the communicator is *aborted* (RCCL ``abort`` through ``_abort_process_group``) so the
+  blocked ``wait()`` raises instead of hanging for the PG timeout.  Gloo fails fast on its own.
 * **Agreement.**  Survivors announce themselves under ``gen<g+1>/alive/<id>``, wait until every
   member either announced or has a stale heartbeat, and the first survivor to finish publishes its
   view with ``compare_set(gen<g+1>/members)`` — every survivor adopts that single decision
@@ -41,18 +44,29 @@ class ExcludedFromWorld(RuntimeError):
     """This rank was declared dead by the survivors (e.g. it stalled past the heartbeat window)."""
 
 
+class ControlStore:
+    """The elastic control store, hosted by a process that is not a training rank (the launcher).
+    Keep the object alive for the lifetime of the job; ``port`` is what ranks connect to."""
+
+    def __init__(self, host: str = "127.0.0.1", port: int = 0, timeout_s: float = 120.0):
+        self.store = dist.TCPStore(host, port, None, True, timedelta(seconds=timeout_s), wait_for_workers=False)
+        self.host, self.port = host, self.store.port
+
+
 class ElasticWorld:
     def __init__(self, member_id: int, world_size: int, master_addr: str = "127.0.0.1", master_port: int = 29600,
                  backend: str | None = None, heartbeat_s: float = 0.5, stale_s: float = 3.0,
-                 pg_timeout_s: float = 30.0, device: torch.device | None = None):
+                 pg_timeout_s: float = 30.0, device: torch.device | None = None, host_store: bool = False):
         self.member_id = int(member_id)
         self.members = list(range(int(world_size)))
         self.backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
         self.heartbeat_s, self.stale_s, self.pg_timeout_s = heartbeat_s, stale_s, pg_timeout_s
         self.device = device
         self.gen = 0
-        self.store = dist.TCPStore(master_addr, master_port, None, self.member_id == 0,
+        self.store = dist.TCPStore(master_addr, master_port, None, bool(host_store),
                                    timedelta(seconds=max(60.0, pg_timeout_s)), wait_for_workers=False)
+        self._seen: dict[int, tuple[int, float]] = {}  # member -> (last counter, local monotonic time it moved)
+        self._seen_lock = threading.Lock()
         self._stop = threading.Event()
         self._beat()
         self._hb = threading.Thread(target=self._heartbeat_loop, daemon=True)
@@ -77,23 +91,37 @@ class ElasticWorld:
                                 world_size=self.world, timeout=timedelta(seconds=self.pg_timeout_s), **kw)
 
     def _beat(self) -> None:
-        self.store.set(f"hb/{self.member_id}", repr(time.time()))
+        self.store.add(f"hb/{self.member_id}", 1)
 
-    def _last_beat(self, m: int) -> float:
+    def _counter(self, m: int) -> int:
         try:
-            return float(self.store.get(f"hb/{m}").decode())
+            return self.store.add(f"hb/{m}", 0)
         except Exception:  # noqa: BLE001
-            return 0.0
+            return -1
 
     def stale_members(self) -> list[int]:
-        now = time.time()
-        return [m for m in self.members if m != self.member_id and now - self._last_beat(m) > self.stale_s]
+        """Members whose heartbeat counter has not moved for ``stale_s`` on THIS process's
+        monotonic clock (no cross-host wall-clock comparison)."""
+        now = time.monotonic()
+        out = []
+        with self._seen_lock:
+            for m in self.members:
+                if m == self.member_id:
+                    continue
+                c = self._counter(m)
+                last = self._seen.get(m)
+                if last is None or c != last[0]:
+                    self._seen[m] = (c, now)
+                elif now - last[1] > self.stale_s:
+                    out.append(m)
+        return out
 
     def _heartbeat_loop(self) -> None:
         while not self._stop.wait(self.heartbeat_s):
             try:
                 self._beat()
-                if self.backend == "nccl" and dist.is_initialized() and self.stale_members():
+                stale = self.stale_members()
+                if self.backend == "nccl" and dist.is_initialized() and stale:
                     self._abort()  # unblock a collective waiting on a dead peer
             except Exception:  # noqa: BLE001  (store gone: the launcher died; nothing to do)
                 pass

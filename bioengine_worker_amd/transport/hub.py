@@ -562,11 +562,19 @@ class Hub:
         else:
             anon = f"anonymouz-{uuid.uuid4().hex[:8]}"
             user = {"id": anon, "email": None, "is_anonymous": True, "roles": []}
-            ws = workspace or f"ws-{anon}"
+            ws = f"ws-{anon}"
+            # an anonymous client only ever gets its own fresh workspace (as on Hypha): joining a
+            # named workspace would let it call that workspace's protected services
+            if workspace and workspace != ws:
+                raise PermissionError(f"anonymous clients cannot join workspace {workspace}")
         cid = client_id or uuid.uuid4().hex[:10]
         key = f"{ws}/{cid}"
         old = self.sessions.get(key)
         if old is not None and not old.closed:
+            # reconnect of the same client replaces its stale session; anyone else is refused
+            # (otherwise any client could evict e.g. the worker and take over its service ids)
+            if old.user.get("id") != user["id"]:
+                raise PermissionError(f"client id {cid} is already in use in workspace {ws}")
             self.close_session(old)
         s = Session(self, ws, cid, user, remote_caller)
         self.sessions[key] = s
@@ -575,9 +583,12 @@ class Hub:
     def close_session(self, s: Session):
         s.closed = True
         for fid in list(s.services):
-            self.services.pop(fid, None)
+            if self.services.get(fid) is not None and self.services[fid].owner is s:
+                self.services.pop(fid, None)
         s.services.clear()
-        self.sessions.pop(s.full_client, None)
+        # only drop the table entry if it is still THIS session (a reconnect may have replaced it)
+        if self.sessions.get(s.full_client) is s:
+            self.sessions.pop(s.full_client, None)
 
     # ------------------------------------------------------------------ services
     def _register(self, s: Session, svc: dict, overwrite: bool = True) -> ObjDict:

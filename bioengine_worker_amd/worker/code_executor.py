@@ -6,7 +6,10 @@ stderr capture, result dict ``{"result", "stdout", "stderr"}`` or ``{"error", "t
 "stdout", "stderr"}``.
 
 Execution happens in a fresh child Python process with ``HIP_VISIBLE_DEVICES`` set to the GPU(s)
-reserved from the node's resource pool, so user code can never disturb the worker.  Unlike the
+reserved from the node's resource pool.  Source-mode code is only *compiled* (dedented, like the
+reference's ``textwrap.dedent`` at ``code_executor.py:258``) in the worker to report syntax errors
+early; it is executed -- module-level statements included -- only in the child, so user code never
+runs on the worker's event loop or in its process.  Unlike the
 reference (which replays captured output after the task finished), stdout/stderr lines are
 streamed to ``write_stdout``/``write_stderr`` *while* the code runs, and a timeout kills the child.
 """
@@ -19,6 +22,7 @@ import os
 import pickle
 import sys
 import tempfile
+import textwrap
 import time
 import traceback
 from pathlib import Path
@@ -30,11 +34,18 @@ from ..transport.schema import schema_method
 from ..utils.permissions import check_permissions, user_identity
 
 
+def compile_source(code: str):
+    return compile(textwrap.dedent(code), "<run_code>", "exec")
+
+
 def load_func_from_source(code: str, function_name: str):
+    """Exec ``code`` (dedented) and return ``function_name`` from it.  Called in the child."""
     ns: dict[str, Any] = {"__name__": "__bioengine_run_code__"}
-    exec(compile(code, "<run_code>", "exec"), ns)  # noqa: S102 - admin-only by design
+    exec(compile_source(code), ns)  # noqa: S102 - admin-only by design
     if function_name not in ns:
         raise ValueError(f"Function '{function_name}' not defined in the provided code")
+    if not callable(ns[function_name]):
+        raise ValueError(f"Object '{function_name}' is not callable")
     return ns[function_name]
 
 
@@ -101,15 +112,14 @@ class CodeExecutor:
             if mode == "pickle":
                 if func_bytes is None:
                     raise ValueError("func_bytes is required in pickle mode")
-                fn = cloudpickle.loads(bytes(func_bytes))
+                job = ("pickle", bytes(func_bytes), None)
             elif mode == "source":
                 if not code:
                     raise ValueError("code is required in source mode")
-                fn = load_func_from_source(code, function_name or "analyze")
+                compile_source(code)  # syntax check only; the child executes it
+                job = ("source", code, function_name or "analyze")
             else:
                 raise ValueError(f"invalid mode '{mode}'")
-            if not callable(fn):
-                raise ValueError(f"Object '{function_name}' is not callable")
         except Exception as e:  # noqa: BLE001
             return {"error": str(e), "traceback": traceback.format_exc()}
         opts = dict(remote_options or {})
@@ -127,7 +137,7 @@ class CodeExecutor:
         d = Path(tempfile.mkdtemp(prefix="be-run-"))
         inp, out = d / "in.pkl", d / "out.pkl"
         try:
-            inp.write_bytes(cloudpickle.dumps((fn, list(args or []), dict(kwargs or {}))))
+            inp.write_bytes(cloudpickle.dumps((job, list(args or []), dict(kwargs or {}))))
             env = dict(os.environ)
             env.update({k: str(v) for k, v in env_vars.items()})
             if ids:

@@ -13,8 +13,18 @@ def main():
 
     install()
     with open(inp, "rb") as f:
-        fn, args, kwargs = pickle.load(f)
+        (kind, body, fname), args, kwargs = pickle.load(f)
     try:
+        if kind == "source":
+            from .code_executor import load_func_from_source
+
+            fn = load_func_from_source(body, fname)
+        else:
+            import cloudpickle
+
+            fn = cloudpickle.loads(body)
+            if not callable(fn):
+                raise ValueError("the unpickled object is not callable")
         res = fn(*args, **kwargs)
         if asyncio.iscoroutine(res):
             res = asyncio.run(res)

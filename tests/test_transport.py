@@ -132,3 +132,35 @@ def test_artifact_versioning_semantics():
         await hub.stop_http()
 
     run(main())
+
+
+@pytest.mark.unit
+def test_anonymous_cannot_join_or_hijack_workspace():
+    """an anonymous client must not join a named workspace (and so call its
+    protected services), and nobody but the same user may replace a live client id."""
+
+    async def main():
+        hub = Hub(name="sec")
+        tok = hub.issue_token("admin", workspace="ws-user-admin")
+        admin = hub.open_session(tok, client_id="worker")
+        await hub.register_service(admin, {"id": "secret", "config": {"visibility": "protected"},
+                                           "peek": lambda: "classified"})
+        with pytest.raises(PermissionError):
+            hub.open_session(None, workspace="ws-user-admin", client_id="spy")
+        with pytest.raises(PermissionError):  # hijack the worker's client id as another user
+            hub.open_session(hub.issue_token("eve", workspace="ws-user-admin"), client_id="worker")
+        anon = hub.open_session(None)
+        assert anon.workspace.startswith("ws-anonymouz-")
+        with pytest.raises(PermissionError):
+            await hub.call(anon, "ws-user-admin/worker:secret", "peek", [], {})
+        assert await hub.call(admin, "ws-user-admin/worker:secret", "peek", [], {}) == "classified"
+        # the same user reconnecting replaces its own stale session; closing the OLD one later
+        # must not drop the new session or its services
+        again = hub.open_session(tok, client_id="worker")
+        await hub.register_service(again, {"id": "secret", "config": {"visibility": "protected"},
+                                           "peek": lambda: "v2"})
+        hub.close_session(admin)
+        assert hub.sessions["ws-user-admin/worker"] is again
+        assert await hub.call(again, "ws-user-admin/worker:secret", "peek", [], {}) == "v2"
+
+    run(main())
