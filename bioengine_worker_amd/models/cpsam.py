@@ -11,7 +11,7 @@ a pixel-shuffle back to 3 x 256 x 256 (dY, dX, cellprob).
   ``encoder.pos_embed``, ``encoder.blocks.{i}.{norm1,attn.qkv,attn.proj,attn.rel_pos_h,
   attn.rel_pos_w,norm2,mlp.lin1,mlp.lin2}``, ``encoder.neck.{0..3}``, ``out``, ``W2``,
   ``diam_labels``, ``diam_mean``) so a ``cpsam`` checkpoint loads with ``weights_only=True``.
-  Reference path + training (``rdrop`` layer dropout as cellpose does during training).
+  Reference path + training (``rdrop`` per-sample stochastic depth as cellpose 4 does).
 * :class:`CPSAMEngine` — bf16 inference on the framework's kernels: hipBLASLt GEMMs, the
   flash-attention kernel with the decomposed rel-pos bias fused into the score tile (the 1024x1024
   bias never exists), residual fused into LayerNorm, bias+GELU fused, the neck's 3x3 conv on the
@@ -151,15 +151,25 @@ class CPSAM(nn.Module):
                 p.copy_(torch.randn(p.shape, generator=gen) * (1.0 / fan_in) ** 0.5)
         return self
 
-    def forward(self, x: torch.Tensor):
-        """x [B, 3, bsize, bsize] -> (flows [B, nout, bsize, bsize], style placeholder [B, 256])."""
+    def forward(self, x: torch.Tensor, keep: torch.Tensor | None = None):
+        """x [B, 3, bsize, bsize] -> (flows [B, nout, bsize, bsize], style placeholder [B, 256]).
+
+        Training-mode stochastic depth as cellpose 4's ``Transformer.forward``: per sample, block i
+        is replaced by the identity with probability ``linspace(0, rdrop, nlay)[i]``
+        (``x * mask + blk(x) * (1 - mask)``).  ``keep`` [B, nlay] (0/1) overrides the random draw."""
         e = self.encoder
         t = e.patch_embed.proj(x).permute(0, 2, 3, 1)
         t = t + e.pos_embed.to(t.dtype)
-        for blk in e.blocks:
-            if self.training and self.rdrop > 0 and torch.rand(()) < self.rdrop:
-                continue
-            t = blk(t)
+        nl = len(e.blocks)
+        if keep is None and self.training and self.rdrop > 0:
+            keep = (torch.rand(x.shape[0], nl, device=x.device) >=
+                    torch.linspace(0, self.rdrop, nl, device=x.device)[None]).to(t.dtype)
+        for i, blk in enumerate(e.blocks):
+            if keep is None:
+                t = blk(t)
+            else:
+                k = keep[:, i].to(t.dtype)[:, None, None, None]
+                t = t * (1 - k) + blk(t) * k
         y = e.neck(t.permute(0, 3, 1, 2))
         y = self.out(y)
         y = F.conv_transpose2d(y, self.W2.to(y.dtype), stride=self.ps)

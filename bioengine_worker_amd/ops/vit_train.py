@@ -1,0 +1,229 @@
+"""ViT training ops (``csrc/kernels/vit_train.hip``, ``attention_bwd.hip``, ``layernorm.hip``).
+
+The autograd-free Cellpose-SAM training engine (``train/cpsam_engine.py``) is built from these plus
+hipBLASLt GEMMs:
+
+* :func:`ln_fwd` — ``xo = x + rs[b] * y`` then ``LayerNorm(xo)`` with saved (mean, rstd).
+* :func:`ln_bwd` — LayerNorm backward fused with the residual-gradient accumulation and the column
+  partials of dw / db / sum(dx).
+* :func:`gelu_fwd` / :func:`gelu_bwd` — bias + exact GELU (pre-activation kept) and its backward
+  with the bias-gradient partials.
+* :func:`scale_cast` — per-sample scaled fp32 -> bf16 cast + column sums (bias gradients).
+* :func:`attn_bwd` — flash-attention backward with the SAM decomposed rel-pos bias gradients.
+
+GPU tensors run the HIP kernels; CPU tensors run the fp32 PyTorch reference of the same math (the
+oracle of the CPU engine test and of the GPU numerics tests).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _native
+
+
+def _rpb(rows: int, target_blocks: int = 512) -> int:
+    return max(4, -(-rows // target_blocks))
+
+
+def _rowscale(rs: torch.Tensor | None, rows: int, rpn: int):
+    if rs is None:
+        return None
+    return rs.float().repeat_interleave(rpn)[:rows, None]
+
+
+# ------------------------------------------------------------------ LayerNorm
+def ln_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor | None = None,
+           rs: torch.Tensor | None = None, rpn: int = 1, xo: torch.Tensor | None = None, eps: float = 1e-6):
+    """Returns (xo, out, stats): xo = x + rs[row // rpn] * y (None when y is None), out = LN(xo or x)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if x.is_cuda:
+        assert x.dtype == torch.bfloat16 and x.is_contiguous()
+        out = torch.empty_like(x)
+        stats = torch.empty(rows, 2, device=x.device, dtype=torch.float32)
+        if y is not None:
+            assert y.shape == x.shape and y.dtype == torch.bfloat16 and y.is_contiguous()
+            xo = torch.empty_like(x) if xo is None else xo
+        else:
+            xo = None
+        _native.call("be_add_layernorm_train", _native.ptr(x), _native.ptr(y),
+                     _native.ptr(rs.float().contiguous() if rs is not None else None), int(rpn), _native.ptr(xo),
+                     _native.ptr(w), _native.ptr(b), _native.ptr(out), _native.ptr(stats), rows, C, float(eps),
+                     _native.stream(x.device))
+        return xo, out, stats
+    xf = x.float().reshape(rows, C)
+    if y is not None:
+        sc = _rowscale(rs, rows, rpn)
+        yf = y.float().reshape(rows, C)
+        xf = xf + (yf * sc if sc is not None else yf)
+        xf = xf.to(x.dtype).float()
+        if xo is None:
+            xo = xf.to(x.dtype).reshape(x.shape)
+        else:
+            xo.copy_(xf.reshape(x.shape))
+    else:
+        xo = None
+    mean = xf.mean(-1)
+    rstd = torch.rsqrt(xf.var(-1, unbiased=False) + eps)
+    out = ((xf - mean[:, None]) * rstd[:, None] * w.float() + b.float()).to(x.dtype).reshape(x.shape)
+    return xo, out, torch.stack([mean, rstd], 1)
+
+
+def ln_bwd(dh: torch.Tensor, x: torch.Tensor, stats: torch.Tensor, w: torch.Tensor,
+           r1: torch.Tensor | None = None, s1: torch.Tensor | None = None, r2: torch.Tensor | None = None,
+           s2: torch.Tensor | None = None, rpn: int = 1, want_dx: bool = True, want_dxb: bool = False,
+           want_col: bool = False):
+    """LayerNorm backward.  Returns (dx fp32 | None, dx bf16 | None, dw, db, colsum(dx) | None) with
+    dx = LN'(dh) + s1[b] r1 + s2[b] r2."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if x.is_cuda:
+        rpb = _rpb(rows)
+        nblk = -(-rows // rpb)
+        dev = x.device
+        dx = torch.empty(rows, C, device=dev, dtype=torch.float32) if want_dx else None
+        dxb = torch.empty(rows, C, device=dev, dtype=torch.bfloat16) if want_dxb else None
+        pdw = torch.empty(nblk, C, device=dev, dtype=torch.float32)
+        pdb = torch.empty(nblk, C, device=dev, dtype=torch.float32)
+        pcol = torch.empty(nblk, C, device=dev, dtype=torch.float32) if want_col else None
+        f = lambda t: None if t is None else t.float().contiguous()
+        _native.call("be_ln_bwd", _native.ptr(dh.contiguous()), _native.ptr(x), _native.ptr(stats),
+                     _native.ptr(w.float().contiguous()), _native.ptr(f(r1)), _native.ptr(f(s1)), _native.ptr(f(r2)),
+                     _native.ptr(f(s2)), int(rpn), _native.ptr(dx), _native.ptr(dxb), _native.ptr(pdw),
+                     _native.ptr(pdb), _native.ptr(pcol), rows, C, rpb, _native.stream(dev))
+        return dx, dxb, pdw.sum(0), pdb.sum(0), (pcol.sum(0) if pcol is not None else None)
+    xf = x.float().reshape(rows, C)
+    d = dh.float().reshape(rows, C)
+    mean, rstd = stats[:, 0:1], stats[:, 1:2]
+    xh = (xf - mean) * rstd
+    g = d * w.float()
+    o = rstd * (g - g.mean(-1, keepdim=True) - xh * (g * xh).mean(-1, keepdim=True))
+    for r, s in ((r1, s1), (r2, s2)):
+        if r is not None:
+            sc = _rowscale(s, rows, rpn)
+            rf = r.float().reshape(rows, C)
+            o = o + (rf * sc if sc is not None else rf)
+    dw, db = (d * xh).sum(0), d.sum(0)
+    return (o if want_dx else None, o.to(dh.dtype) if want_dxb else None, dw, db,
+            o.sum(0) if want_col else None)
+
+
+# ------------------------------------------------------------------ GELU / casts
+def gelu_fwd(f: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    C = f.shape[-1]
+    rows = f.numel() // C
+    if f.is_cuda:
+        g = torch.empty_like(f)
+        _native.call("be_gelu_fwd", _native.ptr(f), _native.ptr(bias.float().contiguous()), _native.ptr(g), rows, C,
+                     _rpb(rows), _native.stream(f.device))
+        return g
+    return F.gelu(f.float() + bias.float()).to(f.dtype)
+
+
+def gelu_bwd(dg: torch.Tensor, f: torch.Tensor, bias: torch.Tensor):
+    """(df, dbias) for g = gelu(f + bias)."""
+    C = f.shape[-1]
+    rows = f.numel() // C
+    if f.is_cuda:
+        rpb = _rpb(rows)
+        df = torch.empty_like(f)
+        pcol = torch.empty(-(-rows // rpb), C, device=f.device, dtype=torch.float32)
+        _native.call("be_gelu_bwd", _native.ptr(dg.contiguous()), _native.ptr(f), _native.ptr(bias.float().contiguous()),
+                     _native.ptr(df), _native.ptr(pcol), rows, C, rpb, _native.stream(f.device))
+        return df, pcol.sum(0)
+    t = f.float() + bias.float()
+    d = 0.5 * (1 + torch.erf(t / math.sqrt(2))) + t * torch.exp(-0.5 * t * t) / math.sqrt(2 * math.pi)
+    df = dg.float() * d
+    return df.to(f.dtype), df.reshape(rows, C).sum(0)
+
+
+def scale_cast(x: torch.Tensor, rs: torch.Tensor | None = None, rpn: int = 1, dtype=torch.bfloat16):
+    """(rs[row // rpn] * x in ``dtype``, column sums of it in fp32)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if x.is_cuda:
+        rpb = _rpb(rows)
+        y = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16)
+        pcol = torch.empty(-(-rows // rpb), C, device=x.device, dtype=torch.float32)
+        _native.call("be_scale_cast", _native.ptr(x.float().contiguous()),
+                     _native.ptr(rs.float().contiguous() if rs is not None else None), int(rpn), _native.ptr(y),
+                     _native.ptr(pcol), rows, C, rpb, _native.stream(x.device))
+        return y, pcol.sum(0)
+    sc = _rowscale(rs, rows, rpn)
+    yf = x.float().reshape(rows, C)
+    if sc is not None:
+        yf = yf * sc
+    return yf.to(dtype).reshape(x.shape), yf.sum(0)
+
+
+# ------------------------------------------------------------------ attention
+def attn_fwd(q, k, v, scale: float, rel_h=None, rel_w=None):
+    """(out [B, N, H, 64], lse [B, H, N] natural log).  q/k/v [B, N, H, 64]."""
+    if q.is_cuda:
+        from .transformer import _attn_fwd_hip
+
+        return _attn_fwd_hip(q, k, v, scale, rel_h, rel_w, want_lse=True)
+    qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if rel_h is not None:
+        B, H, N, Hg = rel_h.shape
+        s = s + (rel_h.float()[..., :, None] + rel_w.float()[..., None, :]).reshape(B, H, N, -1)
+    lse = torch.logsumexp(s, -1)
+    o = torch.matmul(torch.exp(s - lse[..., None]), vf).permute(0, 2, 1, 3)
+    return o.to(q.dtype).contiguous(), lse
+
+
+def attn_bwd(q, k, v, o, do, lse, scale: float, rel_h=None, rel_w=None, dk=None, dv=None):
+    """Flash-attention backward.  q/k/v [B, N, H, 64] (views of a packed qkv are fine), o / do
+    [B, N, H, 64] contiguous, lse [B, H, N].  Returns (dq fp32 [B, N, H, 64], dk, dv, drel_h, drel_w);
+    ``dk``/``dv`` may be passed in as views of a packed gradient buffer (written in place)."""
+    B, N, H, D = q.shape
+    if q.is_cuda:
+        assert D == 64 and q.stride() == k.stride() == v.stride() and q.stride(-1) == 1
+        o = o.contiguous()
+        do = do.contiguous().to(torch.bfloat16)
+        dq = torch.empty(B, N, H, D, device=q.device, dtype=torch.float32)
+        if dk is None:
+            dk = torch.empty(B, N, H, D, device=q.device, dtype=torch.bfloat16)
+        if dv is None:
+            dv = torch.empty(B, N, H, D, device=q.device, dtype=torch.bfloat16)
+        assert dk.stride() == dv.stride() and dk.stride(-1) == 1
+        delta = torch.empty(B * H * N, device=q.device, dtype=torch.float32)
+        Hg = Wg = 0
+        rh = rw = drh = drw = None
+        if rel_h is not None:
+            Hg, Wg = rel_h.shape[-1], rel_w.shape[-1]
+            rh, rw = rel_h.float().contiguous(), rel_w.float().contiguous()
+            drh, drw = torch.empty_like(rh), torch.empty_like(rw)
+        _native.call("be_attn_bwd", _native.ptr(q), _native.ptr(k), _native.ptr(v), q.stride(1), q.stride(2),
+                     q.stride(0), _native.ptr(o), _native.ptr(do), o.stride(1), o.stride(2), o.stride(0),
+                     _native.ptr(lse.contiguous()), _native.ptr(delta), _native.ptr(rh), _native.ptr(rw), Hg, Wg,
+                     _native.ptr(dq), _native.ptr(drh), _native.ptr(drw), _native.ptr(dk), _native.ptr(dv),
+                     dk.stride(1), dk.stride(2), dk.stride(0), B, H, N, D, float(scale), 0, _native.stream(q.device))
+        return dq, dk, dv, drh, drw
+    qf, kf, vf = (t.float().permute(0, 2, 1, 3) for t in (q, k, v))
+    of, gf = o.float().permute(0, 2, 1, 3), do.float().permute(0, 2, 1, 3)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if rel_h is not None:
+        s = s + (rel_h.float()[..., :, None] + rel_w.float()[..., None, :]).reshape(B, H, N, -1)
+    p = torch.exp(s - lse[..., None].float())
+    dvf = torch.matmul(p.transpose(-1, -2), gf)
+    dp = torch.matmul(gf, vf.transpose(-1, -2))
+    ds = p * (dp - (gf * of).sum(-1, keepdim=True))
+    dqf = torch.matmul(ds, kf) * scale
+    dkf = torch.matmul(ds.transpose(-1, -2), qf) * scale
+    drh = drw = None
+    if rel_h is not None:
+        ds5 = ds.reshape(B, H, N, rel_h.shape[-1], rel_w.shape[-1])
+        drh, drw = ds5.sum(-1), ds5.sum(-2)
+    back = lambda t: t.permute(0, 2, 1, 3)
+    dkt, dvt = back(dkf).to(k.dtype), back(dvf).to(v.dtype)
+    if dk is not None:
+        dk.copy_(dkt)
+        dv.copy_(dvt)
+    else:
+        dk, dv = dkt, dvt
+    return back(dqf).contiguous(), dk, dv, drh, drw

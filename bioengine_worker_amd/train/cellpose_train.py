@@ -80,8 +80,11 @@ class CellposeTrainer:
         self.device = torch.device(device)
         self.world = world_size
         self.rank = rank
+        from ..models.cpsam import CPSAM
+
+        self.is_cpsam = isinstance(net, CPSAM)
         self.net = net.to(self.device).train()
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and not self.is_cpsam:
             self.net = self.net.to(memory_format=torch.channels_last)
         self.fp = FlatParams(self.net, self.device)
         if world_size > 1:
@@ -94,10 +97,13 @@ class CellposeTrainer:
         self.lr = cfg.lr
         self.gen = torch.Generator().manual_seed(cfg.seed * 1000 + rank)
         eng = cfg.engine
-        if eng == "auto":
+        if self.is_cpsam:
+            eng = "cpsam"  # explicit fwd/bwd engine (train/cpsam_engine.py) on CPU and GPU
+        elif eng == "auto":
             eng = "hip" if (self.device.type == "cuda" and cfg.norm == "batch") else "autograd"
         self.engine_kind = eng
         self._eng = None
+        self._cpsam_engs: dict = {}
         self._graph = None
         self._graph_io = None
 
@@ -127,6 +133,8 @@ class CellposeTrainer:
 
         with trace.span("train.augment", cuda=True):
             x, lbl = self.augment(imgs, lbls, rescale)
+        if self.engine_kind == "cpsam":
+            return self._step_cpsam(x, lbl)
         if self.engine_kind == "hip":
             return self._step_engine(x, lbl)
         self.fp.zero_grad()
@@ -166,6 +174,43 @@ class CellposeTrainer:
                                   weight_decay=self.cfg.weight_decay, grad_scale=gscale)
         return loss
 
+    def _cpsam_engine(self, B: int):
+        from .cpsam_engine import CPSAMTrainEngine
+
+        eng = self._cpsam_engs.get(B)
+        if eng is None:
+            # all engines of this trainer share one bf16 weight mirror (refreshed by the AdamW kernel)
+            first = next(iter(self._cpsam_engs.values()), None)
+            eng = CPSAMTrainEngine(self.net, self.fp, B, self.device)
+            if first is not None:
+                eng.mirror = first.mirror
+            self._cpsam_engs[B] = eng
+        return eng
+
+    def _step_cpsam(self, x: torch.Tensor, lbl: torch.Tensor) -> torch.Tensor:
+        from ..profiling import trace
+        from .cpsam_engine import stochastic_depth_keep
+
+        eng = self._cpsam_engine(x.shape[0])
+        keep = None
+        if self.net.rdrop > 0:
+            keep = stochastic_depth_keep(x.shape[0], len(eng.blocks), self.net.rdrop, self.device, self.gen)
+        with trace.span("train.fwd_bwd_cpsam", cuda=True):
+            loss = eng.loss_and_backward(x, lbl, keep, on_params_ready=self.ar.mark_ready if self.world > 1 else None)
+        with trace.span("train.grad_allreduce_finish", cuda=True):
+            gscale = self.ar.finish()
+        self.step_count += 1
+        with trace.span("train.adamw", cuda=True):
+            mirror = eng.mirror if eng.mirror is not self.fp.flat else None
+            train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
+                                  weight_decay=self.cfg.weight_decay, grad_scale=gscale, p_bf16=mirror)
+        return loss
+
+    def _refresh_mirrors(self) -> None:
+        for eng in self._cpsam_engs.values():
+            eng.refresh_mirror()
+            break  # shared
+
     def _graph_step(self, eng, x: torch.Tensor, lbl: torch.Tensor) -> torch.Tensor:
         """Replay the captured fwd+bwd on static input buffers (captured on first use per shape)."""
         key = (tuple(x.shape), tuple(lbl.shape), x.dtype)
@@ -191,7 +236,9 @@ class CellposeTrainer:
     def validate(self, imgs: torch.Tensor, lbls: torch.Tensor) -> dict:
         self.net.eval()
         x, lbl = self.augment(imgs, lbls)
-        if self.device.type == "cuda":
+        if self.is_cpsam:
+            y = self._cpsam_engine(x.shape[0]).forward(x, None, save=False)
+        elif self.device.type == "cuda":
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.cfg.autocast_bf16):
                 y = self.net(x.contiguous(memory_format=torch.channels_last))[0]
         else:
@@ -226,6 +273,7 @@ class CellposeTrainer:
             st = torch.tensor([self.step_count], dtype=torch.int64, device=self.fp.flat.device)
             dist.broadcast(st, src=0, group=group)
             self.step_count = int(st.item())
+        self._refresh_mirrors()
 
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:
@@ -244,6 +292,7 @@ class CellposeTrainer:
         for k, v in sd.get("buffers", {}).items():
             if k in bufs:
                 bufs[k].copy_(v.to(bufs[k].device))
+        self._refresh_mirrors()
 
 
 def build_trainer(cfg: TrainConfig, device, world_size: int = 1, rank: int = 0, net: CPnet | None = None,

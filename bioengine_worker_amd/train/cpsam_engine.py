@@ -1,0 +1,314 @@
+"""Cellpose-SAM (``cpsam``) training engine: explicit forward + backward on the framework's kernels.
+
+The reference fine-tunes Cellpose-SAM (``apps/cellpose-finetuning/main.py:1278-1713``; net in
+fp32 after a bf16 load, ``:1350-1358``; AdamW ``:1451-1453``; ``_loss_fn_seg`` ``:1514-1517``;
+SURVEY.md §2.5 K8) through PyTorch autograd.  Here the ViT-L/8 step is written out by hand so every
+hot op is ours and the whole step can be one HIP graph:
+
+forward, per block (pre-norm SAM block, global attention, decomposed rel-pos bias)::
+
+    h1, st1   = LN1(t_in)                                 fused add+LN kernel (stats saved)
+    qkv       = h1 Wqkv^T + b                             hipBLASLt
+    rel_h/w   = q . R_h / R_w                             small batched GEMMs (fp32)
+    a, lse    = flash_attn(q, k, v, rel_h, rel_w)         HIP MFMA kernel (attention.hip)
+    y         = a Wproj^T + b
+    t_mid,h2  = t_in + k_b * y, LN2(t_mid)                fused add+LN (k_b = stochastic-depth keep)
+    f         = h2 W1^T ;  g = gelu(f + b1)               hipBLASLt + HIP GELU
+    m         = g W2^T + b2
+    t_out     = t_mid + k_b * m                           fused into the next block's LN1
+
+backward mirrors it with the HIP LayerNorm/GELU/cast backward kernels (``vit_train.hip``), the
+flash-attention backward with rel-pos gradients (``attention_bwd.hip``), and hipBLASLt dgrad/wgrad
+GEMMs whose fp32 weight gradients land directly in the flat gradient buffer the fused AdamW reads.
+
+Stochastic depth follows cellpose 4's ``Transformer.forward``: per sample and layer, a block is
+dropped with probability ``linspace(0, rdrop, nlay)[layer]`` (``x*mask + blk(x)*(1-mask)``).  Since
+the mask is 0/1, ``t_in + k (y + m)`` with ``t_mid = t_in + k y`` is the same function and the
+same gradients, and keeps every kernel's shape static (graph-capturable).
+
+Precision: bf16 operands with fp32 accumulation, fp32 master weights, LayerNorm statistics,
+softmax, residual-stream gradients and optimizer state (the reference runs fp32; the numerics test
+bounds the difference against an fp32 autograd oracle).  On CPU every op runs its fp32 PyTorch
+reference, so the same engine code is checked against autograd in the CPU suite.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..models.cpsam import CPSAM, get_rel_pos
+from ..ops import vit_train as vt
+from ..parallel.ddp import FlatParams
+
+_MM_OUT_DTYPE: bool | None = None
+
+
+def _wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> None:
+    """out (fp32 [n, k]) = dy^T x with dy [m, n], x [m, k] (bf16 on GPU; fp32 output straight from
+    hipBLASLt when this torch supports ``out_dtype``)."""
+    global _MM_OUT_DTYPE
+    out2 = out.view(out.shape[0], -1)
+    if dy.dtype == torch.bfloat16:
+        if _MM_OUT_DTYPE is None:
+            try:
+                torch.mm(dy[:1].t(), x[:1], out_dtype=torch.float32)
+                _MM_OUT_DTYPE = True
+            except Exception:  # noqa: BLE001
+                _MM_OUT_DTYPE = False
+        if _MM_OUT_DTYPE:
+            out2.copy_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+            return
+    out2.copy_(torch.mm(dy.t(), x))
+
+
+class _Blk:
+    __slots__ = ("p", "w")
+
+    def __init__(self):
+        self.p = {}
+        self.w = {}
+
+
+class CPSAMTrainEngine:
+    """Forward + backward of :class:`CPSAM` at a fixed batch shape ``[B, 3, bsize, bsize]``."""
+
+    def __init__(self, net: CPSAM, fp: FlatParams, B: int, device, eps: float = 1e-6):
+        self.net, self.fp, self.B = net, fp, int(B)
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.cdt = torch.bfloat16 if self.cuda else torch.float32
+        self.eps = eps
+        e = net.encoder
+        self.ps, self.g, self.nout = net.ps, net.grid, net.nout
+        self.D = e.patch_embed.proj.weight.shape[0]
+        self.H = e.blocks[0].attn.num_heads
+        self.hd = self.D // self.H
+        self.N = self.g * self.g
+        self.scale = self.hd ** -0.5
+        self.mirror = fp.flat.to(self.cdt) if self.cdt != torch.float32 else fp.flat
+        off = {id(p): o for p, o in zip(fp.params, fp.offsets)}
+        W = lambda p: self.mirror[off[id(p)]: off[id(p)] + p.numel()].view_as(p)
+        self._W = W
+        self.pe = (e.patch_embed.proj.weight, e.patch_embed.proj.bias)
+        self.pos = e.pos_embed
+        self.blocks = []
+        for blk in e.blocks:
+            b = _Blk()
+            b.p = dict(n1w=blk.norm1.weight, n1b=blk.norm1.bias, qkv_w=blk.attn.qkv.weight, qkv_b=blk.attn.qkv.bias,
+                       proj_w=blk.attn.proj.weight, proj_b=blk.attn.proj.bias, rph=blk.attn.rel_pos_h,
+                       rpw=blk.attn.rel_pos_w, n2w=blk.norm2.weight, n2b=blk.norm2.bias, l1_w=blk.mlp.lin1.weight,
+                       l1_b=blk.mlp.lin1.bias, l2_w=blk.mlp.lin2.weight, l2_b=blk.mlp.lin2.bias)
+            b.w = {k: W(v) for k, v in b.p.items()}
+            self.blocks.append(b)
+        self.neck = e.neck
+        self.outc = net.out
+        g = self.g
+        ar = torch.arange(g, device=self.device)
+        self.rel_idx = (ar[:, None] - ar[None, :] + (g - 1)).long()  # get_rel_pos index at q == k size
+        for blk in e.blocks:
+            if blk.attn.rel_pos_h.shape[0] != 2 * g - 1:
+                raise ValueError("CPSAMTrainEngine needs rel-pos tables sized for the training grid")
+
+    def refresh_mirror(self) -> None:
+        """Re-derive the bf16 weight mirror from the fp32 master (after a load / broadcast)."""
+        if self.mirror is not self.fp.flat:
+            self.mirror.copy_(self.fp.flat)
+
+    # ------------------------------------------------------------------ helpers
+    def _rel_terms(self, q: torch.Tensor, Rh: torch.Tensor, Rw: torch.Tensor):
+        """q [B, N, H, c] -> rel_h [B, H, N, g], rel_w [B, H, N, g] (fp32) as batched GEMMs."""
+        B, g, H, c = self.B, self.g, self.H, self.hd
+        q5 = q.reshape(B, g, g, H, c)
+        # rel_h[b,h,y,x,k] = sum_c q[b,y,x,h,c] Rh[y,k,c]: batch over y
+        qy = q5.permute(1, 0, 2, 3, 4).reshape(g, B * g * H, c).float()
+        rh = torch.bmm(qy, Rh.transpose(1, 2)).reshape(g, B, g, H, g).permute(1, 3, 0, 2, 4)
+        qx = q5.permute(2, 0, 1, 3, 4).reshape(g, B * g * H, c).float()
+        rw = torch.bmm(qx, Rw.transpose(1, 2)).reshape(g, B, g, H, g).permute(1, 3, 2, 0, 4)
+        return rh.reshape(B, H, self.N, g).contiguous(), rw.reshape(B, H, self.N, g).contiguous()
+
+    def _rel_bwd(self, q, Rh, Rw, drh, drw):
+        """-> (dq_rel [B, N, H, c] fp32, dRh [g, g, c], dRw [g, g, c])."""
+        B, g, H, c = self.B, self.g, self.H, self.hd
+        drh5 = drh.reshape(B, H, g, g, g)  # b h y x k
+        drw5 = drw.reshape(B, H, g, g, g)
+        # dq[b,y,x,h,c] = sum_k drh[b,h,y,x,k] Rh[y,k,c] + sum_k drw[b,h,y,x,k] Rw[x,k,c]
+        a = drh5.permute(2, 0, 3, 1, 4).reshape(g, B * g * H, g)          # y, (b x h), k
+        dq_h = torch.bmm(a, Rh).reshape(g, B, g, H, c).permute(1, 0, 2, 3, 4)
+        bw = drw5.permute(3, 0, 2, 1, 4).reshape(g, B * g * H, g)          # x, (b y h), k
+        dq_w = torch.bmm(bw, Rw).reshape(g, B, g, H, c).permute(1, 2, 0, 3, 4)
+        q5 = q.reshape(B, g, g, H, c).float()
+        qy = q5.permute(1, 0, 2, 3, 4).reshape(g, B * g * H, c)            # y, (b x h), c
+        dRh = torch.bmm(a.transpose(1, 2), qy)                              # y, k, c
+        qx = q5.permute(2, 0, 1, 3, 4).reshape(g, B * g * H, c)            # x, (b y h), c
+        dRw = torch.bmm(bw.transpose(1, 2), qx)
+        return (dq_h + dq_w).reshape(B, self.N, H, c), dRh, dRw
+
+    def _table_grad(self, dR: torch.Tensor, out: torch.Tensor) -> None:
+        out.zero_()
+        out.index_add_(0, self.rel_idx.reshape(-1), dR.reshape(-1, dR.shape[-1]))
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, keep: torch.Tensor | None = None, save: bool = True) -> torch.Tensor:
+        """x [B, C<=3, S, S] float -> flows [B, nout, S, S] (compute dtype).  ``keep`` [B, nlay] 0/1
+        (stochastic depth; None = keep all)."""
+        B, ps, g, D, N, H = self.B, self.ps, self.g, self.D, self.N, self.H
+        assert x.shape[0] == B and x.shape[-1] == g * ps and x.shape[-2] == g * ps
+        if x.shape[1] < 3:
+            x = torch.cat([x, x.new_zeros(B, 3 - x.shape[1], *x.shape[2:])], 1)
+        W = self._W
+        patches = x.to(self.cdt).reshape(B, 3, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B * N, 3 * ps * ps)
+        t = F.linear(patches, W(self.pe[0]).reshape(D, -1), W(self.pe[1]))
+        t = (t.view(B, N, D) + W(self.pos).reshape(1, N, D)).reshape(B * N, D).contiguous()
+        saved = {"patches": patches, "keep": keep, "blocks": []}
+        nl = len(self.blocks)
+        # LN1 of block 0
+        _, h1, st1 = vt.ln_fwd(t, self.blocks[0].p["n1w"], self.blocks[0].p["n1b"], eps=self.eps)
+        for i, b in enumerate(self.blocks):
+            w, p = b.w, b.p
+            kb = keep[:, i].contiguous() if keep is not None else None
+            qkv = F.linear(h1, w["qkv_w"], w["qkv_b"]).view(B, N, 3, H, self.hd)
+            q, k_, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+            Rh = get_rel_pos(g, g, p["rph"].detach()).float()
+            Rw = get_rel_pos(g, g, p["rpw"].detach()).float()
+            rel_h, rel_w = self._rel_terms(q, Rh, Rw)
+            a, lse = vt.attn_fwd(q, k_, v, self.scale, rel_h, rel_w)
+            a2 = a.reshape(B * N, D)
+            y = F.linear(a2, w["proj_w"], w["proj_b"])
+            t_mid, h2, st2 = vt.ln_fwd(t, p["n2w"], p["n2b"], y=y, rs=kb, rpn=N, eps=self.eps)
+            f = F.linear(h2, w["l1_w"])
+            gg = vt.gelu_fwd(f, p["l1_b"])
+            m = F.linear(gg, w["l2_w"], w["l2_b"])
+            if save:
+                saved["blocks"].append(dict(t_in=t, st1=st1, h1=h1, qkv=qkv, rel_h=rel_h, rel_w=rel_w, Rh=Rh, Rw=Rw,
+                                            a=a, lse=lse, t_mid=t_mid, st2=st2, h2=h2, f=f, g=gg, keep=kb))
+            if i + 1 < nl:
+                nb = self.blocks[i + 1].p
+                t, h1, st1 = vt.ln_fwd(t_mid, nb["n1w"], nb["n1b"], y=m, rs=kb, rpn=N, eps=self.eps)
+            else:
+                t = self._residual(t_mid, m, kb)
+        # neck: 1x1 conv (GEMM) -> LN2d -> 3x3 conv -> LN2d -> readout -> pixel shuffle
+        n0 = F.linear(t, W(self.neck[0].weight).reshape(256, D))
+        _, n1, sn1 = vt.ln_fwd(n0, self.neck[1].weight, self.neck[1].bias, eps=self.eps)
+        n1i = n1.view(B, g, g, 256).permute(0, 3, 1, 2)  # NCHW view of NHWC memory (channels_last)
+        n2 = F.conv2d(n1i, W(self.neck[2].weight), padding=1)
+        n2r = n2.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
+        _, n3, sn3 = vt.ln_fwd(n2r, self.neck[3].weight, self.neck[3].bias, eps=self.eps)
+        o = F.linear(n3, W(self.outc.weight).reshape(self.outc.weight.shape[0], 256), W(self.outc.bias))
+        yout = o.view(B, g, g, self.nout, ps, ps).permute(0, 3, 1, 4, 2, 5).reshape(B, self.nout, g * ps, g * ps)
+        if save:
+            saved.update(t_last=t, n0=n0, n1=n1, n1i=n1i, sn1=sn1, n2r=n2r, sn3=sn3, n3=n3)
+            self._saved = saved
+        return yout
+
+    @staticmethod
+    def _residual(x, y, kb):
+        if kb is None:
+            return x + y
+        B = kb.shape[0]
+        return (x.view(B, -1) + y.view(B, -1) * kb.to(x.dtype)[:, None]).view(x.shape)
+
+    # ------------------------------------------------------------------ backward
+    @torch.no_grad()
+    def backward(self, dyout: torch.Tensor, on_params_ready=None) -> None:
+        """dyout [B, nout, S, S] -> parameter gradients written into ``fp.grad`` (overwritten).
+        ``on_params_ready(params)`` fires as each group's gradients are final (DDP bucket launch)."""
+        ready = on_params_ready or (lambda ps: None)
+        s = self._saved
+        B, ps, g, D, N, H, hd = self.B, self.ps, self.g, self.D, self.N, self.H, self.hd
+        W = self._W
+        cd = self.cdt
+        # pixel unshuffle of the output gradient -> [B*N, nout*ps*ps]
+        do = dyout.to(cd).reshape(B, self.nout, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B * N, -1).contiguous()
+        outw = W(self.outc.weight).reshape(self.outc.weight.shape[0], 256)
+        self.outc.bias.grad.copy_(do.float().sum(0))
+        _wgrad(do, s["n3"], self.outc.weight.grad)
+        dn3 = torch.mm(do, outw)
+        _, dn2, dw3, db3, _ = vt.ln_bwd(dn3, s["n2r"], s["sn3"], self.neck[3].weight, want_dx=False, want_dxb=True)
+        self.neck[3].weight.grad.copy_(dw3)
+        self.neck[3].bias.grad.copy_(db3)
+        dn2i = dn2.view(B, g, g, 256).permute(0, 3, 1, 2)
+        cw = W(self.neck[2].weight)
+        dn1i, dcw, _ = torch.ops.aten.convolution_backward(dn2i, s["n1i"], cw, None, [1, 1], [1, 1], [1, 1], False,
+                                                           [0, 0], 1, [True, True, False])
+        self.neck[2].weight.grad.copy_(dcw)
+        dn1 = dn1i.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
+        _, dn0, dw1, db1, _ = vt.ln_bwd(dn1, s["n0"], s["sn1"], self.neck[1].weight, want_dx=False, want_dxb=True)
+        self.neck[1].weight.grad.copy_(dw1)
+        self.neck[1].bias.grad.copy_(db1)
+        n0w = W(self.neck[0].weight).reshape(256, D)
+        _wgrad(dn0, s["t_last"], self.neck[0].weight.grad)
+        G = torch.mm(dn0, n0w).float()  # d t_out of the last block (fp32 residual-stream gradient)
+        ready([self.outc.weight, self.outc.bias, self.neck[3].weight, self.neck[3].bias, self.neck[2].weight,
+               self.neck[1].weight, self.neck[1].bias, self.neck[0].weight])
+        for i in range(len(self.blocks) - 1, -1, -1):
+            G = self._block_bwd(self.blocks[i], s["blocks"][i], G)
+            ready(list(self.blocks[i].p.values()))
+        # patch embedding + position embedding
+        self.pos.grad.copy_(G.view(B, N, D).sum(0).view_as(self.pos))
+        Gb, colG = vt.scale_cast(G, dtype=cd)
+        self.pe[1].grad.copy_(colG)
+        _wgrad(Gb, s["patches"], self.pe[0].grad)
+        ready([self.pos, self.pe[0], self.pe[1]])
+        self._saved = None
+
+    def _block_bwd(self, b: _Blk, s: dict, G: torch.Tensor) -> torch.Tensor:
+        B, N, D, H, hd = self.B, self.N, self.D, self.H, self.hd
+        w, p = b.w, b.p
+        kb = s["keep"]
+        # MLP: t_out = t_mid + k m
+        dm, db2 = vt.scale_cast(G, kb, N, dtype=self.cdt)
+        p["l2_b"].grad.copy_(db2)
+        _wgrad(dm, s["g"], p["l2_w"].grad)
+        dg = torch.mm(dm, w["l2_w"])
+        df, db1 = vt.gelu_bwd(dg, s["f"], p["l1_b"])
+        p["l1_b"].grad.copy_(db1)
+        _wgrad(df, s["h2"], p["l1_w"].grad)
+        dh2 = torch.mm(df, w["l1_w"])
+        dt_mid, _, dn2w, dn2b, _ = vt.ln_bwd(dh2, s["t_mid"], s["st2"], p["n2w"], r1=G)
+        p["n2w"].grad.copy_(dn2w)
+        p["n2b"].grad.copy_(dn2b)
+        # attention: t_mid = t_in + k y
+        dy, dbp = vt.scale_cast(dt_mid, kb, N, dtype=self.cdt)
+        p["proj_b"].grad.copy_(dbp)
+        _wgrad(dy, s["a"].reshape(B * N, D), p["proj_w"].grad)
+        da = torch.mm(dy, w["proj_w"]).view(B, N, H, hd)
+        qkv = s["qkv"]
+        dqkv = torch.empty(B, N, 3, H, hd, device=G.device, dtype=self.cdt)
+        dq, _, _, drh, drw = vt.attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], s["a"], da, s["lse"], self.scale,
+                                         s["rel_h"], s["rel_w"], dk=dqkv[:, :, 1], dv=dqkv[:, :, 2])
+        dq_rel, dRh, dRw = self._rel_bwd(qkv[:, :, 0], s["Rh"], s["Rw"], drh, drw)
+        dqkv[:, :, 0] = (dq + dq_rel).to(self.cdt)
+        self._table_grad(dRh, p["rph"].grad)
+        self._table_grad(dRw, p["rpw"].grad)
+        dqkv2 = dqkv.view(B * N, 3 * D)
+        p["qkv_b"].grad.copy_(dqkv2.sum(0, dtype=torch.float32))
+        _wgrad(dqkv2, s["h1"], p["qkv_w"].grad)
+        dh1 = torch.mm(dqkv2, w["qkv_w"])
+        dt_in, _, dn1w, dn1b, _ = vt.ln_bwd(dh1, s["t_in"], s["st1"], p["n1w"], r1=dt_mid)
+        p["n1w"].grad.copy_(dn1w)
+        p["n1b"].grad.copy_(dn1b)
+        return dt_in
+
+    # ------------------------------------------------------------------ step
+    def loss_and_backward(self, x: torch.Tensor, lbl: torch.Tensor, keep: torch.Tensor | None = None,
+                          on_params_ready=None):
+        from ..ops import train_ops
+
+        y = self.forward(x, keep)
+        if self.cuda:
+            loss, dy = train_ops.seg_loss_and_grad(y, lbl)
+        else:
+            yr = y.detach().float().requires_grad_(True)
+            loss = train_ops.seg_loss_ref(yr, lbl)
+            (dy,) = torch.autograd.grad(loss, yr)
+            loss = loss.detach()
+        self.backward(dy, on_params_ready)
+        return loss
+
+
+def stochastic_depth_keep(B: int, nlay: int, rdrop: float, device, generator=None) -> torch.Tensor:
+    """cellpose 4 ``Transformer.forward``: layer i of sample b is dropped with probability
+    ``linspace(0, rdrop, nlay)[i]``.  Returns the 0/1 keep mask [B, nlay] (fp32)."""
+    r = torch.rand(B, nlay, generator=generator).to(device)
+    return (r >= torch.linspace(0, rdrop, nlay, device=device)[None]).float()

@@ -41,11 +41,14 @@ __global__ __launch_bounds__(256) void add_ln_kernel(bf16_t* __restrict__ x, con
                                                      const float* __restrict__ bias, bf16_t* __restrict__ out,
                                                      float* __restrict__ stats, long long rows, int C, float eps,
                                                      int write_x, uint8_t* __restrict__ q8,
-                                                     float* __restrict__ qscale) {
+                                                     float* __restrict__ qscale, bf16_t* __restrict__ xo = nullptr,
+                                                     const float* __restrict__ rs = nullptr, int rpn = 1) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   bf16_t* xr = x + row * C;
+  bf16_t* xw = (xo ? xo : x) + row * C;  // where the updated residual goes (training keeps the input)
+  const float rsc = rs ? rs[row / rpn] : 1.f;  // per-sample scale of y (stochastic depth keep mask)
   float v[NV][8];
   float s = 0.f;
 #pragma unroll
@@ -61,15 +64,15 @@ __global__ __launch_bounds__(256) void add_ln_kernel(bf16_t* __restrict__ x, con
           const float4 g1 = *reinterpret_cast<const float4*>(gamma + c + 4);
           const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[k][j] += g[j] * t[j];
+          for (int j = 0; j < 8; ++j) v[k][j] += rsc * g[j] * t[j];
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[k][j] += t[j];
+          for (int j = 0; j < 8; ++j) v[k][j] += rsc * t[j];
         }
         // the residual stream is bf16: normalise exactly what the next block will read back
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j]));
-        if (write_x) store8(xr + c, v[k]);
+        if (write_x) store8(xw + c, v[k]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[k][j];
@@ -192,6 +195,28 @@ int be_add_layernorm_fp8(void* x, const void* y, const float* gamma, const float
     default: return -1;
   }
 #undef LNQ
+  return BE_CHECK_LAUNCH();
+}
+
+// Training variant: xo = x + rs[row / rpn] * y (x untouched; rs optional per-sample scale), out = LN(xo),
+// stats = (mean, rstd) per row for the backward.  y == null: plain LN of x (xo ignored).
+int be_add_layernorm_train(const void* x, const void* y, const float* rs, int rpn, void* xo, const float* w,
+                           const float* b, void* out, float* stats, long long rows, int C, float eps, hipStream_t s) {
+  if (C % 8 != 0 || C > 64 * 8 * MAXV || !w || !b || !out || !stats) return -1;
+  if (y && !xo) return -2;
+  const int nv = (C / 8 + 63) / 64;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+#define LNT(NV)                                                                                                   \
+  case NV:                                                                                                        \
+    hipLaunchKernelGGL((add_ln_kernel<NV, false>), grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)y,            \
+                       (const float*)nullptr, w, b, (bf16_t*)out, stats, rows, C, eps, y ? 1 : 0, (uint8_t*)nullptr, \
+                       (float*)nullptr, (bf16_t*)xo, rs, rpn > 0 ? rpn : 1);                                      \
+    break;
+  switch (nv) {
+    LNT(1) LNT(2) LNT(3) LNT(4)
+    default: return -1;
+  }
+#undef LNT
   return BE_CHECK_LAUNCH();
 }
 

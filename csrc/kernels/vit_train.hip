@@ -1,0 +1,263 @@
+// Row-wise backward kernels of the ViT training step (Cellpose-SAM fine-tuning, SURVEY.md §2.5 K8;
+// reference training loop apps/cellpose-finetuning/main.py:1468-1546).  Everything between the
+// hipBLASLt GEMMs and the flash-attention kernels is one fused pass each:
+//
+//  * be_ln_bwd        LayerNorm backward from the saved (mean, rstd) + the residual-stream
+//                     gradient accumulation dx = LN'(dh) + s1[b] r1 + s2[b] r2 (fp32, optional bf16
+//                     copy for the next GEMM) + per-block column partials of dw, db and sum(dx)
+//                     (the following projection's bias gradient).
+//  * be_gelu_fwd      g = gelu(f + bias) into a separate buffer (f is kept for the backward).
+//  * be_gelu_bwd      df = dg * gelu'(f + bias) (bf16) + column partials of df (fc1 bias grad).
+//  * be_scale_cast    y = s[b] * x (fp32 -> bf16) + column partials of y (bias grad of the GEMM that
+//                     consumes it); s is the per-sample stochastic-depth keep factor.
+//
+// Column sums are never done with atomics: each block owns a row range and writes one partial row
+// [nblocks, C]; the caller reduces the partials (deterministic, and tiny next to the GEMMs).
+#include "common.h"
+
+namespace {
+
+constexpr int MAXV = 4;  // LN: C <= 64 lanes * 8 * MAXV
+
+__device__ __forceinline__ void ld8(const bf16_t* p, float (&v)[8]) {
+  const u32x4 r = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(r[j]); v[2 * j + 1] = hi_bf(r[j]); }
+}
+__device__ __forceinline__ void st8(bf16_t* p, const float (&v)[8]) {
+  u32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = pack2bf(v[2 * j], v[2 * j + 1]);
+  *reinterpret_cast<u32x4*>(p) = r;
+}
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8f(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// one wave per row (4 rows in flight per block), `rpb` rows per block; column partials reduced over
+// the block's waves through LDS and written as one row of each partial matrix.
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ x,
+                                                     const float* __restrict__ stats, const float* __restrict__ w,
+                                                     const float* __restrict__ r1, const float* __restrict__ s1,
+                                                     const float* __restrict__ r2, const float* __restrict__ s2, int rpn,
+                                                     float* __restrict__ dx, bf16_t* __restrict__ dxb,
+                                                     float* __restrict__ pdw, float* __restrict__ pdb,
+                                                     float* __restrict__ pcol, long long rows, int C, int rpb) {
+  __shared__ float red[4][64 * 8 * MAXV];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1e = min(r0 + rpb, rows);
+  float aw[NV][8], ab[NV][8], ac[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { aw[k][j] = 0.f; ab[k][j] = 0.f; ac[k][j] = 0.f; }
+  for (long long row = r0 + wave; row < r1e; row += 4) {
+    const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    float g[NV][8], xh[NV][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < C) {
+        float d[8], xv[8], ww[8];
+        ld8(dh + row * C + c, d);
+        ld8(x + row * C + c, xv);
+        ld8f(w + c, ww);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[k][j] = (xv[j] - mean) * rstd;
+          g[k][j] = d[j] * ww[j];
+          sg += g[k][j];
+          sgx += g[k][j] * xh[k][j];
+          aw[k][j] += d[j] * xh[k][j];
+          ab[k][j] += d[j];
+        }
+      }
+    }
+    sg = wave_sum(sg) / C;
+    sgx = wave_sum(sgx) / C;
+    const float sc1 = r1 ? (s1 ? s1[row / rpn] : 1.f) : 0.f;
+    const float sc2 = r2 ? (s2 ? s2[row / rpn] : 1.f) : 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < C) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - sg - xh[k][j] * sgx);
+        if (r1) {
+          float t[8];
+          ld8f(r1 + row * C + c, t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += sc1 * t[j];
+        }
+        if (r2) {
+          float t[8];
+          ld8f(r2 + row * C + c, t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += sc2 * t[j];
+        }
+        if (dx) st8f(dx + row * C + c, o);
+        if (dxb) st8(dxb + row * C + c, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ac[k][j] += o[j];
+      }
+    }
+  }
+  // block reduction of the three column partials (waves -> LDS -> one row each)
+  auto flush = [&](float (&acc)[NV][8], float* out) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < C) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[wave][c + j] = acc[k][j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256)
+      out[(long long)blockIdx.x * C + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    __syncthreads();
+  };
+  if (pdw) flush(aw, pdw);
+  if (pdb) flush(ab, pdb);
+  if (pcol) flush(ac, pcol);
+}
+
+__device__ __forceinline__ float gelu_f(float t) { return 0.5f * t * (1.f + erff(t * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_d(float t) {
+  return 0.5f * (1.f + erff(t * 0.70710678118654752f)) + t * 0.3989422804014327f * __expf(-0.5f * t * t);
+}
+
+// elementwise kernels with column partials: a block owns `rpb` rows and all columns; thread t owns
+// the 8-column chunks t, t + 256, ... (NC chunks), so the column sums stay in its registers.
+template <int NC, int MODE>  // MODE 0: gelu fwd, 1: gelu bwd, 2: scale-cast
+__global__ __launch_bounds__(256) void rowcol_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ f,
+                                                     const float* __restrict__ xf, const float* __restrict__ bias,
+                                                     const float* __restrict__ rs, int rpn, bf16_t* __restrict__ out,
+                                                     float* __restrict__ pcol, long long rows, int C, int rpb) {
+  const int C8 = C / 8;
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = min(r0 + rpb, rows);
+  float acc[NC][8];
+  float bb[NC][8];
+#pragma unroll
+  for (int n = 0; n < NC; ++n) {
+    const int ch = threadIdx.x + n * 256;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { acc[n][j] = 0.f; bb[n][j] = 0.f; }
+    if (bias && ch < C8) ld8f(bias + ch * 8, bb[n]);
+  }
+  for (long long row = r0; row < r1; ++row) {
+    const float sc = rs ? rs[row / rpn] : 1.f;
+#pragma unroll
+    for (int n = 0; n < NC; ++n) {
+      const int ch = threadIdx.x + n * 256;
+      if (ch >= C8) continue;
+      const long long e = row * C + ch * 8;
+      float o[8];
+      if (MODE == 0) {
+        float t[8];
+        ld8(f + e, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = gelu_f(t[j] + bb[n][j]);
+      } else if (MODE == 1) {
+        float d[8], t[8];
+        ld8(a + e, d);
+        ld8(f + e, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = d[j] * gelu_d(t[j] + bb[n][j]);
+      } else {
+        float t[8];
+        ld8f(xf + e, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = sc * t[j];
+      }
+      st8(out + e, o);
+      if (MODE != 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[n][j] += o[j];
+      }
+    }
+  }
+  if (MODE != 0 && pcol) {
+#pragma unroll
+    for (int n = 0; n < NC; ++n) {
+      const int ch = threadIdx.x + n * 256;
+      if (ch < C8) st8f(pcol + (long long)blockIdx.x * C + ch * 8, acc[n]);
+    }
+  }
+}
+
+template <int MODE>
+int launch_rowcol(const bf16_t* a, const bf16_t* f, const float* xf, const float* bias, const float* rs, int rpn,
+                  bf16_t* out, float* pcol, long long rows, int C, int rpb, hipStream_t s) {
+  if (C % 8 != 0 || rpb <= 0) return -1;
+  const int nc = (C / 8 + 255) / 256;
+  const dim3 grid((unsigned)((rows + rpb - 1) / rpb));
+  if (rpn <= 0) rpn = 1;
+  switch (nc) {
+    case 1: hipLaunchKernelGGL((rowcol_kernel<1, MODE>), grid, dim3(256), 0, s, a, f, xf, bias, rs, rpn, out, pcol, rows, C, rpb); break;
+    case 2: hipLaunchKernelGGL((rowcol_kernel<2, MODE>), grid, dim3(256), 0, s, a, f, xf, bias, rs, rpn, out, pcol, rows, C, rpb); break;
+    case 3: hipLaunchKernelGGL((rowcol_kernel<3, MODE>), grid, dim3(256), 0, s, a, f, xf, bias, rs, rpn, out, pcol, rows, C, rpb); break;
+    case 4: hipLaunchKernelGGL((rowcol_kernel<4, MODE>), grid, dim3(256), 0, s, a, f, xf, bias, rs, rpn, out, pcol, rows, C, rpb); break;
+    default: return -2;
+  }
+  return BE_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+extern "C" {
+
+// dh: bf16 [rows, C] gradient of the LN output; x: bf16 LN input; stats: (mean, rstd) per row; w: LN
+// weight.  dx (fp32, optional) / dxb (bf16, optional) = LN'(dh) + s1[row/rpn]*r1 + s2[row/rpn]*r2
+// (r*, s* optional; s null = 1).  pdw / pdb / pcol: optional [ceil(rows/rpb), C] partials of
+// sum(dh*xhat), sum(dh), sum(dx).
+int be_ln_bwd(const void* dh, const void* x, const float* stats, const float* w, const float* r1, const float* s1,
+              const float* r2, const float* s2, int rpn, float* dx, void* dxb, float* pdw, float* pdb, float* pcol,
+              long long rows, int C, int rpb, hipStream_t s) {
+  if (C % 8 != 0 || C > 64 * 8 * MAXV || rpb <= 0) return -1;
+  const int nv = (C / 8 + 63) / 64;
+  const dim3 grid((unsigned)((rows + rpb - 1) / rpb));
+  if (rpn <= 0) rpn = 1;
+#define LNB(NV)                                                                                                   \
+  case NV:                                                                                                        \
+    hipLaunchKernelGGL(ln_bwd_kernel<NV>, grid, dim3(256), 0, s, (const bf16_t*)dh, (const bf16_t*)x, stats, w, r1, \
+                       s1, r2, s2, rpn, dx, (bf16_t*)dxb, pdw, pdb, pcol, rows, C, rpb);                            \
+    break;
+  switch (nv) {
+    LNB(1) LNB(2) LNB(3) LNB(4)
+    default: return -1;
+  }
+#undef LNB
+  return BE_CHECK_LAUNCH();
+}
+
+// g = gelu(f + bias) (exact erf GELU), bf16 [rows, C].
+int be_gelu_fwd(const void* f, const float* bias, void* g, long long rows, int C, int rpb, hipStream_t s) {
+  return launch_rowcol<0>(nullptr, (const bf16_t*)f, nullptr, bias, nullptr, 1, (bf16_t*)g, nullptr, rows, C, rpb, s);
+}
+
+// df = dg * gelu'(f + bias) (bf16) + column partials of df [ceil(rows/rpb), C].
+int be_gelu_bwd(const void* dg, const void* f, const float* bias, void* df, float* pcol, long long rows, int C, int rpb,
+                hipStream_t s) {
+  return launch_rowcol<1>((const bf16_t*)dg, (const bf16_t*)f, nullptr, bias, nullptr, 1, (bf16_t*)df, pcol, rows, C,
+                          rpb, s);
+}
+
+// y = rs[row/rpn] * x (fp32 -> bf16; rs null = 1) + column partials of y.
+int be_scale_cast(const float* x, const float* rs, int rpn, void* y, float* pcol, long long rows, int C, int rpb,
+                  hipStream_t s) {
+  return launch_rowcol<2>(nullptr, nullptr, x, nullptr, rs, rpn, (bf16_t*)y, pcol, rows, C, rpb, s);
+}
+
+}  // extern "C"
