@@ -28,6 +28,13 @@ def _rpb(rows: int, target_blocks: int = 512) -> int:
     return max(4, -(-rows // target_blocks))
 
 
+def _colsum(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Column sums of [rows, C] (fp32), written into ``out`` when given (no extra copy)."""
+    if out is None:
+        return p.sum(0, dtype=torch.float32)
+    return torch.sum(p, 0, dtype=torch.float32, out=out.view(-1))
+
+
 def _rowscale(rs: torch.Tensor | None, rows: int, rpn: int):
     if rs is None:
         return None
@@ -75,9 +82,11 @@ def ln_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor | 
 def ln_bwd(dh: torch.Tensor, x: torch.Tensor, stats: torch.Tensor, w: torch.Tensor,
            r1: torch.Tensor | None = None, s1: torch.Tensor | None = None, r2: torch.Tensor | None = None,
            s2: torch.Tensor | None = None, rpn: int = 1, want_dx: bool = True, want_dxb: bool = False,
-           want_col: bool = False):
+           want_col: bool = False, out_dw: torch.Tensor | None = None, out_db: torch.Tensor | None = None,
+           out_col: torch.Tensor | None = None):
     """LayerNorm backward.  Returns (dx fp32 | None, dx bf16 | None, dw, db, colsum(dx) | None) with
-    dx = LN'(dh) + s1[b] r1 + s2[b] r2."""
+    dx = LN'(dh) + s1[b] r1 + s2[b] r2.  ``out_*``: write the reduced sums straight into these (e.g.
+    the parameters' views of the flat gradient buffer)."""
     C = x.shape[-1]
     rows = x.numel() // C
     if x.is_cuda:
@@ -94,7 +103,7 @@ def ln_bwd(dh: torch.Tensor, x: torch.Tensor, stats: torch.Tensor, w: torch.Tens
                      _native.ptr(w.float().contiguous()), _native.ptr(f(r1)), _native.ptr(f(s1)), _native.ptr(f(r2)),
                      _native.ptr(f(s2)), int(rpn), _native.ptr(dx), _native.ptr(dxb), _native.ptr(pdw),
                      _native.ptr(pdb), _native.ptr(pcol), rows, C, rpb, _native.stream(dev))
-        return dx, dxb, pdw.sum(0), pdb.sum(0), (pcol.sum(0) if pcol is not None else None)
+        return dx, dxb, _colsum(pdw, out_dw), _colsum(pdb, out_db), (_colsum(pcol, out_col) if want_col else None)
     xf = x.float().reshape(rows, C)
     d = dh.float().reshape(rows, C)
     mean, rstd = stats[:, 0:1], stats[:, 1:2]
@@ -106,9 +115,9 @@ def ln_bwd(dh: torch.Tensor, x: torch.Tensor, stats: torch.Tensor, w: torch.Tens
             sc = _rowscale(s, rows, rpn)
             rf = r.float().reshape(rows, C)
             o = o + (rf * sc if sc is not None else rf)
-    dw, db = (d * xh).sum(0), d.sum(0)
+    dw, db = _colsum(d * xh, out_dw), _colsum(d, out_db)
     return (o if want_dx else None, o.to(dh.dtype) if want_dxb else None, dw, db,
-            o.sum(0) if want_col else None)
+            _colsum(o, out_col) if want_col else None)
 
 
 # ------------------------------------------------------------------ GELU / casts
@@ -123,7 +132,7 @@ def gelu_fwd(f: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     return F.gelu(f.float() + bias.float()).to(f.dtype)
 
 
-def gelu_bwd(dg: torch.Tensor, f: torch.Tensor, bias: torch.Tensor):
+def gelu_bwd(dg: torch.Tensor, f: torch.Tensor, bias: torch.Tensor, out_db: torch.Tensor | None = None):
     """(df, dbias) for g = gelu(f + bias)."""
     C = f.shape[-1]
     rows = f.numel() // C
@@ -133,14 +142,15 @@ def gelu_bwd(dg: torch.Tensor, f: torch.Tensor, bias: torch.Tensor):
         pcol = torch.empty(-(-rows // rpb), C, device=f.device, dtype=torch.float32)
         _native.call("be_gelu_bwd", _native.ptr(dg.contiguous()), _native.ptr(f), _native.ptr(bias.float().contiguous()),
                      _native.ptr(df), _native.ptr(pcol), rows, C, rpb, _native.stream(f.device))
-        return df, pcol.sum(0)
+        return df, _colsum(pcol, out_db)
     t = f.float() + bias.float()
     d = 0.5 * (1 + torch.erf(t / math.sqrt(2))) + t * torch.exp(-0.5 * t * t) / math.sqrt(2 * math.pi)
     df = dg.float() * d
-    return df.to(f.dtype), df.reshape(rows, C).sum(0)
+    return df.to(f.dtype), _colsum(df.reshape(rows, C), out_db)
 
 
-def scale_cast(x: torch.Tensor, rs: torch.Tensor | None = None, rpn: int = 1, dtype=torch.bfloat16):
+def scale_cast(x: torch.Tensor, rs: torch.Tensor | None = None, rpn: int = 1, dtype=torch.bfloat16,
+               out_col: torch.Tensor | None = None):
     """(rs[row // rpn] * x in ``dtype``, column sums of it in fp32)."""
     C = x.shape[-1]
     rows = x.numel() // C
@@ -151,12 +161,12 @@ def scale_cast(x: torch.Tensor, rs: torch.Tensor | None = None, rpn: int = 1, dt
         _native.call("be_scale_cast", _native.ptr(x.float().contiguous()),
                      _native.ptr(rs.float().contiguous() if rs is not None else None), int(rpn), _native.ptr(y),
                      _native.ptr(pcol), rows, C, rpb, _native.stream(x.device))
-        return y, pcol.sum(0)
+        return y, _colsum(pcol, out_col)
     sc = _rowscale(rs, rows, rpn)
     yf = x.float().reshape(rows, C)
     if sc is not None:
         yf = yf * sc
-    return yf.to(dtype).reshape(x.shape), yf.sum(0)
+    return yf.to(dtype).reshape(x.shape), _colsum(yf, out_col)
 
 
 # ------------------------------------------------------------------ attention

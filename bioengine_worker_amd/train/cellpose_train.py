@@ -104,6 +104,8 @@ class CellposeTrainer:
         self.engine_kind = eng
         self._eng = None
         self._cpsam_engs: dict = {}
+        self._cpsam_graph = None
+        self._cpsam_graph_failed = False
         self._graph = None
         self._graph_io = None
 
@@ -196,7 +198,11 @@ class CellposeTrainer:
         if self.net.rdrop > 0:
             keep = stochastic_depth_keep(x.shape[0], len(eng.blocks), self.net.rdrop, self.device, self.gen)
         with trace.span("train.fwd_bwd_cpsam", cuda=True):
-            loss = eng.loss_and_backward(x, lbl, keep, on_params_ready=self.ar.mark_ready if self.world > 1 else None)
+            if self.cfg.graph and self.device.type == "cuda" and self.world == 1 and not self._cpsam_graph_failed:
+                loss = self._cpsam_graph_step(eng, x, lbl, keep)
+            else:
+                loss = eng.loss_and_backward(x, lbl, keep,
+                                             on_params_ready=self.ar.mark_ready if self.world > 1 else None)
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
@@ -205,6 +211,42 @@ class CellposeTrainer:
             train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
                                   weight_decay=self.cfg.weight_decay, grad_scale=gscale, p_bf16=mirror)
         return loss
+
+    def _cpsam_graph_step(self, eng, x, lbl, keep):
+        """Replay the captured CPSAM fwd+bwd (~1.3k launches at ViT-L) on static buffers; the
+        stochastic-depth mask is drawn on the host and copied in, AdamW runs outside the graph."""
+        key = (tuple(x.shape), tuple(lbl.shape))
+        if self._cpsam_graph is None or self._cpsam_graph[0] != key:
+            xs, ls = x.clone(), lbl.clone()
+            ks = (keep.clone() if keep is not None else
+                  torch.ones(x.shape[0], len(eng.blocks), device=self.device))
+            try:
+                side = torch.cuda.Stream(self.device)
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
+                    for _ in range(2):
+                        eng.loss_and_backward(xs, ls, ks)
+                torch.cuda.current_stream(self.device).wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    out = eng.loss_and_backward(xs, ls, ks)
+            except Exception as e:  # noqa: BLE001  (e.g. a library call that cannot be captured)
+                import logging
+
+                logging.getLogger("bioengine.train").warning("CPSAM graph capture failed (%s); running eagerly", e)
+                self._cpsam_graph_failed = True
+                torch.cuda.synchronize(self.device)
+                return eng.loss_and_backward(x, lbl, keep)
+            self._cpsam_graph = (key, g, xs, ls, ks, out)
+        _, g, xs, ls, ks, out = self._cpsam_graph
+        xs.copy_(x)
+        ls.copy_(lbl)
+        if keep is not None:
+            ks.copy_(keep)
+        else:
+            ks.fill_(1.0)
+        g.replay()
+        return out.clone()
 
     def _refresh_mirrors(self) -> None:
         for eng in self._cpsam_engs.values():
@@ -266,6 +308,7 @@ class CellposeTrainer:
         self.ar = BucketedAllReduce(self.fp, group=group, bucket_mb=self.cfg.bucket_mb,
                                     comm_dtype=torch.bfloat16 if self.cfg.comm_bf16 else None)
         self._graph = self._graph_io = None
+        self._cpsam_graph = None
         if self.world > 1:
             broadcast_params(self.fp, 0, group)
             for t in [self.m, self.v] + [b for b in self.net.buffers() if b.is_floating_point()]:

@@ -40,25 +40,36 @@ from ..models.cpsam import CPSAM, get_rel_pos
 from ..ops import vit_train as vt
 from ..parallel.ddp import FlatParams
 
-_MM_OUT_DTYPE: bool | None = None
+_MM_MODE: int | None = None  # 2: mm(out_dtype=fp32, out=grad view), 1: mm(out_dtype=fp32) + copy, 0: bf16 mm + copy
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> None:
-    """out (fp32 [n, k]) = dy^T x with dy [m, n], x [m, k] (bf16 on GPU; fp32 output straight from
-    hipBLASLt when this torch supports ``out_dtype``)."""
-    global _MM_OUT_DTYPE
+    """out (fp32 [n, k]) = dy^T x with dy [m, n], x [m, k].  On GPU the bf16 GEMM writes fp32 straight
+    into the parameter's view of the flat gradient buffer when this torch supports it."""
+    global _MM_MODE
     out2 = out.view(out.shape[0], -1)
-    if dy.dtype == torch.bfloat16:
-        if _MM_OUT_DTYPE is None:
+    if dy.dtype != torch.bfloat16:
+        torch.mm(dy.t(), x, out=out2)
+        return
+    if _MM_MODE is None:
+        _MM_MODE = 0
+        for mode in (2, 1):
             try:
-                torch.mm(dy[:1].t(), x[:1], out_dtype=torch.float32)
-                _MM_OUT_DTYPE = True
+                probe = torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=torch.float32)
+                if mode == 2:
+                    torch.mm(dy.t(), x, out_dtype=torch.float32, out=probe)
+                else:
+                    torch.mm(dy.t(), x, out_dtype=torch.float32)
+                _MM_MODE = mode
+                break
             except Exception:  # noqa: BLE001
-                _MM_OUT_DTYPE = False
-        if _MM_OUT_DTYPE:
-            out2.copy_(torch.mm(dy.t(), x, out_dtype=torch.float32))
-            return
-    out2.copy_(torch.mm(dy.t(), x))
+                continue
+    if _MM_MODE == 2:
+        torch.mm(dy.t(), x, out_dtype=torch.float32, out=out2)
+    elif _MM_MODE == 1:
+        out2.copy_(torch.mm(dy.t(), x, out_dtype=torch.float32))
+    else:
+        out2.copy_(torch.mm(dy.t(), x))
 
 
 class _Blk:
@@ -221,21 +232,19 @@ class CPSAMTrainEngine:
         # pixel unshuffle of the output gradient -> [B*N, nout*ps*ps]
         do = dyout.to(cd).reshape(B, self.nout, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B * N, -1).contiguous()
         outw = W(self.outc.weight).reshape(self.outc.weight.shape[0], 256)
-        self.outc.bias.grad.copy_(do.float().sum(0))
+        torch.sum(do, 0, dtype=torch.float32, out=self.outc.bias.grad)
         _wgrad(do, s["n3"], self.outc.weight.grad)
         dn3 = torch.mm(do, outw)
-        _, dn2, dw3, db3, _ = vt.ln_bwd(dn3, s["n2r"], s["sn3"], self.neck[3].weight, want_dx=False, want_dxb=True)
-        self.neck[3].weight.grad.copy_(dw3)
-        self.neck[3].bias.grad.copy_(db3)
+        _, dn2, _, _, _ = vt.ln_bwd(dn3, s["n2r"], s["sn3"], self.neck[3].weight, want_dx=False, want_dxb=True,
+                                    out_dw=self.neck[3].weight.grad, out_db=self.neck[3].bias.grad)
         dn2i = dn2.view(B, g, g, 256).permute(0, 3, 1, 2)
         cw = W(self.neck[2].weight)
         dn1i, dcw, _ = torch.ops.aten.convolution_backward(dn2i, s["n1i"], cw, None, [1, 1], [1, 1], [1, 1], False,
                                                            [0, 0], 1, [True, True, False])
         self.neck[2].weight.grad.copy_(dcw)
         dn1 = dn1i.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
-        _, dn0, dw1, db1, _ = vt.ln_bwd(dn1, s["n0"], s["sn1"], self.neck[1].weight, want_dx=False, want_dxb=True)
-        self.neck[1].weight.grad.copy_(dw1)
-        self.neck[1].bias.grad.copy_(db1)
+        _, dn0, _, _, _ = vt.ln_bwd(dn1, s["n0"], s["sn1"], self.neck[1].weight, want_dx=False, want_dxb=True,
+                                    out_dw=self.neck[1].weight.grad, out_db=self.neck[1].bias.grad)
         n0w = W(self.neck[0].weight).reshape(256, D)
         _wgrad(dn0, s["t_last"], self.neck[0].weight.grad)
         G = torch.mm(dn0, n0w).float()  # d t_out of the last block (fp32 residual-stream gradient)
@@ -245,9 +254,8 @@ class CPSAMTrainEngine:
             G = self._block_bwd(self.blocks[i], s["blocks"][i], G)
             ready(list(self.blocks[i].p.values()))
         # patch embedding + position embedding
-        self.pos.grad.copy_(G.view(B, N, D).sum(0).view_as(self.pos))
-        Gb, colG = vt.scale_cast(G, dtype=cd)
-        self.pe[1].grad.copy_(colG)
+        torch.sum(G.view(B, N * D), 0, out=self.pos.grad.view(-1))
+        Gb, _ = vt.scale_cast(G, dtype=cd, out_col=self.pe[1].grad)
         _wgrad(Gb, s["patches"], self.pe[0].grad)
         ready([self.pos, self.pe[0], self.pe[1]])
         self._saved = None
@@ -257,20 +265,16 @@ class CPSAMTrainEngine:
         w, p = b.w, b.p
         kb = s["keep"]
         # MLP: t_out = t_mid + k m
-        dm, db2 = vt.scale_cast(G, kb, N, dtype=self.cdt)
-        p["l2_b"].grad.copy_(db2)
+        dm, _ = vt.scale_cast(G, kb, N, dtype=self.cdt, out_col=p["l2_b"].grad)
         _wgrad(dm, s["g"], p["l2_w"].grad)
         dg = torch.mm(dm, w["l2_w"])
-        df, db1 = vt.gelu_bwd(dg, s["f"], p["l1_b"])
-        p["l1_b"].grad.copy_(db1)
+        df, _ = vt.gelu_bwd(dg, s["f"], p["l1_b"], out_db=p["l1_b"].grad)
         _wgrad(df, s["h2"], p["l1_w"].grad)
         dh2 = torch.mm(df, w["l1_w"])
-        dt_mid, _, dn2w, dn2b, _ = vt.ln_bwd(dh2, s["t_mid"], s["st2"], p["n2w"], r1=G)
-        p["n2w"].grad.copy_(dn2w)
-        p["n2b"].grad.copy_(dn2b)
+        dt_mid, _, _, _, _ = vt.ln_bwd(dh2, s["t_mid"], s["st2"], p["n2w"], r1=G, out_dw=p["n2w"].grad,
+                                       out_db=p["n2b"].grad)
         # attention: t_mid = t_in + k y
-        dy, dbp = vt.scale_cast(dt_mid, kb, N, dtype=self.cdt)
-        p["proj_b"].grad.copy_(dbp)
+        dy, _ = vt.scale_cast(dt_mid, kb, N, dtype=self.cdt, out_col=p["proj_b"].grad)
         _wgrad(dy, s["a"].reshape(B * N, D), p["proj_w"].grad)
         da = torch.mm(dy, w["proj_w"]).view(B, N, H, hd)
         qkv = s["qkv"]
@@ -282,12 +286,11 @@ class CPSAMTrainEngine:
         self._table_grad(dRh, p["rph"].grad)
         self._table_grad(dRw, p["rpw"].grad)
         dqkv2 = dqkv.view(B * N, 3 * D)
-        p["qkv_b"].grad.copy_(dqkv2.sum(0, dtype=torch.float32))
+        torch.sum(dqkv2, 0, dtype=torch.float32, out=p["qkv_b"].grad)
         _wgrad(dqkv2, s["h1"], p["qkv_w"].grad)
         dh1 = torch.mm(dqkv2, w["qkv_w"])
-        dt_in, _, dn1w, dn1b, _ = vt.ln_bwd(dh1, s["t_in"], s["st1"], p["n1w"], r1=dt_mid)
-        p["n1w"].grad.copy_(dn1w)
-        p["n1b"].grad.copy_(dn1b)
+        dt_in, _, _, _, _ = vt.ln_bwd(dh1, s["t_in"], s["st1"], p["n1w"], r1=dt_mid, out_dw=p["n1w"].grad,
+                                      out_db=p["n1b"].grad)
         return dt_in
 
     # ------------------------------------------------------------------ step
