@@ -158,8 +158,10 @@ class AppBuilder:
         rt = dict(opts.get("runtime_env") or {})
         workdir = self.apps_workdir / application_id
         envv = dict(rt.get("env_vars") or {})
-        server_url = getattr(getattr(self.server, "config", None), "public_base_url", None) or \
-            getattr(self.server, "server_url", None) or ""
+        # the URL the worker itself connected with (a local:// hub has no WebSocket endpoint behind
+        # its public HTTP base); for a real Hypha server both are the same
+        server_url = getattr(self.server, "server_url", None) or \
+            getattr(getattr(self.server, "config", None), "public_base_url", None) or ""
         workspace = getattr(getattr(self.server, "config", None), "workspace", None) or ""
         envv.update({
             "HOME": str(workdir), "TMPDIR": str(workdir / "tmp"), "TEMP": str(workdir / "tmp"), "TMP": str(workdir / "tmp"),

@@ -33,7 +33,7 @@ class EvalParams:
     max_size_fraction: float = 0.4
     normalize: bool = True
     tile: bool = True
-    bsize: int = 224
+    bsize: int | None = None  # None: the network's native tile (224 CPnet, 256 Cellpose-SAM)
     tile_overlap: float = 0.1
     compute_masks: bool = True
     #: GPU: split a batch into this many micro-batches and run mask recovery of micro-batch i on a
@@ -66,15 +66,25 @@ def as_batch(images, nchan: int, device=None) -> torch.Tensor:
 
 
 class CellposeRunner:
-    """Batched Cellpose (cyto3-style CPnet) inference on one device."""
+    """Batched Cellpose inference on one device: cyto3-style CPnet (224 tiles, fused MFMA conv engine)
+    or Cellpose-SAM (cellpose 4 ``cpsam``: 256 tiles, 3 channels, ViT-L/8 HIP engine)."""
 
-    def __init__(self, net: CPnet | None = None, device: str | torch.device = "cuda", seed: int = 0):
+    def __init__(self, net=None, device: str | torch.device = "cuda", seed: int = 0):
+        from ..models.cpsam import CPSAM, CPSAMEngine
+
         self.device = torch.device(device)
-        self.net = (net or CPnet().randomize_(seed)).eval()
-        self.nchan = self.net.nchan
+        self.net = (net if net is not None else CPnet().randomize_(seed)).eval()
+        self.is_sam = isinstance(self.net, CPSAM)
+        if self.is_sam:
+            self.nchan = 3
+            self.bsize = int(self.net.bsize)
+            self.engine = CPSAMEngine(self.net, self.device) if self.device.type == "cuda" else None
+        else:
+            self.nchan = self.net.nchan
+            self.bsize = 224
+            self.engine = CPnetEngine(self.net, self.device)
         self.diam_mean = float(self.net.diam_mean.item())
         self.cin_pad = (self.nchan + 7) // 8 * 8
-        self.engine = CPnetEngine(self.net, self.device)
         self._pinned: torch.Tensor | None = None  # host staging for numpy batches (pinned -> async DMA)
         self._plans: dict = {}
 
@@ -82,10 +92,24 @@ class CellposeRunner:
     def _plan(self, H, W, p: EvalParams):
         from .gpu import TilePlan
 
-        key = (H, W, p.bsize, p.tile_overlap)
+        bs = p.bsize or self.bsize
+        key = (H, W, bs, p.tile_overlap)
         if key not in self._plans:
-            self._plans[key] = TilePlan(H, W, p.bsize, p.tile_overlap, device=self.device)
+            self._plans[key] = TilePlan(H, W, bs, p.tile_overlap, device=self.device)
         return self._plans[key]
+
+    def _sam_tiles(self, tiles: torch.Tensor) -> torch.Tensor:
+        """NHWC bf16 tiles [T, by, bx, cpad] -> CPSAM flows [T, 3, by, bx] fp32 (tiles smaller than
+        the network's fixed 256 grid are zero-padded, as cellpose 4 pads small images)."""
+        T, by, bx, _ = tiles.shape
+        bs = self.bsize
+        x = torch.zeros(T, 3, bs, bs, dtype=torch.bfloat16, device=tiles.device)
+        x[:, :, :by, :bx] = tiles[..., :3].permute(0, 3, 1, 2)
+        out = []
+        for i in range(0, T, 64):  # bounded activation memory for very large batches
+            out.append(self.engine(x[i: i + 64]))
+        y = torch.cat(out) if len(out) > 1 else out[0]
+        return y[:, :, :by, :bx].contiguous()
 
     @torch.no_grad()
     def run_net(self, x: torch.Tensor, p: EvalParams) -> tuple[torch.Tensor, torch.Tensor]:
@@ -96,30 +120,44 @@ class CellposeRunner:
                 plan = self._plan(H, W, p)
                 with trace.span("cellpose.tiles_gather", cuda=True, tiles=B * plan.nt):
                     tiles = plan.gather(x, self.cin_pad)
-                with trace.span("cellpose.cpnet", cuda=True, tiles=B * plan.nt):
-                    yt, st = self.engine(tiles)
+                with trace.span("cellpose.net", cuda=True, tiles=B * plan.nt):
+                    if self.is_sam:
+                        yt = self._sam_tiles(tiles)
+                        st = torch.zeros(B * plan.nt, 256, device=x.device)
+                    else:
+                        yt, st = self.engine(tiles)
                 with trace.span("cellpose.blend", cuda=True):
                     y = plan.blend(yt, B)
                 style = st.view(B, plan.nt, -1).sum(1)
+            elif self.is_sam:
+                raise ValueError("Cellpose-SAM inference needs tile=True (fixed 256x256 network grid)")
             else:
                 Hp, Wp = math.ceil(H / 8) * 8, math.ceil(W / 8) * 8
                 xin = torch.zeros(B, Hp, Wp, self.cin_pad, dtype=torch.bfloat16, device=x.device)
                 xin[:, :H, :W, :C] = x.permute(0, 2, 3, 1)
                 y, style = self.engine(xin)
                 y = y[:, :, :H, :W].contiguous()
-            style = style / torch.sqrt((style * style).sum(1, keepdim=True))
+            style = style / torch.sqrt((style * style).sum(1, keepdim=True)).clamp_min(1e-12)
             return y, style
         # CPU oracle path
         ys, styles = [], []
+        bs = p.bsize or self.bsize
         for b in range(B):
             img = x[b].numpy()
             if p.tile:
                 ya, yb = ref.pad_amounts(H)
                 xa, xb = ref.pad_amounts(W)
                 imgp = np.pad(img, ((0, 0), (ya, yb), (xa, xb)))
-                tiles, tys, txs = ref.make_tiles(imgp, p.bsize, p.tile_overlap)
+                tiles, tys, txs = ref.make_tiles(imgp, bs, p.tile_overlap)
                 tt = torch.from_numpy(tiles).float()
-                yt, st, _ = self.net(tt)
+                if self.is_sam:
+                    T, _, by, bx = tt.shape
+                    tp = torch.zeros(T, 3, self.bsize, self.bsize)
+                    tp[:, :, :by, :bx] = tt[:, :3]
+                    yt = self.net(tp)[0][:, :, :by, :bx].detach()
+                    st = torch.zeros(T, 256)
+                else:
+                    yt, st, _ = self.net(tt)
                 yf = ref.average_tiles(yt.numpy(), tys, txs, imgp.shape[1], imgp.shape[2])
                 ys.append(torch.from_numpy(yf[:, ya: ya + H, xa: xa + W].copy()))
                 styles.append(st.sum(0))
@@ -128,7 +166,7 @@ class CellposeRunner:
                 ys.append(yt[0])
                 styles.append(st[0])
         style = torch.stack(styles)
-        return torch.stack(ys), style / torch.sqrt((style * style).sum(1, keepdim=True))
+        return torch.stack(ys), style / torch.sqrt((style * style).sum(1, keepdim=True)).clamp_min(1e-12)
 
     # ---------------------------------------------------------------- full eval
     @torch.no_grad()

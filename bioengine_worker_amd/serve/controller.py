@@ -435,6 +435,9 @@ class ServeController:
         self._task = None
         self._health_last: dict = {}
         self.replica_class_wrappers = []  # callables (DeploymentState, cls) -> cls
+        from .gang import GangManager
+
+        self.gangs = GangManager(self.resources, log_dir)  # multi-rank jobs (serve/gang.py)
 
     def can_place(self, cpus: float, gpus: float, mem: float) -> bool:
         return self.resources.can_fit(cpus, gpus, mem) or any(n.pool.can_fit(cpus, gpus, mem)
@@ -566,6 +569,12 @@ class ServeController:
         return DeploymentHandle(name, app.ingress)
 
     async def call(self, app: str, dep: str, method: str, args, kwargs, model_id: str = ""):
+        if app == "__bioengine__":  # runtime services reachable from replicas over the handle channel
+            if dep == "gang" and method == "run":
+                return await self.gangs.run(*args, **kwargs)
+            if dep == "gang" and method == "status":
+                return self.gangs.status()
+            raise DeploymentUnavailableError(f"unknown runtime service {dep}.{method}")
         a = self.apps.get(app)
         if a is None:
             raise DeploymentUnavailableError(f"application '{app}' is not running")

@@ -113,7 +113,14 @@ class CellposeTrainer:
     def set_lr(self, lr: float):
         self.lr = float(lr)
 
-    def augment(self, imgs: torch.Tensor, lbls: torch.Tensor, rescale=None):
+    def augment(self, imgs, lbls, rescale=None):
+        """Random rotate / flip / resize to ``bsize`` crops (cellpose ``random_rotate_and_resize``).
+        ``imgs`` / ``lbls`` may be lists of differently sized images: each is warped on its own
+        (no cropping to a common size) and the crops are batched."""
+        if isinstance(imgs, (list, tuple)):
+            outs = [self.augment(i[None], l[None], None if rescale is None else [rescale[k]])
+                    for k, (i, l) in enumerate(zip(imgs, lbls))]
+            return torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs])
         B, C, H, W = imgs.shape
         aff, flip, _ = train_ops.random_affine_params(B, H, W, xy=(self.cfg.bsize, self.cfg.bsize),
                                                       scale_range=self.cfg.scale_range, rescale=rescale,
@@ -395,16 +402,26 @@ def synthetic_train_batch(B: int, bsize: int = 256, device="cuda", seed: int = 0
     return imgs_t, lbl
 
 
-def run_training(trainer: CellposeTrainer, train_imgs: torch.Tensor, train_lbls: torch.Tensor, n_epochs: int,
-                 test_imgs: torch.Tensor | None = None, test_lbls: torch.Tensor | None = None,
-                 batch_callback=None, epoch_callback=None, stop_check=None, start_epoch: int = 0) -> dict:
+def _take(x, idx):
+    if torch.is_tensor(x):
+        return x[torch.as_tensor(idx, device=x.device)]
+    return [x[int(i)] for i in idx]
+
+
+def run_training(trainer: CellposeTrainer, train_imgs, train_lbls, n_epochs: int, test_imgs=None, test_lbls=None,
+                 batch_callback=None, epoch_callback=None, stop_check=None, start_epoch: int = 0,
+                 diams=None, rescale: bool = False) -> dict:
     """Epoch loop with the reference's schedule, callbacks and validation cadence.
 
+    ``train_imgs`` / ``train_lbls``: stacked tensors or lists of per-image tensors (any sizes).
+    ``rescale``: scale each crop by its image's cell diameter / the net's ``diam_mean`` (``diams``
+    per image; reference ``rsc = diams / net.diam_mean`` at main.py:1494-1499).
     In DP mode each rank takes a disjoint shard of every epoch's permutation (global batch =
     batch_size * world)."""
     cfg = trainer.cfg
     sched = lr_schedule(cfg.lr, n_epochs)
-    nimg = train_imgs.shape[0]
+    nimg = len(train_imgs)
+    dmean = float(trainer.net.diam_mean.item()) if hasattr(trainer.net, "diam_mean") else 30.0
     losses = np.zeros(n_epochs)
     test_losses: list = [None] * n_epochs
     t0 = time.time()
@@ -419,8 +436,10 @@ def run_training(trainer: CellposeTrainer, train_imgs: torch.Tensor, train_lbls:
             mine = sl[trainer.rank::trainer.world] if trainer.world > 1 else sl
             if len(mine) == 0:
                 mine = sl[:1]
-            idx = torch.as_tensor(mine, device=train_imgs.device)
-            loss = trainer.step(train_imgs[idx], train_lbls[idx])
+            rsc = None
+            if rescale and diams is not None:
+                rsc = [max(float(diams[int(i)]), 1e-3) / dmean for i in mine]
+            loss = trainer.step(_take(train_imgs, mine), _take(train_lbls, mine), rsc)
             lv = float(loss)
             losses[ep] += lv * len(sl)
             if batch_callback is not None:

@@ -49,14 +49,15 @@ async def main_async(a) -> list[dict]:
     # deploy_app's max_ongoing_requests (the app proxy's cap, default 10 as in the reference) bounds
     # how many requests can reach the replica's batcher at once
     aid = await svc.deploy_app(artifact_id="cellpose-finetuning", application_id="cpbench", disable_gpu=a.gpus == 0,
-                               max_ongoing_requests=a.max_ongoing)
+                               max_ongoing_requests=a.max_ongoing, hypha_token=tok,
+                               application_kwargs={"CellposeFinetune": {"default_model": a.model}})
     st = await w.apps_manager.wait_for(aid, timeout=600)
     assert st == "RUNNING", (await svc.get_app_status(application_ids=[aid]))["message"]
     s = await svc.get_app_status(application_ids=[aid])
     app = await admin.get_service(s["service_ids"][0]["websocket_service_id"])
     imgs = [synthetic_cells(1, a.size, a.size, ncells=60, seed=i)[0] for i in range(16)]
     for i in range(3):  # warm-up: model build, kernels, graph pass, batch shapes
-        await asyncio.gather(*[app.infer(input_arrays=[imgs[j % 16]]) for j in range(8)])
+        await asyncio.gather(*[app.infer(input_arrays=[imgs[j % 16]], model=a.model) for j in range(8)])
     results = []
     for conc in a.concurrency:
         lat: list[float] = []
@@ -66,7 +67,7 @@ async def main_async(a) -> list[dict]:
             k = cid
             while time.perf_counter() < stop:
                 t = time.perf_counter()
-                out = await app.infer(input_arrays=[imgs[k % 16]])
+                out = await app.infer(input_arrays=[imgs[k % 16]], model=a.model)
                 lat.append(time.perf_counter() - t)
                 assert out[0]["output"].shape == (a.size, a.size)
                 k += conc
@@ -114,6 +115,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--replica-mode", default="process", choices=["process", "local"])
     ap.add_argument("--max-ongoing", type=int, default=64, help="deploy_app max_ongoing_requests")
+    ap.add_argument("--model", default="cyto3", help="built-in model served (headline: cyto3 CPnet)")
     ap.add_argument("--profile", default=None, metavar="PATH",
                     help="cProfile the worker-side event loop during the highest-concurrency phase")
     a = ap.parse_args()
