@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import base64
 import io
+import json
 import os
 import time
 from datetime import datetime
@@ -153,16 +154,62 @@ class MitoAnalysisDeployment:
     async def analyze_volume(self, volume_npy_b64: str = Field(..., description="3-D stack as base64 .npy bytes (Z,Y,X)."),
                              pixel_size_nm: float = Field(5.0, description="In-plane pixel size in nm."),
                              tile_size: int = Field(512, description="Tile edge length."),
-                             overlap: int = Field(64, description="Tile overlap.")) -> dict:
-        """Slice-wise inference + 3-D connected instances (6-connectivity) with per-instance volume."""
+                             overlap: int = Field(64, description="Tile overlap."),
+                             n_gpus: int = Field(1, description="Shard z-slabs over this many GPUs (gang job, RCCL)."),
+                             gather: str = Field("rank0", description="n_gpus > 1: 'rank0' stitches the label volume on "
+                                                                      "one GPU, 'sharded' keeps per-slab files, "
+                                                                      "'none' returns statistics only."),
+                             return_labels: bool = Field(False, description="Include the label volume (base64 .npy)."),
+                             threshold: float = Field(0.5, description="Foreground probability threshold."),
+                             input_is_probability: bool = Field(False, description="The volume already is a foreground "
+                                                                                   "probability map (skip the model)."),
+                             ) -> dict:
+        """Slice-wise inference + 3-D connected instances (6-connectivity) with per-instance volume;
+        with ``n_gpus > 1`` the z-slabs run as one rank per GPU with globally consistent labels."""
+        import tempfile
+
         import torch
 
         from bioengine_worker_amd.em import volume as vol
 
-        vol_np = np.load(io.BytesIO(base64.b64decode(volume_npy_b64)))
-        dev = self._pipe.device if self._pipe is not None else torch.device("cpu")
-        res = vol.analyze_volume(torch.from_numpy(vol_np.astype(np.float32)).to(dev), self._predict_local, tile_size,
-                                 overlap, self.tile_batch)
-        res["pixel_size_nm"] = pixel_size_nm
-        res["model"] = self.model_id
-        return res
+        raw = base64.b64decode(volume_npy_b64)
+        if int(n_gpus or 1) > 1:
+            from bioengine_worker_amd.serve.gang import run_gang
+
+            if self._pipe is None and not input_is_probability:
+                raise RuntimeError("multi-GPU volumes need the in-process pipeline (no model_runner_service)")
+            work = Path(tempfile.mkdtemp(prefix="em-vol-", dir=os.environ.get("TMPDIR")))
+            vpath, opath = work / "volume.npy", work / "labels.npy"
+            vpath.write_bytes(raw)
+            t0 = time.time()
+            res = await run_gang("bioengine_worker_amd.em.volume:gang_analyze_volume",
+                                 {"volume_path": str(vpath), "out_path": str(opath),
+                                  "model_root": None if input_is_probability else str(self._pipe.root),
+                                  "tile": tile_size, "overlap": overlap, "batch": self.tile_batch, "gather": gather,
+                                  "threshold": float(threshold)},
+                                 world_size=int(n_gpus), gpus_per_rank=1, name=f"em-{work.name[-8:]}")
+            out = dict(res[0])
+            out.update(ranks=[{k: r[k] for k in ("rank", "z_range", "timings_s", "gather_s", "total_s")} for r in res],
+                       n_gpus=int(n_gpus), gather=gather, processing_time_s=round(time.time() - t0, 2))
+            if return_labels and gather == "rank0":
+                out["labels_npy_b64"] = base64.b64encode(opath.read_bytes()).decode()
+            elif gather == "sharded":
+                out["label_shards"] = json.loads(Path(f"{opath}.manifest.json").read_text())
+            if gather != "sharded":
+                import shutil
+
+                shutil.rmtree(work, ignore_errors=True)
+        else:
+            vol_np = np.load(io.BytesIO(raw), allow_pickle=False)
+            dev = self._pipe.device if self._pipe is not None else torch.device("cpu")
+            predict = vol.probability_identity if input_is_probability else self._predict_local
+            out = vol.analyze_volume(torch.from_numpy(vol_np.astype(np.float32)).to(dev), predict,
+                                     tile_size, overlap, self.tile_batch, threshold=float(threshold))
+            labels = out.pop("labels_slab_t")
+            if return_labels:
+                b = io.BytesIO()
+                np.save(b, labels.cpu().numpy())
+                out["labels_npy_b64"] = base64.b64encode(b.getvalue()).decode()
+        out["pixel_size_nm"] = pixel_size_nm
+        out["model"] = self.model_id
+        return out

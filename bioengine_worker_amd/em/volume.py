@@ -237,7 +237,8 @@ def instance_stats(labels: torch.Tensor, n: int, z_offset: int = 0, group=None) 
 
 def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 64, batch: int = 8,
                    threshold: float = 0.5, min_voxels: int = 300, group=None, gather_labels: bool = False,
-                   z_offset: int = 0, gather: str | None = None, timings: bool = False) -> dict:
+                   z_offset: int = 0, gather: str | None = None, timings: bool = False,
+                   norm_range: tuple[float, float] | None = None) -> dict:
     """Single-process (or per-rank) 3-D analysis.  With a process group, ``vol`` is this rank's
     z-slab and results are globally consistent.  ``gather="mask"`` / ``"labels"`` all-gathers the
     stitched foreground mask (uint8) / global instance labels of the whole volume onto every rank
@@ -256,9 +257,11 @@ def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 6
             marks.append((name, time.perf_counter()))
 
     v = vol.float()
-    sample = v.reshape(1, -1)[:, :: max(1, v.numel() // 4_000_000)]
-    p1, p99 = percentiles(sample, (1.0, 99.0))
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    if norm_range is not None:  # the whole volume's percentiles, computed by the caller
+        p1, p99 = (torch.tensor(float(x), device=v.device) for x in norm_range)
+    else:
+        p1, p99 = volume_percentiles(v)
+    if norm_range is None and dist.is_initialized() and dist.get_world_size(group) > 1:
         pr = torch.stack([p1, p99]).to(v.device)
         dist.all_reduce(pr, group=group)
         pr /= dist.get_world_size(group)
@@ -276,6 +279,7 @@ def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 6
     out = {"n_instances": int(keep.sum()), "n_components": n, "volume_shape": list(vol.shape),
            "instances": {k: vv[keep].tolist() for k, vv in stats.items()}}
     mark("stats")
+    out["labels_slab_t"] = labels  # this rank's globally consistent slab labels (device tensor)
     if gather_labels:
         out["labels"] = labels.cpu().numpy()
     if gather == "mask":
@@ -285,4 +289,97 @@ def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 6
     mark("gather")
     if timings:
         out["timings_s"] = {b[0]: round(b[1] - a[1], 4) for a, b in zip(marks, marks[1:])}
+    return out
+
+
+def volume_percentiles(v, device=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """p1 / p99 of a strided ~4 M-voxel sample of the volume (torch tensor or numpy / memmap; the
+    same sample whether the volume is whole or memory-mapped by every rank of a gang)."""
+    from ..search.preprocess import percentiles
+
+    n = int(np.prod(v.shape))
+    step = max(1, n // 4_000_000)
+    if torch.is_tensor(v):
+        sample = v.reshape(1, -1)[:, ::step].float()
+    else:
+        sample = torch.from_numpy(np.ascontiguousarray(np.asarray(v).reshape(-1)[::step]).astype(np.float32))[None]
+    if device is not None:
+        sample = sample.to(device)
+    return percentiles(sample, (1.0, 99.0))
+
+
+def gather_to_rank0(x: torch.Tensor, group=None) -> torch.Tensor | None:
+    """Stitched full volume on rank 0 only (``dist.gather`` of max-depth-padded slabs): every other
+    rank sends its slab once and keeps nothing -- the 2048^3 int32 label volume (34 GB) lands on one
+    GPU instead of on all eight.  Returns the volume on rank 0, None elsewhere."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return x
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    depth = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    depths = [torch.zeros_like(depth) for _ in range(world)]
+    dist.all_gather(depths, depth, group=group)
+    depths = [int(d) for d in depths]
+    zmax = max(depths)
+    buf = torch.zeros((zmax,) + tuple(x.shape[1:]), dtype=torch.uint8 if x.dtype == torch.bool else x.dtype,
+                      device=x.device)
+    buf[: x.shape[0]] = x
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0, group=group)
+    if rank != 0:
+        return None
+    out = torch.cat([parts[r][: depths[r]] for r in range(world)])
+    return out.bool() if x.dtype == torch.bool else out
+
+
+def probability_identity(tiles: torch.Tensor) -> torch.Tensor:
+    """``predict`` for inputs that are already foreground probabilities (normalised 0..1)."""
+    return tiles
+
+
+def gang_analyze_volume(rank: int, world: int, volume_path: str, out_path: str, model_root: str | None,
+                        tile: int = 512,
+                        overlap: int = 64, batch: int = 8, threshold: float = 0.5, min_voxels: int = 300,
+                        gather: str = "rank0") -> dict:
+    """Gang target (``serve/gang.py``): rank r memory-maps its z-slab of the ``.npy`` volume, runs
+    slice-wise tiled inference + 3-D labelling, and the ranks agree on global labels over the
+    process group (RCCL on the GPU node).  ``gather``: ``"rank0"`` stitches the label volume on
+    rank 0 and writes ``out_path`` (``.npy``); ``"sharded"`` leaves each slab where it was computed
+    and writes ``<out_path>.rank<r>.npy`` + the z offsets; ``"none"`` keeps only the statistics."""
+    import json
+    import time
+
+    from ..bioimageio.runner import PredictionPipeline
+
+    group = None
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t0 = time.perf_counter()
+    vol = np.load(volume_path, mmap_mode="r")
+    z0, z1 = slab_bounds(vol.shape[0], rank, world)
+    slab = torch.from_numpy(np.ascontiguousarray(vol[z0:z1])).to(dev)
+    if model_root:
+        pipe = PredictionPipeline(model_root, device=dev)
+        predict = lambda t: next(iter(pipe.predict_tensors(t).values()))
+    else:  # the volume already is a probability map (e.g. from an earlier pass): identity "model"
+        predict = probability_identity
+    p1, p99 = volume_percentiles(vol, dev)  # identical on every rank and to the single-GPU path
+    res = analyze_volume(slab, predict, tile, overlap, batch, threshold, min_voxels, group=group, z_offset=z0,
+                         timings=True, norm_range=(float(p1), float(p99)))
+    t_an = time.perf_counter()
+    out = {"rank": rank, "z_range": [z0, z1], "n_instances": res["n_instances"], "timings_s": res["timings_s"]}
+    if gather == "rank0":
+        full = gather_to_rank0(res["labels_slab_t"], group)
+        if rank == 0:
+            np.save(out_path, full.cpu().numpy())
+    elif gather == "sharded":
+        np.save(f"{out_path}.rank{rank}.npy", res["labels_slab_t"].cpu().numpy())
+        if rank == 0:
+            with open(f"{out_path}.manifest.json", "w") as f:
+                json.dump({"world": world, "z_ranges": [list(slab_bounds(vol.shape[0], r, world)) for r in range(world)],
+                           "files": [f"{out_path}.rank{r}.npy" for r in range(world)]}, f)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    out["gather_s"] = round(time.perf_counter() - t_an, 4)
+    out["total_s"] = round(time.perf_counter() - t0, 4)
+    if rank == 0:
+        out.update(n_components=res["n_components"], volume_shape=list(vol.shape), instances=res["instances"])
     return out

@@ -27,7 +27,7 @@ def test_em_app_e2e(tmp_path, monkeypatch):
         await hub.start_http()
         tok = hub.issue_token("admin-user", workspace="ws-admin")
         w = BioEngineWorker(mode="single-machine", workspace_dir=tmp_path / "be", server_url="local://em", token=tok,
-                            client_id="worker1", log_file="off", head_num_cpus=4, head_num_gpus=0,
+                            client_id="worker1", log_file="off", head_num_cpus=8, head_num_gpus=0,
                             monitoring_interval_seconds=0.5, data_server_url=None)
         await w.start(blocking=False)
         admin = await connect_to_server({"server_url": "local://em", "token": tok})
@@ -49,6 +49,31 @@ def test_em_app_e2e(tmp_path, monkeypatch):
         np.save(buf, (rng.random((4, 96, 96)) * 255).astype(np.uint8))
         rv = await app.analyze_volume(volume_npy_b64=base64.b64encode(buf.getvalue()).decode(), tile_size=64, overlap=16)
         assert rv["volume_shape"] == [4, 96, 96] and "instances" in rv
+        # z-slab sharded over a gang of 2 / 3 ranks (gloo here, RCCL on GPUs): identical labels + stats
+        blobs = np.zeros((9, 64, 64), np.float32)
+        zz, yy, xx = np.mgrid[0:9, 0:64, 0:64]
+        for cz, cy, cx in ((2, 20, 20), (4, 40, 45), (7, 15, 50), (6, 50, 12)):
+            blobs += np.exp(-((zz - cz) ** 2 / 4 + (yy - cy) ** 2 / 30 + (xx - cx) ** 2 / 30))
+        buf = io.BytesIO()
+        np.save(buf, (blobs / blobs.max() * 255).astype(np.uint8))
+        b64 = base64.b64encode(buf.getvalue()).decode()
+        thr = 0.5
+        one = await app.analyze_volume(volume_npy_b64=b64, tile_size=64, overlap=16, return_labels=True,
+                                       input_is_probability=True)
+        l1 = np.load(io.BytesIO(base64.b64decode(one["labels_npy_b64"])))
+        assert l1.max() == 4 and one["n_components"] == 4
+        for n in (2, 3):
+            rn = await app.analyze_volume(volume_npy_b64=b64, tile_size=64, overlap=16, n_gpus=n, gather="rank0",
+                                          return_labels=True, threshold=float(thr),
+                                          input_is_probability=True)
+            ln = np.load(io.BytesIO(base64.b64decode(rn["labels_npy_b64"])))
+            assert np.array_equal(ln, l1), n
+            assert rn["n_instances"] == one["n_instances"] and rn["instances"] == one["instances"]
+            assert [r["z_range"] for r in rn["ranks"]][-1][1] == 9
+        rs = await app.analyze_volume(volume_npy_b64=b64, tile_size=64, overlap=16, n_gpus=2, gather="sharded",
+                                      threshold=float(thr), input_is_probability=True)
+        parts = [np.load(f) for f in rs["label_shards"]["files"]]
+        assert np.array_equal(np.concatenate(parts), l1)
         await svc.stop_worker(blocking=True)
         await admin.disconnect()
 
