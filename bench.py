@@ -11,9 +11,15 @@ Work per GPU is fixed as N grows (weak scaling: every GPU is an independent serv
 reference's scaling model — Ray Serve replicas, ``apps/model-runner/runtime_deployment.py:40-50``).
 
 After the timed inference steps, the same process measures (untimed for the headline):
-  * p50 / p95 latency of single-image requests (batch 1),
-  * fine-tune samples/s: CPnet fwd+bwd + fused AdamW on 256x256 crops with data-parallel gradient
-    all-reduce over RCCL (bucketed, overlapped with backward) — BASELINE config 3,
+  * p50 / p95 latency of single-image requests (batch 1, direct call),
+  * ``imgs_per_sec_cell_like``: the same pipeline with cell-like network outputs (~150 masks per
+    image), so the mask stage does realistic work,
+  * ``served_*``: continuous-batched serving through the full worker stack (hub RPC, router, GPU
+    process replica, ``@serve.batch``), one 512x512 image per request at 1 and 64 clients — BASELINE
+    config 2's "continuous-batched" p50 and throughput,
+  * fine-tune samples/s: CPnet fwd+bwd + fused AdamW on 256x256 crops, and Cellpose-SAM (ViT-L/8,
+    the reference app's model) on the HIP training engine, data-parallel over RCCL when N > 1
+    (bucketed, overlapped with backward) — BASELINE config 3,
 and reports them as extra fields of the one JSON line rank 0 prints.
 
 The reference publishes no number for these metrics (BASELINE.md §2), so ``vs_baseline`` is null;
@@ -152,6 +158,79 @@ def bench_mask_recovery(dev, batch, steps=3):
     return dt / batch * 1e3, float(m.amax(dim=(1, 2)).float().mean().item())
 
 
+def bench_cell_like(runner, imgs, p, steps=3):
+    """The timed inference pipeline with the network's output replaced by CELL-LIKE flows (~150
+    cells per 512x512 image), so seeding, flow QC and hole filling do realistic work: random-init
+    weights give no convergent flows and leave the mask stage nearly idle in the headline run."""
+    from bioengine_worker_amd.train.cellpose_train import labels_to_flows, synthetic_instances
+
+    B = imgs.shape[0]
+    _, labels = synthetic_instances(B, 512, 512, ncells=150, seed=11)
+    lab = torch.from_numpy(labels).to(imgs.device)
+    t = labels_to_flows(lab)
+    y_cell = torch.cat([5.0 * t[:, 1:3], torch.where(lab[:, None] > 0, 5.0, -5.0)], 1).contiguous()
+    x = imgs.float()
+
+    def run():
+        y, _, rescale = runner._net_stage(x, p)  # normalise + tiles + CPnet + blend (real work)
+        y = y_cell if y.shape == y_cell.shape else y
+        return runner.compute_masks(y, p, rescale)
+
+    for _ in range(2):
+        m = run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m = run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return B / dt, float(m.amax(dim=(1, 2)).float().mean().item())
+
+
+def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
+    """Requests through the full serving stack (tools/serve_bench.py): hub RPC -> app service ->
+    router -> GPU-pinned process replica (shared-memory ring) -> @serve.batch continuous batching ->
+    HIP pipeline -> back; one 512x512 image per request, H2D/D2H inside every request."""
+    import argparse as _ap
+    import asyncio
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import serve_bench
+
+    a = _ap.Namespace(size=512, concurrency=list(concurrency), seconds=seconds, gpus=1, replica_mode="process",
+                      max_ongoing=64, model="cyto3", profile=None)
+    res = asyncio.run(serve_bench.main_async(a))
+    out = {}
+    for r in res:
+        c = r["concurrency"]
+        out[f"served_imgs_per_sec_c{c}"] = r["imgs_per_s"]
+        out[f"served_p50_ms_c{c}"] = r["p50_ms"]
+        out[f"served_p95_ms_c{c}"] = r["p95_ms"]
+    return out
+
+
+def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int):
+    """Cellpose-SAM (ViT-L/8, 256x256 crops) fine-tune steps -- the reference app's own training
+    workload -- on the HIP CPSAM engine; with world > 1 data-parallel over RCCL (bucketed, bf16 wire)."""
+    from bioengine_worker_amd.models.cpsam import CPSAM
+    from bioengine_worker_amd.train.cellpose_train import TrainConfig, build_trainer, synthetic_train_batch
+
+    cfg = TrainConfig(batch_size=batch, bsize=256, lr=1e-5, weight_decay=1e-4, bucket_mb=64.0, comm_bf16=world > 1)
+    trainer = build_trainer(cfg, device=dev, world_size=world, rank=rank, net=CPSAM().randomize_(0))
+    data = synthetic_train_batch(batch, 256, device=dev, seed=rank)
+    for _ in range(3):
+        trainer.step(*data)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.step(*data)
+    _barrier(world)
+    dt = _max_over_ranks(time.perf_counter() - t0, world)
+    del trainer
+    torch.cuda.empty_cache()
+    return batch * steps * world / dt, dt / steps * 1e3
+
+
 def bench_train(args, world, rank, dev):
     from bioengine_worker_amd.train.cellpose_train import TrainConfig, synthetic_train_batch, build_trainer
 
@@ -179,6 +258,9 @@ def main():
     ap.add_argument("--train-steps", type=int, default=10)
     ap.add_argument("--chunks", type=int, default=1, help="micro-batches of the two-stream net/mask pipeline")
     ap.add_argument("--no-extras", action="store_true", help="skip latency / train / reference-algorithm extras")
+    ap.add_argument("--no-served", action="store_true", help="skip the served (full worker stack) measurement")
+    ap.add_argument("--served-seconds", type=float, default=4.0, help="seconds per served concurrency level")
+    ap.add_argument("--cpsam-batch", type=int, default=8, help="256x256 crops per step per GPU (Cellpose-SAM)")
     ap.add_argument("--trace", default=None, metavar="PATH",
                     help="after the timed steps, run one more traced step and write a Chrome trace (rank 0)")
     args = ap.parse_args()
@@ -229,8 +311,16 @@ def main():
                 mr_ms, mr_n = bench_mask_recovery(dev, args.batch)
                 out["mask_recovery_ms_per_image_150cells"] = round(mr_ms, 3)
                 out["mask_recovery_masks_per_image"] = mr_n
+                cl, cl_n = bench_cell_like(runner, imgs, p)
+                out["imgs_per_sec_cell_like"] = round(cl, 2)
+                out["cell_like_masks_per_image"] = cl_n
         except Exception as e:  # extras must never take the headline down
             out["extras_error"] = f"latency/ref: {type(e).__name__}: {e}"
+        if world == 1 and not args.no_served:
+            try:
+                out.update(bench_served(args.served_seconds))
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_served"] = f"{type(e).__name__}: {e}"
         try:
             tdt = bench_train(args, world, rank, dev)
             out["finetune_samples_per_sec"] = round(args.train_batch * args.train_steps * world / tdt, 2)
@@ -238,6 +328,19 @@ def main():
                                       "grad_allreduce": "RCCL bucketed, overlapped" if world > 1 else "none (1 GPU)"}
         except Exception as e:
             out["extras_error_train"] = f"{type(e).__name__}: {e}"
+        try:
+            sps, ms = bench_train_cpsam(args, world, rank, dev, args.cpsam_batch, args.train_steps)
+            out["finetune_cpsam_samples_per_sec"] = round(sps, 2)
+            out["finetune_cpsam_config"] = {"model": "Cellpose-SAM ViT-L/8 (dim 1024, 24 blocks)", "crop": 256,
+                                            "batch_per_gpu": args.cpsam_batch, "ms_per_step": round(ms, 3),
+                                            "engine": "HIP fwd/bwd engine, HIP-graph step" if world == 1 else
+                                            "HIP fwd/bwd engine, RCCL bucketed all-reduce (bf16) overlapped",
+                                            "parallelism": f"dp{world}"}
+            if world == 1:
+                sps1, ms1 = bench_train_cpsam(args, world, rank, dev, 1, args.train_steps)
+                out["finetune_cpsam_batch1_samples_per_sec"] = round(sps1, 2)  # the reference's batch size
+        except Exception as e:  # noqa: BLE001
+            out["extras_error_train_cpsam"] = f"{type(e).__name__}: {e}"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
