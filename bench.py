@@ -231,10 +231,10 @@ def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int):
     return batch * steps * world / dt, dt / steps * 1e3
 
 
-def bench_train(args, world, rank, dev):
+def bench_train(args, world, rank, dev, norm="auto"):
     from bioengine_worker_amd.train.cellpose_train import TrainConfig, synthetic_train_batch, build_trainer
 
-    cfg = TrainConfig(batch_size=args.train_batch, bsize=256, lr=1e-5, weight_decay=1e-4)
+    cfg = TrainConfig(batch_size=args.train_batch, bsize=256, lr=1e-5, weight_decay=1e-4, norm=norm)
     trainer = build_trainer(cfg, device=dev, world_size=world, rank=rank)
     batch = synthetic_train_batch(args.train_batch, cfg.bsize, device=dev, seed=rank)
     for _ in range(max(2, args.warmup)):
@@ -325,7 +325,11 @@ def main():
             tdt = bench_train(args, world, rank, dev)
             out["finetune_samples_per_sec"] = round(args.train_batch * args.train_steps * world / tdt, 2)
             out["finetune_config"] = {"crop": 256, "batch_per_gpu": args.train_batch, "optimizer": "fused AdamW (HIP)",
+                                      "norm": "group (DP default)" if world > 1 else "batch (cellpose cyto3)",
                                       "grad_allreduce": "RCCL bucketed, overlapped" if world > 1 else "none (1 GPU)"}
+            if world == 1:  # the DP default (GroupNorm) on one GPU, for comparison with the BN line
+                tdt = bench_train(args, world, rank, dev, norm="group")
+                out["finetune_groupnorm_samples_per_sec"] = round(args.train_batch * args.train_steps / tdt, 2)
         except Exception as e:
             out["extras_error_train"] = f"{type(e).__name__}: {e}"
         try:

@@ -82,7 +82,10 @@ class CellposeRunner:
         else:
             self.nchan = self.net.nchan
             self.bsize = 224
-            self.engine = CPnetEngine(self.net, self.device)
+            if getattr(self.net, "norm_kind", "batch") == "group":
+                self.engine = _GroupNormEngine(self.net, self.device)
+            else:
+                self.engine = CPnetEngine(self.net, self.device)
         self.diam_mean = float(self.net.diam_mean.item())
         self.cin_pad = (self.nchan + 7) // 8 * 8
         self._pinned: torch.Tensor | None = None  # host staging for numpy batches (pinned -> async DMA)
@@ -292,6 +295,41 @@ class CellposeRunner:
                                   max_size_fraction=p.max_size_fraction)
             out.append(torch.from_numpy(m.astype(np.int32)))
         return torch.stack(out)
+
+
+class _GroupNormEngine:
+    """Inference for GroupNorm CPnets (e.g. sessions trained data-parallel): GroupNorm statistics are
+    per image, so nothing folds into the weights; the HIP training engine's forward -- GN statistics
+    kernel + fused conv per layer, no activations saved for a backward -- runs the tiles instead
+    (one engine per tile-batch size).  Non-square tile grids fall back to bf16 autocast PyTorch."""
+
+    def __init__(self, net: CPnet, device):
+        import copy
+
+        from ..parallel.ddp import FlatParams
+
+        self.device = torch.device(device)
+        self.net = copy.deepcopy(net).to(self.device).eval()
+        self.fp = FlatParams(self.net, self.device) if self.device.type == "cuda" else None
+        self._engs: dict = {}
+
+    @torch.no_grad()
+    def __call__(self, tiles: torch.Tensor):
+        from ..train.cpnet_engine import CPnetTrainEngine
+
+        T, by, bx, _ = tiles.shape
+        x = tiles[..., : self.net.nchan].permute(0, 3, 1, 2).float()
+        if by != bx or by % 16 or self.fp is None:
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.device.type == "cuda"):
+                y, style = self.net(x.contiguous())[:2]
+            return y.float().contiguous(), style.float()
+        eng = self._engs.get((T, by))
+        if eng is None:
+            eng = self._engs[(T, by)] = CPnetTrainEngine(self.net, self.fp, T, by, self.device)
+        y = eng.forward(x)
+        style = eng._act["style"].float()
+        eng._act = None
+        return y, style
 
 
 def synthetic_cells(B: int, H: int = 512, W: int = 512, nchan: int = 2, ncells: int = 150, seed: int = 0) -> np.ndarray:

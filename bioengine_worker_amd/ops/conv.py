@@ -119,7 +119,7 @@ def _act_ref(x, x2, scale, shift, relu, inmode):
         xt = xt + x2.permute(0, 3, 1, 2).float()
     C = xt.shape[1]
     if scale is not None:
-        xt = xt * scale.view(1, C, 1, 1)
+        xt = xt * (scale.view(-1, C, 1, 1) if scale.dim() == 2 else scale.view(1, C, 1, 1))
     if shift is not None:
         sh = shift.view(-1, C, 1, 1) if shift.dim() == 2 else shift.view(1, C, 1, 1)
         xt = xt + sh
@@ -224,8 +224,14 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
         assert x2.shape == (N, H, W, Cin) and x2.dtype == torch.bfloat16 and x2.is_contiguous()
     if residual is not None:
         assert residual.shape == (N, H, W, pc.cout) and residual.dtype == torch.bfloat16 and residual.is_contiguous()
+    pscale_ns = 0
     if scale is not None:
-        assert scale.dtype == torch.float32 and scale.numel() == Cin
+        assert scale.dtype == torch.float32 and scale.is_contiguous()
+        if scale.dim() == 2:  # per-image affine (GroupNorm): [N, Cin]
+            assert scale.shape == (N, Cin)
+            pscale_ns = Cin
+        else:
+            assert scale.numel() == Cin
     pshift_ns = 0
     if shift is not None:
         assert shift.dtype == torch.float32 and shift.is_contiguous()
@@ -234,7 +240,7 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
             assert shift.shape == (N, Cin)
     _native.call(
         "be_conv2d_nhwc",
-        _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns,
+        _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns, pscale_ns,
         int(bool(relu)) | (2 if post_relu else 0),
         _native.ptr(pc.wp), _native.ptr(None if no_bias else pc.bias), _native.ptr(residual), _native.ptr(out),
         N, H, W, Hs, Ws, Cin, cout_store, cout_valid, pc.ks, pc.ck, pc.tco, INMODES[inmode], int(out_nchw_f32),

@@ -73,7 +73,7 @@ class BnUnit:
     run_mean: torch.Tensor | None
     run_var: torch.Tensor | None
     relu: bool
-    scale: torch.Tensor      # [C] fp32
+    scale: torch.Tensor      # [C] fp32 (BatchNorm) or [N, C] (GroupNorm)
     shift: torch.Tensor      # [N, C] fp32
     dgamma: torch.Tensor | None = None
     dbeta: torch.Tensor | None = None
@@ -82,12 +82,18 @@ class BnUnit:
 class BnSite:
     """BN statistics + backward of one BN input ``u = T(x) [+ x2] [+ feat]`` shared by 1-2 units.
 
+    ``groups = 0``: BatchNorm (train-mode batch statistics per channel).  ``groups = G``: GroupNorm --
+    statistics per image and group of ``c_valid / G`` channels, so the conv-prologue affine, the
+    mean / rstd and the backward coefficients are per image ([N, C]).
     ``stat`` is a slice of an arena the engine zeroes once per step; ``ticket`` two int32 counters."""
 
     def __init__(self, N: int, C: int, c_valid: int, units: list[BnUnit], stat: torch.Tensor, ticket: torch.Tensor,
-                 eps: float = 1e-5, momentum: float = 0.05, scratch: torch.Tensor | None = None):
+                 eps: float = 1e-5, momentum: float = 0.05, scratch: torch.Tensor | None = None, groups: int = 0):
         assert 1 <= len(units) <= 2
         self.N, self.C, self.c_valid = N, C, c_valid
+        self.groups = int(groups)
+        if self.groups:
+            assert c_valid % self.groups == 0, "GroupNorm groups must divide the channel count"
         self.units = units
         self.stat = stat
         self.ticket = ticket
@@ -96,11 +102,15 @@ class BnSite:
             scratch = torch.empty(SCRATCH_FLOATS, device=stat.device, dtype=torch.float32)
         self.scratch = scratch
         self.eps, self.momentum = eps, momentum
-        assert stat.numel() >= self.stat_numel(N, C)
+        assert stat.numel() >= self.stat_numel(N, C, self.groups)
 
     @staticmethod
-    def stat_numel(N: int, C: int) -> int:
-        return 6 * N * C + 4 * C
+    def stat_numel(N: int, C: int, groups: int = 0) -> int:
+        return 6 * N * C + 4 * (N * C if groups else C)
+
+    @property
+    def _cc(self) -> int:
+        return self.N * self.C if self.groups else self.C
 
     # stat layout (matches conv_train.hip): sum, sq, mean, rstd, sdy0, sdyx0, sdy1, sdyx1, B0, B1
     def _v(self, off: int, n: int) -> torch.Tensor:
@@ -108,11 +118,13 @@ class BnSite:
 
     @property
     def mean(self):
-        return self._v(2 * self.N * self.C, self.C)
+        m = self._v(2 * self.N * self.C, self._cc)
+        return m.view(self.N, self.C) if self.groups else m
 
     @property
     def rstd(self):
-        return self._v(2 * self.N * self.C + self.C, self.C)
+        r = self._v(2 * self.N * self.C + self._cc, self._cc)
+        return r.view(self.N, self.C) if self.groups else r
 
     def _sums(self):
         NC = self.N * self.C
@@ -120,12 +132,19 @@ class BnSite:
 
     def _bwd(self, k):
         NC = self.N * self.C
-        o = 2 * NC + 2 * self.C + 2 * k * NC
+        o = 2 * NC + 2 * self._cc + 2 * k * NC
         return self._v(o, NC).view(self.N, self.C), self._v(o + NC, NC).view(self.N, self.C)
 
     def _b(self):
-        o = 6 * self.N * self.C + 2 * self.C
-        return self._v(o, self.C), self._v(o + self.C, self.C)
+        o = 6 * self.N * self.C + 2 * self._cc
+        b0, b1 = self._v(o, self._cc), self._v(o + self._cc, self._cc)
+        if self.groups:
+            return b0.view(self.N, self.C), b1.view(self.N, self.C)
+        return b0, b1
+
+    def _rows(self, t):
+        """Per-image view [N, 1, 1, C] of a coefficient (BN: broadcast [C])."""
+        return t[:, None, None, :] if t.dim() == 2 else t
 
     def _call(self, which, x, x2, feat, inmode, H, W, dacts=(None, None), dfeat=None, dx=None, dx_acc=False, dx2=None,
               dx2_acc=False):
@@ -142,7 +161,8 @@ class BnSite:
         P = _native.ptr
         conv = [P(a) if (a is None or isinstance(a, torch.Tensor)) else a for a in args]
         _native.call("be_bn_train", which, P(x), P(x2), P(feat), N, Hs, Ws, H, W, C, self.c_valid, INMODES[inmode],
-                     len(self.units), float(self.eps), float(self.momentum), P(self.stat), P(self.ticket), *conv,
+                     len(self.units), float(self.eps), float(self.momentum), self.groups, P(self.stat), P(self.ticket),
+                     *conv,
                      P(dfeat), P(dx), int(dx_acc), P(dx2), int(dx2_acc), P(self.scratch), self.scratch.numel(),
                      _native.stream(x.device))
 
@@ -167,6 +187,8 @@ class BnSite:
         q.copy_((v * v).sum((1, 2)))
         f = feat.float() if feat is not None else torch.zeros(N, C)
         HW = H * W
+        if self.groups:
+            return self._gn_stats_ref(s, q, f, HW)
         cnt = N * HW
         s1 = (s + HW * f).sum(0)
         qq = (q + 2 * f * s + HW * f * f).sum(0)
@@ -188,6 +210,26 @@ class BnSite:
                 uk.run_mean.mul_(1 - m).add_(m * mean[:cv])
                 uk.run_var.mul_(1 - m).add_(m * var[:cv] * cnt / max(cnt - 1, 1))
 
+    def _gn_stats_ref(self, s, q, f, HW):
+        N, C, G, cv = self.N, self.C, self.groups, self.c_valid
+        cg = cv // G
+        s1 = (s + HW * f)[:, :cv].reshape(N, G, cg).sum(2)
+        qq = (q + 2 * f * s + HW * f * f)[:, :cv].reshape(N, G, cg).sum(2)
+        cnt = HW * cg
+        mean = s1 / cnt
+        rstd = 1.0 / torch.sqrt((qq / cnt - mean * mean).clamp_min(0) + self.eps)
+        mc = torch.zeros(N, C)
+        rc = torch.zeros(N, C)
+        mc[:, :cv] = mean.repeat_interleave(cg, 1)
+        rc[:, :cv] = rstd.repeat_interleave(cg, 1)
+        self.mean.copy_(mc)
+        self.rstd.copy_(rc)
+        valid = (torch.arange(C) < cv)[None]
+        for uk in self.units:
+            sc = torch.where(valid, _pad_to(uk.gamma, C)[None] * rc, torch.zeros(()))
+            uk.scale.copy_(sc)
+            uk.shift.copy_(torch.where(valid, (f - mc) * sc + _pad_to(uk.beta, C)[None], torch.zeros(())))
+
     @staticmethod
     def _vref(x, inmode, x2):
         v = _t_ref(x.float(), inmode)
@@ -207,7 +249,9 @@ class BnSite:
             return
         v = self._vref(x, inmode, x2)
         f = feat.float() if feat is not None else torch.zeros(N, C)
-        xh = (v + f[:, None, None, :] - self.mean) * self.rstd
+        xh = (v + f[:, None, None, :] - self._rows(self.mean)) * self._rows(self.rstd)
+        if self.groups:
+            return self._gn_reduce_ref(v, xh, dacts, f, H * W, dfeat)
         cnt = N * H * W
         b0 = torch.zeros(C)
         b1 = torch.zeros(C)
@@ -235,11 +279,42 @@ class BnSite:
             val = self.units[0].scale * sdy + H * W * b0 + b1 * sx
             dfeat.copy_(torch.where(valid, val, torch.zeros(())))
 
+    def _gn_reduce_ref(self, v, xh, dacts, f, HW, dfeat):
+        N, C, G, cv = self.N, self.C, self.groups, self.c_valid
+        cg = cv // G
+        M = HW * cg
+        b0 = torch.zeros(N, G)
+        b1 = torch.zeros(N, G)
+        for k, (uk, da) in enumerate(zip(self.units, dacts)):
+            dy = self._masked(uk, v, da)
+            sdy, sdyx = self._bwd(k)
+            sdy.copy_(dy.sum((1, 2)))
+            sdyx.copy_((dy * xh).sum((1, 2)))
+            b0 -= (uk.scale * sdy)[:, :cv].reshape(N, G, cg).sum(2) / M
+            b1 -= (uk.scale * sdyx)[:, :cv].reshape(N, G, cg).sum(2) / M
+            if uk.dgamma is not None:
+                uk.dgamma.copy_(sdyx.sum(0)[:cv])
+            if uk.dbeta is not None:
+                uk.dbeta.copy_(sdy.sum(0)[:cv])
+        B0, B1 = self._b()
+        B0.zero_()
+        B1.zero_()
+        B0[:, :cv] = b0.repeat_interleave(cg, 1)
+        B1[:, :cv] = b1.repeat_interleave(cg, 1)
+        if dfeat is not None:
+            s, _ = self._sums()
+            sx = (s + HW * (f - self.mean)) * self.rstd
+            sdy, _ = self._bwd(0)
+            val = self.units[0].scale * sdy + HW * B0 + B1 * sx
+            valid = (torch.arange(C) < cv)[None]
+            dfeat.copy_(torch.where(valid, val, torch.zeros(())))
+
     @staticmethod
     def _masked(uk: BnUnit, v: torch.Tensor, da: torch.Tensor) -> torch.Tensor:
         dy = da.float()
         if uk.relu:
-            y = v * uk.scale + uk.shift[:, None, None, :]
+            sc = uk.scale[:, None, None, :] if uk.scale.dim() == 2 else uk.scale
+            y = v * sc + uk.shift[:, None, None, :]
             dy = torch.where(y > 0, dy, torch.zeros(()))
         return dy
 
@@ -257,11 +332,11 @@ class BnSite:
             return
         v = self._vref(x, inmode, x2)
         f = feat.float() if feat is not None else torch.zeros(N, C)
-        xh = (v + f[:, None, None, :] - self.mean) * self.rstd
+        xh = (v + f[:, None, None, :] - self._rows(self.mean)) * self._rows(self.rstd)
         B0, B1 = self._b()
-        du = B0 + B1 * xh
+        du = self._rows(B0) + self._rows(B1) * xh
         for uk, da in zip(self.units, dacts):
-            du = du + uk.scale * self._masked(uk, v, da)
+            du = du + self._rows(uk.scale) * self._masked(uk, v, da)
         if dx2 is not None:
             _store(dx2, du, dx2_acc)
         if dx is not None:
@@ -323,8 +398,10 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, *, ks: int, cin_valid: int, co
     assert dw.dtype == torch.float32 and dw.is_contiguous() and dw.numel() == cout_valid * cin_valid * ks * ks
     if x2 is not None:
         assert inmode == "none" and x2.shape == (N, H, W, Cin) and x2.is_contiguous()
+    pscale_ns = 0
     if scale is not None:
-        assert scale.numel() == Cin and scale.dtype == torch.float32
+        assert scale.numel() in (Cin, N * Cin) and scale.dtype == torch.float32 and scale.is_contiguous()
+        pscale_ns = Cin if scale.dim() == 2 else 0
     pshift_ns = 0
     if shift is not None:
         assert shift.dtype == torch.float32 and shift.is_contiguous()
@@ -335,7 +412,7 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, *, ks: int, cin_valid: int, co
         ws = torch.empty(need, device=x.device, dtype=torch.float32)
     wsb = ws[splits * cout_valid * ks * ks * Cin:]
     _native.call("be_conv_wgrad", _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns,
-                 int(bool(relu)), _native.ptr(dy), _native.ptr(ws), _native.ptr(wsb), _native.ptr(dw), _native.ptr(db),
+                 pscale_ns, int(bool(relu)), _native.ptr(dy), _native.ptr(ws), _native.ptr(wsb), _native.ptr(dw), _native.ptr(db),
                  N, H, W, Hs, Ws, Cin, cin_valid, Cy, cout_valid, ks, INMODES[inmode], splits,
                  _native.stream(x.device))
 

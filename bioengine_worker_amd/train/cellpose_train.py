@@ -40,7 +40,9 @@ class TrainConfig:
     scale_range: float = 0.5
     validation_interval: int = 10
     min_train_masks: int = 5
-    norm: str = "batch"
+    # "auto": BatchNorm (cellpose cyto3) on one GPU, GroupNorm for data-parallel runs -- per-image
+    # statistics make the DP step independent of how the global batch is split across ranks
+    norm: str = "auto"
     autocast_bf16: bool = True
     bucket_mb: float = 16.0
     comm_bf16: bool = False
@@ -100,7 +102,7 @@ class CellposeTrainer:
         if self.is_cpsam:
             eng = "cpsam"  # explicit fwd/bwd engine (train/cpsam_engine.py) on CPU and GPU
         elif eng == "auto":
-            eng = "hip" if (self.device.type == "cuda" and cfg.norm == "batch") else "autograd"
+            eng = "hip" if (self.device.type == "cuda" and cfg.norm in ("batch", "group")) else "autograd"
         self.engine_kind = eng
         self._eng = None
         self._cpsam_engs: dict = {}
@@ -345,8 +347,13 @@ class CellposeTrainer:
         self._refresh_mirrors()
 
 
+def resolve_norm(norm: str, world_size: int) -> str:
+    return ("group" if world_size > 1 else "batch") if norm == "auto" else norm
+
+
 def build_trainer(cfg: TrainConfig, device, world_size: int = 1, rank: int = 0, net: CPnet | None = None,
                   group=None) -> CellposeTrainer:
+    cfg.norm = getattr(net, "norm_kind", None) or resolve_norm(cfg.norm, world_size)
     net = net or CPnet(norm=cfg.norm).randomize_(cfg.seed)
     return CellposeTrainer(net, cfg, device, world_size, rank, group)
 

@@ -91,8 +91,9 @@ class CPnetTrainEngine:
 
     def __init__(self, net: CPnet, fp: FlatParams, B: int, S: int, device, momentum: float = 0.05,
                  act_dtype: torch.dtype | None = None):
-        if net.norm_kind != "batch":
-            raise ValueError("CPnetTrainEngine implements BatchNorm (cellpose cyto3) nets")
+        if net.norm_kind not in ("batch", "group"):
+            raise ValueError(f"CPnetTrainEngine implements BatchNorm / GroupNorm nets, not {net.norm_kind!r}")
+        self.groupnorm = net.norm_kind == "group"
         if S % 16:
             raise ValueError("crop size must be a multiple of 16 (4 pooling levels)")
         self.net = net
@@ -129,10 +130,13 @@ class CPnetTrainEngine:
     def _mk_site(self, bns: list, relus: list, C: int, c_valid: int | None = None) -> _Site:
         units = []
         for bn, relu in zip(bns, relus):
-            units.append(ct.BnUnit(gamma=bn.weight, beta=bn.bias, run_mean=bn.running_mean, run_var=bn.running_var,
-                                   relu=relu, scale=None, shift=None, dgamma=bn.weight.grad, dbeta=bn.bias.grad))
+            units.append(ct.BnUnit(gamma=bn.weight, beta=bn.bias, run_mean=getattr(bn, "running_mean", None),
+                                   run_var=getattr(bn, "running_var", None), relu=relu, scale=None, shift=None,
+                                   dgamma=bn.weight.grad, dbeta=bn.bias.grad))
         s = _Site(bn=None, units=units, C=C)
         s.c_valid = c_valid or C
+        # GroupNorm: groups of the site's norm (shared-input units have the same channel count)
+        s.groups = int(bns[0].num_groups) if isinstance(bns[0], nn.GroupNorm) else 0
         self._sites.append(s)
         return s
 
@@ -172,7 +176,7 @@ class CPnetTrainEngine:
         d, B, S = self.device, self.B, self.S
         f32 = torch.float32
         # ---- BN workspaces (one arena, zeroed once per step) + prologue affines
-        sizes = [ct.BnSite.stat_numel(B, s.C) for s in self._sites]
+        sizes = [ct.BnSite.stat_numel(B, s.C, s.groups) for s in self._sites]
         self._bn_scratch = torch.empty(ct.SCRATCH_FLOATS, device=d, dtype=f32) if self.cuda else None
         tot = sum(sizes) + 2 * len(self._sites) + 64
         self._ws_arena = torch.zeros(tot, device=d, dtype=f32)
@@ -180,10 +184,10 @@ class CPnetTrainEngine:
         tickets = self._ws_arena[sum(sizes):].view(torch.int32)
         for i, (s, n) in enumerate(zip(self._sites, sizes)):
             for u in s.units:
-                u.scale = torch.zeros(s.C, device=d, dtype=f32)
+                u.scale = torch.zeros((B, s.C) if s.groups else (s.C,), device=d, dtype=f32)
                 u.shift = torch.zeros(B, s.C, device=d, dtype=f32)
             s.bn = ct.BnSite(B, s.C, s.c_valid, s.units, self._ws_arena[off: off + n], tickets[2 * i: 2 * i + 2],
-                             momentum=self.momentum, scratch=self._bn_scratch)
+                             momentum=self.momentum, scratch=self._bn_scratch, groups=s.groups)
             off += n
         # ---- packed weights: one bf16 arena + descriptor table (repacked from the fp32 master each step)
         descs, arena_off, max_e = [], 0, 0

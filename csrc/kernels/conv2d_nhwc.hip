@@ -49,7 +49,7 @@ constexpr int TW = 32;  // output tile cols (two 16-pixel MFMA column tiles)
 struct ConvArgs {
   const bf16_t* x;       // [N, Hs, Ws, Cin]
   const bf16_t* x2;      // optional [N, H, W, Cin] added before the affine
-  const float* pscale;   // optional [Cin]
+  const float* pscale;   // optional [N?, Cin] (row stride pscale_ns: 0 => shared over batch; GroupNorm: Cin)
   const float* pshift;   // optional [N?, Cin]  (row stride pshift_ns: 0 => shared over batch)
   const bf16_t* w;       // packed [Cout_pad][nchunk][KP]
   const float* bias;     // optional [Cout]
@@ -57,7 +57,7 @@ struct ConvArgs {
   void* out;             // bf16 NHWC [N,H,W,Cout] or f32 NCHW [N,cout_valid,H,W]
   int N, H, W, Hs, Ws, Cin, Cout, cout_valid;
   int nchunk, KP;
-  int pshift_ns;
+  int pshift_ns, pscale_ns;
   int prelu;           // bit 0: ReLU on the (affine) input; bit 1: ReLU on the output (after bias/residual)
   int out_f32_nchw;
   int tiles_x, tiles_y;
@@ -104,8 +104,9 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
   {  // this thread's 8 channels are the same for every halo unit (NT % CG == 0): prefetch the affine
     const int c = c0 + (tid % C::CG) * 8;
     if (a.pscale) {
-      aff[0] = *reinterpret_cast<const float4*>(a.pscale + c);
-      aff[1] = *reinterpret_cast<const float4*>(a.pscale + c + 4);
+      const float* sc = a.pscale + (size_t)n * a.pscale_ns + c;
+      aff[0] = *reinterpret_cast<const float4*>(sc);
+      aff[1] = *reinterpret_cast<const float4*>(sc + 4);
     }
     if (a.pshift) {
       const float* sr = a.pshift + (size_t)n * a.pshift_ns + c;
@@ -579,7 +580,7 @@ int be_conv2d_set_persist(int blocks) {
 // Returns the K chunk length (padded) the packed weight layout must use for (ks, ck).
 int be_conv2d_packed_kp(int ks, int ck) { return ((ks * ks * ck + 31) / 32) * 32; }
 
-int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const float* pshift, int pshift_ns,
+int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const float* pshift, int pshift_ns, int pscale_ns,
                    int prelu, const void* w, const float* bias, const void* res, void* out, int N, int H, int W,
                    int Hs, int Ws, int Cin, int Cout, int cout_valid, int ks, int ck, int tco, int inmode,
                    int out_f32_nchw, int nw, hipStream_t stream) {
@@ -587,7 +588,7 @@ int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const flo
   if (!(ks == 1 || ks == 3)) return -11;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.x2 = (const bf16_t*)x2; a.pscale = pscale; a.pshift = pshift;
-  a.pshift_ns = pshift_ns; a.prelu = prelu; a.w = (const bf16_t*)w; a.bias = bias;
+  a.pshift_ns = pshift_ns; a.pscale_ns = pscale_ns; a.prelu = prelu; a.w = (const bf16_t*)w; a.bias = bias;
   a.res = (const bf16_t*)res; a.out = out;
   a.N = N; a.H = H; a.W = W; a.Hs = Hs; a.Ws = Ws; a.Cin = Cin; a.Cout = Cout; a.cout_valid = cout_valid;
   a.nchunk = Cin / ck; a.KP = be_conv2d_packed_kp(ks, ck);

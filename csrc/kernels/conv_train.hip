@@ -90,13 +90,13 @@ __device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
 struct WgArgs {
   const bf16_t* x;      // pre-transform input [N, Hs, Ws, Cin]
   const bf16_t* x2;     // optional skip [N, H, W, Cin]
-  const float* pscale;  // [Cin] (null = 1)
+  const float* pscale;  // [N?, Cin] (null = 1; row stride pscale_ns, GroupNorm: Cin)
   const float* pshift;  // [N?, Cin] (null = 0)
   const bf16_t* dy;     // dOut [N, H, W, Cy] (Cy % 8 == 0)
   float* ws;            // partials [splits][cout_valid][Cin][KS*KS] (torch weight layout per split)
   float* wsb;           // optional dbias partials [splits][cout_valid]
   int N, H, W, Hs, Ws, Cin, Cy, cout_valid;
-  int pshift_ns, relu;
+  int pshift_ns, pscale_ns, relu;
   int tiles_x, tiles_y, ntiles, splits;
 };
 
@@ -170,7 +170,7 @@ __device__ __forceinline__ void wg_commit(const WgArgs& a, int t, int ci0, int t
   float sc[8], sh[8];
   {
     const int c = ci0 + (tid % C::CG) * 8;
-    if (a.pscale) ld8(a.pscale + c, sc);
+    if (a.pscale) ld8(a.pscale + (size_t)n * a.pscale_ns + c, sc);
     else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) sc[j] = 1.f;
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 struct BnUnits {
   const float* gamma[2];
   const float* beta[2];
-  float* scale[2];     // [C]
+  float* scale[2];     // [C] (BatchNorm) or [N, C] (GroupNorm)
   float* shift[2];     // [N, C]
   float* run_mean[2];  // optional
   float* run_var[2];
@@ -399,8 +399,11 @@ struct BnArgs {
   const bf16_t* x2;  // optional [N, H, W, C]
   const float* feat; // optional [N, C] (style feature added before the BN)
   int N, Hs, Ws, H, W, C, c_valid, inmode, nunits;
+  int groups;        // 0: BatchNorm (batch statistics per channel); G > 0: GroupNorm, G groups per image
+  int cns;           // per-image stride of the coefficient arrays: 0 (BN) or C (GN)
   float eps, momentum;
-  float* stat;       // workspace: sum[N*C], sq[N*C], mean[C], rstd[C], then bwd: sdy[2][N*C], sdyx[2][N*C], B0[C], B1[C]
+  float* stat;       // workspace: sum[N*C], sq[N*C], mean[CC], rstd[CC], then bwd: sdy[2][N*C], sdyx[2][N*C], B0[CC],
+                     // B1[CC] with CC = C (BN) or N*C (GN: per-image group values broadcast to the channels)
   unsigned* ticket;  // zeroed counters: [0] fwd, [1] bwd
   BnUnits u;
   float* dfeat;      // backward: [N, C]
@@ -412,11 +415,12 @@ struct BnArgs {
 __device__ __forceinline__ float* st_sum(const BnArgs& a) { return a.stat; }
 __device__ __forceinline__ float* st_sq(const BnArgs& a) { return a.stat + (size_t)a.N * a.C; }
 __device__ __forceinline__ float* st_mean(const BnArgs& a) { return a.stat + (size_t)2 * a.N * a.C; }
-__device__ __forceinline__ float* st_rstd(const BnArgs& a) { return st_mean(a) + a.C; }
-__device__ __forceinline__ float* st_sdy(const BnArgs& a, int k) { return st_rstd(a) + a.C + (size_t)k * 2 * a.N * a.C; }
+__device__ __forceinline__ size_t st_cc(const BnArgs& a) { return a.cns ? (size_t)a.N * a.C : (size_t)a.C; }
+__device__ __forceinline__ float* st_rstd(const BnArgs& a) { return st_mean(a) + st_cc(a); }
+__device__ __forceinline__ float* st_sdy(const BnArgs& a, int k) { return st_rstd(a) + st_cc(a) + (size_t)k * 2 * a.N * a.C; }
 __device__ __forceinline__ float* st_sdyx(const BnArgs& a, int k) { return st_sdy(a, k) + (size_t)a.N * a.C; }
-__device__ __forceinline__ float* st_b0(const BnArgs& a) { return st_rstd(a) + a.C + (size_t)4 * a.N * a.C; }
-__device__ __forceinline__ float* st_b1(const BnArgs& a) { return st_b0(a) + a.C; }
+__device__ __forceinline__ float* st_b0(const BnArgs& a) { return st_rstd(a) + st_cc(a) + (size_t)4 * a.N * a.C; }
+__device__ __forceinline__ float* st_b1(const BnArgs& a) { return st_b0(a) + st_cc(a); }
 
 // v = T(x) [+ x2] at output pixel pix (row-major over H x W) for channels c..c+7
 template <int INMODE, bool X2>
@@ -576,14 +580,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnArgs a) {
     for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
   if (pl < PL) {
     float mean[8], rstd[8], f[8], sc[NU][8], sh[NU][8];
+    const size_t cr = (size_t)n * a.cns + c0;  // coefficient row (per image for GroupNorm)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      mean[j] = st_mean(a)[c0 + j];
-      rstd[j] = st_rstd(a)[c0 + j];
+      mean[j] = st_mean(a)[cr + j];
+      rstd[j] = st_rstd(a)[cr + j];
       f[j] = a.feat ? a.feat[(size_t)n * a.C + c0 + j] : 0.f;
 #pragma unroll
       for (int k = 0; k < NU; ++k) {
-        sc[k][j] = a.u.scale[k][c0 + j];
+        sc[k][j] = a.u.scale[k][cr + j];
         sh[k][j] = a.u.shift[k][(size_t)n * a.C + c0 + j];
       }
     }
@@ -651,6 +656,102 @@ __global__ __launch_bounds__(256) void bn_bwd_fin_kernel(BnArgs a) {
   }
 }
 
+// ---- GroupNorm finalise (forward): image n's per-channel sums -> per-(image, group) mean / rstd over
+// H*W*(c_valid/G) values of u = v + feat[n]; the conv-prologue affine becomes per image:
+// scale[n, c] = gamma[c] * rstd[n, g(c)], shift[n, c] = (feat[n, c] - mean[n, g]) * scale[n, c] + beta[c].
+// One block per image (no cross-image dependency, so no last-block ticket).
+__global__ __launch_bounds__(256) void gn_stats_fin_kernel(BnArgs a) {
+  const int n = blockIdx.x, tid = threadIdx.x, HW = a.H * a.W;
+  float* dst[2] = {st_sum(a), st_sq(a)};
+  image_reduce<2>(a, n, dst);
+  __syncthreads();
+  __threadfence_block();
+  const int G = a.groups, cg = a.c_valid / G;
+  const float cnt = (float)HW * (float)cg;
+  __shared__ float gm[256], gr[256];
+  for (int g = tid; g < G; g += 256) {
+    float s1 = 0.f, q = 0.f;
+    for (int c = g * cg; c < (g + 1) * cg; ++c) {
+      const float s = st_sum(a)[(size_t)n * a.C + c], sq = st_sq(a)[(size_t)n * a.C + c];
+      const float f = a.feat ? a.feat[(size_t)n * a.C + c] : 0.f;
+      s1 += s + (float)HW * f;
+      q += sq + 2.f * f * s + (float)HW * f * f;
+    }
+    const float mean = s1 / cnt;
+    gm[g] = mean;
+    gr[g] = 1.f / sqrtf(fmaxf(q / cnt - mean * mean, 0.f) + a.eps);
+  }
+  __syncthreads();
+  for (int c = tid; c < a.C; c += 256) {
+    const bool valid = c < a.c_valid;
+    const int g = valid ? c / cg : 0;
+    const float mean = valid ? gm[g] : 0.f, rstd = valid ? gr[g] : 0.f;
+    const size_t i = (size_t)n * a.C + c;
+    st_mean(a)[i] = mean;
+    st_rstd(a)[i] = rstd;
+    const float f = a.feat ? a.feat[i] : 0.f;
+    for (int k = 0; k < a.nunits; ++k) {
+      const float sc = valid ? a.u.gamma[k][c] * rstd : 0.f;
+      a.u.scale[k][i] = sc;
+      a.u.shift[k][i] = valid ? (f - mean) * sc + a.u.beta[k][c] : 0.f;
+    }
+  }
+}
+
+// ---- GroupNorm finalise (backward): per (image, group) B0 = -sum_{c in g} scale*sum(dy) / M,
+// B1 = -sum scale*sum(dy*xhat) / M (M = H*W*c_valid/G), summed over the units; dgamma / dbeta sum
+// over images (last block); dfeat per (image, channel).
+template <int NU>
+__global__ __launch_bounds__(256) void gn_bwd_fin_kernel(BnArgs a) {
+  const int n = blockIdx.x, tid = threadIdx.x, HW = a.H * a.W;
+  float* dst[2 * NU];
+#pragma unroll
+  for (int k = 0; k < NU; ++k) { dst[2 * k] = st_sdy(a, k); dst[2 * k + 1] = st_sdyx(a, k); }
+  image_reduce<2 * NU>(a, n, dst);
+  __syncthreads();
+  __threadfence_block();
+  const int G = a.groups, cg = a.c_valid / G;
+  const float M = (float)HW * (float)cg;
+  __shared__ float gb0[256], gb1[256];
+  for (int g = tid; g < G; g += 256) {
+    float b0 = 0.f, b1 = 0.f;
+    for (int k = 0; k < NU; ++k)
+      for (int c = g * cg; c < (g + 1) * cg; ++c) {
+        const size_t i = (size_t)n * a.C + c;
+        const float s = a.u.scale[k][i];
+        b0 -= s * st_sdy(a, k)[i] / M;
+        b1 -= s * st_sdyx(a, k)[i] / M;
+      }
+    gb0[g] = b0;
+    gb1[g] = b1;
+  }
+  __syncthreads();
+  for (int c = tid; c < a.C; c += 256) {
+    const bool valid = c < a.c_valid;
+    const size_t i = (size_t)n * a.C + c;
+    const float b0 = valid ? gb0[c / cg] : 0.f, b1 = valid ? gb1[c / cg] : 0.f;
+    st_b0(a)[i] = b0;
+    st_b1(a)[i] = b1;
+    if (a.dfeat) {
+      const float f = a.feat ? a.feat[i] : 0.f;
+      const float sx = (st_sum(a)[i] + (float)HW * (f - st_mean(a)[i])) * st_rstd(a)[i];
+      a.dfeat[i] = valid ? a.u.scale[0][i] * st_sdy(a, 0)[i] + (float)HW * b0 + b1 * sx : 0.f;
+    }
+  }
+  if (!last_block(a.ticket + 1)) return;
+  for (int c = tid; c < a.c_valid; c += 256) {
+    for (int k = 0; k < NU; ++k) {
+      float sdy = 0.f, sdyx = 0.f;
+      for (int m = 0; m < a.N; ++m) {
+        sdy += ld_acq(st_sdy(a, k) + (size_t)m * a.C + c);
+        sdyx += ld_acq(st_sdyx(a, k) + (size_t)m * a.C + c);
+      }
+      if (a.u.dgamma[k]) a.u.dgamma[k][c] = sdyx;
+      if (a.u.dbeta[k]) a.u.dbeta[k][c] = sdy;
+    }
+  }
+}
+
 // ---- backward apply: du at every post-transform pixel, routed into dx (T^T) and dx2
 struct ApplyOut {
   bf16_t* dx;   // [N, Hs, Ws, C] or null
@@ -681,18 +782,22 @@ template <int NU>
 struct Coef {
   float mean[8], rstd[8], b0[8], b1[8], sc[NU][8], sh[NU][8], f[8];
   int n;
+  __device__ void coefs(const BnArgs& a, size_t cr) {
+    ld8(st_mean(a) + cr, mean);
+    ld8(st_rstd(a) + cr, rstd);
+    ld8(st_b0(a) + cr, b0);
+    ld8(st_b1(a) + cr, b1);
+#pragma unroll
+    for (int k = 0; k < NU; ++k) ld8(a.u.scale[k] + cr, sc[k]);
+  }
   __device__ void init(const BnArgs& a, int c0) {
     n = -1;
-    ld8(st_mean(a) + c0, mean);
-    ld8(st_rstd(a) + c0, rstd);
-    ld8(st_b0(a) + c0, b0);
-    ld8(st_b1(a) + c0, b1);
-#pragma unroll
-    for (int k = 0; k < NU; ++k) ld8(a.u.scale[k] + c0, sc[k]);
+    if (!a.cns) coefs(a, c0);  // BatchNorm: one coefficient row for the whole batch
   }
   __device__ void image(const BnArgs& a, int nn, int c0) {
     if (nn == n) return;
     n = nn;
+    if (a.cns) coefs(a, (size_t)nn * a.cns + c0);
 #pragma unroll
     for (int k = 0; k < NU; ++k) ld8(a.u.shift[k] + (size_t)nn * a.C + c0, sh[k]);
     if (a.feat) {
@@ -817,14 +922,17 @@ int bn_dispatch_x2(int which, BnArgs a, ApplyOut o, hipStream_t s) {
   dim3 grid(nb, a.N);
   if (which == 0) {
     hipLaunchKernelGGL((bn_stats_kernel<INMODE, X2>), grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(bn_stats_fin_kernel, dim3(a.N), dim3(256), 0, s, a);
+    if (a.groups) hipLaunchKernelGGL(gn_stats_fin_kernel, dim3(a.N), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(bn_stats_fin_kernel, dim3(a.N), dim3(256), 0, s, a);
   } else if (which == 1) {
     if (a.nunits == 2) {
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<INMODE, X2, 2>), grid, dim3(256), 0, s, a);
-      hipLaunchKernelGGL(bn_bwd_fin_kernel<2>, dim3(a.N), dim3(256), 0, s, a);
+      if (a.groups) hipLaunchKernelGGL(gn_bwd_fin_kernel<2>, dim3(a.N), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL(bn_bwd_fin_kernel<2>, dim3(a.N), dim3(256), 0, s, a);
     } else {
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<INMODE, X2, 1>), grid, dim3(256), 0, s, a);
-      hipLaunchKernelGGL(bn_bwd_fin_kernel<1>, dim3(a.N), dim3(256), 0, s, a);
+      if (a.groups) hipLaunchKernelGGL(gn_bwd_fin_kernel<1>, dim3(a.N), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL(bn_bwd_fin_kernel<1>, dim3(a.N), dim3(256), 0, s, a);
     }
   } else {
     const int PH = INMODE == 1 ? a.Hs : a.H, PW = INMODE == 1 ? a.Ws : a.W;
@@ -838,6 +946,7 @@ int bn_dispatch_x2(int which, BnArgs a, ApplyOut o, hipStream_t s) {
 
 int bn_dispatch(int which, BnArgs a, ApplyOut o, hipStream_t s) {
   if (a.C % 8 || a.C > 256 || 64 % (a.C / 8) || a.nunits < 1 || a.nunits > 2) return -1;
+  if (a.groups && (a.groups > 256 || a.c_valid % a.groups)) return -3;
   const bool x2 = a.x2 != nullptr;
   switch (a.inmode) {
     case 0: return x2 ? bn_dispatch_x2<0, true>(which, a, o, s) : bn_dispatch_x2<0, false>(which, a, o, s);
@@ -890,7 +999,8 @@ extern "C" {
 
 // Weight gradient (+ optional bias gradient) of one fused conv unit.  ws/wsb: fp32 partial workspace
 // sized [splits][cout_valid][ks*ks][Cin] / [splits][cout_valid]; dw: [cout_valid, cin_valid, ks, ks].
-int be_conv_wgrad(const void* x, const void* x2, const float* pscale, const float* pshift, int pshift_ns, int relu,
+int be_conv_wgrad(const void* x, const void* x2, const float* pscale, const float* pshift, int pshift_ns, int pscale_ns,
+                  int relu,
                   const void* dy, float* ws, float* wsb, float* dw, float* db, int N, int H, int W, int Hs, int Ws,
                   int Cin, int cin_valid, int Cy, int cout_valid, int ks, int inmode, int splits, hipStream_t s) {
   if (Cin != 8 && Cin % 32) return -1;
@@ -899,7 +1009,7 @@ int be_conv_wgrad(const void* x, const void* x2, const float* pscale, const floa
   a.x = (const bf16_t*)x; a.x2 = (const bf16_t*)x2; a.pscale = pscale; a.pshift = pshift;
   a.dy = (const bf16_t*)dy; a.ws = ws; a.wsb = db ? wsb : nullptr;
   a.N = N; a.H = H; a.W = W; a.Hs = Hs; a.Ws = Ws; a.Cin = Cin; a.Cy = Cy; a.cout_valid = cout_valid;
-  a.pshift_ns = pshift_ns; a.relu = relu;
+  a.pshift_ns = pshift_ns; a.pscale_ns = pscale_ns; a.relu = relu;
   a.tiles_x = (W + 31) / 32; a.tiles_y = (H + 3) / 4;
   a.ntiles = N * a.tiles_x * a.tiles_y;
   a.splits = splits < a.ntiles ? splits : a.ntiles;
@@ -923,8 +1033,11 @@ int be_conv_wgrad(const void* x, const void* x2, const float* pscale, const floa
 
 // which: 0 = forward statistics + finalise, 1 = backward reduce + finalise, 2 = backward apply.
 // Pointer arrays hold up to two BN units sharing the same input (proj + conv_0 of a res block).
+// groups = 0: BatchNorm (train-mode batch statistics); groups = G: GroupNorm with G groups of the
+// c_valid channels per image (scale / shift / stat coefficient arrays are then per image: [N, C]).
 int be_bn_train(int which, const void* x, const void* x2, const float* feat, int N, int Hs, int Ws, int H, int W, int C,
-                int c_valid, int inmode, int nunits, float eps, float momentum, float* stat, unsigned* ticket,
+                int c_valid, int inmode, int nunits, float eps, float momentum, int groups, float* stat,
+                unsigned* ticket,
                 const float* gamma0, const float* beta0, float* scale0, float* shift0, float* rm0, float* rv0, int relu0,
                 const void* dact0, float* dgamma0, float* dbeta0,
                 const float* gamma1, const float* beta1, float* scale1, float* shift1, float* rm1, float* rv1, int relu1,
@@ -935,6 +1048,7 @@ int be_bn_train(int which, const void* x, const void* x2, const float* feat, int
   a.x = (const bf16_t*)x; a.x2 = (const bf16_t*)x2; a.feat = feat;
   a.N = N; a.Hs = Hs; a.Ws = Ws; a.H = H; a.W = W; a.C = C; a.c_valid = c_valid; a.inmode = inmode;
   a.nunits = nunits; a.eps = eps; a.momentum = momentum; a.stat = stat; a.ticket = ticket;
+  a.groups = groups; a.cns = groups ? C : 0;
   a.u.gamma[0] = gamma0; a.u.beta[0] = beta0; a.u.scale[0] = scale0; a.u.shift[0] = shift0;
   a.u.run_mean[0] = rm0; a.u.run_var[0] = rv0; a.u.relu[0] = relu0; a.u.dact[0] = (const bf16_t*)dact0;
   a.u.dgamma[0] = dgamma0; a.u.dbeta[0] = dbeta0;

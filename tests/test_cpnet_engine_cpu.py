@@ -91,3 +91,35 @@ def test_pack_ref_matches_packed_conv():
     pct = PackedConv.from_weight(wt, cin_pad=32)
     got_t = ct.pack_ref(w, pct.cout_pad, pct.cin_pad, pct.ck, pct.kp, True)
     torch.testing.assert_close(got_t.to(torch.bfloat16), pct.wp)
+
+
+@pytest.mark.parametrize("style_on", [True, False])
+def test_groupnorm_engine_grads_match_autograd(style_on):
+    """GroupNorm CPnet (per-image, per-group statistics; the data-parallel training default) through
+    the same engine: forward and every gradient against autograd."""
+    torch.manual_seed(3)
+    net = CPnet(nbase=(2, 8, 16, 16, 32), style_on=style_on, norm="group").randomize_(3).train()
+    with torch.no_grad():
+        for n, p in net.named_parameters():
+            if p.requires_grad and p.dim() == 1 and "full" not in n:
+                p.add_(0.2 * torch.randn_like(p))  # non-trivial GN affine
+    ref = copy.deepcopy(net)
+    x = torch.randn(3, 2, 32, 32)
+    lbl = torch.zeros(3, 3, 32, 32)
+    lbl[:, 0] = (torch.rand(3, 32, 32) > 0.6).float()
+    lbl[:, 1:] = torch.randn(3, 2, 32, 32) * 0.3
+    loss_ref = train_ops.seg_loss_ref(ref(x)[0], lbl)
+    loss_ref.backward()
+    fp = FlatParams(net, "cpu")
+    eng = CPnetTrainEngine(net, fp, B=3, S=32, device="cpu")
+    loss = eng.loss_and_backward(x, lbl)
+    assert abs(float(loss) - float(loss_ref.detach())) < 1e-5 * max(1.0, abs(float(loss_ref.detach())))
+    named_ref = dict(ref.named_parameters())
+    gmax = max(p.grad.abs().max().item() for p in ref.parameters() if p.grad is not None)
+    for name, p in net.named_parameters():
+        if not p.requires_grad:
+            continue
+        g_ref = named_ref[name].grad
+        err = (p.grad - g_ref).abs().max().item()
+        tol = 2e-4 * g_ref.abs().max().item() + 2e-6 * gmax
+        assert err < tol, f"{name}: err {err:.2e} > tol {tol:.2e}"
