@@ -54,7 +54,9 @@ from bioengine_worker_amd.cellpose.datasets import (  # noqa: F401  (re-exported
     read_image,
 )
 from bioengine_worker_amd.cellpose.model_store import BUILTIN_MODELS
-from bioengine_worker_amd.train.session import now_iso, read_status, to_chw, write_status
+from bioengine_worker_amd.profiling import trace
+from bioengine_worker_amd.serve.batching import offload
+from bioengine_worker_amd.train.session import now_iso, read_status, to_chw, write_status  # noqa: F401
 
 log = logging.getLogger("ray.serve")
 STATUS_STALE_SECONDS = 300.0
@@ -94,6 +96,22 @@ def _user_id(context) -> str | None:
     if isinstance(context, dict) and isinstance(context.get("user"), dict):
         return context["user"].get("id")
     return None
+
+
+def image_chw(img: np.ndarray, nchan: int) -> np.ndarray:
+    """[H,W] / [H,W,C] / [C,H,W] -> [nchan, H, W] in the image's OWN dtype (uint8/uint16 stay
+    integers: half / a quarter of the float32 bytes through the replica ring and over PCIe; the GPU
+    converts while normalising)."""
+    a = np.asarray(img)
+    if a.ndim == 2:
+        a = a[None]
+    elif a.ndim == 3 and a.shape[-1] <= 4 and a.shape[0] > 4:
+        a = np.moveaxis(a, -1, 0)
+    if a.dtype not in (np.uint8, np.uint16, np.float16, np.float32):
+        a = a.astype(np.float32)
+    if a.shape[0] < nchan:
+        a = np.concatenate([a, np.zeros((nchan - a.shape[0],) + a.shape[1:], a.dtype)], 0)
+    return np.ascontiguousarray(a[:nchan])
 
 
 def mask_png_payload(mask: np.ndarray) -> dict:
@@ -238,9 +256,13 @@ class CellposeFinetune:
         assert out[0]["output"].shape == (128, 128)
 
     # ------------------------------------------------------------------ inference (continuous batching)
-    @serve.batch(max_batch_size=32, batch_wait_timeout_s=0.005)
+    @serve.batch(max_batch_size=32, batch_wait_timeout_s=0.005, max_concurrent_batches=2)
     async def _segment_batch(self, reqs: list) -> list:
-        """reqs: [(model_id, image CHW, params dict, want_flows)] -> [(masks, flows | None)]."""
+        """reqs: [(model_id, image CHW, params dict, want_flows)] -> [(masks, flows | None)].
+
+        Two batches are in flight: while one batch's kernels run (under the GPU lock, on the
+        default stream), the other stacks its images or copies its masks back on a side stream
+        into pinned memory, so host work and PCIe transfers hide behind GPU compute."""
         from bioengine_worker_amd.profiling import trace
 
         out = [None] * len(reqs)
@@ -250,21 +272,45 @@ class CellposeFinetune:
             groups.setdefault(key, []).append(i)
         for (mid, shape, _, prm_items), idxs in groups.items():
             runner = await self._runner(mid)
-            with trace.span("app.stack", images=len(idxs)):
-                batch = np.stack([reqs[i][1] for i in idxs])
             prm = dict(prm_items)
             flows_needed = any(reqs[i][3] for i in idxs)
 
             def run():
+                import torch
+
+                with trace.span("app.stack", images=len(idxs)):
+                    batch = np.stack([reqs[i][1] for i in idxs])
                 with self._gpu_lock:
                     with trace.span("app.eval", images=len(idxs)):
                         m, f, _ = runner.eval(batch, **prm)
-                    with trace.span("app.d2h", images=len(idxs)):
-                        m = m.cpu()
-                        f = f.cpu().numpy() if flows_needed else None  # 12 B/pixel D2H only on request
-                return m.numpy(), f
+                    if m.is_cuda:
+                        # uint16 masks (cellpose's dtype when labels fit): low 16 bits + an overflow
+                        # flag, so the copy-back needs a single host sync
+                        m16 = m.to(torch.int16)
+                        over = (m > 65535).any().reshape(1)
+                        ev = torch.cuda.Event()
+                        ev.record()
+                with trace.span("app.d2h", images=len(idxs)):
+                    if not m.is_cuda:
+                        return m.numpy(), (f.numpy() if flows_needed else None)
+                    if getattr(self, "_d2h_stream", None) is None:
+                        self._d2h_stream = torch.cuda.Stream(m.device)
+                    st = self._d2h_stream
+                    with torch.cuda.stream(st):
+                        st.wait_event(ev)
+                        mh = torch.empty(m.shape, dtype=torch.int16, pin_memory=True)
+                        oh = torch.empty(1, dtype=torch.bool, pin_memory=True)
+                        mh.copy_(m16, non_blocking=True)
+                        oh.copy_(over, non_blocking=True)
+                        fh = f.to("cpu", non_blocking=True) if flows_needed else None
+                        for t in (m, m16, over) + ((f,) if f is not None else ()):
+                            t.record_stream(st)
+                    st.synchronize()
+                    if bool(oh[0]):  # more than 65535 objects in an image: int32 labels
+                        return m.cpu().numpy(), (fh.numpy() if fh is not None else None)
+                    return mh.numpy().view(np.uint16), (fh.numpy() if fh is not None else None)
 
-            masks, flows = await asyncio.to_thread(run)
+            masks, flows = await offload(run)
             for j, i in enumerate(idxs):
                 out[i] = (masks[j], flows[j] if flows is not None and reqs[i][3] else None)
         return out
@@ -321,11 +367,14 @@ class CellposeFinetune:
         runner = await self._runner(model_id)
         prm = {"diameter": _opt(diameter), "flow_threshold": float(flow_threshold),
                "cellprob_threshold": float(cellprob_threshold), "niter": int(_opt(niter) or 200)}
-        chw = [to_chw(im, runner.nchan) for im in images]
-        res = await asyncio.gather(*[self._segment_batch((model_id, c, prm, bool(return_flows))) for c in chw])
+        chw = [image_chw(im, runner.nchan) for im in images]
+        with trace.span("app.batched", images=len(chw)):
+            if len(chw) == 1:
+                res = [await self._segment_batch((model_id, chw[0], prm, bool(return_flows)))]
+            else:
+                res = await asyncio.gather(*[self._segment_batch((model_id, c, prm, bool(return_flows))) for c in chw])
         out = []
         for name, (m, f) in zip(names, res):
-            m = m.astype(np.int32)
             item = {"input_path": name, "output": mask_png_payload(m) if json_safe else m}
             if return_flows:
                 fl = [flow_rgb(f[:2]), f[:2], f[2]]

@@ -8,15 +8,23 @@ idle and the queue is short — so latency at low load stays ~one batch-of-1, an
 load approaches the full-batch rate.  The reference has no cross-request batching at all
 (model-runner runtime ``max_ongoing_requests=1``, ``apps/model-runner/runtime_deployment.py:40``).
 
+With ``max_concurrent_batches=2`` a second batch is dispatched only when a FULL batch is queued, so
+at saturation the host side of one batch overlaps the GPU side of the next while moderate load
+still forms one well-filled batch at a time.
+
 Per-batch statistics (size histogram, queue wait) are kept for router metrics.
 """
 from __future__ import annotations
 
 import asyncio
 import collections
+import contextvars
 import functools
 import inspect
+import os
 import time
+
+_current: contextvars.ContextVar = contextvars.ContextVar("bioengine_batch", default=None)
 
 
 class _BatchQueue:
@@ -53,8 +61,10 @@ class _BatchQueue:
         * Otherwise the previous batch's size: clients whose results just went out are on their way
           back (closed loop), so forming a batch from the one request that slipped in meanwhile
           would alternate 1-image and N-image batches.
-        * A lone client (previous batch of 1, slow arrivals) never waits."""
-        if self.gap_ewma < 0.5 * self.timeout:
+        * A lone client never waits: a closed loop of one client with a fast service also arrives
+          faster than half the timeout, but its batches stay at 1 (open-loop load grows the
+          batch by itself, since requests queue while the device is busy)."""
+        if self.last_batch > 1 and self.gap_ewma < 0.5 * self.timeout:
             return self.max_batch_size
         return min(self.max_batch_size, self.last_batch)
 
@@ -64,6 +74,12 @@ class _BatchQueue:
                 self.event.clear()
                 await self.event.wait()
             await self.sem.acquire()
+            # A second concurrent batch only starts full: it overlaps the running batch's host work
+            # (stacking, D2H, result encoding) at high load, but at moderate load two half-empty
+            # batches would cost more GPU time than one full one.
+            while self.inflight > 0 and len(self.queue) < self.max_batch_size:
+                self.event.clear()
+                await self.event.wait()
             # Device idle and queue short: give stragglers a bounded window to join.
             target = self.fill_target()
             if self.inflight == 0 and len(self.queue) < target and self.timeout > 0:
@@ -99,6 +115,7 @@ class _BatchQueue:
             kw = {}
             for k in items[0][1]:
                 kw[k] = [it[1].get(k) for it in items]
+            tok = _current.set((self, len(items)))
             try:
                 res = self.fn(self.owner, *cols, **kw) if self.owner is not None else self.fn(*cols, **kw)
                 if inspect.isawaitable(res):
@@ -113,9 +130,31 @@ class _BatchQueue:
                 for (_, _, fut, _) in items:
                     if not fut.done():
                         fut.set_exception(e)
+            finally:
+                _current.reset(tok)
         finally:
             self.inflight -= 1
             self.sem.release()
+            self.event.set()  # wake a dispatcher waiting for a full queue or an idle device
+
+
+#: ``BIOENGINE_BATCH_INLINE=0`` always offloads to a thread (A/B switch for :func:`offload`)
+_INLINE = os.environ.get("BIOENGINE_BATCH_INLINE", "1") != "0"
+
+
+async def offload(fn, *args, **kwargs):
+    """Run blocking (GPU) work of a batched function.  A lone request on an idle queue -- batch of
+    one, nothing queued behind it, no other batch in flight -- runs inline on the event loop: the
+    two thread hand-offs of ``asyncio.to_thread`` are the largest serving cost left at concurrency
+    1, and there is nothing for the loop to do meanwhile (a request arriving during the call
+    would wait for the device anyway).  Everything else goes to a worker thread so the loop keeps
+    forming the next batch."""
+    cur = _current.get()
+    if cur is not None and _INLINE:
+        q, n = cur
+        if n == 1 and not q.queue and q.inflight == 1:
+            return fn(*args, **kwargs)
+    return await asyncio.to_thread(fn, *args, **kwargs)
 
 
 def batch(_func=None, *, max_batch_size: int = 10, batch_wait_timeout_s: float = 0.01, max_concurrent_batches: int = 1):

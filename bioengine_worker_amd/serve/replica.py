@@ -200,8 +200,42 @@ def loads(frames: list):
     return pickle.loads(frames[0], buffers=frames[1:])
 
 
-#: out-of-band payloads at least this large travel through the shared-memory ring
-RING_MIN_BYTES = 2 << 20
+#: out-of-band payloads at least this large travel through the shared-memory ring (one memcpy in,
+#: one out) instead of being streamed through the socket buffer in ~200 KB chunks, each chunk a
+#: sender/reader wake-up
+RING_MIN_BYTES = 64 << 10
+#: messages whose socket part is at most this large are sent straight from the event loop (no
+#: worker-thread hop); anything that could block on a full socket or ring goes through a thread
+INLINE_MAX_BYTES = 128 << 10
+
+
+def _ring_bytes(lens) -> int:
+    return sum(8 + ((int(n) + 7) & ~7) for n in lens)
+
+
+def _send_locked(conn, frames, ring) -> None:
+    if ring is not None:
+        ring.write(frames[1:])
+        conn.send(("ring", len(frames)))
+        conn.send_bytes(frames[0])
+        return
+    conn.send(len(frames))
+    for f in frames:
+        conn.send_bytes(f)
+
+
+def _route(frames, ring):
+    """(ring to use or None, bytes that would cross the socket)."""
+    bufs = frames[1:]
+    lens = [b.nbytes for b in bufs]
+    if ring is not None and bufs and sum(lens) >= RING_MIN_BYTES and ring.fits(lens):
+        return ring, len(frames[0]), lens
+    return None, len(frames[0]) + sum(lens), lens
+
+
+def _send_prepared(conn, lock, frames, ring):
+    with lock:
+        _send_locked(conn, frames, ring)
 
 
 def send_frames(conn, lock: threading.Lock, obj, ring=None):
@@ -209,18 +243,27 @@ def send_frames(conn, lock: threading.Lock, obj, ring=None):
     out-of-band buffers go through shared memory and only the pickle header crosses the socket.
     Ring write and socket send happen under the same lock, so both lanes stay in message order."""
     frames = dumps(obj)
-    bufs = frames[1:]
-    with lock:
-        if ring is not None and bufs:
-            lens = [b.nbytes for b in bufs]
-            if sum(lens) >= RING_MIN_BYTES and ring.fits(lens):
-                ring.write(bufs)
-                conn.send(("ring", len(frames)))
-                conn.send_bytes(frames[0])
-                return
-        conn.send(len(frames))
-        for f in frames:
-            conn.send_bytes(f)
+    use, _, _ = _route(frames, ring)
+    _send_prepared(conn, lock, frames, use)
+
+
+async def send_async(conn, lock: threading.Lock, obj, ring=None):
+    """:func:`send_frames` from an event loop.  A message that cannot block -- small socket part
+    and, for ring payloads, room in the ring right now -- is written inline (saves two thread
+    wake-ups per message, the dominant cost of a small request); the rest goes through a thread."""
+    frames = dumps(obj)
+    use, sock_bytes, lens = _route(frames, ring)
+    inline = sock_bytes <= INLINE_MAX_BYTES
+    if inline and use is not None:
+        st = use.stats()
+        inline = st["capacity"] - st["queued_bytes"] >= _ring_bytes(lens)
+    if inline and lock.acquire(blocking=False):
+        try:
+            _send_locked(conn, frames, use)
+        finally:
+            lock.release()
+        return
+    await asyncio.to_thread(_send_prepared, conn, lock, frames, use)
 
 
 def recv_frames(conn, ring=None):
@@ -230,6 +273,11 @@ def recv_frames(conn, ring=None):
         return loads([head] + [ring.read() for _ in range(n[1] - 1)])
     frames = [conn.recv_bytes() for _ in range(n)]
     return loads(frames)
+
+
+def reader_mode() -> str:
+    """``BE_REPLICA_READER``: ``loop`` (default; fd readiness on the event loop) or ``thread``."""
+    return os.environ.get("BE_REPLICA_READER", "loop")
 
 
 def ring_capacity() -> int:
@@ -314,8 +362,14 @@ class ProcessReplica(ReplicaBase):
         for r in (self.tx, self.rx):  # the child opened both before connecting: drop the names
             if r is not None:
                 r.unlink()
-        self._reader = threading.Thread(target=self._read_loop, daemon=True)
-        self._reader.start()
+        if self.rx is not None and reader_mode() == "loop":
+            # bulk payloads ride the ring, so socket messages are small: read them on the event loop
+            # when the fd turns readable (no reader-thread -> loop hand-off per message)
+            self._reader = None
+            self.loop.add_reader(self.conn.fileno(), self._on_readable)
+        else:
+            self._reader = threading.Thread(target=self._read_loop, daemon=True)
+            self._reader.start()
         fut = self.loop.create_future()
         self.pending[0] = fut
         await asyncio.to_thread(send_frames, self.conn, self.send_lock,
@@ -339,6 +393,23 @@ class ProcessReplica(ReplicaBase):
                 msg = ("fatal", repr(e))
             self.loop.call_soon_threadsafe(self._dispatch, msg)
         self.loop.call_soon_threadsafe(self._on_exit)
+
+    def _on_readable(self):
+        try:
+            while self.conn.poll():
+                try:
+                    msg = recv_frames(self.conn, self.rx)
+                except (EOFError, OSError):
+                    raise
+                except Exception as e:  # undecodable result
+                    msg = ("fatal", repr(e))
+                self._dispatch(msg)
+        except (EOFError, OSError):
+            try:
+                self.loop.remove_reader(self.conn.fileno())
+            except (OSError, ValueError):
+                pass
+            self._on_exit()
 
     def _dispatch(self, msg):
         kind = msg[0]
@@ -368,7 +439,7 @@ class ProcessReplica(ReplicaBase):
         except BaseException as e:  # noqa: BLE001
             out = ("hresult", rid, False, e)
         try:
-            await asyncio.to_thread(send_frames, self.conn, self.send_lock, out, self.tx)
+            await send_async(self.conn, self.send_lock, out, self.tx)
         except Exception:
             pass
 
@@ -393,8 +464,8 @@ class ProcessReplica(ReplicaBase):
         self.ongoing += 1
         try:
             with self.inflight.track(method, faults.current_deadline()):
-                await asyncio.to_thread(send_frames, self.conn, self.send_lock,
-                                        ("call", rid, method, args, kwargs, model_id, faults.current_deadline()), self.tx)
+                await send_async(self.conn, self.send_lock,
+                                 ("call", rid, method, args, kwargs, model_id, faults.current_deadline()), self.tx)
                 return await fut
         finally:
             self.ongoing -= 1

@@ -27,12 +27,12 @@ class _ChildRouter:
 
     async def call(self, app, dep, method, args, kwargs, model_id=""):
         from ..runtime import faults as _faults
-        from .replica import send_frames
+        from .replica import send_async
 
         rid = next(self.rids)
         fut = self.loop.create_future()
         self.pending[rid] = fut
-        await asyncio.to_thread(send_frames, self.conn, self.lock, ("hcall", rid, app, dep, method, args, kwargs, model_id,
+        await send_async(self.conn, self.lock, ("hcall", rid, app, dep, method, args, kwargs, model_id,
                                                                     _faults.current_deadline()),
                                 self.ring)
         return await fut
@@ -43,7 +43,7 @@ async def _main():
 
     from . import context as rctx
     from . import controller as ctrl_mod
-    from .replica import _resolve_result, recv_frames, send_frames
+    from .replica import _resolve_result, reader_mode, recv_frames, send_async, send_frames
 
     # GPU replicas run their device work on worker threads that hold the GIL between launches; a
     # 0.5 ms switch interval (default 5 ms) keeps the request reader and event loop responsive
@@ -74,10 +74,10 @@ async def _main():
                 continue
             loop.call_soon_threadsafe(inbox.put_nowait, msg)
 
-    threading.Thread(target=reader, daemon=True).start()
     obj = None
     ctx = None
 
+    from ..profiling import trace
     from ..runtime import faults
     from .replica import builtin_gpu_check
 
@@ -86,7 +86,7 @@ async def _main():
     async def handle_call(rid, method, args, kwargs, model_id, deadline=None):
         # never cancelled in the child: the entry stays until the user code returns
         with faults.deadline_scope(deadline=deadline):
-            with inflight.track(method, deadline):
+            with inflight.track(method, deadline), trace.span(f"child.{method}", cat="replica"):
                 await _handle_call(rid, method, args, kwargs, model_id)
 
     async def _handle_call(rid, method, args, kwargs, model_id):
@@ -120,9 +120,47 @@ async def _main():
             rctx.reset_model_id(mtok)
             rctx.reset_current(tok)
         try:
-            await asyncio.to_thread(send_frames, conn, lock, out, tx)
+            await send_async(conn, lock, out, tx)
         except Exception as e:  # result not picklable
-            await asyncio.to_thread(send_frames, conn, lock, ("result", rid, False, RuntimeError(f"unpicklable result: {e}")), tx)
+            await send_async(conn, lock, ("result", rid, False, RuntimeError(f"unpicklable result: {e}")), tx)
+
+    def dispatch(msg):
+        kind = msg[0]
+        if kind == "call":
+            _, rid, method, args, kwargs, model_id, deadline = msg
+            asyncio.ensure_future(handle_call(rid, method, args, kwargs, model_id, deadline))
+        elif kind == "hresult":
+            _, rid, ok, val = msg
+            fut = router.pending.pop(rid, None)
+            if fut is not None and not fut.done():
+                if ok:
+                    fut.set_result(val)
+                else:
+                    fut.set_exception(val if isinstance(val, BaseException) else RuntimeError(str(val)))
+        else:
+            inbox.put_nowait(msg)
+
+    def on_readable():
+        # bulk payloads ride the ring, so socket messages are small: decode them on the loop as the
+        # fd turns readable and start calls directly (no reader-thread and inbox hand-offs)
+        try:
+            while conn.poll():
+                try:
+                    msg = recv_frames(conn, rx)
+                except (EOFError, OSError):
+                    raise
+                except Exception as e:  # noqa: BLE001
+                    print(f"replica: undecodable message: {e!r}", flush=True)
+                    continue
+                dispatch(msg)
+        except (EOFError, OSError):
+            loop.remove_reader(conn.fileno())
+            inbox.put_nowait(("stop",))
+
+    if rx is not None and reader_mode() == "loop":
+        loop.add_reader(conn.fileno(), on_readable)
+    else:
+        threading.Thread(target=reader, daemon=True).start()
 
     while True:
         msg = await inbox.get()
@@ -154,6 +192,10 @@ async def _main():
         elif kind == "stop":
             break
     try:
+        loop.remove_reader(conn.fileno())
+    except (OSError, ValueError):
+        pass
+    try:
         conn.close()
     except Exception:
         pass
@@ -184,7 +226,21 @@ def main():
     from ..compat import install
 
     install()
-    asyncio.run(_main())
+    prof_path = os.environ.get("BE_REPLICA_PROFILE")  # cProfile of the replica's event-loop thread
+    if not prof_path:
+        asyncio.run(_main())
+        return
+    import cProfile
+    import pstats
+
+    prof = cProfile.Profile()
+    prof.enable()
+    try:
+        asyncio.run(_main())
+    finally:
+        prof.disable()
+        with open(prof_path.replace("{pid}", str(os.getpid())), "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
 
 
 if __name__ == "__main__":
