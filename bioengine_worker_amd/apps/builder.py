@@ -9,7 +9,9 @@ Behavioural parity with the reference builder (``bioengine/apps/builder.py``):
 * actor options rewritten: ``num_gpus=0`` when GPU is disabled, runtime env vars ``HOME``,
   ``TMPDIR``, ``HYPHA_SERVER_URL``, ``HYPHA_WORKSPACE``, ``HYPHA_ARTIFACT_ID``,
   ``BIOENGINE_WORKER_SERVICE_ID`` (``:385-398``), secrets (keys starting with ``_``) masked as
-  ``*****`` until the replica's ``__init__`` (``:381-383,652-654``), pip requirements recorded;
+  ``*****`` until the replica's ``__init__`` (``:381-383,652-654``); ``runtime_env.pip`` pinned
+  (``:345-372``) and satisfied before deployment by :mod:`.requirements` (installed offline from
+  ``BIOENGINE_WHEELHOUSE`` into the app's ``site-packages``, else ``DEPLOY_FAILED`` naming them);
 * lifecycle wrapping (``:532-890``): ``__init__`` (workdir, state flags, ``self.bioengine_datasets``),
   ``async_init`` (once), ``test_deployment`` (background, failure => unhealthy) and
   ``check_health`` (lazy init + test + datasets ping + user check);
@@ -30,6 +32,7 @@ import copy
 import inspect
 import logging
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 from functools import wraps
@@ -41,6 +44,7 @@ import yaml
 
 from ..serve.api import Application, Deployment, deployment as serve_deployment
 from ..utils.artifact_utils import validate_manifest
+from .requirements import update_requirements
 
 SECRET_MASK = "*****"
 
@@ -128,10 +132,23 @@ class AppBuilder:
         from ..compat import install
 
         install()
+        site = self.apps_workdir / application_id / "site-packages"
+        if site.is_dir() and str(site) not in sys.path:  # requirements installed by an earlier deploy
+            from .requirements import _APP_PATHS
+
+            _APP_PATHS.add(str(site))
+            sys.path.insert(0, str(site))
         mod_name = f"bioengine_app_{application_id.replace('-', '_')}_{Path(py).stem}"
         ns: dict[str, Any] = {"__name__": mod_name, "__file__": f"<{artifact_id}/{py}>", "__builtins__": __builtins__}
         ns.update({k: v for k, v in env_vars.items()})
-        exec(compile(code, f"<{artifact_id}/{py}>", "exec"), ns)  # noqa: S102 - app code is the artifact's content
+        try:
+            exec(compile(code, f"<{artifact_id}/{py}>", "exec"), ns)  # noqa: S102 - app code is the artifact's content
+        except ModuleNotFoundError as e:
+            raise ModuleNotFoundError(
+                f"'{py}' of artifact '{artifact_id}' imports '{e.name}' at module level, which is not installed on "
+                f"this worker. Import it inside the deployment's methods and list it in "
+                f"ray_actor_options.runtime_env.pip (installed from BIOENGINE_WHEELHOUSE at deploy time).",
+                name=e.name) from e
         obj = ns.get(class_name)
         if obj is None:
             raise ValueError(f"Class '{class_name}' not found in '{py}' of artifact '{artifact_id}'")
@@ -173,6 +190,13 @@ class AppBuilder:
             envv[k] = SECRET_MASK
         if hypha_token:
             envv["HYPHA_TOKEN"] = SECRET_MASK
+        pip = [str(r) for r in (rt.get("pip") or [])]
+        if pip:
+            # pinned like the reference (worker's httpx/pydantic added, >=/~= -> ==); resolved and, if
+            # needed, installed from the wheelhouse into the app's site-packages before deployment
+            rt["pip"] = update_requirements(pip)
+            site = str(workdir / "site-packages")
+            envv["PYTHONPATH"] = site + (os.pathsep + envv["PYTHONPATH"] if envv.get("PYTHONPATH") else "")
         rt["env_vars"] = envv
         opts["runtime_env"] = rt
         return opts
@@ -360,6 +384,11 @@ class AppBuilder:
         ekw = dict(application_kwargs.get(user_entry_cls.__name__) or {})
         self.validate_kwargs(user_entry_cls, ekw, set(handles))
         root = entry.bind(**ekw, **handles)
+        pip_reqs: list[str] = []
+        for _, d in deps:
+            for r in ((d.ray_actor_options or {}).get("runtime_env") or {}).get("pip") or []:
+                if r not in pip_reqs:
+                    pip_reqs.append(r)
         resources = {"num_cpus": 0.0, "num_gpus": 0.0, "memory": 0.0}
         for _, d in deps:
             lo, _, init = d.config.min_max_replicas()
@@ -381,6 +410,7 @@ class AppBuilder:
             "last_updated_by": last_updated_by, "auto_redeploy": auto_redeploy, "debug": debug,
             "frontend_entry": manifest.get("frontend_entry"), "ice_servers": ice_servers,
             "deployments": [ip for ip in paths], "hypha_token_set": bool(hypha_token),
+            "pip_requirements": pip_reqs,
         }
         self.log.info(f"Built application '{application_id}' from '{artifact_id}' (version {version}); "
                       f"methods: {meta['available_methods']}")

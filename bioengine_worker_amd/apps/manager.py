@@ -165,6 +165,14 @@ class AppsManager:
         rec = self.apps[aid]
         built = rec["built"]
         try:
+            reqs = built.metadata.get("pip_requirements") or []
+            if reqs:
+                from . import requirements
+
+                rec["message"] = f"Resolving pip requirements {reqs}"
+                rec["pip"] = await asyncio.to_thread(requirements.ensure, reqs,
+                                                     self.builder.apps_workdir / aid / "site-packages")
+                rec["message"] = ""
             handle = await self.controller.deploy_application(built.root, name=aid, route_prefix=f"/{aid}")
             bridge = AppServiceBridge(aid, built, handle, self.server_url, self.token,
                                       self.server.config.workspace, self.server.config.client_id, self.log)
