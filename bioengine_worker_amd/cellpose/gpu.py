@@ -7,10 +7,10 @@ per-mask job lists).  The semantics are those of :mod:`bioengine_worker_amd.cell
 """
 from __future__ import annotations
 
-import numpy as np
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 from ..ops import _native
@@ -132,26 +132,60 @@ def _jobs_tensor(b, lab, y0, x0, ly, lx, scratch) -> torch.Tensor:
     return torch.stack([w0, w1, w2, scratch.long()], 1).contiguous()
 
 
-def _split_jobs(bbox_valid, labs_b, labs_l, lds_elems_fn, lds_budget, scratch_elems_fn):
-    """Returns (small_jobs, big_jobs, scratch_size) for masks given their bboxes."""
+def _plan_jobs(bbox_valid, labs_b, labs_l, lds_fn, caps, scratch_fn, valid=None):
+    """Bucket masks by their LDS need with ONE host sync.
+
+    Bucket k < len(caps) holds masks with caps[k-1] < need <= caps[k]; bucket len(caps) holds the
+    masks too big for LDS, which get scratch offsets.  Jobs are sorted by bucket on the device and
+    only the per-bucket counts (+ the scratch total) come back to the host, so the slices below
+    are views -- replacing one boolean-index gather (a nonzero + sync, ~75 us) per field and bucket.
+    ``valid`` (optional bool per row) drops rows without a separate nonzero (and its sync).
+    Returns ``(jobs_by_bucket: list of [n_k, 4] int64 views, scratch_total)``."""
     y0, y1, x0, x1 = bbox_valid.unbind(1)
     ly, lx = y1 - y0 + 1, x1 - x0 + 1
-    need = lds_elems_fn(ly, lx)
-    small = need <= lds_budget
+    need = lds_fn(ly, lx)
     dev = bbox_valid.device
-    sj = _jobs_tensor(labs_b[small], labs_l[small], y0[small], x0[small], ly[small], lx[small],
-                      torch.full((int(small.sum()),), -1, dtype=torch.long, device=dev))
-    big = ~small
-    nb = int(big.sum())
-    if nb:
-        sz = scratch_elems_fn(ly[big], lx[big])
-        off = torch.cumsum(sz, 0) - sz
-        bj = _jobs_tensor(labs_b[big], labs_l[big], y0[big], x0[big], ly[big], lx[big], off)
-        total = int(sz.sum())
-    else:
-        bj = sj[:0]
-        total = 0
-    return sj, bj, total
+    edges = torch.tensor(caps, dtype=need.dtype, device=dev)
+    bucket = torch.bucketize(need, edges)  # need <= caps[k]  ->  k
+    nb = len(caps) + 1
+    if valid is not None:
+        bucket = torch.where(valid, bucket, torch.full_like(bucket, nb))  # dropped rows sort last
+    order = torch.argsort(bucket, stable=True)
+    counts = torch.bincount(bucket, minlength=nb + 1)[:nb]
+    big = bucket[order] == len(caps)
+    ly_s, lx_s = ly[order], lx[order]
+    sz = torch.where(big, scratch_fn(ly_s, lx_s), torch.zeros_like(ly_s)).long()
+    off = torch.cumsum(sz, 0) - sz
+    scr = torch.where(big, off, torch.full_like(off, -1))
+    jobs = _jobs_tensor(labs_b[order], labs_l[order], y0[order], x0[order], ly_s, lx_s, scr)
+    host = torch.cat([counts.long(), sz.sum().view(1)]).cpu().tolist()  # the one sync
+    out, start = [], 0
+    for k in range(nb):
+        out.append(jobs[start:start + host[k]])
+        start += host[k]
+    return out, int(host[nb])
+
+
+def _plan_masks(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps):
+    """Device-side :func:`_plan_jobs` (one ``be_cp_plan_masks`` launch + one host sync): returns
+    ``(jobs_by_bucket, scratch_total, niter_img)``; ``kind`` 0 = diffusion (LDS need / scratch of
+    :func:`_diffuse_lds_bytes` / :func:`_diffuse_scratch_doubles`, and cellpose's per-image
+    ``niter_img``), 1 = hole filling (``R`` bytes).  Job order inside a bucket is arbitrary."""
+    B, nlab = bbox.shape[:2]
+    dev = bbox.device
+    n = B * nlab
+    nb = len(caps) + 1
+    jobs = torch.empty(nb, max(n, 1), 4, dtype=torch.int64, device=dev)
+    counts = torch.zeros(nb, dtype=torch.int32, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    niter_img = torch.zeros(B, dtype=torch.int32, device=dev)
+    carr = (ctypes.c_int * max(1, len(caps)))(*[int(c) for c in caps])
+    vptr = _native.ptr(valid.contiguous().view(torch.uint8)) if valid is not None else None
+    _native.call("be_cp_plan_masks", _native.ptr(bbox.contiguous()), vptr, B, nlab, kind, ctypes.addressof(carr),
+                 len(caps), _native.ptr(jobs), _native.ptr(counts), _native.ptr(tot), _native.ptr(niter_img),
+                 _native.stream(dev))
+    host = torch.cat([counts.long(), tot]).cpu().tolist()  # the one sync
+    return [jobs[k, :host[k]] for k in range(nb)], int(host[nb]), niter_img
 
 
 def _diffuse_lds_bytes(ly, lx):
@@ -168,6 +202,17 @@ def _diffuse_scratch_doubles(ly, lx):
 #: bucket's LDS, so small masks run many blocks per CU (one 48 KiB reservation per mask allowed 3).
 DIFFUSE_BUCKETS = ((6 * 1024, 64), (12 * 1024, 128), (24 * 1024, 256), (48 * 1024, 256), (80 * 1024, 512),
                    (LDS_DIFFUSE_BYTES, 512))
+#: rows per work item of the diffusion sweep (``BE_DIFFUSE_DV``): a smaller DV gives every mask
+#: proportionally more threads (buckets scale up to 1024) and a shorter serial LDS chain per sweep
+DIFFUSE_DV = 4
+
+
+def _diffuse_dv() -> int:
+    return int(os.environ.get("BE_DIFFUSE_DV", DIFFUSE_DV))
+
+
+def _diffuse_buckets(dv: int):
+    return tuple((cap, min(1024, t * (8 // dv))) for cap, t in DIFFUSE_BUCKETS)
 
 
 _DEBUG_STATS = os.environ.get("BIOENGINE_MASK_STATS", "0") == "1"
@@ -189,33 +234,31 @@ def _side_streams(dev):
     return _SIDE_STREAMS[key]
 
 
-def _bucket_small(sj):
-    """Split the one-workgroup diffusion jobs into LDS buckets (host sync happens here, before any
-    diffusion kernel is queued)."""
-    w2 = sj[:, 2]
-    need = _diffuse_lds_bytes(w2 & 0xFFFFFFFF, w2 >> 32)
-    if _DEBUG_STATS:
-        print(f"[diffuse_small] masks={sj.shape[0]} mean_area_box={float(((w2 & 0xFFFFFFFF) * (w2 >> 32)).float().mean()):.0f} "
-              f"buckets={[int(((need > a) & (need <= b[0])).sum()) for a, b in zip((0,) + tuple(c for c, _ in DIFFUSE_BUCKETS), DIFFUSE_BUCKETS)]}",
-              flush=True)
+def _bucket_small(slices):
+    """(bucket index, LDS cap, threads, jobs) of the non-empty one-workgroup buckets, largest first
+    (they set the critical path)."""
     out = []
-    lo = 0
-    for i, (cap, threads) in enumerate(DIFFUSE_BUCKETS):
-        jobs = sj[(need > lo) & (need <= cap)].contiguous()
-        lo = cap
-        if jobs.shape[0]:
-            out.append((i, cap, threads, jobs))
-    return out[::-1]  # largest masks first: they set the critical path
+    for i, (cap, threads) in enumerate(_diffuse_buckets(_diffuse_dv())):
+        if slices[i].shape[0]:
+            out.append((i, cap, threads, slices[i]))
+    if _DEBUG_STATS:
+        print(f"[diffuse_small] buckets={[int(x.shape[0]) for x in slices[:-1]]} big={int(slices[-1].shape[0])}", flush=True)
+    return out[::-1]
 
 
-def _diffuse_small(Mc, buckets, niter_img, L, st) -> None:
+def _diffuse_small(Mc, buckets, niter_img, L, st, ready=None) -> None:
+    """``ready``: event recorded on the current stream once the inputs exist; the buckets start
+    from it instead of from the stream's tail, so they run alongside the big-mask kernel."""
     B, H, W = Mc.shape
     concurrent = Mc.is_cuda and N_SIDE_STREAMS > 0
     if concurrent:
         main = torch.cuda.current_stream(Mc.device)
         sides = _side_streams(Mc.device)
         for sd in sides:
-            sd.wait_stream(main)
+            if ready is not None:
+                sd.wait_event(ready)
+            else:
+                sd.wait_stream(main)
     for i, cap, threads, jobs in buckets:
         if concurrent:
             sd = sides[i % len(sides)]
@@ -225,7 +268,7 @@ def _diffuse_small(Mc, buckets, niter_img, L, st) -> None:
         else:
             sptr = st
         _native.call("be_cp_diffuse_nt", _native.ptr(Mc), _native.ptr(jobs), jobs.shape[0], H, W,
-                     _native.ptr(niter_img), _native.ptr(L), cap, threads, sptr)
+                     _native.ptr(niter_img), _native.ptr(L), cap, threads, _diffuse_dv(), sptr)
     if concurrent:
         for sd in sides:
             main.wait_stream(sd)
@@ -299,7 +342,8 @@ def mask_bboxes(M: torch.Tensor, nlab: int) -> torch.Tensor:
     return bbox
 
 
-def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: int | None = None):
+def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: int | None = None,
+                       nlab: int | None = None):
     """Heat-diffusion flows of label images M [B, H, W] int32 (labels 1..n, contiguous per image).
 
     Returns (mu [B, 2, H, W] fp32, err_sum [B, nlab] fp32 or None, counts [B, nlab]).  When ``dp``
@@ -307,30 +351,34 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
     """
     B, H, W = M.shape
     dev = M.device
-    nlab = int(M.max().item()) + 1 if M.numel() else 1
+    if nlab is None:  # an upper bound on the labels + 1 is enough (absent labels have no pixels)
+        nlab = int(M.max().item()) + 1 if M.numel() else 1
     mu = torch.zeros(B, 2, H, W, dtype=torch.float32, device=dev)
     counts = label_counts(M, nlab)
     if nlab <= 1:
         return mu, (torch.zeros(B, nlab, device=dev) if dp is not None else None), counts
     bbox = mask_bboxes(M, nlab)
-    present = bbox[..., 1] >= 0
-    present[:, 0] = False
-    ext = (bbox[..., 1] - bbox[..., 0] + bbox[..., 3] - bbox[..., 2] + 4).clamp(min=0) * present
-    niter_img = (2 * ext.max(dim=1).values).to(torch.int32) if niter is None else torch.full((B,), niter, dtype=torch.int32, device=dev)
-    idx = present.nonzero()
-    labs_b, labs_l = idx[:, 0].int(), idx[:, 1].int()
-    bb = bbox[idx[:, 0], idx[:, 1]]
-    sj, bj, ssize = _split_jobs(bb, labs_b, labs_l, _diffuse_lds_bytes, LDS_DIFFUSE_BYTES, _diffuse_scratch_doubles)
+    slices, ssize, niter_img = _plan_masks(bbox, None, 0, [c for c, _ in DIFFUSE_BUCKETS])
+    if niter is not None:
+        niter_img = torch.full((B,), niter, dtype=torch.int32, device=dev)
+    bj = slices[-1]
     L = torch.zeros(B, H, W, dtype=torch.float64, device=dev)
     scratch = torch.empty(max(ssize, 1), dtype=torch.float64, device=dev)
     st = _native.stream(dev)
     Mc = M.contiguous()
-    buckets = _bucket_small(sj) if sj.shape[0] else []
+    buckets = _bucket_small(slices)
     ws = None
-    if bj.shape[0]:  # first: its cooperative grid must be co-resident, so it goes in on an idle device
+    ready = None
+    if bj.shape[0] and Mc.is_cuda and buckets:
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(dev))
+    if bj.shape[0]:
+        # first, on an idle device: its few cooperative workgroups are all resident before the
+        # bucket kernels (which never wait on it) fill the remaining CUs, so its grid barrier
+        # cannot starve; it then runs alongside the buckets instead of ~1 ms alone on ~24 CUs
         ws = _diffuse_big(Mc, bj, niter_img, scratch, L, st)
     if buckets:
-        _diffuse_small(Mc, buckets, niter_img, L, st)
+        _diffuse_small(Mc, buckets, niter_img, L, st, ready=ready)
     err = None
     dpp = None
     bstride = 0
@@ -353,10 +401,12 @@ def _renumber(M: torch.Tensor, keep: torch.Tensor) -> torch.Tensor:
     return torch.gather(lut, 1, M.reshape(B, -1).long()).reshape(M.shape).to(torch.int32)
 
 
-def fill_holes_gpu(M: torch.Tensor, min_size: int = 15) -> torch.Tensor:
+def fill_holes_gpu(M: torch.Tensor, min_size: int = 15, nlab: int | None = None) -> torch.Tensor:
+    """``nlab``: optional upper bound on the labels + 1 (saves the host sync on ``M.max()``)."""
     B, H, W = M.shape
     dev = M.device
-    nlab = int(M.max().item()) + 1 if M.numel() else 1
+    if nlab is None:
+        nlab = int(M.max().item()) + 1 if M.numel() else 1
     if nlab <= 1:
         return M.clone()
     counts = label_counts(M, nlab)
@@ -366,13 +416,10 @@ def fill_holes_gpu(M: torch.Tensor, min_size: int = 15) -> torch.Tensor:
     keep[:, 0] = False
     lut = (torch.cumsum(keep.int(), dim=1) * keep.int()).to(torch.int32).contiguous()
     bbox = mask_bboxes(M, nlab)
-    idx = keep.nonzero()
     out = torch.zeros_like(M)
-    if idx.shape[0] == 0:
+    (sj, bj), ssize, _ = _plan_masks(bbox, keep, 1, [LDS_FILL_BYTES])
+    if sj.shape[0] + bj.shape[0] == 0:
         return out
-    bb = bbox[idx[:, 0], idx[:, 1]]
-    sj, bj, ssize = _split_jobs(bb, idx[:, 0].int(), idx[:, 1].int(), lambda ly, lx: (ly + 2) * (lx + 2),
-                                LDS_FILL_BYTES, lambda ly, lx: (ly + 2) * (lx + 2))
     scratch = torch.empty(max(ssize, 1), dtype=torch.uint8, device=dev)
     st = _native.stream(dev)
     Mc = M.contiguous()
@@ -405,14 +452,16 @@ def follow_and_label(y: torch.Tensor, niter: int = 200, cellprob_threshold: floa
     keys = torch.full((B, cap), torch.iinfo(torch.int64).max, dtype=torch.int64, device=dev)
     nseeds = torch.zeros(B, dtype=torch.int32, device=dev)
     _native.call("be_cp_seeds", _native.ptr(hist), B, Hp, Wp, _native.ptr(keys), _native.ptr(nseeds), cap, st)
-    keys_sorted, _ = torch.sort(keys, dim=1)
-    kmax = int(nseeds.max().item()) if B else 0  # host sync: sizes the expansion grid
+    kmax = int(nseeds.max().item()) if B else 0  # host sync: sizes the sort and the expansion grid
     kmax = min(kmax, cap)
     M1 = torch.zeros(B, Hp, Wp, dtype=torch.int32, device=dev)
     M0 = torch.zeros(B, H, W, dtype=torch.int32, device=dev)
     if kmax == 0:
         return M0
-    _native.call("be_cp_expand", _native.ptr(hist), _native.ptr(keys_sorted), _native.ptr(nseeds), B, Hp, Wp, cap, kmax,
+    # seeds are compacted at the front of each row: sort only the first kmax slots (a few hundred)
+    # instead of the whole cap-wide buffer of sentinels
+    keys_sorted, _ = torch.sort(keys[:, :kmax].contiguous(), dim=1)
+    _native.call("be_cp_expand", _native.ptr(hist), _native.ptr(keys_sorted), _native.ptr(nseeds), B, Hp, Wp, kmax, kmax,
                  _native.ptr(M1), st)
     nlab = kmax + 1
     counts = torch.zeros(B, nlab, dtype=torch.int32, device=dev)
@@ -427,9 +476,10 @@ def compute_masks_gpu(y: torch.Tensor, niter: int = 200, cellprob_threshold: flo
                       min_size: int = 15, max_size_fraction: float = 0.4) -> torch.Tensor:
     """Full Cellpose mask recovery for a batch: y [B, 3, H, W] -> masks [B, H, W] int32."""
     M = follow_and_label(y, niter, cellprob_threshold, max_size_fraction)
-    if flow_threshold is not None and flow_threshold > 0 and int(M.max().item()) > 0:
-        _, err, counts = masks_to_flows_gpu(M, dp=y)
+    nlab = int(M.max().item()) + 1 if M.numel() else 1  # the one label-count sync; QC only removes labels
+    if flow_threshold is not None and flow_threshold > 0 and nlab > 1:
+        _, err, counts = masks_to_flows_gpu(M, dp=y, nlab=nlab)
         merr = err / counts.clamp(min=1).float()
         keep = (counts > 0) & ~(merr > flow_threshold)
         M = _renumber(M, keep)
-    return fill_holes_gpu(M, min_size)
+    return fill_holes_gpu(M, min_size, nlab=nlab)

@@ -9,27 +9,49 @@
 // exceeds the LDS budget are tiled across many workgroups with time-blocked sweeps and a grid
 // barrier per block of iterations (diffuse_tiled_kernel).  Centres are exact medians from
 // row/column histograms in LDS, ties broken in raster order with a 64-bit atomicMin key.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
 
 constexpr int MT = 256;
+constexpr int kDiffuseVariant = 0;
+
+// Run-length scans: one thread walks RL consecutive pixels of one row and issues its atomics once
+// per run of equal labels instead of once per pixel (labels come in long horizontal runs, so this
+// is ~RL x fewer atomics on the same few hundred counters).
+constexpr int RL = 16;
 
 // bbox[b, lab] = (ymin, ymax, xmin, xmax); init (INT_MAX, -1, INT_MAX, -1) by the caller.
 __global__ __launch_bounds__(256) void bbox_kernel(const int* __restrict__ M, int B, int H, int W, int nlab,
                                                    int* __restrict__ bbox) {
+  const int segs = (W + RL - 1) / RL;
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int HW = H * W;
-  if (gid >= (long long)B * HW) return;
-  const int lab = M[gid];
-  if (lab <= 0) return;
-  const int b = (int)(gid / HW), p = (int)(gid % HW);
-  const int y = p / W, x = p % W;
-  int* bb = bbox + ((size_t)b * nlab + lab) * 4;
-  atomicMin(bb + 0, y);
-  atomicMax(bb + 1, y);
-  atomicMin(bb + 2, x);
-  atomicMax(bb + 3, x);
+  if (gid >= (long long)B * H * segs) return;
+  const int seg = (int)(gid % segs);
+  const long long row = gid / segs;  // b * H + y
+  const int b = (int)(row / H), y = (int)(row % H);
+  const int* Mr = M + row * W;
+  const int x0 = seg * RL, x1 = min(x0 + RL, W);
+  int cur = 0, xs = x0;
+  auto flush = [&](int lab, int a, int e) {
+    if (lab <= 0) return;
+    int* bb = bbox + ((size_t)b * nlab + lab) * 4;
+    atomicMin(bb + 0, y);
+    atomicMax(bb + 1, y);
+    atomicMin(bb + 2, a);
+    atomicMax(bb + 3, e);
+  };
+  for (int x = x0; x < x1; ++x) {
+    const int lab = Mr[x];
+    if (lab != cur) {
+      flush(cur, xs, x - 1);
+      cur = lab;
+      xs = x;
+    }
+  }
+  flush(cur, xs, x1 - 1);
 }
 
 struct MaskJob {
@@ -41,10 +63,11 @@ struct MaskJob {
 // The heat field spans hundreds of orders of magnitude far from the centre of large masks (T decays
 // like exp(-d^2/t)); cellpose runs it in float64 for that reason and so do we (gfx950 runs fp64 VALU
 // at full vector rate, and this kernel is latency/LDS bound anyway).
-template <bool USE_LDS, int MT = 256>
+template <bool USE_LDS, int MT = 256, int DV = 8>
 __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs, int H,
                                                      int W, const int* __restrict__ niter_img, double* __restrict__ scratch,
-                                                     double* __restrict__ Lout, int* __restrict__ centers_out) {
+                                                     double* __restrict__ Lout, int* __restrict__ centers_out,
+                                                     int variant = 0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const MaskJob J = jobs[blockIdx.x];
   const int RY = J.ly + 2, RX = J.lx + 2, R = RY * RX;
@@ -120,12 +143,73 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
   // Column-segment register blocking: a work item is DV consecutive rows of one column; the three
   // horizontal 3-sums it needs per row are formed once and slid down the segment, so a cell costs
   // ~3 reads instead of 9.  Non-mask cells hold 0 in both buffers, so neighbour reads need no mask.
-  constexpr int DV = 8;
   const int nseg = (RY - 2 + DV - 1) / DV;
   const int nitems = (RX - 2) * nseg;
   double* cur = T0;
   double* nxt = T1;
-  for (int it = 0; it < niter; ++it) {
+  if (USE_LDS && variant == 2) {
+    // One barrier per sweep: the centre source is folded into the sweep (T' = A (T + e_c) adds 1
+    // to the 9-sums of the centre's 3x3 neighbourhood) instead of a separate write + barrier, and
+    // a work item loads all DV+2 row sums of its segment at once (independent ds_reads in flight
+    // instead of a DV-deep dependent chain).  Rows past the box clamp to its last (all-zero) ring
+    // row, so every read stays inside T.
+    const int cy = ce / RX, cx = ce % RX;
+    for (int it = 0; it < niter; ++it) {
+      for (int w = tid; w < nitems; w += MT) {
+        const int x = 1 + w % (RX - 2);
+        const int y0 = 1 + (w / (RX - 2)) * DV;
+        const int nrow = RY - 1 - y0;  // >= 1 rows of this segment lie inside the box
+        const double* c = cur + (y0 - 1) * RX + x;
+        double h[DV + 2];
+#pragma unroll
+        for (int r = 0; r < DV + 2; ++r) {
+          const double* cr = c + min(r, nrow + 1) * RX;
+          h[r] = cr[-1] + cr[0] + cr[1];
+        }
+        const bool nearx = x - cx <= 1 && cx - x <= 1;
+#pragma unroll
+        for (int r = 0; r < DV; ++r) {
+          if (r < nrow) {
+            const int y = y0 + r;
+            const int e = y * RX + x;
+            double sum = h[r] + h[r + 1] + h[r + 2];
+            if (nearx && y - cy <= 1 && cy - y <= 1) sum += 1.0;
+            nxt[e] = inm[e] ? sum * (1.0 / 9.0) : 0.0;
+          }
+        }
+      }
+      __syncthreads();
+      double* t = cur; cur = nxt; nxt = t;
+    }
+  }
+  if (USE_LDS && variant == 1) {  // sliding-window sweep with the centre source folded in: one barrier
+    const int cy = ce / RX, cx = ce % RX;
+    for (int it = 0; it < niter; ++it) {
+      for (int w = tid; w < nitems; w += MT) {
+        const int x = 1 + w % (RX - 2);
+        const int y0 = 1 + (w / (RX - 2)) * DV;
+        const int y1 = min(y0 + DV, RY - 1);
+        const bool nearx = x - cx <= 1 && cx - x <= 1;
+        const double* c = cur + (y0 - 1) * RX + x;
+        double hp = c[-1] + c[0] + c[1];
+        c += RX;
+        double hc = c[-1] + c[0] + c[1];
+        for (int y = y0; y < y1; ++y) {
+          c += RX;
+          const double hn = c[-1] + c[0] + c[1];
+          const int e = y * RX + x;
+          double sum = hp + hc + hn;
+          if (nearx && y - cy <= 1 && cy - y <= 1) sum += 1.0;
+          nxt[e] = inm[e] ? sum * (1.0 / 9.0) : 0.0;
+          hp = hc;
+          hc = hn;
+        }
+      }
+      __syncthreads();
+      double* t = cur; cur = nxt; nxt = t;
+    }
+  }
+  for (int it = 0; (USE_LDS && variant != 0) ? false : it < niter; ++it) {
     if (tid == 0) cur[ce] += 1.0;
     __syncthreads();
     for (int w = tid; w < nitems; w += MT) {
@@ -250,22 +334,27 @@ __global__ __launch_bounds__(MT) void diffuse_tiled_kernel(const int* __restrict
       const int x = tid & (DT_RG - 1);
       const int sr0 = (tid / DT_RG) * (DT_RG * DT_RG / MT);
       const bool xl = x > 0, xr = x < DT_RG - 1;
+      // centre source folded into the sweep (see diffuse_kernel): one barrier per step, and all
+      // row sums of a thread's column segment are loaded before any is used
+      constexpr int SEG = DT_RG * DT_RG / MT;
+      const bool nearx = x - cx <= 1 && cx - x <= 1;
+      (void)cl;
       for (int s = 0; s < steps; ++s) {
-        if (tid == 0 && cl >= 0) a[cl] += 1.0;
-        __syncthreads();
         auto hsum = [&](int r) -> double {
           if (r < 0 || r >= DT_RG) return 0.0;
           const double* c = a + r * DT_RG + x;
           return (xl ? c[-1] : 0.0) + c[0] + (xr ? c[1] : 0.0);
         };
-        double hp = hsum(sr0 - 1), hc = hsum(sr0);
-#pragma unroll 4
-        for (int i = 0; i < DT_RG * DT_RG / MT; ++i) {
-          const double hn = hsum(sr0 + i + 1);
-          const int q = (sr0 + i) * DT_RG + x;
-          b[q] = mk[q] ? (hp + hc + hn) * (1.0 / 9.0) : 0.0;
-          hp = hc;
-          hc = hn;
+        double h[SEG + 2];
+#pragma unroll
+        for (int i = 0; i < SEG + 2; ++i) h[i] = hsum(sr0 - 1 + i);
+#pragma unroll
+        for (int i = 0; i < SEG; ++i) {
+          const int y = sr0 + i;
+          const int q = y * DT_RG + x;
+          double sum = h[i] + h[i + 1] + h[i + 2];
+          if (nearx && y - cy <= 1 && cy - y <= 1) sum += 1.0;
+          b[q] = mk[q] ? sum * (1.0 / 9.0) : 0.0;
         }
         __syncthreads();
         double* tmp = a; a = b; b = tmp;
@@ -380,12 +469,32 @@ __global__ __launch_bounds__(MT) void fill_holes_kernel(const int* __restrict__ 
   }
 }
 
+// LDS variant with a block size matched to the masks (the launcher buckets small masks by their
+// LDS need, so a 20x20 mask no longer reserves the 48 KiB of the largest one).  dv = rows per work
+// item of the sliding-window sweep: 4 gives each mask twice the lanes and half the serial LDS
+// chain per iteration of 8 (the sweep is latency-bound: SQ_WAIT_ANY 45-67 % of wave cycles).
+template <int T, int DV>
+static void launch_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, double* Lout,
+                              int lds_bytes, int variant, hipStream_t s) {
+  if (lds_bytes > 64 * 1024) {  // > 64 KiB of dynamic LDS (up to the 160 KiB of a CU) needs the opt-in
+    static int attr = 0;
+    if (attr < lds_bytes) {
+      const hipError_t ae = hipFuncSetAttribute(reinterpret_cast<const void*>(diffuse_kernel<true, T, DV>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+      if (ae != hipSuccess) fprintf(stderr, "be_cp_diffuse_nt: hipFuncSetAttribute(%d): %s\n", lds_bytes, hipGetErrorString(ae));
+      attr = lds_bytes;
+    }
+  }
+  hipLaunchKernelGGL((diffuse_kernel<true, T, DV>), dim3(njobs), dim3(T), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
+                     niter_img, nullptr, Lout, nullptr, variant);
+}
+
 }  // namespace
 
 extern "C" {
 
 int be_cp_bbox(const int* M, int B, int H, int W, int nlab, int* bbox, hipStream_t s) {
-  const long long n = (long long)B * H * W;
+  const long long n = (long long)B * H * ((W + RL - 1) / RL);
   hipLaunchKernelGGL(bbox_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, B, H, W, nlab, bbox);
   return BE_CHECK_LAUNCH();
 }
@@ -403,44 +512,27 @@ int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const
   return BE_CHECK_LAUNCH();
 }
 
-// LDS variant with a block size matched to the masks (the launcher buckets small masks by their
-// LDS need, so a 20x20 mask no longer reserves the 48 KiB of the largest one — 3 blocks/CU — and
-// runs one wave instead of four mostly idle ones).
 int be_cp_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, double* Lout,
-                     int lds_bytes, int threads, hipStream_t s) {
+                     int lds_bytes, int threads, int dv, hipStream_t s) {
   if (njobs == 0) return 0;
   if (lds_bytes <= 0) return -1;
-  switch (threads) {
-    case 64:
-      hipLaunchKernelGGL((diffuse_kernel<true, 64>), dim3(njobs), dim3(64), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
-                         niter_img, nullptr, Lout, nullptr);
-      break;
-    case 128:
-      hipLaunchKernelGGL((diffuse_kernel<true, 128>), dim3(njobs), dim3(128), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
-                         niter_img, nullptr, Lout, nullptr);
-      break;
-    case 256:
-      hipLaunchKernelGGL((diffuse_kernel<true, 256>), dim3(njobs), dim3(256), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
-                         niter_img, nullptr, Lout, nullptr);
-      break;
-    case 512: {
-      static int attr_set = 0;
-      if (!attr_set) {  // > 64 KiB of dynamic LDS (up to the 160 KiB of a CU) needs the opt-in
-        const hipError_t ae = hipFuncSetAttribute(reinterpret_cast<const void*>(diffuse_kernel<true, 512>),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-        if (ae != hipSuccess) fprintf(stderr, "be_cp_diffuse_nt: hipFuncSetAttribute(%d): %s\n", lds_bytes, hipGetErrorString(ae));
-        attr_set = 1;
-      }
-      hipLaunchKernelGGL((diffuse_kernel<true, 512>), dim3(njobs), dim3(512), lds_bytes, s, M, (const MaskJob*)jobs, H, W,
-                         niter_img, nullptr, Lout, nullptr);
-      break;
-    }
-    default:
-      return -2;
-  }
+  // sweep variant (A/B switch, read per call): 0 = source write + 2 barriers per iteration,
+  // 1 = source folded into the sliding-window sweep, 2 = folded + all row loads issued together
+  const char* ev = getenv("BE_DIFFUSE_VARIANT");
+  const int variant = ev ? atoi(ev) : kDiffuseVariant;
+#define BE_DNT(T, D)                                                                                   \
+  if (threads == T && dv == D) {                                                                     \
+    launch_diffuse_nt<T, D>(M, jobs, njobs, H, W, niter_img, Lout, lds_bytes, variant, s);           \
+  } else
+  BE_DNT(64, 8) BE_DNT(128, 8) BE_DNT(256, 8) BE_DNT(512, 8) BE_DNT(1024, 8)
+  BE_DNT(64, 4) BE_DNT(128, 4) BE_DNT(256, 4) BE_DNT(512, 4) BE_DNT(1024, 4)
+  BE_DNT(64, 2) BE_DNT(128, 2) BE_DNT(256, 2) BE_DNT(512, 2) BE_DNT(1024, 2)
+  return -2;
+#undef BE_DNT
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)
-    fprintf(stderr, "be_cp_diffuse_nt(njobs=%d, lds=%d, threads=%d): %s\n", njobs, lds_bytes, threads, hipGetErrorString(e));
+    fprintf(stderr, "be_cp_diffuse_nt(njobs=%d, lds=%d, threads=%d, dv=%d): %s\n", njobs, lds_bytes, threads, dv,
+            hipGetErrorString(e));
   return (int)e;
 }
 
@@ -509,24 +601,110 @@ int be_cp_fill_holes(const int* M, const void* jobs, int njobs, int H, int W, co
 
 int be_cp_mask_job_bytes() { return (int)sizeof(MaskJob); }
 
+// Job planning for the per-mask kernels in one launch (replaces ~80 small torch ops and their host
+// gaps): every (image, label) with a box and (optional) valid[] flag computes its LDS need,
+// picks the first bucket with caps[k] >= need (k = ncap: too big for LDS -> scratch offset from
+// an atomic cursor), and appends its MaskJob to jobs[k][slot].  kind 0 = diffusion (need =
+// 16R + 4(RY+RX) + R + 16 bytes, scratch = the fp64 slab of _diffuse_scratch_doubles), kind 1 =
+// hole filling (need = R bytes, scratch = R bytes).  niter_img[b] (kind 0) = 2 * max over the
+// image's masks of (ly + lx + 4), cellpose's per-image iteration count.
+// counts: [ncap + 1] int32 zeroed; scratch_total: int64 zeroed; niter_img: [B] int32 zeroed.
+int be_cp_plan_masks(const int* bbox, const unsigned char* valid, int B, int nlab, int kind, const int* caps, int ncap,
+                     long long* jobs, int* counts, long long* scratch_total, int* niter_img, hipStream_t s);
+}  // extern "C"
+
+namespace {
+struct Caps8 {
+  int v[8];
+};
+
+__global__ __launch_bounds__(256) void plan_masks_kernel(const int* __restrict__ bbox, const unsigned char* __restrict__ valid,
+                                                         int B, int nlab, int kind, Caps8 caps, int ncap,
+                                                         MaskJob* __restrict__ jobs, int* __restrict__ counts,
+                                                         unsigned long long* __restrict__ scratch_total,
+                                                         int* __restrict__ niter_img) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)B * nlab;
+  if (i >= n) return;
+  const int b = (int)(i / nlab), lab = (int)(i % nlab);
+  const int* bb = bbox + i * 4;
+  const int y0 = bb[0], y1 = bb[1], x0 = bb[2], x1 = bb[3];
+  if (lab == 0 || y1 < 0) return;
+  const int ly = y1 - y0 + 1, lx = x1 - x0 + 1;
+  if (kind == 0) atomicMax(niter_img + b, 2 * (ly + lx + 2));  // 2 * ((y1-y0)+(x1-x0)+4)
+  if (valid && !valid[i]) return;
+  const long long RY = ly + 2, RX = lx + 2, R = RY * RX;
+  const long long need = kind == 0 ? 16 * R + 4 * (RY + RX) + R + 16 : R;
+  int k = 0;
+  while (k < ncap && need > caps.v[k]) ++k;
+  long long scr = -1;
+  if (k == ncap) {
+    const long long sz = kind == 0 ? 2 * R + (RY + RX + 1) / 2 + (R + 7) / 8 + 2 : R;
+    scr = (long long)atomicAdd(scratch_total, (unsigned long long)sz);
+  }
+  const int slot = atomicAdd(counts + k, 1);
+  MaskJob J;
+  J.b = b;
+  J.lab = lab;
+  J.y0 = y0;
+  J.x0 = x0;
+  J.ly = ly;
+  J.lx = lx;
+  J.scratch = scr;
+  jobs[(size_t)k * n + slot] = J;
+}
+}  // namespace
+
+extern "C" {
+int be_cp_plan_masks(const int* bbox, const unsigned char* valid, int B, int nlab, int kind, const int* caps, int ncap,
+                     long long* jobs, int* counts, long long* scratch_total, int* niter_img, hipStream_t s) {
+  if (ncap < 0 || ncap > 8) return -1;
+  Caps8 c{};
+  for (int k = 0; k < ncap; ++k) c.v[k] = caps[k];  // host array
+  const long long n = (long long)B * nlab;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(plan_masks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bbox, valid, B, nlab, kind, c,
+                     ncap, reinterpret_cast<MaskJob*>(jobs), counts, reinterpret_cast<unsigned long long*>(scratch_total),
+                     niter_img);
+  return BE_CHECK_LAUNCH();
+}
+
 }  // extern "C"
 
 // Pixel count per label (label 0 skipped, so background never contends on one counter).
 namespace {
+// Run-length form: RL consecutive pixels per thread (segments never straddle images), one atomic
+// per run of equal labels.
 __global__ __launch_bounds__(256) void label_counts_kernel(const int* __restrict__ M, long long n, int HW, int nlab,
                                                            int* __restrict__ counts) {
+  const int segs = (HW + RL - 1) / RL;
+  const long long nseg = (n / HW) * segs;
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int lab = M[i];
-    if (lab > 0) atomicAdd(counts + (size_t)(i / HW) * nlab + lab, 1);
+  for (long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += stride) {
+    const long long b = g / segs;
+    const int p0 = (int)(g % segs) * RL, p1 = min(p0 + RL, HW);
+    const int* Mb = M + b * HW;
+    int* cb = counts + (size_t)b * nlab;
+    int cur = 0, run = 0;
+    for (int p = p0; p < p1; ++p) {
+      const int lab = Mb[p];
+      if (lab != cur) {
+        if (cur > 0) atomicAdd(cb + cur, run);
+        cur = lab;
+        run = 0;
+      }
+      ++run;
+    }
+    if (cur > 0) atomicAdd(cb + cur, run);
   }
 }
 }  // namespace
 
 extern "C" int be_label_counts(const int* M, int B, int HW, int nlab, int* counts, hipStream_t s) {
   const long long n = (long long)B * HW;
-  int blocks = (int)((n + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
+  const long long nseg = (long long)B * ((HW + RL - 1) / RL);
+  int blocks = (int)((nseg + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(label_counts_kernel, dim3(blocks), dim3(256), 0, s, M, n, HW, nlab, counts);
   return BE_CHECK_LAUNCH();

@@ -85,6 +85,53 @@ def test_compute_masks_gpu_matches_reference(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", [0, 1])
+def test_plan_masks_kernel_matches_torch_planner(gpu, kind):
+    """be_cp_plan_masks (one launch) vs the torch planner it replaces: same jobs per bucket (order
+    inside a bucket is free), same scratch total, same per-image iteration counts."""
+    from bioengine_worker_amd.cellpose import gpu as cg
+
+    g = torch.Generator().manual_seed(3)
+    B, H, W = 3, 200, 180
+    M = torch.zeros(B, H, W, dtype=torch.int32)
+    for b in range(B):
+        lab = 0
+        for _ in range(40):
+            h, w = int(torch.randint(2, 40, (1,), generator=g)), int(torch.randint(2, 40, (1,), generator=g))
+            y, x = int(torch.randint(0, H - h, (1,), generator=g)), int(torch.randint(0, W - w, (1,), generator=g))
+            lab += 1
+            M[b, y:y + h, x:x + w] = lab
+        M[b, 5:170, 3:150][M[b, 5:170, 3:150] == 0] = lab + 1  # one mask bigger than any LDS bucket
+    M = M.to(gpu)
+    nlab = int(M.max()) + 1
+    bbox = cg.mask_bboxes(M, nlab)
+    if kind == 0:
+        caps, lds, scr, valid = [c for c, _ in cg.DIFFUSE_BUCKETS], cg._diffuse_lds_bytes, cg._diffuse_scratch_doubles, None
+    else:
+        caps, lds, scr = [cg.LDS_FILL_BYTES], (lambda ly, lx: (ly + 2) * (lx + 2)), (lambda ly, lx: (ly + 2) * (lx + 2))
+        valid = torch.rand(B, nlab, generator=g).to(gpu) > 0.3
+    got, tot, niter = cg._plan_masks(bbox, valid, kind, caps)
+    present = bbox[..., 1] >= 0
+    present[:, 0] = False
+    keep = present if valid is None else present & valid
+    ar = torch.arange(B * nlab, device=gpu)
+    want, wtot = cg._plan_jobs(bbox.view(-1, 4), (ar // nlab).int(), (ar % nlab).int(), lds, caps, scr,
+                               valid=keep.view(-1))
+    assert sum(int(x.shape[0]) for x in got) == int(keep.sum())
+    assert kind == 1 or got[-1].shape[0] >= 1  # the diffusion plan has a beyond-LDS mask
+    for a, b in zip(got, want):
+        ka = sorted(map(tuple, a[:, :3].tolist()))
+        kb = sorted(map(tuple, b[:, :3].tolist()))
+        assert ka == kb
+    assert tot == wtot
+    big = got[-1][:, 3].tolist()
+    assert len(set(big)) == len(big) and all(x >= 0 for x in big) and all(x == -1 for x in got[0][:, 3].tolist())
+    if kind == 0:
+        ext = (bbox[..., 1] - bbox[..., 0] + bbox[..., 3] - bbox[..., 2] + 4).clamp(min=0) * present
+        assert torch.equal(niter, (2 * ext.max(dim=1).values).int())
+
+
+@pytest.mark.gpu
 def test_fill_holes_gpu(gpu):
     from bioengine_worker_amd.cellpose.gpu import fill_holes_gpu
 
