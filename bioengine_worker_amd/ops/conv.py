@@ -14,12 +14,17 @@ kernel's tap-major K layout by :class:`PackedConv`.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import torch
 import torch.nn.functional as F
 
 from . import _native
+
+#: input-channel chunk of 1x1 convs whose padded Cin is a multiple of 64 (32 or 64)
+CK_1X1 = 64
 
 INMODES = {"none": 0, "up2": 1, "pool2": 2}
 
@@ -49,8 +54,13 @@ class PackedConv:
     wp: torch.Tensor | None = None
 
     @staticmethod
-    def choose(cin_pad: int, cout: int) -> tuple[int, int]:
+    def choose(cin_pad: int, cout: int, ks: int = 3) -> tuple[int, int]:
         ck = 8 if cin_pad % 32 else 32
+        # 1x1 convs (the resblock projections) have one K step per 32-channel chunk, so their
+        # chunk loop is pure load latency: wider chunks halve the serial steps (BE_CONV_CK1)
+        ck1 = int(os.environ.get("BE_CONV_CK1", CK_1X1))
+        if ks == 1 and ck1 == 64 and cin_pad % 64 == 0:
+            ck = 64
         if cout <= 16:
             tco = 16
         elif cout <= 32:
@@ -67,7 +77,7 @@ class PackedConv:
         cin_pad = cin_pad or _round_up(cin, 8)
         if cin_pad % 32 and cin_pad != 8:
             cin_pad = _round_up(cin_pad, 32)
-        ck, tco = cls.choose(cin_pad, cout)
+        ck, tco = cls.choose(cin_pad, cout, ks)
         cout_k = max(cout, cout_pad_to or 0)
         cout_pad = _round_up(cout_k, tco)
         kp = ((ks * ks * ck + 31) // 32) * 32

@@ -70,7 +70,7 @@ struct Cfg {
   static constexpr int TH = 2 * NW;
   static constexpr int HH = TH + KS - 1;
   static constexpr int HW_ = TW + KS - 1;
-  static constexpr int PSTR = CK == 8 ? 24 : CK + 16;  // dwords/pixel = 8 (mod 64) for CK=32; CK=8: 12
+  static constexpr int PSTR = CK == 8 ? 24 : CK + 16;  // dwords/pixel = 8 (mod 16) for CK=32/64; CK=8: 12
   static constexpr int KSTEPS = (KS * KS * CK + 31) / 32;
   static constexpr int KPL = KSTEPS * 32;
   static constexpr int WSTR = KPL + 16;
@@ -601,6 +601,7 @@ int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const flo
   } else {
     if (ck == 8) return dispatch_tco<1, 8>(tco, inmode, x2p, nw, a, stream);
     if (ck == 32) return dispatch_tco<1, 32>(tco, inmode, x2p, nw, a, stream);
+    if (ck == 64) return dispatch_tco<1, 64>(tco, inmode, x2p, nw, a, stream);
   }
   return -12;
 }
