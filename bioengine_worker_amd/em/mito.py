@@ -8,8 +8,9 @@ normalisation; 512 tiles with 64 overlap, reflect-padded edge tiles, Gaussian wi
 regionprops area / axis lengths / eccentricity / centroid (:256-271).
 
 Dense stages are HIP kernels (``imageproc.hip``: CCL; ``morphology.hip``: blend, disk morphology,
-EDT, max filter, moments); the priority-flood watershed and the greedy peak spacing run in the C++
-host runtime (``csrc/runtime/watershed.cpp``).  skimage is not available in this image, so
+EDT, max filter, moments; ``em_watershed.hip``: marker watershed 2-D/3-D and the 3-D EDT); the
+greedy peak spacing and the CPU priority-flood watershed (oracle and CPU path) run in the C++ host
+runtime (``csrc/runtime/watershed.cpp``).  skimage is not available in this image, so
 exact parity with it is "unpinned": every stage is tested against scipy/numpy oracles of the same
 definition (tests/test_em_*.py).
 """
@@ -65,7 +66,7 @@ def infer_tiled(img: torch.Tensor, predict: Callable[[torch.Tensor], torch.Tenso
     w = gaussian_window(tile).to(img.device)
     out = torch.empty(C, H, W, dtype=torch.float32, device=img.device)
     if img.is_cuda:
-        _native.call("be_blend_gather", _native.ptr(probs), C, 1, H, W, 1, len(ys), len(xs), stride, 1, tile,
+        _native.call("be_blend_gather", _native.ptr(probs), C, 1, H, W, 1, len(ys), len(xs), stride, 1, 1, tile,
                      _native.ptr(w), _native.ptr(w), _native.ptr(w), _native.ptr(out), _native.stream(img.device))
     else:
         out = blend_reference(probs, H, W, ys, xs, tile)
@@ -197,21 +198,177 @@ def watershed(neg_dist: np.ndarray, markers: np.ndarray, mask: np.ndarray, conn:
     return out
 
 
+def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor | None = None,
+                  max_local: int = 32, check_every: int = 4, max_sweeps: int = 100000) -> torch.Tensor:
+    """Marker watershed of ``elev`` ([H, W] or [D, H, W] fp32, device) with 4/6-connectivity as the
+    parallel minimax-path fixpoint of ``em_watershed.hip`` (skimage ``watershed(elev, markers,
+    mask=mask)``; ties between basins may resolve differently from the CPU priority flood).
+    Sweeps repeat until no tile changes (checked every ``check_every`` launches)."""
+    dev = elev.device
+    shape = tuple(elev.shape)
+    D, H, W = (1,) + shape if elev.dim() == 2 else shape
+    n = D * H * W
+    mk = markers.to(torch.int32).contiguous()
+    if int(mk.max()) > _ws_max_label():
+        raise ValueError(f"watershed_gpu supports up to {_ws_max_label()} markers")
+    e = elev.float().contiguous()
+    m = mask.to(torch.uint8).contiguous() if mask is not None else None
+    key = torch.empty(n, dtype=torch.int64, device=dev)
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    changed = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = _native.stream(dev)
+    _native.call("be_ws_init", _native.ptr(e), _native.ptr(mk), _native.ptr(m), n, _native.ptr(key), _native.ptr(flags), st)
+    sweeps = 0
+    while sweeps < max_sweeps:
+        changed.zero_()
+        for _ in range(check_every):
+            _native.call("be_ws_relax", _native.ptr(e), _native.ptr(flags), _native.ptr(key), D, H, W, max_local,
+                         _native.ptr(changed), st)
+        sweeps += check_every
+        if int(changed.item()) == 0:
+            break
+    out = torch.empty(shape, dtype=torch.int32, device=dev)
+    _native.call("be_ws_labels", _native.ptr(key), _native.ptr(flags), n, _native.ptr(out), st)
+    return out
+
+
+_WS_MAX = None
+
+
+def _ws_max_label() -> int:
+    global _WS_MAX
+    if _WS_MAX is None:
+        _WS_MAX = int(_native.hip().be_ws_max_label())
+    return _WS_MAX
+
+
+def edt3d(mask: torch.Tensor) -> torch.Tensor:
+    """Exact 3-D Euclidean distance to the nearest background voxel (scipy
+    ``distance_transform_edt`` on a [D, H, W] volume, unit spacing)."""
+    D, H, W = mask.shape
+    dev = mask.device
+    if not mask.is_cuda:
+        from scipy import ndimage
+
+        return torch.from_numpy(ndimage.distance_transform_edt(mask.cpu().numpy()).astype(np.float32))
+    m = mask.to(torch.uint8).contiguous()
+    dist = torch.empty(D, H, W, dtype=torch.float32, device=dev)
+    tmp = torch.empty_like(dist)
+    v = torch.empty(D * H * W, dtype=torch.int32, device=dev)
+    z = torch.empty(D * H * W + D * max(H, W), dtype=torch.float64, device=dev)
+    _native.call("be_edt3d", _native.ptr(m), _native.ptr(dist), _native.ptr(tmp), _native.ptr(v), _native.ptr(z), D, H, W,
+                 _native.stream(dev))
+    return dist
+
+
+def max_filter3d(x: torch.Tensor, r: int) -> torch.Tensor:
+    """Cubic (2r+1)^3 maximum filter, nearest-edge mode (scipy ``maximum_filter(size=2r+1)``)."""
+    D, H, W = x.shape
+    if not x.is_cuda:
+        from scipy import ndimage
+
+        return torch.from_numpy(ndimage.maximum_filter(x.float().numpy(), size=2 * r + 1, mode="nearest"))
+    a = x.float().contiguous()
+    t, o = torch.empty_like(a), torch.empty_like(a)
+    st = _native.stream(a.device)
+    _native.call("be_max_filter_1d", _native.ptr(a), _native.ptr(t), D, H, W, r, 0, st)   # along x
+    _native.call("be_max_filter_1d", _native.ptr(t), _native.ptr(o), D, H, W, r, 1, st)   # along y
+    _native.call("be_max_filter_1d", _native.ptr(o), _native.ptr(t), 1, D, H * W, r, 1, st)  # along z
+    return t
+
+
+def peak_local_max3d(dist: torch.Tensor, closed: torch.Tensor, min_distance: int = 8) -> np.ndarray:
+    """skimage ``peak_local_max(dist, min_distance, labels=closed)`` on a volume (exclude_border)."""
+    D, H, W = dist.shape
+    b = min_distance
+    inner = torch.zeros_like(closed)
+    if D > 2 * b and H > 2 * b and W > 2 * b:
+        inner[b:D - b, b:H - b, b:W - b] = True
+    lm = closed & inner
+    img = torch.where(lm, dist, torch.full_like(dist, -3.0e38))
+    mx = max_filter3d(img, min_distance)
+    cand = (img == mx) & (img > float(dist.min())) & lm
+    zyx = cand.nonzero()
+    if zyx.shape[0] == 0:
+        return np.zeros((0, 3), np.int64)
+    order = torch.sort(-img[zyx[:, 0], zyx[:, 1], zyx[:, 2]], stable=True).indices
+    return ensure_spacing(zyx[order].cpu().numpy(), min_distance).astype(np.int64)
+
+
+def _markers_from_peaks(peaks: np.ndarray, shape, device) -> torch.Tensor:
+    """One marker label per peak (peaks are >= min_distance apart, so ``measure.label`` of the
+    peak image gives each its own component), numbered in raster order like ``measure.label``."""
+    mk = torch.zeros(shape, dtype=torch.int32, device=device)
+    if len(peaks):
+        pk = np.asarray(peaks)[np.lexsort(np.asarray(peaks).T[::-1])]
+        mk[tuple(torch.from_numpy(pk).to(device).T)] = torch.arange(1, len(pk) + 1, dtype=torch.int32, device=device)
+    return mk
+
+
 def prob_to_instances(prob: torch.Tensor, threshold: float = 0.5, min_size: int = 300, closing_radius: int = 4,
-                      min_distance: int = 8) -> np.ndarray:
-    """[H, W] probability (GPU) -> int32 instance labels (numpy)."""
+                      min_distance: int = 8, gpu_watershed: bool = True) -> np.ndarray:
+    """[H, W] probability (GPU) -> int32 instance labels (numpy).  The watershed runs on the GPU
+    (``gpu_watershed``) or in the C++ priority flood of the host runtime."""
     binary = remove_small_objects(prob > threshold, min_size, conn=4)
     if not bool(binary.any()):
         return np.zeros(tuple(prob.shape), np.int32)
     closed = binary_closing_disk(binary, closing_radius)
     dist = edt(closed)
     peaks = peak_local_max(dist, closed, min_distance)
+    if gpu_watershed and prob.is_cuda:
+        markers = _markers_from_peaks(peaks, tuple(closed.shape), prob.device)
+        return watershed_gpu(-dist, markers, closed).cpu().numpy()
     m = torch.zeros_like(closed)
     if len(peaks):
         pk = torch.from_numpy(peaks).to(prob.device)
         m[pk[:, 0], pk[:, 1]] = True
     markers, _ = compact_labels(ccl(m, 8))
     return watershed((-dist).cpu().numpy(), markers.cpu().numpy(), closed.cpu().numpy(), conn=1)
+
+
+def prob_to_instances_3d(mask: torch.Tensor, min_size: int = 300, closing_radius: int = 4, min_distance: int = 8,
+                         gpu_watershed: bool = True) -> tuple[torch.Tensor, int]:
+    """Foreground volume [D, H, W] (bool, GPU) -> (int32 instance labels, count): the 3-D form of
+    the reference post-processing -- remove components under ``min_size`` voxels (6-connected),
+    binary closing with a disk per z-slice, 3-D EDT, 3-D peak_local_max, marker watershed on
+    -EDT (6-connected) -- so touching objects are split instead of merged by plain CCL."""
+    from .volume import ccl3d
+
+    dev = mask.device
+    roots = ccl3d(mask)
+    flat = roots.reshape(-1).long()
+    fg = flat >= 0
+    cnt = torch.zeros(flat.numel(), dtype=torch.int32, device=dev)
+    cnt.index_add_(0, flat[fg], torch.ones(int(fg.sum()), dtype=torch.int32, device=dev))
+    keep = torch.zeros_like(flat, dtype=torch.bool)
+    keep[fg] = cnt[flat[fg]] >= min_size
+    binary = keep.reshape(mask.shape)
+    if not bool(binary.any()):
+        return torch.zeros(mask.shape, dtype=torch.int32, device=dev), 0
+    D, H, W = binary.shape
+    closed = binary
+    if closing_radius > 0 and not mask.is_cuda:
+        from scipy import ndimage
+
+        yy, xx = np.mgrid[-closing_radius:closing_radius + 1, -closing_radius:closing_radius + 1]
+        disk = (yy ** 2 + xx ** 2) <= closing_radius ** 2
+        b = binary.numpy()
+        closed = torch.from_numpy(np.stack([ndimage.binary_closing(b[z], structure=disk) for z in range(D)]))
+    elif closing_radius > 0:
+        m8 = binary.to(torch.uint8).contiguous()
+        tmp, out = torch.empty_like(m8), torch.empty_like(m8)
+        st = _native.stream(dev)
+        _native.call("be_morph_disk", _native.ptr(m8), _native.ptr(tmp), D, H, W, closing_radius, 0, 0, st)
+        _native.call("be_morph_disk", _native.ptr(tmp), _native.ptr(out), D, H, W, closing_radius, 1, 0, st)
+        closed = out.bool()
+    dist = edt3d(closed)
+    peaks = peak_local_max3d(dist, closed, min_distance)
+    markers = _markers_from_peaks(peaks, (D, H, W), dev)
+    if gpu_watershed and mask.is_cuda:
+        labels = watershed_gpu(-dist, markers, closed)
+    else:
+        labels = torch.from_numpy(watershed((-dist).cpu().numpy(), markers.cpu().numpy(), closed.cpu().numpy(), conn=1)).to(dev)
+    return labels, int(len(peaks))
 
 
 def prob_to_instances_cpu(prob: np.ndarray) -> np.ndarray:

@@ -90,6 +90,57 @@ def slice_probabilities(vol: torch.Tensor, predict, tile: int = 512, overlap: in
     return out
 
 
+def infer_tiled_3d(vol: torch.Tensor, predict, tile: int = 128, tile_z: int = 32, overlap: int = 16,
+                   overlap_z: int = 8, batch: int = 4) -> torch.Tensor:
+    """3-D tiled inference with z-overlap blending (SURVEY.md §2.5 K14, 3-D generalisation of the
+    reference's 2-D Gaussian tile blend, ``analysis_deployment.py:124-156``).
+
+    ``vol`` [D, H, W] (normalised) is cut into ``tile_z x tile x tile`` blocks with ``overlap_z`` /
+    ``overlap`` voxels of overlap (reflect/replicate padded at the far edges); ``predict`` maps
+    [B, 1, tz, t, t] -> [B, C, tz, t, t]; predictions are blended with the separable window
+    ``exp(-2 z^2) exp(-2 y^2) exp(-2 x^2)`` by the HIP gather-blend kernel (fp32 accumulation, no
+    atomics: every output voxel gathers its <= 8 covering tiles).  Returns [C, D, H, W]."""
+    D, H, W = vol.shape
+    tz, t = min(tile_z, D), min(tile, H, W)
+    sz, sxy = max(1, tz - overlap_z), max(1, t - overlap)
+    zs, ys, xs = (list(range(0, D, sz)) if D > tz else [0]), list(range(0, H, sxy)), list(range(0, W, sxy))
+    pad = (0, max(0, xs[-1] + t - W), 0, max(0, ys[-1] + t - H), 0, max(0, zs[-1] + tz - D))
+    big = any(p >= dim for p, dim in zip(pad[::2], (W, H, D)))
+    padded = torch.nn.functional.pad(vol[None, None].float(), pad, mode="replicate" if big else "reflect")[0, 0]
+    coords = [(z, y, x) for z in zs for y in ys for x in xs]
+    outs = []
+    for i in range(0, len(coords), batch):
+        blk = torch.stack([padded[z:z + tz, y:y + t, x:x + t] for z, y, x in coords[i:i + batch]])[:, None]
+        outs.append(predict(blk).float())
+    probs = torch.cat(outs).contiguous()
+    C = probs.shape[1]
+    wz, wxy = mito.gaussian_window(tz).to(vol.device), mito.gaussian_window(t).to(vol.device)
+    if vol.is_cuda:
+        out = torch.empty(C, D, H, W, dtype=torch.float32, device=vol.device)
+        _native.call("be_blend_gather", _native.ptr(probs), C, D, H, W, len(zs), len(ys), len(xs), sxy, sz, tz, t,
+                     _native.ptr(wz), _native.ptr(wxy), _native.ptr(wxy), _native.ptr(out), _native.stream(vol.device))
+        return out
+    return blend3d_reference(probs, D, H, W, zs, ys, xs, tz, t)
+
+
+def blend3d_reference(probs: torch.Tensor, D: int, H: int, W: int, zs, ys, xs, tz: int, t: int) -> torch.Tensor:
+    """float64 scatter-add oracle of :func:`infer_tiled_3d`'s blend."""
+    C = probs.shape[1]
+    wz, wxy = mito.gaussian_window(tz).double(), mito.gaussian_window(t).double()
+    win = wz[:, None, None] * wxy[None, :, None] * wxy[None, None, :]
+    acc = torch.zeros(C, D, H, W, dtype=torch.float64)
+    wacc = torch.zeros(D, H, W, dtype=torch.float64)
+    k = 0
+    for z in zs:
+        for y in ys:
+            for x in xs:
+                dz, dy, dx = min(tz, D - z), min(t, H - y), min(t, W - x)
+                acc[:, z:z + dz, y:y + dy, x:x + dx] += probs[k, :, :dz, :dy, :dx].double().cpu() * win[:dz, :dy, :dx]
+                wacc[z:z + dz, y:y + dy, x:x + dx] += win[:dz, :dy, :dx]
+                k += 1
+    return (acc / wacc.clamp(min=1e-300)).float()
+
+
 def _union_find_pairs(pairs: np.ndarray, n: int) -> np.ndarray:
     """Connected components of the label-adjacency graph: root (smallest member) per label 0..n-1."""
     if len(pairs) == 0:
@@ -235,15 +286,52 @@ def instance_stats(labels: torch.Tensor, n: int, z_offset: int = 0, group=None) 
             "centroid_z": acc[1, 1:] / c, "centroid_y": acc[2, 1:] / c, "centroid_x": acc[3, 1:] / c}
 
 
+def split_instances_sharded(mask: torch.Tensor, group=None, min_size: int = 300, closing_radius: int = 4,
+                            min_distance: int = 8) -> tuple[torch.Tensor, int]:
+    """Touching objects split by the 3-D marker watershed (:func:`mito.prob_to_instances_3d`) for a
+    z-sharded foreground mask: the uint8 mask slabs are gathered onto rank 0 (``dist.gather``; the
+    full label volume never exists on the other ranks), rank 0 runs the GPU pipeline on the whole
+    volume (a watershed basin can cross any slab face), and each rank gets its label slab back with
+    one ``dist.scatter``.  Single process: runs in place.  Returns (this rank's labels, count)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return mito.prob_to_instances_3d(mask, min_size, closing_radius, min_distance)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    depth = torch.tensor([mask.shape[0]], dtype=torch.int64, device=mask.device)
+    depths = [torch.zeros_like(depth) for _ in range(world)]
+    dist.all_gather(depths, depth, group=group)
+    depths = [int(d) for d in depths]
+    zmax = max(depths)
+    full = gather_to_rank0(mask, group)
+    n = torch.zeros(1, dtype=torch.int64, device=mask.device)
+    parts = None
+    if rank == 0:
+        labels, k = mito.prob_to_instances_3d(full, min_size, closing_radius, min_distance)
+        n[0] = k
+        parts, z = [], 0
+        for r in range(world):
+            buf = torch.zeros((zmax,) + tuple(mask.shape[1:]), dtype=torch.int32, device=mask.device)
+            buf[: depths[r]] = labels[z: z + depths[r]]
+            parts.append(buf)
+            z += depths[r]
+        del labels, full
+    mine = torch.empty((zmax,) + tuple(mask.shape[1:]), dtype=torch.int32, device=mask.device)
+    dist.scatter(mine, parts, src=0, group=group)
+    dist.broadcast(n, src=0, group=group)
+    return mine[: mask.shape[0]].contiguous(), int(n.item())
+
+
 def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 64, batch: int = 8,
                    threshold: float = 0.5, min_voxels: int = 300, group=None, gather_labels: bool = False,
                    z_offset: int = 0, gather: str | None = None, timings: bool = False,
-                   norm_range: tuple[float, float] | None = None) -> dict:
+                   norm_range: tuple[float, float] | None = None, split_touching: bool = False,
+                   closing_radius: int = 4, min_distance: int = 8) -> dict:
     """Single-process (or per-rank) 3-D analysis.  With a process group, ``vol`` is this rank's
     z-slab and results are globally consistent.  ``gather="mask"`` / ``"labels"`` all-gathers the
     stitched foreground mask (uint8) / global instance labels of the whole volume onto every rank
     (``out["mask"]`` / ``out["labels_full"]``, device tensors); ``gather_labels`` returns this
-    rank's slab labels as numpy."""
+    rank's slab labels as numpy.  ``split_touching`` replaces connected components by the 3-D
+    reference post-processing (closing, EDT, peaks, marker watershed) so touching mitochondria
+    become separate instances (:func:`split_instances_sharded`)."""
     import time
 
     from ..search.preprocess import percentiles
@@ -272,7 +360,10 @@ def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 6
     mark("inference")
     mask = prob > threshold
     del prob, vn, v
-    labels, n = label_sharded(mask, group)
+    if split_touching:
+        labels, n = split_instances_sharded(mask, group, min_voxels, closing_radius, min_distance)
+    else:
+        labels, n = label_sharded(mask, group)
     mark("label")
     stats = instance_stats(labels, n, z_offset, group)
     keep = stats["voxels"] >= min_voxels

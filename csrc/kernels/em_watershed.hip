@@ -1,0 +1,261 @@
+// EM instance separation on the GPU (reference
+// apps/fibsem-mito-analysis/analysis_deployment.py:160-176): marker-controlled watershed on -EDT in
+// 2-D and 3-D, and the 3-D exact Euclidean distance transform it floods.
+//
+// Watershed as a parallel fixpoint.  skimage's watershed is a priority flood: pixels leave a heap
+// in order of (elevation, insertion age) and take the label of the neighbour that inserted them.
+// Its GPU form here follows the flood's own recursion: every mask voxel q takes its label from the
+// neighbour p with the smallest key, key = (c = flooding level at which the voxel leaves the heap,
+// h = breadth-first steps inside that level's plateau -- the heap's FIFO age --, label), and
+//     key(q) = ( max(elev(q), c_p),  elev(q) > c_p ? 0 : h_p + 1,  label_p ).
+// (c, h) strictly increase from p to q, so the labels follow a DAG and the fixpoint is unique: any
+// update order reaches it.  Workgroups stage a 16x16(xTZ) tile + 1-voxel halo of packed 64-bit
+// keys in LDS, relax Gauss-Seidel style until the tile is stable, write back, and the host
+// repeats launches until no tile changed.  A key packs ordered-float(c):32 | h:12 | label:20 into
+// one word, so a relaxation never pairs one label's cost with another label (no torn updates).
+// Tie-breaking inside equal (c, h) can differ from the heap's insertion order, so boundary voxels
+// between basins may differ from the CPU priority flood (csrc/runtime/watershed.cpp) -- the GPU
+// test bounds that fraction.
+//
+// EDT 3-D: Felzenszwalb-Huttenlocher separable passes -- a 1-D scan along z (squared distance to
+// the nearest background voxel in the column), then the lower envelope of parabolas along y and
+// along x (fp64 intersections, like the 2-D be_edt in morphology.hip), sqrt at the end.
+#include "common.h"
+
+namespace {
+
+constexpr int WS_TX = 16, WS_TY = 16;
+constexpr unsigned long long WS_NONE = ~0ull;
+constexpr int WS_LABEL_BITS = 20;
+constexpr unsigned WS_LABEL_MASK = (1u << WS_LABEL_BITS) - 1u;
+constexpr unsigned WS_HOP_MAX = 4095u;
+
+__device__ __forceinline__ unsigned ordered(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ unsigned long long pack_key(unsigned c, unsigned h, unsigned lab) {
+  return ((unsigned long long)c << 32) | ((unsigned long long)(h < WS_HOP_MAX ? h : WS_HOP_MAX) << WS_LABEL_BITS) |
+         (unsigned long long)lab;
+}
+
+// key[p]: WS_NONE = unreached.  fixed[p] = marker voxel (keeps its initial key).  Each block owns a
+// TZ x 16 x 16 tile; LDS holds tile + halo of keys, elevations and mask/fixed flags.
+template <int TZ>
+__global__ __launch_bounds__(WS_TX* WS_TY* TZ) void ws_relax_kernel(const float* __restrict__ elev,
+                                                                      const unsigned char* __restrict__ flags,
+                                                                      unsigned long long* __restrict__ key, int D, int H,
+                                                                      int W, int tiles_x, int tiles_y, int max_local,
+                                                                      int* __restrict__ changed) {
+  constexpr int HX = WS_TX + 2, HY = WS_TY + 2, HZ = TZ == 1 ? 1 : TZ + 2;
+  constexpr int NH = HX * HY * HZ;
+  constexpr int NT = WS_TX * WS_TY * TZ;
+  __shared__ unsigned long long k_s[NH];
+  __shared__ unsigned e_s[NH];
+  __shared__ unsigned char f_s[NH];  // bit0 = in mask, bit1 = fixed (marker)
+  __shared__ int any_s;
+  const int tid = threadIdx.x;
+  const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
+  const int bz = blockIdx.y;
+  const int x0 = bx * WS_TX - 1, y0 = by * WS_TY - 1, z0 = TZ == 1 ? bz : bz * TZ - 1;
+  for (int e = tid; e < NH; e += NT) {
+    const int lx = e % HX, ly = (e / HX) % HY, lz = e / (HX * HY);
+    const int gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
+    unsigned long long kv = WS_NONE;
+    unsigned ev = 0xffffffffu;
+    unsigned char fv = 0;
+    if (gx >= 0 && gx < W && gy >= 0 && gy < H && gz >= 0 && gz < D) {
+      const long long g = ((long long)gz * H + gy) * W + gx;
+      kv = key[g];
+      ev = ordered(elev[g]);
+      fv = flags[g];
+    }
+    k_s[e] = kv;
+    e_s[e] = ev;
+    f_s[e] = fv;
+  }
+  if (tid == 0) any_s = 0;
+  __syncthreads();
+  const int tx = tid % WS_TX, ty = (tid / WS_TX) % WS_TY, tz = tid / (WS_TX * WS_TY);
+  const int c = (tz + (TZ == 1 ? 0 : 1)) * HX * HY + (ty + 1) * HX + (tx + 1);
+  const int gx = x0 + 1 + tx, gy = y0 + 1 + ty, gz = TZ == 1 ? z0 : z0 + 1 + tz;
+  const bool active = gx < W && gy < H && gz < D && (f_s[c] & 1) && !(f_s[c] & 2);
+  const unsigned ep = e_s[c];
+  bool mine = false;  // this voxel improved at least once
+  for (int it = 0; it < max_local; ++it) {
+    bool ch = false;
+    if (active) {
+      // the flood labels a voxel from the neighbour that leaves the heap first: take the
+      // neighbour with the smallest key and derive this voxel's key from it
+      unsigned long long bn = WS_NONE;
+      const int nb[6] = {c - 1, c + 1, c - HX, c + HX, c - HX * HY, c + HX * HY};
+      const int nn = TZ == 1 ? 4 : 6;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        if (j >= nn) break;
+        const unsigned long long kq = k_s[nb[j]];
+        if (kq < bn) bn = kq;
+      }
+      if (bn != WS_NONE) {
+        const unsigned cq = (unsigned)(bn >> 32);
+        const unsigned hq = (unsigned)((bn >> WS_LABEL_BITS) & WS_HOP_MAX);
+        const unsigned lab = (unsigned)(bn & WS_LABEL_MASK);
+        const unsigned long long nk = pack_key(ep > cq ? ep : cq, ep > cq ? 0u : hq + 1u, lab);
+        if (nk != k_s[c]) {
+          k_s[c] = nk;
+          ch = true;
+          mine = true;
+        }
+      }
+    }
+    if (__syncthreads_or(ch) == 0) break;
+  }
+  if (mine) {
+    key[((long long)gz * H + gy) * W + gx] = k_s[c];
+    any_s = 1;
+  }
+  __syncthreads();
+  if (tid == 0 && any_s) atomicOr(changed, 1);
+}
+
+__global__ void ws_init_kernel(const float* __restrict__ elev, const int* __restrict__ markers,
+                               const unsigned char* __restrict__ mask, long long n, unsigned long long* __restrict__ key,
+                               unsigned char* __restrict__ flags) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int m = markers[i];
+  const bool in = mask == nullptr || mask[i];
+  unsigned char f = in ? 1 : 0;
+  unsigned long long k = WS_NONE;
+  if (in && m > 0) {
+    f |= 2;
+    k = pack_key(ordered(elev[i]), 0u, (unsigned)m);
+  }
+  key[i] = k;
+  flags[i] = f;
+}
+
+__global__ void ws_labels_kernel(const unsigned long long* __restrict__ key, const unsigned char* __restrict__ flags,
+                                 long long n, int* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long k = key[i];
+  out[i] = ((flags[i] & 1) && k != WS_NONE) ? (int)(k & WS_LABEL_MASK) : 0;
+}
+
+// ---------------------------------------------------------------- 3-D EDT
+// z scan: f[z, y, x] = (distance along z to the nearest background voxel)^2, or INF
+__global__ void edt3_z(const unsigned char* __restrict__ fg, float* __restrict__ f, int D, int H, int W) {
+  const long long col = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long HW = (long long)H * W;
+  if (col >= HW) return;
+  int last = -1;
+  for (int z = 0; z < D; ++z) {
+    if (!fg[z * HW + col]) last = z;
+    f[z * HW + col] = last < 0 ? -1.f : (float)(z - last);
+  }
+  last = -1;
+  for (int z = D - 1; z >= 0; --z) {
+    if (!fg[z * HW + col]) last = z;
+    float d = f[z * HW + col];
+    if (last >= 0 && (d < 0.f || (float)(last - z) < d)) d = (float)(last - z);
+    f[z * HW + col] = d < 0.f ? 3.0e38f : d * d;
+  }
+}
+
+// lower envelope of parabolas along one axis: lines of length L, element stride `st`, line bases
+// from (line / inner) * outer_st + (line % inner) * inner_st.  f == 3e38 marks "no site".
+__global__ void edt3_axis(const float* __restrict__ fin, float* __restrict__ fout, int* __restrict__ vbuf,
+                          double* __restrict__ zbuf, long long nlines, int L, long long st, long long inner,
+                          long long inner_st, long long outer_st, int take_sqrt) {
+  const long long line = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (line >= nlines) return;
+  const long long base = (line / inner) * outer_st + (line % inner) * inner_st;
+  int* v = vbuf + line * L;
+  double* z = zbuf + line * (L + 1);
+  int k = -1;
+  for (int q = 0; q < L; ++q) {
+    const float fq = fin[base + q * st];
+    if (fq >= 3.0e38f) continue;
+    if (k < 0) {
+      k = 0; v[0] = q; z[0] = -1e300; z[1] = 1e300;
+      continue;
+    }
+    double s;
+    for (;;) {
+      const int p = v[k];
+      const double fp = fin[base + p * st];
+      s = ((double)fq + (double)q * q - (fp + (double)p * p)) / (2.0 * (q - p));
+      if (s <= z[k] && k > 0) { --k; continue; }
+      break;
+    }
+    ++k; v[k] = q; z[k] = s; z[k + 1] = 1e300;
+  }
+  if (k < 0) {
+    for (int q = 0; q < L; ++q) fout[base + q * st] = 3.0e38f;
+    return;
+  }
+  int j = 0;
+  for (int q = 0; q < L; ++q) {
+    while (z[j + 1] < (double)q) ++j;
+    const double d = (double)(q - v[j]);
+    const double r = d * d + (double)fin[base + v[j] * st];
+    fout[base + q * st] = take_sqrt ? (float)sqrt(r) : (float)r;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Marker watershed on elev (e.g. -EDT) restricted to mask (uint8, optional), markers int32 (>0),
+// D = 1 for 2-D.  key: [n] uint64 scratch, flags: [n] uint8 scratch, changed: 1 int (device).
+// One call = one relaxation sweep over all tiles; returns 0 and the caller loops while *changed.
+int be_ws_init(const float* elev, const int* markers, const unsigned char* mask, long long n, unsigned long long* key,
+               unsigned char* flags, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ws_init_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, elev, markers, mask, n, key, flags);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_ws_relax(const float* elev, const unsigned char* flags, unsigned long long* key, int D, int H, int W, int max_local,
+                int* changed, hipStream_t s) {
+  const int tiles_x = (W + WS_TX - 1) / WS_TX, tiles_y = (H + WS_TY - 1) / WS_TY;
+  if (D == 1) {
+    hipLaunchKernelGGL(ws_relax_kernel<1>, dim3(tiles_x * tiles_y, 1), dim3(WS_TX * WS_TY), 0, s, elev, flags, key, D, H, W,
+                       tiles_x, tiles_y, max_local, changed);
+  } else {
+    constexpr int TZ = 4;
+    hipLaunchKernelGGL(ws_relax_kernel<TZ>, dim3(tiles_x * tiles_y, (D + TZ - 1) / TZ), dim3(WS_TX * WS_TY * TZ), 0, s,
+                       elev, flags, key, D, H, W, tiles_x, tiles_y, max_local, changed);
+  }
+  return BE_CHECK_LAUNCH();
+}
+
+int be_ws_labels(const unsigned long long* key, const unsigned char* flags, long long n, int* out, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(ws_labels_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, key, flags, n, out);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_ws_max_label() { return (int)WS_LABEL_MASK; }
+
+// 3-D EDT of fg [D, H, W] uint8 -> dist fp32.  tmp: [D*H*W] fp32; v: [D*H*W] int scratch;
+// z: [D*H*W + D*max(H, W)] double scratch (L + 1 per line).
+int be_edt3d(const unsigned char* fg, float* dist, float* tmp, int* v, double* z, int D, int H, int W, hipStream_t s) {
+  const long long HW = (long long)H * W;
+  if ((long long)D * HW == 0) return 0;
+  hipLaunchKernelGGL(edt3_z, dim3((unsigned)((HW + 255) / 256)), dim3(256), 0, s, fg, dist, D, H, W);
+  // along y: lines = D*W, line (zz, x) base = zz*HW + x, stride W
+  long long nl = (long long)D * W;
+  hipLaunchKernelGGL(edt3_axis, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, dist, tmp, v, z, nl, H, (long long)W,
+                     (long long)W, 1LL, HW, 0);
+  // along x: lines = D*H, line (zz, y) base = (zz*H + y)*W, stride 1
+  nl = (long long)D * H;
+  hipLaunchKernelGGL(edt3_axis, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, s, tmp, dist, v, z, nl, W, 1LL, nl,
+                     (long long)W, 0LL, 1);
+  return BE_CHECK_LAUNCH();
+}
+
+}  // extern "C"

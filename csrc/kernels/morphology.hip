@@ -22,15 +22,15 @@ inline unsigned nblk(long long n) { return (unsigned)((n + 255) / 256); }
 
 // probs [T, C, tile, tile(, tile)] tile t = (iz*ny + iy)*nx + ix at (iz, iy, ix) * stride; out [C, D, H, W]
 __global__ void blend_gather(const float* __restrict__ probs, int C, int D, int H, int W, int nz, int ny, int nx,
-                             int stride, int tz, int tile, const float* __restrict__ wz, const float* __restrict__ wy,
-                             const float* __restrict__ wx, float* __restrict__ out) {
+                             int stride, int stride_z, int tz, int tile, const float* __restrict__ wz,
+                             const float* __restrict__ wy, const float* __restrict__ wx, float* __restrict__ out) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long vox = (long long)D * H * W;
   if (gid >= vox) return;
   const int z = (int)(gid / ((long long)H * W));
   const int y = (int)((gid / W) % H);
   const int x = (int)(gid % W);
-  const int sz = D > 1 ? stride : 1;
+  const int sz = D > 1 ? stride_z : 1;  // z tiles (3-D models): own depth tz and z overlap
   const int iz1 = min(z / sz, nz - 1), iy1 = min(y / stride, ny - 1), ix1 = min(x / stride, nx - 1);
   // first tile whose extent [i*stride, i*stride + tile) still contains the pixel (floor division)
   const int iz0 = (D > 1 && z >= tz) ? (z - tz) / sz + 1 : 0;
@@ -178,12 +178,12 @@ __global__ void label_moments(const int* __restrict__ lab, int B, int H, int W, 
 
 extern "C" {
 
-int be_blend_gather(const float* probs, int C, int D, int H, int W, int nz, int ny, int nx, int stride, int tz,
-                    int tile, const float* wz, const float* wy, const float* wx, float* out, hipStream_t s) {
+int be_blend_gather(const float* probs, int C, int D, int H, int W, int nz, int ny, int nx, int stride, int stride_z,
+                    int tz, int tile, const float* wz, const float* wy, const float* wx, float* out, hipStream_t s) {
   const long long vox = (long long)D * H * W;
   if (vox == 0) return 0;
-  hipLaunchKernelGGL(blend_gather, dim3(nblk(vox)), dim3(256), 0, s, probs, C, D, H, W, nz, ny, nx, stride, tz, tile, wz,
-                     wy, wx, out);
+  hipLaunchKernelGGL(blend_gather, dim3(nblk(vox)), dim3(256), 0, s, probs, C, D, H, W, nz, ny, nx, stride, stride_z, tz,
+                     tile, wz, wy, wx, out);
   return BE_CHECK_LAUNCH();
 }
 

@@ -54,10 +54,15 @@ def test_prob_to_instances_gpu_matches_cpu_path(gpu):
     from bioengine_worker_amd.em import mito
 
     p = _blobs(seed=3)
-    got = mito.prob_to_instances(torch.from_numpy(p).to(gpu))
+    # GPU dense stages + the C++ priority flood: identical to the CPU path
+    got = mito.prob_to_instances(torch.from_numpy(p).to(gpu), gpu_watershed=False)
     ref = mito.prob_to_instances_cpu(p)
     assert got.max() == ref.max() > 3
     assert np.array_equal(got, ref)
+    # all-GPU (marker watershed fixpoint): same instances, basin-boundary ties may differ
+    full = mito.prob_to_instances(torch.from_numpy(p).to(gpu))
+    fg = ref > 0
+    assert full.max() == ref.max() and np.array_equal(full > 0, fg) and float((full[fg] == ref[fg]).mean()) > 0.98
     pg = mito.region_properties(got, 5.0, gpu)
     pc = mito.region_properties(ref, 5.0, "cpu")
     assert np.allclose(pg["area_um2"], pc["area_um2"]) and np.allclose(pg["eccentricity"], pc["eccentricity"], atol=1e-6)

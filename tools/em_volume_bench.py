@@ -48,7 +48,11 @@ def main():
     ap.add_argument("--tile", type=int, default=512)
     ap.add_argument("--overlap", type=int, default=64)
     ap.add_argument("--batch", type=int, default=32, help="tiles per model call")
-    ap.add_argument("--gather", default="mask", choices=["mask", "labels", "none"])
+    ap.add_argument("--gather", default="mask", choices=["mask", "labels", "rank0", "sharded", "none"],
+                    help="mask/labels: all-gather onto every rank; rank0: dist.gather of the label volume onto "
+                         "rank 0 only; sharded: labels stay on the rank that computed them")
+    ap.add_argument("--split-touching", action="store_true",
+                    help="3-D closing + EDT + peaks + GPU marker watershed instead of plain CCL")
     a = ap.parse_args()
 
     world, rank, local = int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0))
@@ -80,7 +84,16 @@ def main():
         dist.barrier()
     t = time.perf_counter()
     res = analyze_volume(slab, predict, a.tile, a.overlap, a.batch, group=None, z_offset=z0,
-                         gather=None if a.gather == "none" else a.gather, timings=True)
+                         gather=a.gather if a.gather in ("mask", "labels") else None, timings=True,
+                         split_touching=a.split_touching)
+    if a.gather == "rank0":
+        from bioengine_worker_amd.em.volume import gather_to_rank0
+
+        tg = time.perf_counter()
+        full = gather_to_rank0(res["labels_slab_t"])
+        torch.cuda.synchronize()
+        res["timings_s"]["gather_rank0"] = round(time.perf_counter() - tg, 4)
+        res["rank0_volume_shape"] = list(full.shape) if full is not None else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -95,7 +108,8 @@ def main():
                           "n_gpus": world, "seconds": round(dt, 3), "volume": [a.z, a.yx, a.yx],
                           "tiles_per_slice": len(range(0, a.yx, a.tile - a.overlap)) ** 2, "tile": a.tile,
                           "overlap": a.overlap, "n_instances": res["n_instances"], "n_components": res["n_components"],
-                          "gathered": a.gather, "timings_s": res["timings_s"], "dtype": "bf16 (graph-pass U-Net)",
+                          "gathered": a.gather, "split_touching": a.split_touching,
+                          "timings_s": res["timings_s"], "dtype": "bf16 (graph-pass U-Net)",
                           "data": "synthetic EM-like uint8 volume, random-init U-Net weights"}), flush=True)
     if world > 1:
         dist.destroy_process_group()
