@@ -14,9 +14,15 @@
 
 4. does the same for 3-D models: ``Conv3d`` (1x1x1 / 3x3x3, stride 1, "same" zero padding)
    + ``BatchNorm3d`` + ``ReLU`` become :class:`HipConv3d` (``ops/conv3d.py``: depth-tap
-   decomposition onto the same MFMA kernel), activations run ``channels_last_3d`` (NDHWC).
+   decomposition onto the same MFMA kernel), activations run ``channels_last_3d`` (NDHWC);
+5. ``GroupNorm`` / ``InstanceNorm2d`` (+ ``ReLU``) in front of an eligible conv run in that
+   conv's input prologue (:class:`HipNormConv2d`, per-image affine from fp32 statistics);
+6. ``ConvTranspose2d(k=2, s=2)`` becomes a 1x1 MFMA conv + depth-to-space
+   (:class:`HipConvTranspose2x2`) and ``Conv2d(k=2, s=2)`` space-to-depth + a 1x1 MFMA conv
+   (:class:`HipConvStride2x2`).
 
-Convolutions that do not match (strided, dilated, grouped, 5x5, ...) stay on MIOpen.
+TorchScript-only weights go through :mod:`.ts_convert` (frozen graph rewrite).  Convolutions that
+do not match (3x3 strided, dilated, grouped, 5x5, ...) stay on MIOpen.
 """
 from __future__ import annotations
 
@@ -125,12 +131,155 @@ class HipConv3d(nn.Module):
         return f"{self.cin}, {self.cout}, k={self.pc.ks}, post_relu={self.post_relu}"
 
 
+def _group_affine(yh: torch.Tensor, groups: int, weight, bias, eps: float):
+    """Per-image, per-channel (scale, shift) [N, C] that apply GroupNorm to the NHWC tensor ``yh``
+    (statistics in fp32): what the next conv's prologue consumes instead of a normalised copy."""
+    N, H, W, C = yh.shape
+    var, mean = torch.var_mean(yh.float().view(N, H * W, groups, C // groups), dim=(1, 3), unbiased=False)
+    rstd = torch.rsqrt(var + eps)  # [N, G]
+    rstd_c = rstd.repeat_interleave(C // groups, dim=1)
+    mean_c = mean.repeat_interleave(C // groups, dim=1)
+    g = weight.float().view(1, C) if weight is not None else torch.ones(1, C, device=yh.device)
+    b = bias.float().view(1, C) if bias is not None else torch.zeros(1, C, device=yh.device)
+    scale = (rstd_c * g).contiguous()
+    return scale, (b - mean_c * scale).contiguous()
+
+
+def _norm_params(norm: nn.Module):
+    if isinstance(norm, nn.GroupNorm):
+        return norm.num_groups, norm.weight, norm.bias, norm.eps
+    return norm.num_features, norm.weight, norm.bias, norm.eps  # InstanceNorm2d: one group per channel
+
+
+def _instance_norm_ok(m: nn.Module) -> bool:
+    return isinstance(m, nn.InstanceNorm2d) and not m.track_running_stats
+
+
+class HipNormConv2d(nn.Module):
+    """GroupNorm / InstanceNorm (+ ReLU) of the incoming activation fused into the PROLOGUE of the
+    following conv: the statistics are reduced from the producer's NHWC output and the per-image
+    affine + ReLU are applied while the conv stages its input tiles in LDS (the same per-image
+    prologue the GroupNorm training engine uses), so the normalised tensor never exists."""
+
+    def __init__(self, norm: nn.Module, relu: bool, conv: nn.Conv2d, post_relu: bool = False):
+        super().__init__()
+        self.groups, w, b, self.eps = _norm_params(norm)
+        self.register_buffer("gn_weight", None if w is None else w.detach().float().clone())
+        self.register_buffer("gn_bias", None if b is None else b.detach().float().clone())
+        self.relu = relu
+        self.conv = HipConv2d(conv, post_relu)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            w = None if self.gn_weight is None else self.gn_weight.to(x.device).float()
+            b = None if self.gn_bias is None else self.gn_bias.to(x.device).float()
+            h = F.group_norm(x.float(), self.groups, w, b, self.eps)
+            return self.conv((torch.relu(h) if self.relu else h).to(x.dtype))
+        hc = self.conv
+        if hc._dev != x.device:
+            hc.pc.to(x.device)
+            hc._dev = x.device
+        N, C, H, W = x.shape
+        xh = x.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        scale, shift = _group_affine(xh, self.groups, self.gn_weight, self.gn_bias, self.eps)
+        if C != hc.pc.cin_pad:
+            xh = F.pad(xh, (0, hc.pc.cin_pad - C))
+            scale = F.pad(scale, (0, hc.pc.cin_pad - C))
+            shift = F.pad(shift, (0, hc.pc.cin_pad - C))
+        if hc.nchw_out:
+            return fused_conv2d(xh, hc.pc, scale=scale, shift=shift, relu=self.relu, out_nchw_f32=True,
+                                cout_valid=hc.cout, post_relu=hc.post_relu)
+        y = fused_conv2d(xh, hc.pc, scale=scale, shift=shift, relu=self.relu, post_relu=hc.post_relu)
+        return y.permute(0, 3, 1, 2)
+
+
+class HipConvTranspose2x2(nn.Module):
+    """ConvTranspose2d(k=2, stride=2) as a 1x1 MFMA conv to 4*Cout channels (one per output
+    sub-pixel) followed by a depth-to-space shuffle: each output pixel (2y+dy, 2x+dx) is
+    W[:, :, dy, dx]^T x[y, x] + b."""
+
+    def __init__(self, ct: nn.ConvTranspose2d):
+        super().__init__()
+        w = ct.weight.detach().float()  # [Cin, Cout, 2, 2]
+        self.cin, self.cout = w.shape[0], w.shape[1]
+        w1 = w.permute(2, 3, 1, 0).reshape(4 * self.cout, self.cin, 1, 1)  # row (dy*2+dx)*Cout + co
+        b1 = None if ct.bias is None else ct.bias.detach().float().repeat(4)
+        self.ref = ct
+        self.pc = PackedConv.from_weight(w1, b1)
+        self._dev = None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            return self.ref.to(x.device).float()(x.float()).to(x.dtype)
+        if self._dev != x.device:
+            self.pc.to(x.device)
+            self._dev = x.device
+        N, C, H, W = x.shape
+        xh = x.to(torch.bfloat16).permute(0, 2, 3, 1)
+        if C != self.pc.cin_pad:
+            xh = F.pad(xh, (0, self.pc.cin_pad - C))
+        y = fused_conv2d(xh.contiguous(), self.pc)  # [N, H, W, 4*Cout]
+        y = y.view(N, H, W, 2, 2, self.cout).permute(0, 1, 3, 2, 4, 5).reshape(N, 2 * H, 2 * W, self.cout)
+        return y.permute(0, 3, 1, 2)
+
+    def extra_repr(self) -> str:
+        return f"{self.cin}, {self.cout}, k=2, s=2 (1x1 MFMA + depth-to-space)"
+
+
+class HipConvStride2x2(nn.Module):
+    """Conv2d(k=2, stride=2) (strided-conv downsampling) as space-to-depth + a 1x1 MFMA conv over
+    4*Cin channels: out[y, x] = sum_{dy,dx} W[:, :, dy, dx] x[2y+dy, 2x+dx]."""
+
+    def __init__(self, conv: nn.Conv2d, post_relu: bool = False):
+        super().__init__()
+        w = conv.weight.detach().float()  # [Cout, Cin, 2, 2]
+        self.cin, self.cout = w.shape[1], w.shape[0]
+        w1 = w.permute(0, 2, 3, 1).reshape(self.cout, 4 * self.cin, 1, 1)  # col (dy*2+dx)*Cin + ci
+        self.post_relu = post_relu
+        self.ref = conv
+        self.nchw_out = self.cout % 4 != 0
+        self.pc = PackedConv.from_weight(w1, None if conv.bias is None else conv.bias.detach().float(),
+                                         cout_pad_to=16 if self.nchw_out else None)
+        self._dev = None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            y = self.ref.to(x.device).float()(x.float())
+            return (torch.relu(y) if self.post_relu else y).to(x.dtype)
+        if self._dev != x.device:
+            self.pc.to(x.device)
+            self._dev = x.device
+        N, C, H, W = x.shape
+        xh = x.to(torch.bfloat16).permute(0, 2, 3, 1)[:, : H // 2 * 2, : W // 2 * 2]
+        xs = xh.reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4 * C)
+        if 4 * C != self.pc.cin_pad:
+            xs = F.pad(xs, (0, self.pc.cin_pad - 4 * C))
+        xs = xs.contiguous()
+        if self.nchw_out:
+            return fused_conv2d(xs, self.pc, out_nchw_f32=True, cout_valid=self.cout, post_relu=self.post_relu)
+        return fused_conv2d(xs, self.pc, post_relu=self.post_relu).permute(0, 3, 1, 2)
+
+
+def _ct2x2_ok(m) -> bool:
+    return (type(m) is nn.ConvTranspose2d and m.kernel_size == (2, 2) and m.stride == (2, 2) and m.padding == (0, 0)
+            and m.output_padding == (0, 0) and m.dilation == (1, 1) and m.groups == 1)
+
+
+def _s2_ok(m) -> bool:
+    return (type(m) is nn.Conv2d and m.kernel_size == (2, 2) and m.stride == (2, 2) and m.padding == (0, 0)
+            and m.dilation == (1, 1) and m.groups == 1)
+
+
 def _hip_conv(conv, post_relu: bool = False):
     return HipConv3d(conv, post_relu) if isinstance(conv, nn.Conv3d) else HipConv2d(conv, post_relu)
 
 
 def _ok(conv) -> bool:
     return _eligible3d(conv) if isinstance(conv, nn.Conv3d) else _eligible(conv)
+
+
+def _is_norm(m) -> bool:
+    return isinstance(m, nn.GroupNorm) or _instance_norm_ok(m)
 
 
 def _rewrite(mod: nn.Module, stats: dict) -> None:
@@ -140,6 +289,41 @@ def _rewrite(mod: nn.Module, stats: dict) -> None:
             i = 0
             while i < len(items):
                 k, m = items[i]
+                # [GroupNorm|InstanceNorm, (ReLU), Conv] -> the norm runs in the conv's prologue
+                if _is_norm(m):
+                    j = i + 1
+                    relu = j < len(items) and isinstance(items[j][1], nn.ReLU)
+                    j += 1 if relu else 0
+                    nxt = items[j][1] if j < len(items) else None
+                    if type(nxt) is nn.Conv2d and _eligible(nxt):
+                        post = j + 1 < len(items) and isinstance(items[j + 1][1], nn.ReLU)
+                        child._modules[k] = HipNormConv2d(m, relu, nxt, post_relu=post)
+                        if relu:
+                            child._modules[items[i + 1][0]] = nn.Identity()
+                        child._modules[items[j][0]] = nn.Identity()
+                        if post:
+                            child._modules[items[j + 1][0]] = nn.Identity()
+                            stats["relu_fused"] += 1
+                        stats["norm_fused"] += 1
+                        stats["convs"] += 1
+                        i = j + 1 + (1 if post else 0)
+                        continue
+                    stats["norm_unfused"] += 1
+                    i += 1
+                    continue
+                if _ct2x2_ok(m):
+                    child._modules[k] = HipConvTranspose2x2(m)
+                    stats["conv_transpose"] += 1
+                    i += 1
+                    continue
+                if _s2_ok(m):
+                    relu = i + 1 < len(items) and isinstance(items[i + 1][1], nn.ReLU)
+                    child._modules[k] = HipConvStride2x2(m, post_relu=relu)
+                    if relu:
+                        child._modules[items[i + 1][0]] = nn.Identity()
+                    stats["strided"] += 1
+                    i += 2 if relu else 1
+                    continue
                 if type(m) in _CONV:
                     conv = m
                     j = i + 1
@@ -162,6 +346,12 @@ def _rewrite(mod: nn.Module, stats: dict) -> None:
                     continue
                 _rewrite(m, stats)
                 i += 1
+        elif _ct2x2_ok(child):
+            setattr(mod, name, HipConvTranspose2x2(child))
+            stats["conv_transpose"] += 1
+        elif _s2_ok(child):
+            setattr(mod, name, HipConvStride2x2(child))
+            stats["strided"] += 1
         elif type(child) in _CONV and _ok(child):
             setattr(mod, name, _hip_conv(child))
             stats["convs"] += 1
@@ -174,7 +364,8 @@ def _rewrite(mod: nn.Module, stats: dict) -> None:
 def optimize_for_mi355x(model: nn.Module, device=None) -> tuple[nn.Module, dict]:
     """In-place graph pass (model must be in eval mode).  Returns (model, stats)."""
     model.eval()
-    stats = {"convs": 0, "bn_folded": 0, "relu_fused": 0, "skipped": 0}
+    stats = {"convs": 0, "bn_folded": 0, "relu_fused": 0, "skipped": 0, "norm_fused": 0, "norm_unfused": 0,
+             "conv_transpose": 0, "strided": 0}
     _rewrite(model, stats)
     if device is not None:
         model.to(device)

@@ -24,38 +24,49 @@ MODEL_SRC = textwrap.dedent('''
     import torch.nn as nn
 
 
-    def conv_block(cin, cout):
+    def _norm(kind, c):
+        if kind == "group":
+            return nn.GroupNorm(min(8, c), c)
+        if kind == "instance":
+            return nn.InstanceNorm2d(c, affine=True)
+        return nn.BatchNorm2d(c)
+
+
+    def conv_block(cin, cout, norm="batch"):
         return nn.Sequential(
-            nn.Conv2d(cin, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True),
-            nn.Conv2d(cout, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+            nn.Conv2d(cin, cout, 3, padding=1), _norm(norm, cout), nn.ReLU(inplace=True),
+            nn.Conv2d(cout, cout, 3, padding=1), _norm(norm, cout), nn.ReLU(inplace=True))
 
 
     class UNet2d(nn.Module):
-        def __init__(self, in_channels=1, out_channels=2, features=(32, 64, 128, 256), final_activation="Sigmoid"):
+        def __init__(self, in_channels=1, out_channels=2, features=(32, 64, 128, 256), final_activation="Sigmoid",
+                     norm="batch", down="pool"):
             super().__init__()
             self.encoders = nn.ModuleList()
+            self.downs = nn.ModuleList()
             c = in_channels
             for f in features[:-1]:
-                self.encoders.append(conv_block(c, f))
+                self.encoders.append(conv_block(c, f, norm))
+                # 2x2 max-pool, or a learned 2x2 stride-2 convolution
+                self.downs.append(nn.MaxPool2d(2) if down == "pool" else nn.Conv2d(f, f, 2, stride=2))
                 c = f
-            self.pool = nn.MaxPool2d(2)
-            self.base = conv_block(c, features[-1])
+            self.base = conv_block(c, features[-1], norm)
             self.ups = nn.ModuleList()
             self.decoders = nn.ModuleList()
             c = features[-1]
             for f in reversed(features[:-1]):
                 self.ups.append(nn.ConvTranspose2d(c, f, 2, stride=2))
-                self.decoders.append(conv_block(2 * f, f))
+                self.decoders.append(conv_block(2 * f, f, norm))
                 c = f
             self.head = nn.Conv2d(c, out_channels, 1)
             self.act = getattr(nn, final_activation)() if final_activation else nn.Identity()
 
         def forward(self, x):
             skips = []
-            for enc in self.encoders:
+            for enc, down in zip(self.encoders, self.downs):
                 x = enc(x)
                 skips.append(x)
-                x = self.pool(x)
+                x = down(x)
             x = self.base(x)
             for up, dec, s in zip(self.ups, self.decoders, reversed(skips)):
                 x = dec(torch.cat([s, up(x)], dim=1))
@@ -111,15 +122,17 @@ MODEL3D_SRC = textwrap.dedent('''
 
 
 def _randomize_bn(net: torch.nn.Module, seed: int) -> None:
-    """Non-trivial eval statistics so BN folding is exercised."""
+    """Non-trivial eval statistics / affines so BN folding and GN/IN prologues are exercised."""
     g = torch.Generator().manual_seed(seed)
     with torch.no_grad():
         for m in net.modules():
             if isinstance(m, (torch.nn.BatchNorm2d, torch.nn.BatchNorm3d)):
                 m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
                 m.running_var.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
-                m.weight.copy_(torch.rand(m.num_features, generator=g) * 0.5 + 0.75)
-                m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+            if isinstance(m, (torch.nn.BatchNorm2d, torch.nn.BatchNorm3d, torch.nn.GroupNorm, torch.nn.InstanceNorm2d)) \
+                    and m.weight is not None:
+                m.weight.copy_(torch.rand(m.weight.shape[0], generator=g) * 0.5 + 0.75)
+                m.bias.copy_(torch.randn(m.bias.shape[0], generator=g) * 0.1)
 
 
 def load_module(path: Path, name: str = "bioimageio_model_src"):
@@ -131,13 +144,16 @@ def load_module(path: Path, name: str = "bioimageio_model_src"):
 
 def write_unet2d_package(out: str | Path, model_id: str = "demo-unet2d", in_channels: int = 1, out_channels: int = 2,
                          features=(32, 64, 128, 256), test_shape=(1, 1, 256, 256), seed: int = 0,
-                         torchscript: bool = True) -> Path:
+                         torchscript: bool = True, norm: str = "batch", down: str = "pool",
+                         state_dict: bool = True) -> Path:
+    """``norm``: batch / group / instance; ``down``: pool / conv (2x2 stride-2); ``state_dict=False``
+    writes a TorchScript-only package (the traced module is the only weights entry)."""
     out = Path(out)
     out.mkdir(parents=True, exist_ok=True)
     (out / "model.py").write_text(MODEL_SRC)
     mod = load_module(out / "model.py", f"pkg_{model_id.replace('-', '_')}")
     kwargs = {"in_channels": in_channels, "out_channels": out_channels, "features": list(features),
-              "final_activation": "Sigmoid"}
+              "final_activation": "Sigmoid", "norm": norm, "down": down}
     torch.manual_seed(seed)
     net = mod.UNet2d(**kwargs)
     _randomize_bn(net, seed)
@@ -161,11 +177,16 @@ def write_unet2d_package(out: str | Path, model_id: str = "demo-unet2d", in_chan
         "architecture": {"source": "model.py", "sha256": sha256_file(out / "model.py"), "callable": "UNet2d",
                          "kwargs": kwargs},
         "pytorch_version": "2.5"}}
-    if torchscript:
+    if torchscript or not state_dict:
         ts = torch.jit.trace(net, x[:, :, :64, :64])
         ts.save(str(out / "weights_torchscript.pt"))
         weights["torchscript"] = {"source": "weights_torchscript.pt", "sha256": sha256_file(out / "weights_torchscript.pt"),
-                                  "pytorch_version": "2.5", "parent": "pytorch_state_dict"}
+                                  "pytorch_version": "2.5"}
+        if state_dict:
+            weights["torchscript"]["parent"] = "pytorch_state_dict"
+    if not state_dict:
+        del weights["pytorch_state_dict"]
+        (out / "weights.pt").unlink()
     (out / "README.md").write_text(f"# {model_id}\n\nDemo 2-D U-Net (random weights) for the MI355X model runner.\n")
     rdf = {
         "format_version": "0.5.3", "type": "model", "id": model_id, "name": f"Demo U-Net 2D ({model_id})",

@@ -75,8 +75,13 @@ class PredictionPipeline:
     def _load(self, fmt, entry, optimize):
         root = self.root or Path(".")
         if fmt == "torchscript":
-            m = torch.jit.load(str(root / _src(entry)), map_location=self.device)
-            return m.eval()
+            m = torch.jit.load(str(root / _src(entry)), map_location=self.device).eval()
+            if optimize and self.device.type == "cuda":
+                from .ts_convert import optimize_torchscript
+
+                m, self.convert_stats = optimize_torchscript(m)
+                self.optimized = self.convert_stats["convs"] > 0
+            return m
         from .package import load_module
 
         arch = entry.get("architecture") if isinstance(entry, dict) else None
@@ -140,9 +145,11 @@ class PredictionPipeline:
     def _forward(self, xs: list[torch.Tensor]) -> list[torch.Tensor]:
         with torch.no_grad():
             if self.optimized:
+                # eager graph pass: the whole model is bf16; TorchScript rewrite: fp32 graph whose
+                # HIP convs take bf16 NHWC internally (a channels-last input is already NHWC)
+                dt = torch.float32 if self.weights_format == "torchscript" else torch.bfloat16
                 fmt = {4: torch.channels_last, 5: torch.channels_last_3d}
-                xs = [x.to(torch.bfloat16).contiguous(memory_format=fmt[x.dim()]) if x.dim() in fmt else
-                      x.to(torch.bfloat16) for x in xs]
+                xs = [x.to(dt).contiguous(memory_format=fmt[x.dim()]) if x.dim() in fmt else x.to(dt) for x in xs]
             y = self.model(*xs)
         ys = list(y) if isinstance(y, (tuple, list)) else [y]
         return [t.float() for t in ys]

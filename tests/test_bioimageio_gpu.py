@@ -61,3 +61,54 @@ def test_blocked_inference_gpu(gpu, pkg):
     tiled = pipe.predict(x, blocksize=8)["probabilities"]
     assert whole.shape == tiled.shape == (1, 2, 700, 530)
     assert np.corrcoef(whole.ravel(), tiled.ravel())[0, 1] > 0.98
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm,down", [("group", "conv"), ("instance", "pool")])
+def test_graph_pass_norm_and_strided_unets(gpu, tmp_path, norm, down):
+    """GroupNorm / InstanceNorm run in the next conv's prologue, 2x2 stride-2 convs as
+    space-to-depth + 1x1, transposed convs as 1x1 + depth-to-space: fp32-oracle numerics and the
+    package test through the optimised pipeline."""
+    import yaml
+
+    from bioengine_worker_amd.bioimageio.convert import optimize_for_mi355x
+    from bioengine_worker_amd.bioimageio.testing import test_model
+
+    p = write_unet2d_package(tmp_path / norm, f"gpu-{norm}", test_shape=(1, 1, 128, 128), torchscript=False,
+                             norm=norm, down=down, features=(32, 64, 128, 256))
+    mod = load_module(p / "model.py", f"gpu_{norm}_src")
+    kw = yaml.safe_load((p / "rdf.yaml").read_text())["weights"]["pytorch_state_dict"]["architecture"]["kwargs"]
+    net = mod.UNet2d(**kw).eval()
+    net.load_state_dict(torch.load(p / "weights.pt", weights_only=True))
+    x = torch.randn(2, 1, 128, 160)
+    with torch.no_grad():
+        ref = net.to(gpu)(x.to(gpu)).float().cpu()
+    net2, stats = optimize_for_mi355x(net, gpu)
+    assert stats["norm_fused"] == 7 and stats["conv_transpose"] == 3
+    assert stats["strided"] == (3 if down == "conv" else 0)
+    with torch.no_grad():
+        y = net2(x.to(gpu).bfloat16().contiguous(memory_format=torch.channels_last)).float().cpu()
+    assert (y - ref).abs().max() < 0.05, (y - ref).abs().max()
+    rep = test_model(p)
+    assert rep["status"] == "passed", rep
+    assert rep["details"][2]["optimized"] is True
+
+
+@pytest.mark.gpu
+def test_torchscript_only_package_is_optimized(gpu, tmp_path):
+    from bioengine_worker_amd.bioimageio import ts_convert
+    from bioengine_worker_amd.bioimageio.runner import PredictionPipeline
+    from bioengine_worker_amd.bioimageio.testing import test_model
+
+    p = write_unet2d_package(tmp_path / "ts", "gpu-ts-only", test_shape=(1, 1, 128, 128), state_dict=False)
+    pipe = PredictionPipeline(p, device=gpu)
+    assert pipe.weights_format == "torchscript" and pipe.optimized
+    assert pipe.convert_stats["convs"] == 15 and pipe.convert_stats["relu_fused"] == 14
+    before = ts_convert.COUNTS["hip"]
+    x = np.load(p / "test_input.npy")
+    y = pipe.predict(x)["probabilities"]
+    assert ts_convert.COUNTS["hip"] - before >= 15  # the convs ran on the HIP kernel
+    assert np.abs(y - np.load(p / "test_output.npy")).max() < 0.05
+    rep = test_model(p)
+    assert rep["status"] == "passed", rep
+    assert rep["details"][2]["optimized"] is True
