@@ -24,8 +24,18 @@ CHUNK = 1 << 20  # database rows per GEMM chunk
 
 
 class VectorIndex:
-    def __init__(self, dim: int = 768, device=None, ivf_threshold: int = 5_000_000, nprobe: int = 64):
+    """Tiers (reference FlatIP / IVFFlat / IVFPQ): ``index_type="auto"`` keeps exact bf16 search up
+    to ``ivf_threshold`` vectors, IVF-Flat above it and IVF-PQ (``search/ivfpq.py``, m=96 x 8 bit)
+    from ``ivfpq_threshold``; ``"flat"`` / ``"ivf"`` / ``"ivfpq"`` force a tier."""
+
+    def __init__(self, dim: int = 768, device=None, ivf_threshold: int = 5_000_000, nprobe: int = 64,
+                 index_type: str = "auto", ivfpq_threshold: int = 50_000_000, pq_m: int = 96, refine: int = 4):
         self.dim = dim
+        self.refine = refine  # IVF-PQ: re-rank refine*k PQ candidates with the stored vectors (0 = off)
+        self.kind = index_type
+        self.ivfpq_threshold = ivfpq_threshold
+        self.pq_m = pq_m
+        self.pq = None
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu"))
         self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
@@ -43,16 +53,33 @@ class VectorIndex:
 
     @property
     def index_type(self) -> str:
+        if self.pq is not None:
+            return self.pq.index_type
         return f"IVFFlat-GPU(nlist={self.centroids.shape[0]})" if self.centroids is not None else "FlatIP-GPU"
 
     def add(self, x) -> None:
         x = torch.as_tensor(np.asarray(x, np.float32) if not torch.is_tensor(x) else x).to(self.device, self.dtype)
         assert x.dim() == 2 and x.shape[1] == self.dim
         self.vecs = torch.cat([self.vecs, x], 0)
-        if self.centroids is not None:
+        if self.pq is not None:
+            self.pq.add(x.float())
+        elif self.kind == "ivfpq" or (self.kind == "auto" and self.ntotal >= self.ivfpq_threshold):
+            self.train_ivfpq()
+        elif self.centroids is not None:
             self._assign_new(x, self.ntotal - x.shape[0])
-        elif self.ntotal >= self.ivf_threshold:
+        elif self.kind == "ivf" or (self.kind == "auto" and self.ntotal >= self.ivf_threshold):
             self.train_ivf()
+
+    def train_ivfpq(self, nlist: int | None = None) -> None:
+        from .ivfpq import IVFPQIndex, default_nlist
+
+        n = self.ntotal
+        nl = nlist or min(default_nlist(n), max(1, n // 39))
+        pq = IVFPQIndex(self.dim, nl, self.pq_m, self.nprobe, self.device)
+        pq.train(self.vecs.float())
+        pq.add(self.vecs.float())
+        self.pq = pq
+        self.centroids = None
 
     def train_ivf(self, nlist: int | None = None, iters: int = 10, seed: int = 0) -> None:
         n = self.ntotal
@@ -89,6 +116,22 @@ class VectorIndex:
         k_eff = min(k, self.ntotal)
         if k_eff == 0:
             return np.full((Q, k), -np.inf, np.float32), np.full((Q, k), -1, np.int64)
+        if self.pq is not None:
+            if not self.refine or self.vecs.shape[0] != self.ntotal:
+                return self.pq.search(q.float(), k)
+            # IVF-PQ shortlist of refine*k, re-scored exactly with the stored vectors (IVFPQ+R)
+            _, cand = self.pq.search(q.float(), self.refine * k)
+            c = torch.from_numpy(cand).to(self.device)
+            ok = c >= 0
+            s = torch.einsum("qd,qkd->qk", q.float(), self.vecs[c.clamp(min=0)].float())
+            s = torch.where(ok, s, torch.full_like(s, -float("inf")))
+            ts, ti = torch.topk(s, min(k, s.shape[1]), dim=1)
+            ids = torch.where(torch.isfinite(ts), torch.gather(c, 1, ti), torch.full_like(ti, -1))
+            S = np.full((Q, k), -np.inf, np.float32)
+            I = np.full((Q, k), -1, np.int64)
+            S[:, : ts.shape[1]] = ts.cpu().numpy()
+            I[:, : ids.shape[1]] = ids.cpu().numpy()
+            return S, I
         if self.centroids is None:
             best_s = torch.full((Q, 0), -float("inf"), device=self.device)
             best_i = torch.empty(Q, 0, dtype=torch.long, device=self.device)
@@ -126,6 +169,10 @@ class VectorIndex:
         out.mkdir(parents=True, exist_ok=True)
         t0 = time.time()
         np.save(out / "vectors.npy", self.vecs.float().cpu().numpy().astype(np.float16))
+        if self.pq is not None:
+            self.pq.save(out)
+        else:
+            (out / "ivfpq_info.json").unlink(missing_ok=True)
         if self.centroids is not None:
             np.save(out / "ivf_centroids.npy", self.centroids.float().cpu().numpy())
         else:
@@ -146,6 +193,11 @@ class VectorIndex:
         v = np.load(p)  # allow_pickle=False
         idx = cls(dim=v.shape[1], device=device)
         idx.vecs = torch.from_numpy(v.astype(np.float32)).to(idx.device, idx.dtype)
+        if (out / "ivfpq_info.json").exists():
+            from .ivfpq import IVFPQIndex
+
+            idx.pq = IVFPQIndex.load(out, device=idx.device)
+            return idx
         c = out / "ivf_centroids.npy"
         if c.exists():
             idx.centroids = torch.from_numpy(np.load(c)).to(idx.device, idx.dtype)

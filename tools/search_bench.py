@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Cell-image-search latency per index tier (reference README: <5 ms Flat, <100 ms IVFPQ at 58 M
+vectors, ``apps/cell-image-search/README.md:130-134``).
+
+Synthetic clustered, L2-normalised 768-d embeddings (random cluster centres + noise) live on the
+GPU; for each N the bench builds the exact bf16 Flat tier and the IVF-PQ tier (m=96 x 8 bit,
+nlist per the reference range, nprobe=64; with and without exact re-ranking of 4k candidates) and
+reports p50 / p95 latency of a single query and of a 64-query batch (top-20), recall@20 against
+the exact ranking, and build time.  One JSON line per (N, tier).
+Usage: ``python tools/search_bench.py --n 1000000,10000000``
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def synth(n, d, dev, seed=0, chunk=1 << 22):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    centres = torch.nn.functional.normalize(torch.randn(4096, d, device=dev, generator=g), dim=1)
+    out = torch.empty(n, d, dtype=torch.bfloat16, device=dev)
+    for i in range(0, n, chunk):
+        m = min(chunk, n - i)
+        c = centres[torch.randint(0, 4096, (m,), device=dev, generator=g)]
+        out[i:i + m] = torch.nn.functional.normalize(c + 0.6 * torch.randn(m, d, device=dev, generator=g) / d ** 0.5 * 8,
+                                                     dim=1).bfloat16()
+    return out
+
+
+def timeit(fn, reps):
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2], ts[int(0.95 * (len(ts) - 1))]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", default="1000000,10000000")
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    from bioengine_worker_amd.search.index import VectorIndex
+    from bioengine_worker_amd.search.ivfpq import IVFPQIndex, default_nlist
+
+    dev = torch.device("cuda", 0)
+    for n in [int(v) for v in a.n.split(",")]:
+        x = synth(n, a.dim, dev)
+        gq = torch.Generator(device=dev).manual_seed(7)
+        qidx = torch.randint(0, n, (64,), device=dev, generator=gq)
+        q = torch.nn.functional.normalize(x[qidx].float() + 0.02 * torch.randn(64, a.dim, device=dev, generator=gq), dim=1)
+        flat = VectorIndex(dim=a.dim, device=dev, index_type="flat")
+        flat.vecs = x
+        gt = flat.search(q, a.k)[1]
+        for name, fn in (("flat_q1", lambda: flat.search(q[:1], a.k)), ("flat_q64", lambda: flat.search(q, a.k))):
+            fn()
+            p50, p95 = timeit(fn, a.reps)
+            print(json.dumps({"n": n, "tier": "FlatIP-GPU bf16", "query": name, "p50_ms": round(p50, 3),
+                              "p95_ms": round(p95, 3), "recall@20": 1.0}), flush=True)
+        t0 = time.perf_counter()
+        nl = default_nlist(n)
+        pq = IVFPQIndex(dim=a.dim, nlist=nl, m=96, nprobe=64, device=dev)
+        pq.train(x.float() if n <= 2_000_000 else x[torch.randperm(n, device=dev)[:2_000_000]].float())
+        pq.add(x)
+        torch.cuda.synchronize()
+        build = time.perf_counter() - t0
+        vi = VectorIndex(dim=a.dim, device=dev, index_type="ivfpq", refine=4)
+        vi.vecs, vi.pq = x, pq
+        for tier, search in (("IVFPQ-GPU m=96 nprobe=64", pq.search), ("IVFPQ-GPU + exact rerank 4k", vi.search)):
+            got = search(q, a.k)[1]
+            rec = float(np.mean([len(set(g) & set(r)) / a.k for g, r in zip(gt, got)]))
+            for name, qq in (("q1", q[:1]), ("q64", q)):
+                search(qq, a.k)
+                p50, p95 = timeit(lambda: search(qq, a.k), a.reps)
+                print(json.dumps({"n": n, "tier": tier, "query": name, "p50_ms": round(p50, 3), "p95_ms": round(p95, 3),
+                                  "recall@20": round(rec, 4), "nlist": pq.nlist, "build_s": round(build, 2),
+                                  "codes_gb": round(pq.codes.numel() / 1e9, 3)}), flush=True)
+        del x, flat, pq, vi
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
