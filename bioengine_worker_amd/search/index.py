@@ -102,8 +102,10 @@ class VectorIndex:
         a = torch.cat([(x[i:i + CHUNK] @ self.centroids.T).argmax(1) for i in range(0, x.shape[0], CHUNK)]).int()
         self.assign = torch.cat([self.assign, a])
         order = torch.argsort(self.assign, stable=True)
-        counts = torch.bincount(self.assign.long(), minlength=self.centroids.shape[0]).tolist()
-        self.lists = list(torch.split(order, counts))
+        counts = torch.bincount(self.assign.long(), minlength=self.centroids.shape[0])
+        self.sorted_ids = order  # vector ids grouped by list
+        self.list_off = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0)])
+        self.lists = list(torch.split(order, counts.tolist()))
 
     # ------------------------------------------------------------------ search
     @torch.no_grad()
@@ -143,22 +145,43 @@ class VectorIndex:
                 best_s, j = torch.topk(best_s, min(k_eff, best_s.shape[1]), dim=1)
                 best_i = torch.gather(best_i, 1, j)
         else:
-            probes = torch.topk((q @ self.centroids.T).float(), min(self.nprobe, self.centroids.shape[0]), dim=1).indices
-            best_s = torch.full((Q, k_eff), -float("inf"), device=self.device)
-            best_i = torch.full((Q, k_eff), -1, dtype=torch.long, device=self.device)
-            for qi in range(Q):
-                cand = torch.cat([self.lists[int(c)] for c in probes[qi].tolist()])
-                if cand.numel() == 0:
-                    continue
-                s = (self.vecs[cand] @ q[qi]).float()
-                ts, ti = torch.topk(s, min(k_eff, s.numel()))
-                best_s[qi, : ts.numel()] = ts
-                best_i[qi, : ts.numel()] = cand[ti]
+            best_s, best_i = self._search_ivf(q, k_eff)
         S = np.full((Q, k), -np.inf, np.float32)
         I = np.full((Q, k), -1, np.int64)
         S[:, : best_s.shape[1]] = best_s.cpu().numpy()
         I[:, : best_i.shape[1]] = best_i.cpu().numpy()
         return S, I
+
+    def _search_ivf(self, q: torch.Tensor, k: int, q_chunk: int = 8):
+        """Batched IVF-Flat: every query's probed lists become one padded candidate row (list-sorted
+        vector ids, located through the list offsets), scored with one batched GEMM per query chunk
+        and reduced with a single top-k -- no per-query Python loop."""
+        nl = self.centroids.shape[0]
+        probes = torch.topk((q @ self.centroids.T).float(), min(self.nprobe, nl), dim=1).indices
+        sizes = (self.list_off[1:] - self.list_off[:-1])[probes]  # [Q, nprobe]
+        cand_off = torch.cumsum(sizes, 1) - sizes
+        stride = int(sizes.sum(1).max())
+        Q = q.shape[0]
+        best_s = torch.full((Q, k), -float("inf"), device=self.device)
+        best_i = torch.full((Q, k), -1, dtype=torch.long, device=self.device)
+        if stride == 0:
+            return best_s, best_i
+        slots = torch.arange(stride, device=self.device)
+        for a in range(0, Q, q_chunk):
+            b = min(Q, a + q_chunk)
+            sl = slots.expand(b - a, stride).contiguous()
+            p = (torch.searchsorted(cand_off[a:b].contiguous(), sl, right=True) - 1).clamp(min=0)
+            lists = torch.gather(probes[a:b], 1, p)
+            within = sl - torch.gather(cand_off[a:b], 1, p)
+            valid = within < torch.gather(sizes[a:b], 1, p)
+            rows = (self.list_off[lists] + within).clamp(max=self.sorted_ids.numel() - 1)
+            ids = self.sorted_ids[rows]
+            sc = torch.bmm(self.vecs[ids], q[a:b, :, None]).squeeze(-1).float()
+            sc = torch.where(valid, sc, torch.full_like(sc, -float("inf")))
+            ts, ti = torch.topk(sc, min(k, stride), dim=1)
+            best_s[a:b, : ts.shape[1]] = ts
+            best_i[a:b, : ts.shape[1]] = torch.where(torch.isfinite(ts), torch.gather(ids, 1, ti), torch.full_like(ti, -1))
+        return best_s, best_i
 
     def reconstruct_batch(self, ids) -> np.ndarray:
         return self.vecs[torch.as_tensor(np.asarray(ids), device=self.device)].float().cpu().numpy()
