@@ -279,8 +279,11 @@ class CellposeFinetune:
                 import torch
 
                 with trace.span("app.stack", images=len(idxs)):
-                    batch = np.stack([reqs[i][1] for i in idxs])
+                    batch = self._stage_batch([reqs[i][1] for i in idxs], runner)
                 with self._gpu_lock:
+                    if torch.is_tensor(batch) and batch.is_cuda:  # H2D issued on the copy stream
+                        torch.cuda.current_stream(batch.device).wait_stream(self._h2d_stream)
+                        batch.record_stream(torch.cuda.current_stream(batch.device))
                     with trace.span("app.eval", images=len(idxs)):
                         m, f, _ = runner.eval(batch, **prm)
                     if m.is_cuda:
@@ -314,6 +317,24 @@ class CellposeFinetune:
             for j, i in enumerate(idxs):
                 out[i] = (masks[j], flows[j] if flows is not None and reqs[i][3] else None)
         return out
+
+    def _stage_batch(self, images: list, runner):
+        """Stack the batch straight into pinned host memory (one copy) and start its H2D on a copy
+        stream before taking the GPU lock, so the transfer overlaps the other in-flight batch's
+        kernels instead of sitting on the critical path."""
+        import torch
+
+        dev = getattr(runner, "device", None)
+        if dev is None or torch.device(dev).type != "cuda":
+            return np.stack(images)
+        a0 = images[0]
+        tdt = torch.from_numpy(np.empty(0, a0.dtype)).dtype
+        host = torch.empty((len(images),) + tuple(a0.shape), dtype=tdt, pin_memory=True)
+        np.stack(images, out=host.numpy())
+        if getattr(self, "_h2d_stream", None) is None:
+            self._h2d_stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(self._h2d_stream):
+            return host.to(dev, non_blocking=True)
 
     async def _images_from_artifact(self, artifact: str, paths: list[str]) -> list[np.ndarray]:
         server = await self._hub()
