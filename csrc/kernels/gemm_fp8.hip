@@ -13,7 +13,7 @@
 //   256x256 (8 waves, 128x64 per wave), K-step 128; chosen by shape so the grid fills 256 CUs while
 //   the bigger tiles halve the L2->LDS bytes per FLOP.  Both operands are staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR
 //   round trip) into two LDS buffers; the LDS image is linear per wave-instruction and the 16-byte
-//   chunk index of each 128-byte row is XOR-swizzled with (row & 7) on the SOURCE address and on
+//   chunk index of each 128-byte row is XOR-swizzled (frag_swz: conflict-free ds_read_b128) on the SOURCE address and on
 //   the ds_read address (cdna_hip_programming.md §5.4 rule 21), so the 16 rows a fragment read
 //   touches fall on distinct bank groups.
 // * The next K-tile's DMA stays in flight across the barrier (raw s_barrier + counted vmcnt),
@@ -38,16 +38,24 @@ typedef __attribute__((address_space(3))) void lds_void;
 // lgkmcnt[11:8]=15 | vmcnt[5:4] at [15:14].
 constexpr int waitcnt_vm(int n) { return (n & 0xf) | (0x7 << 4) | (0xf << 8) | ((n >> 4) << 14); }
 
+// XOR applied to the 16-byte chunk index of tile row `row`.  A ds_read_b128 of read_frag serves
+// four 16-lane groups, each = rows {0-3,12-15} at chunk c plus rows {4-11} at chunk c+2 (or the
+// mirror); two 128-byte rows share one 256-byte bank row, so the slot of (row, c) is
+// 8*(row&1) + (c ^ swz).  swz = row & 7 maps rows 4-11 onto the slots of rows 0-3/12-15 (every group
+// 2-way: SQ_LDS_BANK_CONFLICT = 4 cycles per read, measured); swz = (row >> 1) & 5 puts all 16
+// lanes of every group on distinct slots (exhaustive check over the four groups, both halves).
+__device__ __forceinline__ int frag_swz(int row) { return (row >> 1) & 5; }
+
 // Stage one R x 128-byte tile (rows r0.., k-bytes k0..) of a [rows, ld] fp8 matrix into LDS.
 // Each wave-instruction writes 8 rows (1 KiB, lane-linear); row groups go round-robin over waves.
 template <int R, int NW>
 __device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ g, long long ld, int r0, int rmax, int k0,
                                            uint8_t* lds_tile, int wave, int lane) {
   const int rin = lane >> 3;
-  const int chunk = (lane & 7) ^ rin;  // inverse swizzle on the source (involution)
 #pragma unroll
   for (int j = 0; j < R / 8 / NW; ++j) {
     const int grp = j * NW + wave;
+    const int chunk = (lane & 7) ^ frag_swz(grp * 8 + rin);  // inverse swizzle on the source (involution)
     int gr = r0 + grp * 8 + rin;
     gr = gr < rmax ? gr : rmax - 1;  // clamp ragged edges to a valid row; results are masked at store
     const uint8_t* src = g + (long long)gr * ld + k0 + chunk * 16;
@@ -59,7 +67,7 @@ __device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ g, long l
 // lane l holds row (l & 15), k-bytes [32*(l>>4), +32) as two swizzled 16-byte chunks.
 __device__ __forceinline__ i32x8 read_frag(const uint8_t* lds_tile, int row, int lane) {
   const int c0 = 2 * (lane >> 4);
-  const int sw = row & 7;
+  const int sw = frag_swz(row);
   const uint8_t* base = lds_tile + row * 128;
   const u32x4 lo = *reinterpret_cast<const u32x4*>(base + ((c0 ^ sw) << 4));
   const u32x4 hi = *reinterpret_cast<const u32x4*>(base + (((c0 + 1) ^ sw) << 4));
@@ -69,10 +77,25 @@ __device__ __forceinline__ i32x8 read_frag(const uint8_t* lds_tile, int row, int
   return f;
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// GELU(x) = x * Phi(x) with a branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, far below
+// the bf16 output's 2^-9 relative step): one v_rcp, one v_exp and a handful of FMAs, where the
+// library erff takes range branches that diverge inside a wave.
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float erf_z = 1.f - p * __expf(-z * z);  // erf(|x| / sqrt 2)
+  const float phi = 0.5f + 0.5f * copysignf(erf_z, x);
+  return x * phi;
+}
 
 // Block tile BM x BN = (WAVES_M * 16 * TM) x (WAVES_N * 16 * TN); each wave owns TM x TN MFMA tiles.
-template <int TM, int TN, int WAVES_M, int WAVES_N, int EPI>  // EPI 0: scale + bias, 1: + GELU(erf)
+// PRIO: s_setprio(1) around the MFMA cluster (cdna_hip_programming.md T5).
+template <int TM, int TN, int WAVES_M, int WAVES_N, int EPI, bool PRIO = false>  // EPI 0: scale + bias, 1: + GELU(erf)
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ W, const float* __restrict__ sx,
     const float* __restrict__ sw, const float* __restrict__ bias, bf16_t* __restrict__ Y, int M, int N, int K,
@@ -113,6 +136,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
     i32x8 bx[TM];
 #pragma unroll
     for (int b = 0; b < TM; ++b) bx[b] = read_frag(xt, wm + b * 16 + (lane & 15), lane);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int a = 0; a < TN; ++a) {
       const i32x8 aw = read_frag(wt, wn + a * 16 + (lane & 15), lane);
@@ -121,6 +145,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
         acc[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(aw, bx[b], acc[a][b], 0, 0, 0, E8M0_ONE, 0,
                                                                      E8M0_ONE);
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // WAR: the next iteration restages the buffer read here
   }
@@ -151,17 +176,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
   }
 }
 
-template <int TM, int TN, int WAVES_M, int WAVES_N>
+template <int TM, int TN, int WAVES_M, int WAVES_N, bool PRIO = false>
 int launch_gemm(const void* xq, const void* wq, const float* sx, const float* sw, const float* bias, void* y, int M,
                 int N, int K, int epi, hipStream_t s) {
   constexpr int BM = WAVES_M * 16 * TM, BN = WAVES_N * 16 * TN;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const dim3 grid((unsigned)(tiles_m * tiles_n)), block(64 * WAVES_M * WAVES_N);
   if (epi == 1)
-    hipLaunchKernelGGL((gemm_fp8_kernel<TM, TN, WAVES_M, WAVES_N, 1>), grid, block, 0, s, (const uint8_t*)xq,
+    hipLaunchKernelGGL((gemm_fp8_kernel<TM, TN, WAVES_M, WAVES_N, 1, PRIO>), grid, block, 0, s, (const uint8_t*)xq,
                        (const uint8_t*)wq, sx, sw, bias, (bf16_t*)y, M, N, K, tiles_n);
   else
-    hipLaunchKernelGGL((gemm_fp8_kernel<TM, TN, WAVES_M, WAVES_N, 0>), grid, block, 0, s, (const uint8_t*)xq,
+    hipLaunchKernelGGL((gemm_fp8_kernel<TM, TN, WAVES_M, WAVES_N, 0, PRIO>), grid, block, 0, s, (const uint8_t*)xq,
                        (const uint8_t*)wq, sx, sw, bias, (bf16_t*)y, M, N, K, tiles_n);
   return BE_CHECK_LAUNCH();
 }
@@ -221,7 +246,8 @@ extern "C" {
 // Y[M,N] bf16 = epi(Xq[M,K] e4m3 . Wq[N,K]^T e4m3 * sx[M] * sw[N] + bias[N]); epi 0 = none, 1 = GELU.
 // K % 128 == 0, N % 4 == 0; any M.  cfg selects the block tile (0 = by shape):
 //   1: 128x128 (4 waves, 64x64 each)   2: 256x128 (8 waves)   3: 128x256 (8 waves)
-//   4: 256x256 (8 waves, 128x64 each)
+//   4: 256x256 (8 waves, 128x64 each).  The 128x128 tile raises the wave priority around its MFMA
+//   cluster (+0-13 %, profiles/r02/fp8_gemm_bench_r02.md); on 256x256 that costs 6 %.
 int be_gemm_fp8(const void* xq, const void* wq, const float* sx, const float* sw, const float* bias, void* y, int M,
                 int N, int K, int epi, int cfg, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 4 != 0) return -1;
@@ -230,7 +256,7 @@ int be_gemm_fp8(const void* xq, const void* wq, const float* sx, const float* sw
     cfg = (K >= 2048 && t256 >= 256) ? 4 : 1;
   }
   switch (cfg) {
-    case 1: return launch_gemm<4, 4, 2, 2>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
+    case 1: return launch_gemm<4, 4, 2, 2, true>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     case 2: return launch_gemm<4, 4, 4, 2>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     case 3: return launch_gemm<4, 4, 2, 4>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     case 4: return launch_gemm<8, 4, 2, 4>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);

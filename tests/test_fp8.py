@@ -78,7 +78,8 @@ def test_gemm_fp8_matches_reference(gpu, M, N, K, gelu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tile_cfg", [1, 2, 3, 4])
-@pytest.mark.parametrize("M,N,K", [(1000, 640, 384), (257, 256, 128)])
+@pytest.mark.parametrize("M,N,K", [(1000, 640, 384), (257, 256, 128), (300, 516, 256), (520, 768, 3072),
+                                   (16448, 2304, 768)])
 def test_gemm_fp8_tile_configs(gpu, tile_cfg, M, N, K):
     g = torch.Generator().manual_seed(tile_cfg)
     x = (torch.randn(M, K, generator=g) + torch.arange(K) / K).bfloat16()
@@ -89,6 +90,10 @@ def test_gemm_fp8_tile_configs(gpu, tile_cfg, M, N, K):
     lin.to(gpu)
     y = linear_fp8(xq.to(gpu), sx.to(gpu), lin.wq, lin.sw, lin.bias, tile_cfg=tile_cfg).float().cpu()
     assert (y - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
+    if M == 300:  # GELU epilogue on a ragged shape with two K-tiles
+        refg = linear_fp8_ref(xq, sx, lin.wq.cpu(), lin.sw.cpu(), lin.bias.cpu(), gelu=True).float()
+        yg = linear_fp8(xq.to(gpu), sx.to(gpu), lin.wq, lin.sw, lin.bias, True, tile_cfg=tile_cfg).float().cpu()
+        assert (yg - refg).abs().max().item() <= 1e-2 * refg.abs().max().item() + 1e-2
 
 
 @pytest.mark.gpu
