@@ -171,6 +171,21 @@ def _plan_masks(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps)
     ``(jobs_by_bucket, scratch_total, niter_img)``; ``kind`` 0 = diffusion (LDS need / scratch of
     :func:`_diffuse_lds_bytes` / :func:`_diffuse_scratch_doubles`, and cellpose's per-image
     ``niter_img``), 1 = hole filling (``R`` bytes).  Job order inside a bucket is arbitrary."""
+    return _plan_finish([_plan_launch(bbox, valid, kind, caps)])[0]
+
+
+def _plan_finish(launched: list) -> list:
+    """Read back the bucket sizes of several :func:`_plan_launch` plans with ONE host sync."""
+    host = torch.cat([torch.cat([counts.long(), tot]) for _, counts, tot, _ in launched]).cpu().tolist()
+    out, o = [], 0
+    for jobs, counts, _, niter_img in launched:
+        nb = counts.shape[0]
+        out.append(([jobs[k, :host[o + k]] for k in range(nb)], int(host[o + nb]), niter_img))
+        o += nb + 1
+    return out
+
+
+def _plan_launch(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps):
     B, nlab = bbox.shape[:2]
     dev = bbox.device
     n = B * nlab
@@ -184,8 +199,7 @@ def _plan_masks(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps)
     _native.call("be_cp_plan_masks", _native.ptr(bbox.contiguous()), vptr, B, nlab, kind, ctypes.addressof(carr),
                  len(caps), _native.ptr(jobs), _native.ptr(counts), _native.ptr(tot), _native.ptr(niter_img),
                  _native.stream(dev))
-    host = torch.cat([counts.long(), tot]).cpu().tolist()  # the one sync
-    return [jobs[k, :host[k]] for k in range(nb)], int(host[nb]), niter_img
+    return jobs, counts, tot, niter_img
 
 
 def _diffuse_lds_bytes(ly, lx):
@@ -202,6 +216,7 @@ def _diffuse_scratch_doubles(ly, lx):
 #: bucket's LDS, so small masks run many blocks per CU (one 48 KiB reservation per mask allowed 3).
 DIFFUSE_BUCKETS = ((6 * 1024, 64), (12 * 1024, 128), (24 * 1024, 256), (48 * 1024, 256), (80 * 1024, 512),
                    (LDS_DIFFUSE_BYTES, 512))
+DIFFUSE_CAPS = [c for c, _ in DIFFUSE_BUCKETS]
 #: rows per work item of the diffusion sweep (``BE_DIFFUSE_DV``): a smaller DV gives every mask
 #: proportionally more threads (buckets scale up to 1024) and a shorter serial LDS chain per sweep
 DIFFUSE_DV = 4
@@ -248,7 +263,12 @@ def _bucket_small(slices):
 
 def _diffuse_small(Mc, buckets, niter_img, L, st, ready=None) -> None:
     """``ready``: event recorded on the current stream once the inputs exist; the buckets start
-    from it instead of from the stream's tail, so they run alongside the big-mask kernel."""
+    from it instead of from the stream's tail, so they run alongside the big-mask kernel.
+
+    Every bucket kernel runs ``niter`` dependent sweeps, so its time grows with its mask size and a
+    stream's tail is the sum of its buckets: the buckets (largest first) go to the queues in snake
+    order (0, 1, .., n-1, n-1, .., 0), and without a big-mask kernel the main stream is one of the
+    queues (4 hardware queues per process: main + 3 side streams)."""
     B, H, W = Mc.shape
     concurrent = Mc.is_cuda and N_SIDE_STREAMS > 0
     if concurrent:
@@ -259,12 +279,18 @@ def _diffuse_small(Mc, buckets, niter_img, L, st, ready=None) -> None:
                 sd.wait_event(ready)
             else:
                 sd.wait_stream(main)
-    for i, cap, threads, jobs in buckets:
+        queues = sides if ready is not None else [None] + sides  # None = the main stream itself
+        nq = len(queues)
+    for k, (i, cap, threads, jobs) in enumerate(buckets):
         if concurrent:
-            sd = sides[i % len(sides)]
-            for t in (jobs, Mc, niter_img, L):
-                t.record_stream(sd)
-            sptr = ctypes.c_void_p(sd.cuda_stream)
+            r = k % (2 * nq)
+            sd = queues[r if r < nq else 2 * nq - 1 - r]
+            if sd is None:
+                sptr = st
+            else:
+                for t in (jobs, Mc, niter_img, L):
+                    t.record_stream(sd)
+                sptr = ctypes.c_void_p(sd.cuda_stream)
         else:
             sptr = st
         _native.call("be_cp_diffuse_nt", _native.ptr(Mc), _native.ptr(jobs), jobs.shape[0], H, W,
@@ -343,22 +369,25 @@ def mask_bboxes(M: torch.Tensor, nlab: int) -> torch.Tensor:
 
 
 def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: int | None = None,
-                       nlab: int | None = None):
+                       nlab: int | None = None, counts: torch.Tensor | None = None, plan=None):
     """Heat-diffusion flows of label images M [B, H, W] int32 (labels 1..n, contiguous per image).
 
     Returns (mu [B, 2, H, W] fp32, err_sum [B, nlab] fp32 or None, counts [B, nlab]).  When ``dp``
     ([B, >=2, H, W] network output) is given, err_sum[b, l] = sum over mask l of |mu - dp/5|^2.
+    ``counts`` / ``plan`` (label_counts and a kind-0 plan of the same labels) skip recomputing them.
     """
     B, H, W = M.shape
     dev = M.device
     if nlab is None:  # an upper bound on the labels + 1 is enough (absent labels have no pixels)
         nlab = int(M.max().item()) + 1 if M.numel() else 1
     mu = torch.zeros(B, 2, H, W, dtype=torch.float32, device=dev)
-    counts = label_counts(M, nlab)
+    if counts is None:
+        counts = label_counts(M, nlab)
     if nlab <= 1:
         return mu, (torch.zeros(B, nlab, device=dev) if dp is not None else None), counts
-    bbox = mask_bboxes(M, nlab)
-    slices, ssize, niter_img = _plan_masks(bbox, None, 0, [c for c, _ in DIFFUSE_BUCKETS])
+    if plan is None:
+        plan = _plan_masks(mask_bboxes(M, nlab), None, 0, DIFFUSE_CAPS)
+    slices, ssize, niter_img = plan
     if niter is not None:
         niter_img = torch.full((B,), niter, dtype=torch.int32, device=dev)
     bj = slices[-1]
@@ -414,10 +443,23 @@ def fill_holes_gpu(M: torch.Tensor, min_size: int = 15, nlab: int | None = None)
     if min_size > 0:
         keep &= counts >= min_size
     keep[:, 0] = False
-    lut = (torch.cumsum(keep.int(), dim=1) * keep.int()).to(torch.int32).contiguous()
-    bbox = mask_bboxes(M, nlab)
+    plan = _plan_masks(mask_bboxes(M, nlab), keep, 1, [LDS_FILL_BYTES])
+    return _fill_run(M, _rank_lut(keep), nlab, plan)
+
+
+def _rank_lut(keep: torch.Tensor) -> torch.Tensor:
+    """keep [B, nlab] bool -> int32 lut: kept label -> its rank 1..k (id order), dropped -> 0."""
+    keep = keep.clone()
+    keep[:, 0] = False
+    return (torch.cumsum(keep.int(), dim=1) * keep.int()).to(torch.int32).contiguous()
+
+
+def _fill_run(M: torch.Tensor, lut: torch.Tensor, nlab: int, plan) -> torch.Tensor:
+    """Hole filling of the planned jobs (a kind-1 plan); jobs whose lut entry is 0 write nothing."""
+    B, H, W = M.shape
+    dev = M.device
     out = torch.zeros_like(M)
-    (sj, bj), ssize, _ = _plan_masks(bbox, keep, 1, [LDS_FILL_BYTES])
+    (sj, bj), ssize, _ = plan
     if sj.shape[0] + bj.shape[0] == 0:
         return out
     scratch = torch.empty(max(ssize, 1), dtype=torch.uint8, device=dev)
@@ -433,8 +475,9 @@ def fill_holes_gpu(M: torch.Tensor, min_size: int = 15, nlab: int | None = None)
 
 
 def follow_and_label(y: torch.Tensor, niter: int = 200, cellprob_threshold: float = 0.0,
-                     max_size_fraction: float = 0.4) -> torch.Tensor:
-    """Network output y [B, 3, H, W] -> raw masks M0 [B, H, W] int32 (before QC / fill)."""
+                     max_size_fraction: float = 0.4, with_bound: bool = False):
+    """Network output y [B, 3, H, W] -> raw masks M0 [B, H, W] int32 (before QC / fill); with
+    ``with_bound`` also an upper bound on its labels + 1 (known from the seed count, no extra sync)."""
     B, _, H, W = y.shape
     dev = y.device
     st = _native.stream(dev)
@@ -457,7 +500,7 @@ def follow_and_label(y: torch.Tensor, niter: int = 200, cellprob_threshold: floa
     M1 = torch.zeros(B, Hp, Wp, dtype=torch.int32, device=dev)
     M0 = torch.zeros(B, H, W, dtype=torch.int32, device=dev)
     if kmax == 0:
-        return M0
+        return (M0, 1) if with_bound else M0
     # seeds are compacted at the front of each row: sort only the first kmax slots (a few hundred)
     # instead of the whole cap-wide buffer of sentinels
     keys_sorted, _ = torch.sort(keys[:, :kmax].contiguous(), dim=1)
@@ -469,17 +512,33 @@ def follow_and_label(y: torch.Tensor, niter: int = 200, cellprob_threshold: floa
                  _native.ptr(counts), nlab, st)
     big = H * W * max_size_fraction
     keep = (counts > 0) & (counts <= big)
-    return _renumber(M0, keep)
+    M = _renumber(M0, keep)
+    return (M, nlab) if with_bound else M
 
 
 def compute_masks_gpu(y: torch.Tensor, niter: int = 200, cellprob_threshold: float = 0.0, flow_threshold: float = 0.4,
                       min_size: int = 15, max_size_fraction: float = 0.4) -> torch.Tensor:
     """Full Cellpose mask recovery for a batch: y [B, 3, H, W] -> masks [B, H, W] int32."""
-    M = follow_and_label(y, niter, cellprob_threshold, max_size_fraction)
-    nlab = int(M.max().item()) + 1 if M.numel() else 1  # the one label-count sync; QC only removes labels
-    if flow_threshold is not None and flow_threshold > 0 and nlab > 1:
-        _, err, counts = masks_to_flows_gpu(M, dp=y, nlab=nlab)
-        merr = err / counts.clamp(min=1).float()
-        keep = (counts > 0) & ~(merr > flow_threshold)
-        M = _renumber(M, keep)
-    return fill_holes_gpu(M, min_size, nlab=nlab)
+    M, nlab = follow_and_label(y, niter, cellprob_threshold, max_size_fraction, with_bound=True)
+    if nlab <= 1:
+        return M
+    # Label counts, boxes and BOTH job plans (QC diffusion, hole filling) come from the raw labels,
+    # read back with one host sync.  QC only drops labels: the fill then runs on the raw ids with
+    # QC-dropped masks zeroed (identical geometry to renumbering first) and a lut that ranks the
+    # labels kept by QC and min_size in id order (= QC renumber followed by the fill's renumber).
+    counts = label_counts(M, nlab)
+    bbox = mask_bboxes(M, nlab)
+    fill_keep = counts > 0
+    if min_size > 0:
+        fill_keep &= counts >= min_size
+    fill_keep[:, 0] = False
+    qc = flow_threshold is not None and flow_threshold > 0
+    plans = _plan_finish(([_plan_launch(bbox, None, 0, DIFFUSE_CAPS)] if qc else [])
+                         + [_plan_launch(bbox, fill_keep, 1, [LDS_FILL_BYTES])])
+    if qc:
+        _, err, _ = masks_to_flows_gpu(M, dp=y, nlab=nlab, counts=counts, plan=plans[0])
+        qc_keep = (counts > 0) & ~(err / counts.clamp(min=1).float() > flow_threshold)
+        qc_keep[:, 0] = False
+        M = torch.gather(qc_keep.to(torch.int32), 1, M.reshape(M.shape[0], -1).long()).reshape(M.shape) * M
+        fill_keep &= qc_keep
+    return _fill_run(M.contiguous(), _rank_lut(fill_keep), nlab, plans[-1])

@@ -276,10 +276,12 @@ class CPnetEngine:
 
     def _style_shifts(self, style: torch.Tensor) -> dict:
         st = style if self.style_on else torch.zeros_like(style)
-        shifts_all = styleops.style_shifts(st, self.style_w, self.style_b, self.style_s, self.style_t)
+        return self._split_shifts(styleops.style_shifts(st, self.style_w, self.style_b, self.style_s, self.style_t))
+
+    def _split_shifts(self, shifts_all: torch.Tensor) -> dict:
         out = {}
-        for (i, k, off, c) in self._feat_slices:
-            out[(i, k)] = shifts_all[:, off: off + c].contiguous()
+        for (i, k, off, c) in self._feat_slices:  # row-strided views: the conv reads them in place
+            out[(i, k)] = shifts_all[:, off: off + c]
         return out
 
     @torch.no_grad()
@@ -294,8 +296,9 @@ class CPnetEngine:
             x1 = e["c1"](h, residual=proj)
             h = e["c2"](x1)
             xd.append(e["c3"](h, residual=x1))
-        style = styleops.make_style(xd[-1])
-        shifts = self._style_shifts(style)
+        style, shifts_all = styleops.style_and_shifts(xd[-1], self.style_w, self.style_b, self.style_s, self.style_t,
+                                                      self.style_on)
+        shifts = self._split_shifts(shifts_all)
         nup = len(self.up)
         xcur = xd[-1]
         for i in range(nup - 1, -1, -1):

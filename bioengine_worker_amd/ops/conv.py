@@ -190,6 +190,20 @@ def choose_nw(pc: PackedConv, H: int, W: int, inmode: str = "none", has_x2: bool
     return 4
 
 
+def _affine_stride(t: torch.Tensor | None, N: int, C: int) -> int:
+    """Row stride (elements) of a per-image [N, C] fp32 affine, 0 for a shared [C] one."""
+    if t is None:
+        return 0
+    assert t.dtype == torch.float32
+    if t.dim() == 2:
+        assert t.shape == (N, C) and t.stride(1) == 1, "per-image affine must be [N, C] with unit column stride"
+        ns = t.stride(0) if N > 1 else C
+        assert ns % 4 == 0 and t.data_ptr() % 16 == 0, "per-image affine rows must be 16-byte aligned"
+        return ns
+    assert t.is_contiguous() and t.numel() == C
+    return 0
+
+
 def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=None, relu=False, residual=None,
                  inmode: str = "none", out_nchw_f32: bool = False, cout_valid: int | None = None,
                  nw: int | None = None, post_relu: bool = False, out: torch.Tensor | None = None,
@@ -234,20 +248,10 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
         assert x2.shape == (N, H, W, Cin) and x2.dtype == torch.bfloat16 and x2.is_contiguous()
     if residual is not None:
         assert residual.shape == (N, H, W, pc.cout) and residual.dtype == torch.bfloat16 and residual.is_contiguous()
-    pscale_ns = 0
-    if scale is not None:
-        assert scale.dtype == torch.float32 and scale.is_contiguous()
-        if scale.dim() == 2:  # per-image affine (GroupNorm): [N, Cin]
-            assert scale.shape == (N, Cin)
-            pscale_ns = Cin
-        else:
-            assert scale.numel() == Cin
-    pshift_ns = 0
-    if shift is not None:
-        assert shift.dtype == torch.float32 and shift.is_contiguous()
-        pshift_ns = Cin if shift.dim() == 2 else 0
-        if shift.dim() == 2:
-            assert shift.shape == (N, Cin)
+    # per-image affines ([N, Cin], GroupNorm scale / style shift) may be row-strided views (e.g. column
+    # slices of one stacked style GEMM output): rows are read as float4 runs at n * row_stride + c
+    pscale_ns = _affine_stride(scale, N, Cin)
+    pshift_ns = _affine_stride(shift, N, Cin)
     _native.call(
         "be_conv2d_nhwc",
         _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns, pscale_ns,

@@ -13,7 +13,7 @@ import torch
 
 from . import _native
 
-_native.register_hip_signatures({"be_nhwc_channel_sum": "ppiiiiis"})
+_native.register_hip_signatures({"be_nhwc_channel_sum": "ppiiiiis", "be_style_shift": "piifppppiipps"})
 
 
 def nhwc_channel_sum(x: torch.Tensor, square: bool = False) -> torch.Tensor:
@@ -41,3 +41,21 @@ def make_style(x: torch.Tensor) -> torch.Tensor:
 def style_shifts(style: torch.Tensor, w: torch.Tensor, b: torch.Tensor, s: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
     feat = torch.addmm(b, style, w.t())
     return torch.addcmul(t, feat, s)
+
+
+def style_and_shifts(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, s: torch.Tensor, t: torch.Tensor,
+                     style_on: bool = True) -> tuple[torch.Tensor, torch.Tensor]:
+    """(make_style(x), style_shifts(style or 0, w, b, s, t)) for NHWC ``x``: on the GPU the pooled sum
+    is one reduction launch and everything after it ONE kernel (``be_style_shift``)."""
+    N, H, W_, C = x.shape
+    J = w.shape[0]
+    if not x.is_cuda or C % 4 or C > 1024:
+        st = make_style(x)
+        return st, style_shifts(st if style_on else torch.zeros_like(st), w, b, s, t)
+    sums = nhwc_channel_sum(x)
+    style = torch.empty(N, C, device=x.device, dtype=torch.float32)
+    shifts = torch.empty(N, J, device=x.device, dtype=torch.float32)
+    _native.call("be_style_shift", _native.ptr(sums), N, C, 1.0 / float(H * W_), _native.ptr(w), _native.ptr(b),
+                 _native.ptr(s), _native.ptr(t), J, int(bool(style_on)), _native.ptr(style), _native.ptr(shifts),
+                 _native.stream(x.device))
+    return style, shifts

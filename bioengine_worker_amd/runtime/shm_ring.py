@@ -26,6 +26,11 @@ class RingClosed(RuntimeError):
     pass
 
 
+def _populate_default() -> int:
+    """Pre-fault ring mappings (``BE_RING_POPULATE``, default on): see ``map_ring`` in shm_ring.cpp."""
+    return 0 if os.environ.get("BE_RING_POPULATE", "1") in ("0", "false", "no") else 1
+
+
 def _addr(buf) -> int:
     """Address of a (possibly read-only) contiguous buffer without copying it."""
     a = np.frombuffer(buf, dtype=np.uint8)
@@ -43,18 +48,20 @@ class ShmRing:
         self._rt = _native.runtime()
 
     @classmethod
-    def create(cls, capacity: int = 256 << 20, name: str | None = None) -> "ShmRing":
+    def create(cls, capacity: int = 256 << 20, name: str | None = None, populate: bool | None = None) -> "ShmRing":
         name = name or f"/be-ring-{os.getpid()}-{uuid.uuid4().hex[:10]}"
         h = ctypes.c_void_p()
-        rc = _native.runtime().be_rt_ring_create(name.encode(), int(capacity), ctypes.byref(h))
+        pop = _populate_default() if populate is None else int(bool(populate))
+        rc = _native.runtime().be_rt_ring_create(name.encode(), int(capacity), ctypes.byref(h), pop)
         if rc != 0:
             raise OSError(-rc, f"shm ring create {name}: {os.strerror(-rc)}")
         return cls(h.value, name, True)
 
     @classmethod
-    def open(cls, name: str) -> "ShmRing":
+    def open(cls, name: str, populate: bool | None = None) -> "ShmRing":
         h = ctypes.c_void_p()
-        rc = _native.runtime().be_rt_ring_open(name.encode(), ctypes.byref(h))
+        pop = _populate_default() if populate is None else int(bool(populate))
+        rc = _native.runtime().be_rt_ring_open(name.encode(), ctypes.byref(h), pop)
         if rc != 0:
             raise OSError(-rc, f"shm ring open {name}: {os.strerror(-rc)}")
         return cls(h.value, name, False)
@@ -83,8 +90,9 @@ class ShmRing:
             raise OSError(-rc, f"shm ring write: {os.strerror(-rc)}")
 
     # ------------------------------------------------------------------ consumer
-    def read(self, timeout_s: float | None = 60.0) -> bytearray:
-        """Next frame's payload as a fresh (writable) bytearray."""
+    def read(self, timeout_s: float | None = 60.0) -> np.ndarray:
+        """Next frame's payload as a fresh writable uint8 array (``np.empty``: no zero-fill pass before
+        the copy, unlike ``bytearray(n)``)."""
         n = ctypes.c_int64()
         rc = self._rt.be_rt_ring_next_len(self._h, ctypes.byref(n), -1 if timeout_s is None else int(timeout_s * 1e6))
         if rc == EAGAIN_TIMEOUT:
@@ -93,9 +101,8 @@ class ShmRing:
             raise RingClosed(self.name)
         if rc != 0:
             raise OSError(-rc, f"shm ring wait: {os.strerror(-rc)}")
-        out = bytearray(n.value)
-        dst = (ctypes.c_char * len(out)).from_buffer(out) if out else None
-        rc = self._rt.be_rt_ring_read(self._h, dst, n.value)
+        out = np.empty(n.value, np.uint8)
+        rc = self._rt.be_rt_ring_read(self._h, ctypes.c_void_p(out.ctypes.data if n.value else 0), n.value)
         if rc != 0:
             raise OSError(-rc, "shm ring read")
         return out

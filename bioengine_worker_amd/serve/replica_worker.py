@@ -241,6 +241,7 @@ def main():
         prof.disable()
         with open(prof_path.replace("{pid}", str(os.getpid())), "w") as f:
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
+            pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(80)
 
 
 if __name__ == "__main__":

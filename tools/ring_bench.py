@@ -35,8 +35,8 @@ async def run(ring_mb: int, sizes, reps: int) -> dict:
     ctrl_mod.set_controller(None)
     h = await serve.run(Echo.bind(), name=f"echo{ring_mb}")
     out = {}
-    for mb in sizes:
-        a = np.ones(mb * (1 << 18), np.float32)
+    for kib in sizes:
+        a = np.ones(kib * 256, np.float32)
         await h.echo.remote(a)
         t = []
         for _ in range(reps):
@@ -44,7 +44,7 @@ async def run(ring_mb: int, sizes, reps: int) -> dict:
             await h.echo.remote(a)
             t.append(time.perf_counter() - t0)
         ms = 1e3 * float(np.median(t))
-        out[f"{mb}MiB"] = {"ms": round(ms, 3), "GB/s": round(2 * a.nbytes / ms / 1e6, 2)}
+        out[f"{kib}KiB"] = {"ms": round(ms, 3), "GB/s": round(2 * a.nbytes / ms / 1e6, 2)}
     await serve.delete(f"echo{ring_mb}")
     ctrl_mod.set_controller(None)
     return out
@@ -53,7 +53,7 @@ async def run(ring_mb: int, sizes, reps: int) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--sizes", default="1,16,64,256")
+    ap.add_argument("--sizes", default="4,1024,16384,65536,262144", help="payload sizes in KiB")
     a = ap.parse_args()
     sizes = [int(s) for s in a.sizes.split(",")]
     res = {"socket": asyncio.run(run(0, sizes, a.reps)), "shm_ring": asyncio.run(run(512, sizes, a.reps))}

@@ -59,6 +59,14 @@ async def main_async(a) -> list[dict]:
     for i in range(3):  # warm-up: model build, kernels, graph pass, batch shapes
         await asyncio.gather(*[app.infer(input_arrays=[imgs[j % 16]], model=a.model) for j in range(8)])
     results = []
+    if a.layer == "handle":  # bypass the hub RPC + app-service bridge: router -> replica only
+        handle = w.apps_manager.apps[aid]["bridge"].handle
+
+        class _H:
+            async def infer(self, **kw):
+                return await handle.infer.remote(**kw)
+
+        app = _H()
     for conc in a.concurrency:
         lat: list[float] = []
         stop = time.perf_counter() + a.seconds
@@ -87,13 +95,14 @@ async def main_async(a) -> list[dict]:
 
             prof.disable()
             buf = io.StringIO()
-            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
+            pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(120)
             Path(a.profile).write_text(buf.getvalue())
         ms = np.array(lat) * 1e3
         r = {"concurrency": conc, "requests": len(lat), "imgs_per_s": round(len(lat) / dt, 1),
              "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
              "p99_ms": round(float(np.percentile(ms, 99)), 2), "image": [a.size, a.size, 2], "gpus": a.gpus,
-             "replica_mode": os.environ["BIOENGINE_REPLICA_MODE"]}
+             "replica_mode": os.environ["BIOENGINE_REPLICA_MODE"], "layer": a.layer}
         results.append(r)
         print(json.dumps(r), flush=True)
     st = await svc.get_app_status(application_ids=[aid])
@@ -115,6 +124,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--replica-mode", default="process", choices=["process", "local"])
     ap.add_argument("--max-ongoing", type=int, default=64, help="deploy_app max_ongoing_requests")
+    ap.add_argument("--layer", default="hub", choices=["hub", "handle"],
+                    help="hub: client -> hub RPC -> app service -> router (default); handle: router directly")
     ap.add_argument("--model", default="cyto3", help="built-in model served (headline: cyto3 CPnet)")
     ap.add_argument("--profile", default=None, metavar="PATH",
                     help="cProfile the worker-side event loop during the highest-concurrency phase")
