@@ -533,7 +533,10 @@ def compute_masks_gpu(y: torch.Tensor, niter: int = 200, cellprob_threshold: flo
         fill_keep &= counts >= min_size
     fill_keep[:, 0] = False
     qc = flow_threshold is not None and flow_threshold > 0
-    plans = _plan_finish(([_plan_launch(bbox, None, 0, DIFFUSE_CAPS)] if qc else [])
+    # masks below min_size are dropped whatever their flow error: the QC diffusion skips them (the
+    # plan still takes cellpose's per-image niter over ALL masks, so the kept masks' flows are
+    # unchanged)
+    plans = _plan_finish(([_plan_launch(bbox, fill_keep, 0, DIFFUSE_CAPS)] if qc else [])
                          + [_plan_launch(bbox, fill_keep, 1, [LDS_FILL_BYTES])])
     if qc:
         _, err, _ = masks_to_flows_gpu(M, dp=y, nlab=nlab, counts=counts, plan=plans[0])

@@ -147,6 +147,73 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
   const int nitems = (RX - 2) * nseg;
   double* cur = T0;
   double* nxt = T1;
+  // Sparse sweep (the default whenever it fits): candidate masks are thin and irregular (flow-QC
+  // census of the headline batch: 212 masks per image filling 14 % of their boxes), so sweeping
+  // the whole box wastes most of the LDS traffic.  Each thread instead owns up to SP_K of the
+  // mask's own pixels, balanced by rank (pixel r -> thread r % MT), kept in registers for all
+  // iterations; a pixel update reads its 3x3 neighbourhood (non-mask cells hold 0 in both
+  // buffers).  The centre source is folded into the reads of that one cell (cur[ce] + 1.0, the
+  // value variant 0 stores before its sweep) and every sum is formed in variant 0's order, so the
+  // result is bit-identical to the dense sweep with one barrier per iteration instead of two.
+  constexpr int SP_K = 4;
+  const bool sparse = USE_LDS && variant == 0 && total <= SP_K * MT && total * 5 < R * 3;
+  if (sparse) {
+    const int cy = ce / RX, cx = ce % RX;
+    // rank the mask pixels: per-thread counts over contiguous cell ranges, wave + block scans
+    const int seg = (R + MT - 1) / MT;
+    const int e0 = tid * seg, e1 = min(R, e0 + seg);
+    int c = 0;
+    for (int e = e0; e < e1; ++e) c += inm[e];
+    int incl = c;
+    const int lane = tid & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    __shared__ int wsum[MT / 64];
+    if (lane == 63) wsum[tid >> 6] = incl;
+    __syncthreads();
+    int rank = incl - c;
+    for (int w = 0; w < (tid >> 6); ++w) rank += wsum[w];
+    int* list = reinterpret_cast<int*>(T1);  // 8R bytes >= 4 * total: free until the sweep starts
+    for (int e = e0; e < e1; ++e)
+      if (inm[e]) list[rank++] = e;
+    __syncthreads();
+    int own[SP_K];
+    int nown = 0;
+#pragma unroll
+    for (int j = 0; j < SP_K; ++j) {
+      const int r = tid + j * MT;
+      own[j] = r < total ? list[r] : 0;
+      nown += r < total;
+    }
+    __syncthreads();
+    for (int e = tid; e < R; e += MT) T1[e] = 0.0;
+    __syncthreads();
+    for (int it = 0; it < niter; ++it) {
+#pragma unroll
+      for (int j = 0; j < SP_K; ++j) {
+        if (j < nown) {
+          const int e = own[j];
+          const double* cp = cur + e;
+          const int dy = cy - e / RX + 1, dx = cx - e % RX + 1;
+          const int pos = (dy >= 0 && dy <= 2 && dx >= 0 && dx <= 2) ? dy * 3 + dx : -1;
+          double v[3][3];  // (+ 0.0 is exact for the non-negative heat values)
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) v[r][q] = cp[(r - 1) * RX + (q - 1)] + (r * 3 + q == pos ? 1.0 : 0.0);
+          const double hp = v[0][0] + v[0][1] + v[0][2];
+          const double hc = v[1][0] + v[1][1] + v[1][2];
+          const double hn = v[2][0] + v[2][1] + v[2][2];
+          nxt[e] = (hp + hc + hn) * (1.0 / 9.0);
+        }
+      }
+      __syncthreads();
+      double* t = cur; cur = nxt; nxt = t;
+    }
+  }
   if (USE_LDS && variant == 2) {
     // One barrier per sweep: the centre source is folded into the sweep (T' = A (T + e_c) adds 1
     // to the 9-sums of the centre's 3x3 neighbourhood) instead of a separate write + barrier, and
@@ -209,7 +276,8 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
       double* t = cur; cur = nxt; nxt = t;
     }
   }
-  for (int it = 0; (USE_LDS && variant != 0) ? false : it < niter; ++it) {
+  const bool dense0 = !sparse && (!USE_LDS || variant == 0 || variant == 3);  // 3 = variant 0 forced dense
+  for (int it = 0; dense0 && it < niter; ++it) {
     if (tid == 0) cur[ce] += 1.0;
     __syncthreads();
     for (int w = tid; w < nitems; w += MT) {
@@ -516,8 +584,9 @@ int be_cp_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, co
                      int lds_bytes, int threads, int dv, hipStream_t s) {
   if (njobs == 0) return 0;
   if (lds_bytes <= 0) return -1;
-  // sweep variant (A/B switch, read per call): 0 = source write + 2 barriers per iteration,
-  // 1 = source folded into the sliding-window sweep, 2 = folded + all row loads issued together
+  // sweep variant (A/B switch, read per call): 0 = sparse pixel-list sweep where it fits (see
+  // diffuse_kernel), else source write + 2 barriers per iteration; 1 = source folded into the
+  // sliding-window sweep, 2 = folded + all row loads issued together; 3 = variant 0 always dense
   const char* ev = getenv("BE_DIFFUSE_VARIANT");
   const int variant = ev ? atoi(ev) : kDiffuseVariant;
 #define BE_DNT(T, D)                                                                                   \

@@ -215,3 +215,39 @@ def test_normalize99_radix_select_matches_sort_and_numpy(gpu, shape, kind):
         np.testing.assert_allclose(a[0, 0].cpu().numpy(), (xn - p1) / (p99 - p1), rtol=1e-4, atol=1e-4)
     normalize99(xd)  # second call reuses the (self-clearing) workspace
     torch.testing.assert_close(normalize99(xd), b, rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_sparse_diffusion_bit_identical_to_dense(gpu):
+    """The sparse pixel-list sweep (default for thin / irregular masks) gives exactly the dense
+    sweep's flows: same sums in the same order, centre source folded into the reads."""
+    import os
+
+    from bioengine_worker_amd.cellpose import gpu as cg
+
+    rng = np.random.default_rng(5)
+    M = np.zeros((2, 200, 220), np.int32)
+    lab = 0
+    for b in range(2):
+        for _ in range(40):  # random walks: thin, branching, low box fill
+            lab += 1
+            y, x = rng.integers(10, 190), rng.integers(10, 210)
+            for _ in range(rng.integers(20, 160)):
+                M[b, y, x] = lab
+                y = int(np.clip(y + rng.integers(-1, 2), 1, 198))
+                x = int(np.clip(x + rng.integers(-1, 2), 1, 218))
+    Mt = torch.from_numpy(M).to(gpu)
+    old = os.environ.get("BE_DIFFUSE_VARIANT")
+    try:
+        os.environ["BE_DIFFUSE_VARIANT"] = "3"
+        dense, _, _ = cg.masks_to_flows_gpu(Mt)
+        os.environ["BE_DIFFUSE_VARIANT"] = "0"
+        sparse, _, _ = cg.masks_to_flows_gpu(Mt)
+    finally:
+        if old is None:
+            os.environ.pop("BE_DIFFUSE_VARIANT", None)
+        else:
+            os.environ["BE_DIFFUSE_VARIANT"] = old
+    torch.cuda.synchronize()
+    assert dense.abs().sum() > 0
+    assert torch.equal(dense, sparse)
