@@ -145,8 +145,31 @@ def _requires_of_target(target: Path) -> list[str]:
     return out
 
 
+def env_target(requirements: list[str]) -> Path:
+    """Shared install directory of one ``runtime_env.pip`` set (keyed by the pinned requirements),
+    under ``BIOENGINE_ENV_CACHE`` (default ``~/.bioengine/envs``)."""
+    import hashlib
+
+    key = hashlib.sha1("\n".join(sorted(update_requirements(list(requirements)))).encode()).hexdigest()[:16]
+    root = Path(os.environ.get("BIOENGINE_ENV_CACHE", Path.home() / ".bioengine" / "envs"))
+    return root / key
+
+
+def runtime_env_path(runtime_env: dict | None) -> str | None:
+    """Satisfy a task's ``runtime_env["pip"]`` (reference: Ray installs it per task/actor) and return
+    the directory a child process must put on PYTHONPATH (None when nothing had to be installed).
+    Raises :class:`MissingRequirementsError` naming what stays unsatisfied."""
+    reqs = list((runtime_env or {}).get("pip") or [])
+    if isinstance((runtime_env or {}).get("pip"), dict):  # {"packages": [...]} form
+        reqs = list(runtime_env["pip"].get("packages") or [])
+    if not reqs:
+        return None
+    info = ensure(reqs, env_target(reqs), add_to_sys_path=False)
+    return info["target"]
+
+
 def ensure(requirements: list[str], target: str | Path, wheel_dirs: list[str] | None = None,
-           timeout_s: float = 600.0) -> dict:
+           timeout_s: float = 600.0, add_to_sys_path: bool = True) -> dict:
     """Satisfy ``requirements`` for one application (blocking; run it in a thread).
 
     Returns ``{"pinned", "satisfied", "installed", "target"}``; raises
@@ -185,7 +208,7 @@ def ensure(requirements: list[str], target: str | Path, wheel_dirs: list[str] | 
         detail = ("no wheelhouse configured (set BIOENGINE_WHEELHOUSE to a directory of wheels)"
                   if not wheel_dirs else f"not satisfiable from the wheelhouse {wheel_dirs}")
         raise MissingRequirementsError(missing, detail)
-    if paths:  # in-process replicas import from the target too
+    if paths and add_to_sys_path:  # in-process replicas import from the target too
         _APP_PATHS.add(paths[0])
         if paths[0] not in sys.path:
             sys.path.insert(0, paths[0])

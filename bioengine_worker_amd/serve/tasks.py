@@ -73,8 +73,12 @@ def _resources():
     return get_controller().resources
 
 
-def _run_isolated(fn, args, kwargs, gpu_ids, env_vars: dict) -> object:
+def _run_isolated(fn, args, kwargs, gpu_ids, env_vars: dict, runtime_env: dict | None = None) -> object:
     import cloudpickle
+
+    from ..apps.requirements import runtime_env_path
+
+    pip_path = runtime_env_path(runtime_env)  # raises MissingRequirementsError before anything runs
 
     d = Path(tempfile.mkdtemp(prefix="be-task-"))
     inp, out = d / "in.pkl", d / "out.pkl"
@@ -84,6 +88,8 @@ def _run_isolated(fn, args, kwargs, gpu_ids, env_vars: dict) -> object:
     if gpu_ids:
         env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, gpu_ids))
     root = str(Path(__file__).resolve().parents[2])
+    if pip_path:
+        root = pip_path + os.pathsep + root
     env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     p = subprocess.run([sys.executable, "-m", "bioengine_worker_amd.serve.task_worker", str(inp), str(out)], env=env,
                        capture_output=True, text=True)
@@ -146,7 +152,7 @@ class RemoteFunction:
                     _RES_LOCK.wait(0.2)
                 ids = res.reserve(min(num_cpus, res.total_cpu), num_gpus, 0)
             try:
-                return _run_isolated(fn, a, k, ids, env_vars)
+                return _run_isolated(fn, a, k, ids, env_vars, rt)
             finally:
                 with _RES_LOCK:
                     res.release(min(num_cpus, res.total_cpu), num_gpus, 0, ids)

@@ -129,6 +129,12 @@ class CodeExecutor:
         cpus = float(opts.get("num_cpus", 1) or 0)
         gpus = float(opts.get("num_gpus", 0) or 0)
         env_vars = dict((opts.get("runtime_env") or {}).get("env_vars") or {})
+        try:  # runtime_env.pip: installed from the local wheelhouse into a shared per-set directory
+            from ..apps.requirements import runtime_env_path
+
+            pip_path = await asyncio.to_thread(runtime_env_path, opts.get("runtime_env"))
+        except Exception as e:  # noqa: BLE001
+            return {"error": f"runtime_env pip requirements: {e}", "traceback": traceback.format_exc()}
         self.log.info(f"User '{uid}' runs '{function_name}' (remote_options={json.dumps(opts, default=str)})")
         try:
             ids = await self._reserve(cpus, gpus, 0)
@@ -143,6 +149,8 @@ class CodeExecutor:
             if ids:
                 env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, ids))
             root = str(Path(__file__).resolve().parents[2])
+            if pip_path:
+                root = pip_path + os.pathsep + root
             env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
             proc = await asyncio.create_subprocess_exec(sys.executable, "-u", "-m", "bioengine_worker_amd.worker.exec_child",
                                                         str(inp), str(out), env=env, stdout=asyncio.subprocess.PIPE,

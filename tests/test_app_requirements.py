@@ -135,3 +135,44 @@ def test_deploy_installs_requirements_or_reports_deploy_failed(tmp_path, monkeyp
 
     asyncio.run(asyncio.wait_for(main(), 280))
     reset_local_hubs()
+
+
+def test_code_executor_runtime_env_pip(tmp_path, monkeypatch, wheelhouse):
+    """run_code honours remote_options.runtime_env.pip: installed from the wheelhouse into a shared
+    per-set directory on the child's PYTHONPATH, or a clear error naming what is missing."""
+    from bioengine_worker_amd.worker.code_executor import CodeExecutor
+
+    monkeypatch.setenv("BIOENGINE_ENV_CACHE", str(tmp_path / "envs"))
+    ex = CodeExecutor(admin_users=["admin"])
+    ctx = {"user": {"id": "admin", "email": "admin"}}
+    code = "def analyze():\n    import bioengine_testdep\n    return bioengine_testdep.VALUE\n"
+
+    async def run(pip):
+        return await ex.run_code(code=code, function_name="analyze", mode="source", args=None, kwargs=None,
+                                 remote_options={"runtime_env": {"pip": pip}}, write_stdout=None, write_stderr=None,
+                                 timeout=120, context=ctx)
+
+    monkeypatch.setenv("BIOENGINE_WHEELHOUSE", str(wheelhouse))
+    out = asyncio.run(run(["bioengine-testdep==0.1.0"]))
+    assert out.get("result") == "wheel-ok", out
+    assert list((tmp_path / "envs").iterdir())  # the shared install directory
+    bad = asyncio.run(run(["bioengine-testdep-missing"]))
+    assert "bioengine-testdep-missing" in bad["error"]
+
+
+def test_isolated_task_runtime_env_pip(tmp_path, monkeypatch, wheelhouse):
+    from bioengine_worker_amd.serve import tasks
+
+    monkeypatch.setenv("BIOENGINE_ENV_CACHE", str(tmp_path / "envs"))
+    monkeypatch.setenv("BIOENGINE_WHEELHOUSE", str(wheelhouse))
+
+    def value():
+        import bioengine_testdep
+
+        return bioengine_testdep.VALUE
+
+    ref = tasks.remote(runtime_env={"pip": ["bioengine-testdep==0.1.0"]})(value).remote()
+    assert tasks.get(ref, timeout=120) == "wheel-ok"
+    ref = tasks.remote(runtime_env={"pip": ["bioengine-testdep-missing"]})(value).remote()
+    with pytest.raises(Exception, match="bioengine-testdep-missing"):
+        tasks.get(ref, timeout=120)
