@@ -185,18 +185,22 @@ def _plan_finish(launched: list) -> list:
     return out
 
 
-def _plan_launch(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps):
+def _plan_launch(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps, counts: torch.Tensor | None = None):
+    """``counts`` (kind 0): per-label pixel counts; the too-big-for-LDS masks then split into a
+    big-sparse bucket (``len(caps)``) and the tiled one (last)."""
     B, nlab = bbox.shape[:2]
     dev = bbox.device
     n = B * nlab
-    nb = len(caps) + 1
+    split = kind == 0 and counts is not None
+    nb = len(caps) + 1 + int(split)
     jobs = torch.empty(nb, max(n, 1), 4, dtype=torch.int64, device=dev)
     counts = torch.zeros(nb, dtype=torch.int32, device=dev)
     tot = torch.zeros(1, dtype=torch.int64, device=dev)
     niter_img = torch.zeros(B, dtype=torch.int32, device=dev)
     carr = (ctypes.c_int * max(1, len(caps)))(*[int(c) for c in caps])
     vptr = _native.ptr(valid.contiguous().view(torch.uint8)) if valid is not None else None
-    _native.call("be_cp_plan_masks", _native.ptr(bbox.contiguous()), vptr, B, nlab, kind, ctypes.addressof(carr),
+    cptr = _native.ptr(counts.contiguous()) if split else None
+    _native.call("be_cp_plan_masks", _native.ptr(bbox.contiguous()), vptr, cptr, B, nlab, kind, ctypes.addressof(carr),
                  len(caps), _native.ptr(jobs), _native.ptr(counts), _native.ptr(tot), _native.ptr(niter_img),
                  _native.stream(dev))
     return jobs, counts, tot, niter_img
@@ -261,7 +265,7 @@ def _bucket_small(slices):
     return out[::-1]
 
 
-def _diffuse_small(Mc, buckets, niter_img, L, st, ready=None) -> None:
+def _diffuse_small(Mc, buckets, niter_img, L, st, ready=None, scratch=None) -> None:
     """``ready``: event recorded on the current stream once the inputs exist; the buckets start
     from it instead of from the stream's tail, so they run alongside the big-mask kernel.
 
@@ -288,11 +292,15 @@ def _diffuse_small(Mc, buckets, niter_img, L, st, ready=None) -> None:
             if sd is None:
                 sptr = st
             else:
-                for t in (jobs, Mc, niter_img, L):
+                for t in (jobs, Mc, niter_img, L) + ((scratch,) if scratch is not None else ()):
                     t.record_stream(sd)
                 sptr = ctypes.c_void_p(sd.cuda_stream)
         else:
             sptr = st
+        if i < 0:  # big-sparse bucket: global-scratch heat field, one workgroup per mask
+            _native.call("be_cp_diffuse_sparse_big", _native.ptr(Mc), _native.ptr(jobs), jobs.shape[0], H, W,
+                         _native.ptr(niter_img), _native.ptr(scratch), _native.ptr(L), sptr)
+            continue
         _native.call("be_cp_diffuse_nt", _native.ptr(Mc), _native.ptr(jobs), jobs.shape[0], H, W,
                      _native.ptr(niter_img), _native.ptr(L), cap, threads, _diffuse_dv(), sptr)
     if concurrent:
@@ -306,11 +314,15 @@ _TILE_PARAMS: tuple | None = None
 BIG_MASK_MODE = "tiled"
 
 
-def _diffuse_big(Mc, bj, niter_img, scratch, L, st) -> None:
-    """Diffusion of masks too large for one workgroup's LDS (see diffuse_tiled_kernel)."""
+def _diffuse_big(Mc, bj, niter_img, scratch, L, st, between=None) -> None:
+    """Diffusion of masks too large for one workgroup's LDS (see diffuse_tiled_kernel).
+    ``between()`` runs after the short per-mask centre kernel is queued and before the long
+    cooperative sweep (the caller releases its other streams there)."""
     global _TILE_PARAMS
     B, H, W = Mc.shape
     if BIG_MASK_MODE == "block":
+        if between is not None:
+            between()
         _native.call("be_cp_diffuse", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], H, W, _native.ptr(niter_img),
                      _native.ptr(scratch), _native.ptr(L), 0, st)
         return None
@@ -337,9 +349,12 @@ def _diffuse_big(Mc, bj, niter_img, scratch, L, st) -> None:
               f"niter={niter_img.tolist()}", flush=True)
     centers = torch.empty(bj.shape[0], dtype=torch.int32, device=Mc.device)
     ws = torch.zeros(4, dtype=torch.int32, device=Mc.device)
-    _native.call("be_cp_diffuse_tiled", _native.ptr(Mc), _native.ptr(bj), bj.shape[0], _native.ptr(tiles),
-                 tiles.shape[0], H, W, _native.ptr(niter_img), _native.ptr(scratch), _native.ptr(L),
-                 _native.ptr(centers), _native.ptr(ws), st)
+    args = (_native.ptr(Mc), _native.ptr(bj), bj.shape[0], _native.ptr(tiles), tiles.shape[0], H, W,
+            _native.ptr(niter_img), _native.ptr(scratch), _native.ptr(L), _native.ptr(centers), _native.ptr(ws))
+    _native.call("be_cp_diffuse_tiled", *args, 1, st)
+    if between is not None:
+        between()
+    _native.call("be_cp_diffuse_tiled", *args, 2, st)
     return ws  # ws[1] != 0 <=> the grid barrier timed out; checked by the caller after queuing the rest
 
 
@@ -369,24 +384,25 @@ def mask_bboxes(M: torch.Tensor, nlab: int) -> torch.Tensor:
 
 
 def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: int | None = None,
-                       nlab: int | None = None, counts: torch.Tensor | None = None, plan=None):
+                       nlab: int | None = None, counts: torch.Tensor | None = None, plan=None, want_mu: bool = True):
     """Heat-diffusion flows of label images M [B, H, W] int32 (labels 1..n, contiguous per image).
 
     Returns (mu [B, 2, H, W] fp32, err_sum [B, nlab] fp32 or None, counts [B, nlab]).  When ``dp``
     ([B, >=2, H, W] network output) is given, err_sum[b, l] = sum over mask l of |mu - dp/5|^2.
-    ``counts`` / ``plan`` (label_counts and a kind-0 plan of the same labels) skip recomputing them.
+    ``counts`` / ``plan`` (label_counts and a kind-0 plan of the same labels) skip recomputing them;
+    ``want_mu=False`` (flow QC: only the errors are used) returns ``mu=None`` and skips its writes.
     """
     B, H, W = M.shape
     dev = M.device
     if nlab is None:  # an upper bound on the labels + 1 is enough (absent labels have no pixels)
         nlab = int(M.max().item()) + 1 if M.numel() else 1
-    mu = torch.zeros(B, 2, H, W, dtype=torch.float32, device=dev)
+    mu = torch.zeros(B, 2, H, W, dtype=torch.float32, device=dev) if (want_mu or dp is None) else None
     if counts is None:
         counts = label_counts(M, nlab)
     if nlab <= 1:
         return mu, (torch.zeros(B, nlab, device=dev) if dp is not None else None), counts
     if plan is None:
-        plan = _plan_masks(mask_bboxes(M, nlab), None, 0, DIFFUSE_CAPS)
+        plan = _plan_finish([_plan_launch(mask_bboxes(M, nlab), None, 0, DIFFUSE_CAPS, counts)])[0]
     slices, ssize, niter_img = plan
     if niter is not None:
         niter_img = torch.full((B,), niter, dtype=torch.int32, device=dev)
@@ -396,18 +412,27 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
     st = _native.stream(dev)
     Mc = M.contiguous()
     buckets = _bucket_small(slices)
+    if len(slices) == len(DIFFUSE_BUCKETS) + 2 and slices[len(DIFFUSE_BUCKETS)].shape[0]:
+        # big sparse masks: the longest-running launches (niter sweeps of the largest boxes), so
+        # they head the queue order
+        buckets.insert(0, (-1, 0, 1024, slices[len(DIFFUSE_BUCKETS)]))
     ws = None
     ready = None
     if bj.shape[0] and Mc.is_cuda and buckets:
         ready = torch.cuda.Event()
-        ready.record(torch.cuda.current_stream(dev))
+
+        def release():  # the buckets start once the big masks' centre kernel is done
+            ready.record(torch.cuda.current_stream(dev))
+    else:
+        release = None
     if bj.shape[0]:
-        # first, on an idle device: its few cooperative workgroups are all resident before the
-        # bucket kernels (which never wait on it) fill the remaining CUs, so its grid barrier
-        # cannot starve; it then runs alongside the buckets instead of ~1 ms alone on ~24 CUs
-        ws = _diffuse_big(Mc, bj, niter_img, scratch, L, st)
+        # first, on an idle device: the centre kernel runs alone (~0.07 ms instead of ~0.36 ms
+        # among the bucket kernels), then the cooperative tiled sweep -- the critical path -- is
+        # queued right behind it; its few workgroups are resident before the bucket kernels
+        # (which never wait on it) fill the remaining CUs, so its grid barrier cannot starve
+        ws = _diffuse_big(Mc, bj, niter_img, scratch, L, st, between=release)
     if buckets:
-        _diffuse_small(Mc, buckets, niter_img, L, st, ready=ready)
+        _diffuse_small(Mc, buckets, niter_img, L, st, ready=ready, scratch=scratch)
     err = None
     dpp = None
     bstride = 0
@@ -536,10 +561,10 @@ def compute_masks_gpu(y: torch.Tensor, niter: int = 200, cellprob_threshold: flo
     # masks below min_size are dropped whatever their flow error: the QC diffusion skips them (the
     # plan still takes cellpose's per-image niter over ALL masks, so the kept masks' flows are
     # unchanged)
-    plans = _plan_finish(([_plan_launch(bbox, fill_keep, 0, DIFFUSE_CAPS)] if qc else [])
+    plans = _plan_finish(([_plan_launch(bbox, fill_keep, 0, DIFFUSE_CAPS, counts)] if qc else [])
                          + [_plan_launch(bbox, fill_keep, 1, [LDS_FILL_BYTES])])
     if qc:
-        _, err, _ = masks_to_flows_gpu(M, dp=y, nlab=nlab, counts=counts, plan=plans[0])
+        _, err, _ = masks_to_flows_gpu(M, dp=y, nlab=nlab, counts=counts, plan=plans[0], want_mu=False)
         qc_keep = (counts > 0) & ~(err / counts.clamp(min=1).float() > flow_threshold)
         qc_keep[:, 0] = False
         M = torch.gather(qc_keep.to(torch.int32), 1, M.reshape(M.shape[0], -1).long()).reshape(M.shape) * M

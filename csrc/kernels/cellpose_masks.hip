@@ -63,6 +63,11 @@ struct MaskJob {
 // The heat field spans hundreds of orders of magnitude far from the centre of large masks (T decays
 // like exp(-d^2/t)); cellpose runs it in float64 for that reason and so do we (gfx950 runs fp64 VALU
 // at full vector rate, and this kernel is latency/LDS bound anyway).
+constexpr int FG_RUN = 4;  // pixels per thread in flow_grad_kernel
+
+// Largest mask the one-workgroup sparse sweep takes from global scratch: 1024 threads x SP_K (4).
+constexpr int SPARSE_BIG_PX = 4096;
+
 template <bool USE_LDS, int MT = 256, int DV = 8>
 __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs, int H,
                                                      int W, const int* __restrict__ niter_img, double* __restrict__ scratch,
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
   // value variant 0 stores before its sweep) and every sum is formed in variant 0's order, so the
   // result is bit-identical to the dense sweep with one barrier per iteration instead of two.
   constexpr int SP_K = 4;
-  const bool sparse = USE_LDS && variant == 0 && total <= SP_K * MT && total * 5 < R * 3;
+  const bool sparse = variant == 0 && total <= SP_K * MT && total * 5 < R * 3;
   if (sparse) {
     const int cy = ce / RX, cx = ce % RX;
     // rank the mask pixels: per-thread counts over contiguous cell ranges, wave + block scans
@@ -180,21 +185,23 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
     for (int e = e0; e < e1; ++e)
       if (inm[e]) list[rank++] = e;
     __syncthreads();
-    int own[SP_K];
+    int own[SP_K];  // empty slots point at the centre (interior, so its 3x3 reads stay in the box)
     int nown = 0;
 #pragma unroll
     for (int j = 0; j < SP_K; ++j) {
       const int r = tid + j * MT;
-      own[j] = r < total ? list[r] : 0;
+      own[j] = r < total ? list[r] : ce;
       nown += r < total;
     }
     __syncthreads();
     for (int e = tid; e < R; e += MT) T1[e] = 0.0;
     __syncthreads();
     for (int it = 0; it < niter; ++it) {
+      // every slot's reads are issued unconditionally (one batch of independent ds_reads instead
+      // of a branch per slot); only the stores are predicated
 #pragma unroll
       for (int j = 0; j < SP_K; ++j) {
-        if (j < nown) {
+        {
           const int e = own[j];
           const double* cp = cur + e;
           const int dy = cy - e / RX + 1, dx = cx - e % RX + 1;
@@ -207,7 +214,7 @@ __global__ __launch_bounds__(MT) void diffuse_kernel(const int* __restrict__ M, 
           const double hp = v[0][0] + v[0][1] + v[0][2];
           const double hc = v[1][0] + v[1][1] + v[1][2];
           const double hn = v[2][0] + v[2][1] + v[2][2];
-          nxt[e] = (hp + hc + hn) * (1.0 / 9.0);
+          if (j < nown) nxt[e] = (hp + hc + hn) * (1.0 / 9.0);
         }
       }
       __syncthreads();
@@ -322,6 +329,13 @@ constexpr int DT_K = CP_DT_K;
 constexpr int DT_CORE = 64 - 2 * DT_K;
 constexpr int DT_RG = DT_CORE + 2 * DT_K;  // 64
 constexpr int DT_LDS = 2 * DT_RG * DT_RG * 8 + DT_RG * DT_RG;
+// threads per tile workgroup: the sweep is one column segment of DT_RG^2 / DT_MT rows per thread,
+// so 1024 threads make a step ~4x shorter than 256 did (the big masks' tiled sweep is the critical
+// path of flow QC on a few dozen CUs; the other CUs are busy with the LDS buckets meanwhile).
+#ifndef CP_DT_MT
+#define CP_DT_MT 1024
+#endif
+constexpr int DT_MT = CP_DT_MT;
 
 __device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned target, unsigned* timeout_flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -351,7 +365,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned target, uns
 
 // tiles: int4 {job, ry0, rx0, 0} (core origin in the job's padded box coordinates).
 // bar[0] = arrival counter, bar[1] = timeout flag (both zeroed by the launcher).
-__global__ __launch_bounds__(MT) void diffuse_tiled_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs,
+__global__ __launch_bounds__(DT_MT) void diffuse_tiled_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs,
                                                            int njobs, const int4* __restrict__ tiles, int ntiles, int H,
                                                            int W, const int* __restrict__ niter_img,
                                                            const int* __restrict__ centers, double* scratch,
@@ -378,7 +392,7 @@ __global__ __launch_bounds__(MT) void diffuse_tiled_kernel(const int* __restrict
       double* nxt = scratch + J.scratch + ((r & 1) ? 0 : R);
       const int oy = td.y - DT_K, ox = td.z - DT_K;  // region origin in box coordinates
       const int* Mb = M + (size_t)J.b * H * W;
-      for (int e = tid; e < DT_RG * DT_RG; e += MT) {
+      for (int e = tid; e < DT_RG * DT_RG; e += DT_MT) {
         const int ry = oy + e / DT_RG, rx = ox + e % DT_RG;
         unsigned char m = 0;
         double v = 0.0;
@@ -400,11 +414,11 @@ __global__ __launch_bounds__(MT) void diffuse_tiled_kernel(const int* __restrict
       // thread = one column x, rows [r0, r0 + 16): the whole region is swept every step (cells
       // outside the shrinking valid window turn to garbage that never reaches the core).
       const int x = tid & (DT_RG - 1);
-      const int sr0 = (tid / DT_RG) * (DT_RG * DT_RG / MT);
+      const int sr0 = (tid / DT_RG) * (DT_RG * DT_RG / DT_MT);
       const bool xl = x > 0, xr = x < DT_RG - 1;
       // centre source folded into the sweep (see diffuse_kernel): one barrier per step, and all
       // row sums of a thread's column segment are loaded before any is used
-      constexpr int SEG = DT_RG * DT_RG / MT;
+      constexpr int SEG = DT_RG * DT_RG / DT_MT;
       const bool nearx = x - cx <= 1 && cx - x <= 1;
       (void)cl;
       for (int s = 0; s < steps; ++s) {
@@ -428,7 +442,7 @@ __global__ __launch_bounds__(MT) void diffuse_tiled_kernel(const int* __restrict
         double* tmp = a; a = b; b = tmp;
       }
       double* Lb = Lout + (size_t)J.b * H * W;
-      for (int e = tid; e < DT_CORE * DT_CORE; e += MT) {
+      for (int e = tid; e < DT_CORE * DT_CORE; e += DT_MT) {
         const int ly_ = DT_K + e / DT_CORE, lx_ = DT_K + e % DT_CORE;
         const int ry = oy + ly_, rx = ox + lx_;
         if (ry >= RY || rx >= RX) continue;
@@ -450,31 +464,49 @@ __global__ __launch_bounds__(MT) void diffuse_tiled_kernel(const int* __restrict
 __global__ __launch_bounds__(256) void flow_grad_kernel(const int* __restrict__ M, const double* __restrict__ L, int B, int H,
                                                         int W, float* __restrict__ mu, const float* __restrict__ dp,
                                                         long long dp_bstride, float* __restrict__ err, int nlab) {
+  // FG_RUN consecutive pixels of one row per thread: the squared flow errors of a run of equal
+  // labels are summed in registers and flushed with one atomic (was one atomic per mask pixel)
+  const int WG = (W + FG_RUN - 1) / FG_RUN;
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int HW = H * W;
-  if (gid >= (long long)B * HW) return;
-  const int lab = M[gid];
-  const int b = (int)(gid / HW), p = (int)(gid % HW);
-  const int y = p / W, x = p % W;
-  float gy = 0.f, gx = 0.f;
-  if (lab > 0) {
-    const double* Lb = L + (size_t)b * HW;
-    const double up = y > 0 ? Lb[p - W] : 0.0, dn = y < H - 1 ? Lb[p + W] : 0.0;
-    const double lf = x > 0 ? Lb[p - 1] : 0.0, rt = x < W - 1 ? Lb[p + 1] : 0.0;
-    const double dgy = dn - up, dgx = rt - lf;
-    const double nrm = sqrt(dgy * dgy + dgx * dgx) + 1e-60;
-    gy = (float)(dgy / nrm);
-    gx = (float)(dgx / nrm);
-    if (dp && err) {
-      const float* db = dp + (size_t)b * dp_bstride;
-      const float ey = gy - db[p] * 0.2f, ex = gx - db[HW + p] * 0.2f;
-      atomicAdd(err + (size_t)b * nlab + lab, ey * ey + ex * ex);
+  if (gid >= (long long)B * H * WG) return;
+  const int b = (int)(gid / ((long long)H * WG));
+  const int rem = (int)(gid % ((long long)H * WG));
+  const int y = rem / WG, x0 = (rem % WG) * FG_RUN;
+  const double* Lb = L + (size_t)b * HW;
+  const float* db = dp ? dp + (size_t)b * dp_bstride : nullptr;
+  int run_lab = 0;
+  float run = 0.f;
+#pragma unroll
+  for (int k = 0; k < FG_RUN; ++k) {
+    const int x = x0 + k;
+    if (x >= W) break;
+    const int p = y * W + x;
+    const int lab = M[(size_t)b * HW + p];
+    float gy = 0.f, gx = 0.f;
+    if (lab > 0) {
+      const double up = y > 0 ? Lb[p - W] : 0.0, dn = y < H - 1 ? Lb[p + W] : 0.0;
+      const double lf = x > 0 ? Lb[p - 1] : 0.0, rt = x < W - 1 ? Lb[p + 1] : 0.0;
+      const double dgy = dn - up, dgx = rt - lf;
+      const double nrm = sqrt(dgy * dgy + dgx * dgx) + 1e-60;
+      gy = (float)(dgy / nrm);
+      gx = (float)(dgx / nrm);
+      if (db && err) {
+        const float ey = gy - db[p] * 0.2f, ex = gx - db[HW + p] * 0.2f;
+        if (lab != run_lab) {
+          if (run_lab > 0) atomicAdd(err + (size_t)b * nlab + run_lab, run);
+          run_lab = lab;
+          run = 0.f;
+        }
+        run += ey * ey + ex * ex;
+      }
+    }
+    if (mu) {
+      mu[(size_t)b * 2 * HW + p] = gy;
+      mu[(size_t)b * 2 * HW + HW + p] = gx;
     }
   }
-  if (mu) {
-    mu[(size_t)b * 2 * HW + p] = gy;
-    mu[(size_t)b * 2 * HW + HW + p] = gx;
-  }
+  if (run_lab > 0) atomicAdd(err + (size_t)b * nlab + run_lab, run);
 }
 
 // Hole filling: background of the box (+1 ring) that is 4-connected to the ring is "outside";
@@ -580,6 +612,16 @@ int be_cp_diffuse(const int* M, const void* jobs, int njobs, int H, int W, const
   return BE_CHECK_LAUNCH();
 }
 
+// Big masks the sparse sweep can take (plan bucket ncap): one 1024-thread workgroup per mask, heat
+// field in global scratch (L2-resident: a box of R cells holds 16 R bytes), SP_K pixels per thread.
+int be_cp_diffuse_sparse_big(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img,
+                             double* scratch, double* Lout, hipStream_t s) {
+  if (njobs == 0) return 0;
+  hipLaunchKernelGGL((diffuse_kernel<false, 1024, 4>), dim3(njobs), dim3(1024), 0, s, M, (const MaskJob*)jobs, H, W,
+                     niter_img, scratch, Lout, nullptr, 0);
+  return BE_CHECK_LAUNCH();
+}
+
 int be_cp_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, double* Lout,
                      int lds_bytes, int threads, int dv, hipStream_t s) {
   if (njobs == 0) return 0;
@@ -615,13 +657,18 @@ int be_cp_diffuse_tile_params(int* out3) {
 // Big masks, multi-workgroup: centres (one block per mask), then one cooperative launch for all
 // iterations.  tiles: int4 per tile (see diffuse_tiled_kernel); ws: >= 16 bytes of device memory
 // (barrier counter + timeout flag); centers: njobs ints.  Returns 1 if the barrier timed out.
+// stages: bit 0 = the per-mask centre kernel, bit 1 = the cooperative tiled sweep (the caller can
+// start other streams' work between the two, once the short centre kernel is queued).
 int be_cp_diffuse_tiled(const int* M, const void* jobs, int njobs, const void* tiles, int ntiles, int H, int W,
-                        const int* niter_img, double* scratch, double* Lout, int* centers, unsigned* ws,
+                        const int* niter_img, double* scratch, double* Lout, int* centers, unsigned* ws, int stages,
                         hipStream_t s) {
   if (njobs == 0 || ntiles == 0) return 0;
-  hipLaunchKernelGGL((diffuse_kernel<false>), dim3(njobs), dim3(MT), 0, s, M, (const MaskJob*)jobs, H, W, niter_img,
-                     scratch, Lout, centers);
-  if (BE_CHECK_LAUNCH()) return -1;
+  if (stages & 1) {
+    hipLaunchKernelGGL((diffuse_kernel<false>), dim3(njobs), dim3(MT), 0, s, M, (const MaskJob*)jobs, H, W, niter_img,
+                       scratch, Lout, centers);
+    if (BE_CHECK_LAUNCH()) return -1;
+  }
+  if (!(stages & 2)) return 0;
   static int max_grid = 0;
   if (max_grid == 0) {
     int dev = 0, ncu = 0, per_cu = 0;
@@ -629,7 +676,7 @@ int be_cp_diffuse_tiled(const int* M, const void* jobs, int njobs, const void* t
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(diffuse_tiled_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                         DT_LDS);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(diffuse_tiled_kernel), MT,
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(diffuse_tiled_kernel), DT_MT,
                                                  DT_LDS);
     max_grid = max(1, ncu * max(1, per_cu));
   }
@@ -639,7 +686,7 @@ int be_cp_diffuse_tiled(const int* M, const void* jobs, int njobs, const void* t
   const int4* tp = (const int4*)tiles;
   void* args[] = {(void*)&M, (void*)&jp, (void*)&njobs, (void*)&tp, (void*)&ntiles, (void*)&H, (void*)&W,
                   (void*)&niter_img, (void*)&centers, (void*)&scratch, (void*)&Lout, (void*)&ws};
-  hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(diffuse_tiled_kernel), dim3(grid), dim3(MT),
+  hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(diffuse_tiled_kernel), dim3(grid), dim3(DT_MT),
                                             args, DT_LDS, s);
   if (e != hipSuccess) {
     fprintf(stderr, "be_cp_diffuse_tiled: cooperative launch failed: %s\n", hipGetErrorString(e));
@@ -650,7 +697,7 @@ int be_cp_diffuse_tiled(const int* M, const void* jobs, int njobs, const void* t
 
 int be_cp_flow_grad(const int* M, const double* L, int B, int H, int W, float* mu, const float* dp, long long dp_bstride,
                     float* err, int nlab, hipStream_t s) {
-  const long long n = (long long)B * H * W;
+  const long long n = (long long)B * H * ((W + FG_RUN - 1) / FG_RUN);
   hipLaunchKernelGGL(flow_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, M, L, B, H, W, mu, dp, dp_bstride,
                      err, nlab);
   return BE_CHECK_LAUNCH();
@@ -677,9 +724,10 @@ int be_cp_mask_job_bytes() { return (int)sizeof(MaskJob); }
 // 16R + 4(RY+RX) + R + 16 bytes, scratch = the fp64 slab of _diffuse_scratch_doubles), kind 1 =
 // hole filling (need = R bytes, scratch = R bytes).  niter_img[b] (kind 0) = 2 * max over the
 // image's masks of (ly + lx + 4), cellpose's per-image iteration count.
-// counts: [ncap + 1] int32 zeroed; scratch_total: int64 zeroed; niter_img: [B] int32 zeroed.
-int be_cp_plan_masks(const int* bbox, const unsigned char* valid, int B, int nlab, int kind, const int* caps, int ncap,
-                     long long* jobs, int* counts, long long* scratch_total, int* niter_img, hipStream_t s);
+// counts: [ncap + 1] (+1 with cnts) int32 zeroed; scratch_total: int64 zeroed; niter_img: [B] int32 zeroed.
+int be_cp_plan_masks(const int* bbox, const unsigned char* valid, const int* cnts, int B, int nlab, int kind,
+                     const int* caps, int ncap, long long* jobs, int* counts, long long* scratch_total, int* niter_img,
+                     hipStream_t s);
 }  // extern "C"
 
 namespace {
@@ -688,6 +736,7 @@ struct Caps8 {
 };
 
 __global__ __launch_bounds__(256) void plan_masks_kernel(const int* __restrict__ bbox, const unsigned char* __restrict__ valid,
+                                                         const int* __restrict__ cnts,
                                                          int B, int nlab, int kind, Caps8 caps, int ncap,
                                                          MaskJob* __restrict__ jobs, int* __restrict__ counts,
                                                          unsigned long long* __restrict__ scratch_total,
@@ -706,8 +755,15 @@ __global__ __launch_bounds__(256) void plan_masks_kernel(const int* __restrict__
   const long long need = kind == 0 ? 16 * R + 4 * (RY + RX) + R + 16 : R;
   int k = 0;
   while (k < ncap && need > caps.v[k]) ++k;
+  // kind 0 with pixel counts: a too-big-for-LDS mask that the sparse sweep can take (box fill
+  // < 60 %, <= SPARSE_BIG_PX pixels) goes to bucket ncap (one workgroup, heat field in global
+  // scratch), the rest to bucket ncap + 1 (the tiled multi-workgroup kernel)
+  if (k == ncap && kind == 0 && cnts) {
+    const long long c = cnts[i];
+    if (!(c * 5 < R * 3 && c <= SPARSE_BIG_PX)) k = ncap + 1;
+  }
   long long scr = -1;
-  if (k == ncap) {
+  if (k >= ncap) {
     const long long sz = kind == 0 ? 2 * R + (RY + RX + 1) / 2 + (R + 7) / 8 + 2 : R;
     scr = (long long)atomicAdd(scratch_total, (unsigned long long)sz);
   }
@@ -725,14 +781,17 @@ __global__ __launch_bounds__(256) void plan_masks_kernel(const int* __restrict__
 }  // namespace
 
 extern "C" {
-int be_cp_plan_masks(const int* bbox, const unsigned char* valid, int B, int nlab, int kind, const int* caps, int ncap,
-                     long long* jobs, int* counts, long long* scratch_total, int* niter_img, hipStream_t s) {
+// cnts (optional, kind 0): per-label pixel counts [B, nlab]; with it the jobs form ncap + 2 buckets
+// (LDS caps..., big-sparse, tiled) instead of ncap + 1.
+int be_cp_plan_masks(const int* bbox, const unsigned char* valid, const int* cnts, int B, int nlab, int kind,
+                     const int* caps, int ncap, long long* jobs, int* counts, long long* scratch_total, int* niter_img,
+                     hipStream_t s) {
   if (ncap < 0 || ncap > 8) return -1;
   Caps8 c{};
   for (int k = 0; k < ncap; ++k) c.v[k] = caps[k];  // host array
   const long long n = (long long)B * nlab;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(plan_masks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bbox, valid, B, nlab, kind, c,
+  hipLaunchKernelGGL(plan_masks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bbox, valid, cnts, B, nlab, kind, c,
                      ncap, reinterpret_cast<MaskJob*>(jobs), counts, reinterpret_cast<unsigned long long*>(scratch_total),
                      niter_img);
   return BE_CHECK_LAUNCH();
