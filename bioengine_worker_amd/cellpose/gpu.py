@@ -192,18 +192,21 @@ def _plan_launch(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps
     dev = bbox.device
     n = B * nlab
     split = kind == 0 and counts is not None
+    if split:
+        assert counts.shape == (B, nlab) and counts.dtype == torch.int32
+        px_counts = counts.contiguous()
     nb = len(caps) + 1 + int(split)
     jobs = torch.empty(nb, max(n, 1), 4, dtype=torch.int64, device=dev)
-    counts = torch.zeros(nb, dtype=torch.int32, device=dev)
+    bucket_n = torch.zeros(nb, dtype=torch.int32, device=dev)
     tot = torch.zeros(1, dtype=torch.int64, device=dev)
     niter_img = torch.zeros(B, dtype=torch.int32, device=dev)
     carr = (ctypes.c_int * max(1, len(caps)))(*[int(c) for c in caps])
     vptr = _native.ptr(valid.contiguous().view(torch.uint8)) if valid is not None else None
-    cptr = _native.ptr(counts.contiguous()) if split else None
+    cptr = _native.ptr(px_counts) if split else None
     _native.call("be_cp_plan_masks", _native.ptr(bbox.contiguous()), vptr, cptr, B, nlab, kind, ctypes.addressof(carr),
-                 len(caps), _native.ptr(jobs), _native.ptr(counts), _native.ptr(tot), _native.ptr(niter_img),
+                 len(caps), _native.ptr(jobs), _native.ptr(bucket_n), _native.ptr(tot), _native.ptr(niter_img),
                  _native.stream(dev))
-    return jobs, counts, tot, niter_img
+    return jobs, bucket_n, tot, niter_img
 
 
 def _diffuse_lds_bytes(ly, lx):
