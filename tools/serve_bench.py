@@ -59,7 +59,7 @@ async def main_async(a) -> list[dict]:
     for i in range(3):  # warm-up: model build, kernels, graph pass, batch shapes
         await asyncio.gather(*[app.infer(input_arrays=[imgs[j % 16]], model=a.model) for j in range(8)])
     results = []
-    if a.layer == "handle":  # bypass the hub RPC + app-service bridge: router -> replica only
+    if getattr(a, "layer", "hub") == "handle":  # bypass the hub RPC + app-service bridge: router -> replica only
         handle = w.apps_manager.apps[aid]["bridge"].handle
 
         class _H:
@@ -102,7 +102,7 @@ async def main_async(a) -> list[dict]:
         r = {"concurrency": conc, "requests": len(lat), "imgs_per_s": round(len(lat) / dt, 1),
              "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
              "p99_ms": round(float(np.percentile(ms, 99)), 2), "image": [a.size, a.size, 2], "gpus": a.gpus,
-             "replica_mode": os.environ["BIOENGINE_REPLICA_MODE"], "layer": a.layer}
+             "replica_mode": os.environ["BIOENGINE_REPLICA_MODE"], "layer": getattr(a, "layer", "hub")}
         results.append(r)
         print(json.dumps(r), flush=True)
     st = await svc.get_app_status(application_ids=[aid])
