@@ -78,7 +78,7 @@ def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, wq: torch.Tensor, sw: torch.T
     """``epi(xq . wq^T * sx * sw + bias)`` -> bf16 [..., N]; xq e4m3fn [..., K], wq e4m3fn [N, K].
 
     ``tile_cfg`` picks the kernel's block tile (0 = by shape; 1 = 128x128, 2 = 256x128, 3 = 128x256,
-    4 = 256x256) — exposed for the tile sweep in ``tools/fp8_bench.py``."""
+    4 = 256x256, 5 / 6 = 128x128 on 8 waves) — exposed for the tile sweep in ``tools/fp8_bench.py``."""
     if not xq.is_cuda:
         return linear_fp8_ref(xq, sx, wq, sw, bias, gelu)
     K = xq.shape[-1]

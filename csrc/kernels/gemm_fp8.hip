@@ -246,20 +246,25 @@ extern "C" {
 // Y[M,N] bf16 = epi(Xq[M,K] e4m3 . Wq[N,K]^T e4m3 * sx[M] * sw[N] + bias[N]); epi 0 = none, 1 = GELU.
 // K % 128 == 0, N % 4 == 0; any M.  cfg selects the block tile (0 = by shape):
 //   1: 128x128 (4 waves, 64x64 each)   2: 256x128 (8 waves)   3: 128x256 (8 waves)
-//   4: 256x256 (8 waves, 128x64 each).  The 128x128 tile raises the wave priority around its MFMA
+//   4: 256x256 (8 waves, 128x64 each)  5 / 6: 128x128 on 8 waves (64x32 / 32x64 each).  The 128x128 tiles raise
+//   the wave priority around their MFMA
 //   cluster (+0-13 %, profiles/r02/fp8_gemm_bench_r02.md); on 256x256 that costs 6 %.
 int be_gemm_fp8(const void* xq, const void* wq, const float* sx, const float* sw, const float* bias, void* y, int M,
                 int N, int K, int epi, int cfg, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 4 != 0) return -1;
-  if (cfg == 0) {  // measured (profiles/fp8_gemm_bench.jsonl): 256x256 only pays for long K on a full grid
+  if (cfg == 0) {  // measured (profiles/r02/fp8_gemm_bench_r02.md): 256x256 only pays for long K on a full
+                   // grid; otherwise 128x128 on 8 waves (+10-15 % over 4 waves at K = 768; 16 waves: no gain)
     const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    cfg = (K >= 2048 && t256 >= 256) ? 4 : 1;
+    cfg = (K >= 2048 && t256 >= 256) ? 4 : 6;
   }
   switch (cfg) {
     case 1: return launch_gemm<4, 4, 2, 2, true>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     case 2: return launch_gemm<4, 4, 4, 2>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     case 3: return launch_gemm<4, 4, 2, 4>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     case 4: return launch_gemm<8, 4, 2, 4>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
+    // 128x128 tiles on 8 waves (64x32 / 32x64 per wave): 4 waves per SIMD at 2 blocks/CU
+    case 5: return launch_gemm<4, 2, 2, 4, true>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
+    case 6: return launch_gemm<2, 4, 4, 2, true>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     default: return -2;
   }
 }

@@ -77,7 +77,7 @@ def test_gemm_fp8_matches_reference(gpu, M, N, K, gelu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tile_cfg", [1, 2, 3, 4])
+@pytest.mark.parametrize("tile_cfg", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(1000, 640, 384), (257, 256, 128), (300, 516, 256), (520, 768, 3072),
                                    (16448, 2304, 768)])
 def test_gemm_fp8_tile_configs(gpu, tile_cfg, M, N, K):

@@ -38,7 +38,7 @@ def main():
         fl = 2.0 * Mi * N * K
         t8 = bench(lambda: linear_fp8(xq, sx, lin.wq, lin.sw, lin.bias, gelu))
         tcfg = {c: round(fl / bench(lambda: linear_fp8(xq, sx, lin.wq, lin.sw, lin.bias, gelu, tile_cfg=c)) / 1e12, 1)
-                for c in (1, 2, 3, 4)}
+                for c in (1, 2, 3, 4, 5, 6)}
         tq = bench(lambda: quantize_rows(x))
         tqg = bench(lambda: quantize_rows(x, gelu=True))
         wb, bb = w.bfloat16(), b.bfloat16()
