@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from ..models.cpnet import CPnet, CPnetEngine
+from ..ops.resize import resize_bilinear
 from ..profiling import trace
 from . import reference as ref
 
@@ -41,6 +42,7 @@ class EvalParams:
     #: latency-bound kernels and host syncs that leaves most CUs idle on its own).
     pipeline_chunks: int = 1  # measured: 2 -> -9 %, 4 -> -18 % (latency-bound mask stages run once per chunk)
     pipeline_min_chunk: int = 4
+    max_tiles: int = 0  # network tiles per launch (0 = sized to free HBM, CellposeRunner.tile_budget)
 
 
 def as_batch(images, nchan: int, device=None) -> torch.Tensor:
@@ -101,6 +103,40 @@ class CellposeRunner:
             self._plans[key] = TilePlan(H, W, bs, p.tile_overlap, device=self.device)
         return self._plans[key]
 
+    #: HBM bytes one 224^2 CPnet tile keeps live at the forward's peak (measured on MI355X: 23.0-23.4
+    #: MB per tile at 16 / 64 tiles, max_memory_allocated over one engine call; rounded up)
+    TILE_ACT_BYTES = 32 << 20
+
+    def tile_budget(self, p: EvalParams | None = None) -> int:
+        """Tiles per network launch: what the free HBM holds (288 GB MI355X: ~8k tiles of 224^2, a
+        ~20k x 20k image) with a quarter kept back; ``EvalParams.max_tiles`` caps it explicitly."""
+        cap = getattr(p, "max_tiles", 0) if p is not None else 0
+        if self.device.type != "cuda":
+            return cap or (1 << 30)
+        free, _ = torch.cuda.mem_get_info(self.device)
+        n = max(1, int(free * 0.75) // self.TILE_ACT_BYTES)
+        return min(n, cap) if cap else n
+
+    def _tile_queue(self, tiles: torch.Tensor, p: EvalParams):
+        """Spatial tile queue: the tiles of one batch (or one huge image) go through the network in
+        launches of at most :meth:`tile_budget` tiles, written into one output buffer that the blend
+        then reads -- an image larger than the HBM-resident activation budget is tiled, not an OOM
+        (SURVEY.md §5 "tile queues sized to HBM"; the per-tile outputs are 0.6 MB each)."""
+        T = tiles.shape[0]
+        budget = self.tile_budget(p)
+        if T <= budget:
+            return self.engine(tiles)
+        yt = st = None
+        for i in range(0, T, budget):
+            y_i, s_i = self.engine(tiles[i: i + budget])
+            if yt is None:
+                yt = torch.empty((T,) + tuple(y_i.shape[1:]), dtype=y_i.dtype, device=y_i.device)
+                st = torch.empty((T,) + tuple(s_i.shape[1:]), dtype=s_i.dtype, device=s_i.device)
+            yt[i: i + y_i.shape[0]] = y_i
+            st[i: i + s_i.shape[0]] = s_i
+            del y_i, s_i
+        return yt, st
+
     def _sam_tiles(self, tiles: torch.Tensor) -> torch.Tensor:
         """NHWC bf16 tiles [T, by, bx, cpad] -> CPSAM flows [T, 3, by, bx] fp32 (tiles smaller than
         the network's fixed 256 grid are zero-padded, as cellpose 4 pads small images)."""
@@ -128,7 +164,7 @@ class CellposeRunner:
                         yt = self._sam_tiles(tiles)
                         st = torch.zeros(B * plan.nt, 256, device=x.device)
                     else:
-                        yt, st = self.engine(tiles)
+                        yt, st = self._tile_queue(tiles, p)
                 with trace.span("cellpose.blend", cuda=True):
                     y = plan.blend(yt, B)
                 style = st.view(B, plan.nt, -1).sum(1)
@@ -209,9 +245,9 @@ class CellposeRunner:
             rescale = self.diam_mean / float(p.diameter)
         if abs(rescale - 1.0) > 1e-3:
             Hs, Ws = max(8, int(round(H * rescale))), max(8, int(round(W * rescale)))
-            xs = F.interpolate(x, size=(Hs, Ws), mode="bilinear", align_corners=False)
+            xs = resize_bilinear(x, (Hs, Ws))
             y, style = self.run_net(xs, p)
-            y = F.interpolate(y, size=(H, W), mode="bilinear", align_corners=False)
+            y = resize_bilinear(y, (H, W))
         else:
             y, style = self.run_net(x, p)
         if not p.compute_masks:
@@ -230,9 +266,9 @@ class CellposeRunner:
             rescale = self.diam_mean / float(p.diameter)
         if abs(rescale - 1.0) > 1e-3:
             Hs, Ws = max(8, int(round(H * rescale))), max(8, int(round(W * rescale)))
-            xs = F.interpolate(x, size=(Hs, Ws), mode="bilinear", align_corners=False)
+            xs = resize_bilinear(x, (Hs, Ws))
             y, style = self.run_net(xs, p)
-            y = F.interpolate(y, size=(H, W), mode="bilinear", align_corners=False)
+            y = resize_bilinear(y, (H, W))
         else:
             y, style = self.run_net(x, p)
         return y, style, rescale

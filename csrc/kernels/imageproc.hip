@@ -175,7 +175,46 @@ inline unsigned nblk(long long n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
 
+// Bilinear resize of fp32 planes with torch's align_corners=False convention (cellpose resizes
+// images to the model diameter and the flows back with cv2/torch bilinear; reference
+// cellpose/transforms.py resize_image): src = max(0, (dst + 0.5) * in / out - 0.5), edge-clamped
+// right/bottom neighbour.  One lane per output pixel; consecutive lanes along x read neighbouring
+// source texels of one or two rows (L2 / L1 friendly).
+__global__ void resize_bilinear_f32(const float* __restrict__ in, float* __restrict__ out, long long planes, int ih,
+                                    int iw, int oh, int ow) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = planes * oh * ow;
+  if (gid >= n) return;
+  const int ox = (int)(gid % ow);
+  const int oy = (int)((gid / ow) % oh);
+  const long long pl = gid / ((long long)oh * ow);
+  const float ry = (float)ih / (float)oh, rx = (float)iw / (float)ow;
+  float sy = ry * ((float)oy + 0.5f) - 0.5f;
+  float sx = rx * ((float)ox + 0.5f) - 0.5f;
+  sy = sy < 0.f ? 0.f : sy;
+  sx = sx < 0.f ? 0.f : sx;
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int yp = y0 < ih - 1 ? 1 : 0, xp = x0 < iw - 1 ? 1 : 0;
+  const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const float* p = in + pl * ih * iw;
+  const float* r0 = p + (long long)y0 * iw + x0;
+  const float* r1 = r0 + (long long)yp * iw;
+  out[gid] = ly0 * (lx0 * r0[0] + lx1 * r0[xp]) + ly1 * (lx0 * r1[0] + lx1 * r1[xp]);
+}
+
 extern "C" {
+
+// in [planes, ih, iw] fp32 -> out [planes, oh, ow] fp32.
+int be_resize_bilinear(const float* in, float* out, long long planes, int ih, int iw, int oh, int ow, hipStream_t s) {
+  const long long n = planes * oh * ow;
+  if (n == 0) return 0;
+  if (ih <= 0 || iw <= 0 || oh <= 0 || ow <= 0) return -1;
+  hipLaunchKernelGGL(resize_bilinear_f32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, planes, ih, iw,
+                     oh, ow);
+  return BE_CHECK_LAUNCH();
+}
+
 
 // mask uint8 [B, H, W] -> labels int32 [B, H, W] (root linear index within the image, -1 background)
 int be_ccl_conn(const void* mask, int B, int H, int W, int conn, int* labels, hipStream_t s) {
