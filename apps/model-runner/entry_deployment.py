@@ -223,7 +223,7 @@ class EntryDeployment:
     async def infer(self, model_id: str = Field(..., description="Model id."),
                     inputs: Union[np.ndarray, Dict[str, Union[np.ndarray, str]], str] = Field(..., description=(
                         "Array, {input_id: array|url|file_path}, or a URL / uploaded file path.")),
-                    weights_format: Optional[str] = Field(None, description="pytorch_state_dict | torchscript"),
+                    weights_format: Optional[str] = Field(None, description="pytorch_state_dict | torchscript | onnx (tensorflow formats: not in this runtime). None picks the first available in that order."),
                     device: Optional[Literal["cuda", "cpu"]] = Field(None, description="Target device."),
                     default_blocksize_parameter: Optional[int] = Field(None, description="Tiling block size parameter."),
                     sample_id: Optional[str] = Field("sample", description="Request id for logs."),

@@ -145,9 +145,10 @@ def load_module(path: Path, name: str = "bioimageio_model_src"):
 def write_unet2d_package(out: str | Path, model_id: str = "demo-unet2d", in_channels: int = 1, out_channels: int = 2,
                          features=(32, 64, 128, 256), test_shape=(1, 1, 256, 256), seed: int = 0,
                          torchscript: bool = True, norm: str = "batch", down: str = "pool",
-                         state_dict: bool = True) -> Path:
+                         state_dict: bool = True, onnx: bool = False) -> Path:
     """``norm``: batch / group / instance; ``down``: pool / conv (2x2 stride-2); ``state_dict=False``
-    writes a TorchScript-only package (the traced module is the only weights entry)."""
+    writes a TorchScript-only package (the traced module is the only weights entry), or an ONNX-only
+    one with ``onnx=True, torchscript=False``; ``onnx=True`` adds ``weights.onnx`` (own exporter)."""
     out = Path(out)
     out.mkdir(parents=True, exist_ok=True)
     (out / "model.py").write_text(MODEL_SRC)
@@ -177,7 +178,15 @@ def write_unet2d_package(out: str | Path, model_id: str = "demo-unet2d", in_chan
         "architecture": {"source": "model.py", "sha256": sha256_file(out / "model.py"), "callable": "UNet2d",
                          "kwargs": kwargs},
         "pytorch_version": "2.5"}}
-    if torchscript or not state_dict:
+    if onnx:
+        from .onnx_export import export_onnx
+
+        info = export_onnx(net, out / "weights.onnx", input_name="raw", output_name="probabilities")
+        weights["onnx"] = {"source": "weights.onnx", "sha256": sha256_file(out / "weights.onnx"),
+                           "opset_version": info["opset"]}
+        if state_dict:
+            weights["onnx"]["parent"] = "pytorch_state_dict"
+    if torchscript or (not state_dict and not onnx):
         ts = torch.jit.trace(net, x[:, :, :64, :64])
         ts.save(str(out / "weights_torchscript.pt"))
         weights["torchscript"] = {"source": "weights_torchscript.pt", "sha256": sha256_file(out / "weights_torchscript.pt"),

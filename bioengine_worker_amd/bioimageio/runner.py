@@ -2,6 +2,10 @@
 ``create_prediction_pipeline`` + ``predict_sample_with/without_blocking`` as called by
 apps/model-runner/runtime_deployment.py:187-312).
 
+ONNX weights run on :class:`.onnx_runtime.OnnxModule` (file parsed by :mod:`.onnx_proto`, the same
+conv fusions applied on the dataflow graph); TensorFlow formats are rejected with the missing runtime
+named (not importable in this image).
+
 MI355X specifics: pytorch_state_dict models go through :func:`convert.optimize_for_mi355x`
 (fused NHWC MFMA convs, bf16 channels-last); with blocking, tiles are cut on the GPU and pushed
 through the network in batches (``tile_batch`` tiles per forward) instead of one by one, and the
@@ -20,8 +24,8 @@ import torch.nn.functional as F
 from . import processing
 from .spec import TensorSpec, load_rdf, tensors, weights_entries
 
-PREFERRED_FORMATS = ("pytorch_state_dict", "torchscript")
-UNSUPPORTED = {"onnx": "onnxruntime", "tensorflow_saved_model": "tensorflow", "keras_hdf5": "tensorflow"}
+PREFERRED_FORMATS = ("pytorch_state_dict", "torchscript", "onnx")
+UNSUPPORTED = {"tensorflow_saved_model": "tensorflow", "keras_hdf5": "tensorflow"}
 
 
 def _src(v):
@@ -74,6 +78,16 @@ class PredictionPipeline:
     # ------------------------------------------------------------------ model
     def _load(self, fmt, entry, optimize):
         root = self.root or Path(".")
+        if fmt == "onnx":  # own graph executor (onnx_runtime.py); no onnxruntime in this image
+            from .onnx_runtime import OnnxModule
+
+            opt = optimize and self.device.type == "cuda"
+            m = OnnxModule.from_file(root / _src(entry), optimize=opt)
+            self.convert_stats = m.stats
+            fused = m.stats["convs"] + m.stats["strided"] + m.stats["conv_transpose"]
+            self.optimized = opt and fused > 0
+            m = m.to(self.device)
+            return m.to(torch.bfloat16) if self.optimized else m
         if fmt == "torchscript":
             m = torch.jit.load(str(root / _src(entry)), map_location=self.device).eval()
             if optimize and self.device.type == "cuda":
