@@ -98,8 +98,11 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t* p, bool ok) {
 }
 
 // ------------------------------------------------------------------ dQ (+ drel, delta)
+// 4-wave blocks are register-capped to 256 VGPRs so TWO waves share each SIMD (the unconstrained
+// build took 264 / 376 VGPRs -> one wave per SIMD, SQ_WAIT_ANY ~65 % of wave cycles in dkv).
 template <int NW, int BIAS>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(BwdArgs a) {
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 2 : 1, NW == 4 ? 2 : 1)))
+void attn_bwd_dq_kernel(BwdArgs a) {
   constexpr int NT = NW * 64;
   constexpr int CHUNKS = 2 * TT * (HD / 8);
   constexpr int CPT = (CHUNKS + NT - 1) / NT;
@@ -257,7 +260,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq_kernel(BwdArgs a) {
 
 // ------------------------------------------------------------------ dK, dV
 template <int NW, int BIAS>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(BwdArgs a) {
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 2 : 1, NW == 4 ? 2 : 1)))
+void attn_bwd_dkv_kernel(BwdArgs a) {
   constexpr int NT = NW * 64;
   constexpr int QCH = 2 * TT * (HD / 8);       // Q + dO tile chunks (bf16 x 8)
   constexpr int WCH = BIAS ? TT * 32 / 4 : 0;   // rel_w tile chunks (fp32 x 4)
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_kernel(BwdArgs a) {
     commit();
     __syncthreads();
     if (t + 1 < ntiles) issue(t + 1);
-#pragma unroll
+#pragma unroll 1  // one 32-query half at a time: keeps dkv<4, 1> at 254 VGPRs without spills
     for (int qb = 0; qb < 2; ++qb) {
       f32x16 s, dp;
 #pragma unroll
