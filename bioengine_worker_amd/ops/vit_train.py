@@ -237,3 +237,64 @@ def attn_bwd(q, k, v, o, do, lse, scale: float, rel_h=None, rel_w=None, dk=None,
     else:
         dk, dv = dkt, dvt
     return back(dqf).contiguous(), dk, dv, drh, drw
+
+
+# ---------------------------------------------------------------------------- SAM rel-pos terms
+def relpos_fwd_ref(q, Rh, Rw):
+    """q [B, N, H, c] (N = g*g), Rh / Rw [g, g, c] -> rel_h, rel_w [B, H, N, g] fp32 (oracle)."""
+    B, N, H, c = q.shape
+    g = Rh.shape[0]
+    q5 = q.float().reshape(B, g, g, H, c)
+    rh = torch.einsum("byxhc,ykc->bhyxk", q5, Rh.float()).reshape(B, H, N, g)
+    rw = torch.einsum("byxhc,xkc->bhyxk", q5, Rw.float()).reshape(B, H, N, g)
+    return rh.contiguous(), rw.contiguous()
+
+
+def relpos_fwd(q, Rh, Rw):
+    """rel_h / rel_w on MFMA (``relpos.hip``) for the 32 x 32 grid / head_dim 64; torch otherwise."""
+    B, N, H, c = q.shape
+    g = Rh.shape[0]
+    if not (q.is_cuda and g == 32 and c == 64 and N == g * g and q.dtype == torch.bfloat16 and q.stride(-1) == 1):
+        return relpos_fwd_ref(q, Rh, Rw)
+    rh = torch.empty(B, H, N, g, device=q.device, dtype=torch.float32)
+    rw = torch.empty_like(rh)
+    _native.call("be_relpos_fwd", _native.ptr(q), q.stride(1), q.stride(2), q.stride(0),
+                 _native.ptr(Rh.float().contiguous()), _native.ptr(Rw.float().contiguous()), _native.ptr(rh),
+                 _native.ptr(rw), B, H, g, c, _native.stream(q.device))
+    return rh, rw
+
+
+def relpos_bwd_ref(q, Rh, Rw, drh, drw):
+    """-> (dq_rel [B, N, H, c] fp32, dRh [g, g, c], dRw [g, g, c]) (oracle)."""
+    B, N, H, c = q.shape
+    g = Rh.shape[0]
+    q5 = q.float().reshape(B, g, g, H, c)
+    dh = drh.float().reshape(B, H, g, g, g)
+    dw = drw.float().reshape(B, H, g, g, g)
+    dq = torch.einsum("bhyxk,ykc->byxhc", dh, Rh.float()) + torch.einsum("bhyxk,xkc->byxhc", dw, Rw.float())
+    dRh = torch.einsum("bhyxk,byxhc->ykc", dh, q5)
+    dRw = torch.einsum("bhyxk,byxhc->xkc", dw, q5)
+    return dq.reshape(B, N, H, c), dRh, dRw
+
+
+def relpos_bwd_(q, Rh, Rw, drh, drw, dq, out_q, grad_rh, grad_rw, rel_idx):
+    """Fused backward of the rel-pos terms: ``out_q`` (bf16 view, e.g. the q slot of a packed dqkv
+    gradient) = dq + dq_rel; ``grad_rh`` / ``grad_rw`` (the [2g-1, c] table gradients) overwritten
+    with the gathered dRh / dRw (rel_idx [g, g] = y - k + g - 1).  ``dq`` (fp32) is clobbered."""
+    B, N, H, c = q.shape
+    g = Rh.shape[0]
+    if q.is_cuda and g == 32 and c == 64 and N == g * g and q.stride(-1) == 1 and dq.stride(-1) == 1 \
+            and out_q.stride(-1) == 1 and grad_rh.is_contiguous() and grad_rw.is_contiguous():
+        grad_rh.zero_()
+        grad_rw.zero_()
+        _native.call("be_relpos_bwd", _native.ptr(drh), _native.ptr(drw), _native.ptr(Rh.float().contiguous()),
+                     _native.ptr(Rw.float().contiguous()), _native.ptr(dq), dq.stride(1), dq.stride(2), dq.stride(0),
+                     _native.ptr(out_q), out_q.stride(1), out_q.stride(2), out_q.stride(0), _native.ptr(q),
+                     q.stride(1), q.stride(2), q.stride(0), _native.ptr(grad_rh), _native.ptr(grad_rw), B, H, g, c,
+                     _native.stream(q.device))
+        return
+    dq_rel, dRh, dRw = relpos_bwd_ref(q, Rh, Rw, drh, drw)
+    out_q.copy_((dq.float() + dq_rel).to(out_q.dtype))
+    for dR, out in ((dRh, grad_rh), (dRw, grad_rw)):
+        out.zero_()
+        out.index_add_(0, rel_idx.reshape(-1), dR.reshape(-1, dR.shape[-1]).to(out.dtype))

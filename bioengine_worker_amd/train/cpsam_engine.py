@@ -9,7 +9,7 @@ forward, per block (pre-norm SAM block, global attention, decomposed rel-pos bia
 
     h1, st1   = LN1(t_in)                                 fused add+LN kernel (stats saved)
     qkv       = h1 Wqkv^T + b                             hipBLASLt
-    rel_h/w   = q . R_h / R_w                             small batched GEMMs (fp32)
+    rel_h/w   = q . R_h / R_w                             MFMA per (b, h, grid line) (relpos.hip)
     a, lse    = flash_attn(q, k, v, rel_h, rel_w)         HIP MFMA kernel (attention.hip)
     y         = a Wproj^T + b
     t_mid,h2  = t_in + k_b * y, LN2(t_mid)                fused add+LN (k_b = stochastic-depth keep)
@@ -64,7 +64,15 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> None:
                 break
             except Exception:  # noqa: BLE001
                 continue
-    if _MM_MODE == 2:
+    m, n, k = dy.shape[0], dy.shape[1], x.shape[1]
+    if _MM_MODE == 2 and m >= 4096 and m % 4 == 0 and n * k <= 3072 * 1024:
+        # split-K: the [n, k] output is <= 192 hipBLASLt 128x128 tiles, under one per CU, so the
+        # m = B*N reduction runs as 4 batched slices + an fp32 sum (profiles/r02/attn/wgrad.jsonl:
+        # proj 57.8 -> 37.7 us, qkv 87.6 -> 74.6 us; the 4096-wide fc1 / fc2 outputs gain nothing)
+        ws = torch.empty(4, n, k, device=dy.device, dtype=torch.float32)
+        torch.bmm(dy.reshape(4, m // 4, n).transpose(1, 2), x.reshape(4, m // 4, k), out_dtype=torch.float32, out=ws)
+        torch.sum(ws, 0, out=out2)
+    elif _MM_MODE == 2:
         torch.mm(dy.t(), x, out_dtype=torch.float32, out=out2)
     elif _MM_MODE == 1:
         out2.copy_(torch.mm(dy.t(), x, out_dtype=torch.float32))
@@ -182,7 +190,7 @@ class CPSAMTrainEngine:
             q, k_, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             Rh = get_rel_pos(g, g, p["rph"].detach()).float()
             Rw = get_rel_pos(g, g, p["rpw"].detach()).float()
-            rel_h, rel_w = self._rel_terms(q, Rh, Rw)
+            rel_h, rel_w = vt.relpos_fwd(q, Rh, Rw) if self.cuda else self._rel_terms(q, Rh, Rw)
             a, lse = vt.attn_fwd(q, k_, v, self.scale, rel_h, rel_w)
             a2 = a.reshape(B * N, D)
             y = F.linear(a2, w["proj_w"], w["proj_b"])
@@ -281,10 +289,14 @@ class CPSAMTrainEngine:
         dqkv = torch.empty(B, N, 3, H, hd, device=G.device, dtype=self.cdt)
         dq, _, _, drh, drw = vt.attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], s["a"], da, s["lse"], self.scale,
                                          s["rel_h"], s["rel_w"], dk=dqkv[:, :, 1], dv=dqkv[:, :, 2])
-        dq_rel, dRh, dRw = self._rel_bwd(qkv[:, :, 0], s["Rh"], s["Rw"], drh, drw)
-        dqkv[:, :, 0] = (dq + dq_rel).to(self.cdt)
-        self._table_grad(dRh, p["rph"].grad)
-        self._table_grad(dRw, p["rpw"].grad)
+        if self.cuda:  # relpos.hip: dq + dq_rel -> the bf16 q slot, table grads gathered in place
+            vt.relpos_bwd_(qkv[:, :, 0], s["Rh"], s["Rw"], drh, drw, dq, dqkv[:, :, 0], p["rph"].grad, p["rpw"].grad,
+                           self.rel_idx)
+        else:
+            dq_rel, dRh, dRw = self._rel_bwd(qkv[:, :, 0], s["Rh"], s["Rw"], drh, drw)
+            dqkv[:, :, 0] = (dq + dq_rel).to(self.cdt)
+            self._table_grad(dRh, p["rph"].grad)
+            self._table_grad(dRw, p["rpw"].grad)
         dqkv2 = dqkv.view(B * N, 3 * D)
         torch.sum(dqkv2, 0, dtype=torch.float32, out=p["qkv_b"].grad)
         _wgrad(dqkv2, s["h1"], p["qkv_w"].grad)

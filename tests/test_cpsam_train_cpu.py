@@ -67,3 +67,23 @@ def test_stochastic_depth_schedule():
     assert drop[0] == 0.0
     assert abs(float(drop[-1]) - 0.4) < 0.03
     assert abs(float(drop[12]) - 0.4 * 12 / 23) < 0.03
+
+
+def test_relpos_oracles_match_engine_batched_gemms():
+    """vit_train.relpos_*_ref (the oracle of relpos.hip) == the engine's torch formulation."""
+    from bioengine_worker_amd.ops import vit_train as vt
+
+    net = CPSAM(dim=128, depth=1, heads=2, ps=8, bsize=64).randomize_(0)
+    eng = CPSAMTrainEngine(net, FlatParams(net, "cpu"), 2, "cpu")
+    torch.manual_seed(0)
+    B, g, H, c = eng.B, eng.g, eng.H, eng.hd
+    q = torch.randn(B, g * g, H, c)
+    Rh, Rw = torch.randn(g, g, c), torch.randn(g, g, c)
+    rh, rw = eng._rel_terms(q, Rh, Rw)
+    rh2, rw2 = vt.relpos_fwd_ref(q, Rh, Rw)
+    assert torch.allclose(rh, rh2, atol=1e-4) and torch.allclose(rw, rw2, atol=1e-4)
+    drh, drw = torch.randn_like(rh), torch.randn_like(rw)
+    dq, dRh, dRw = eng._rel_bwd(q, Rh, Rw, drh, drw)
+    dq2, dRh2, dRw2 = vt.relpos_bwd_ref(q, Rh, Rw, drh, drw)
+    for a, b in ((dq, dq2), (dRh, dRh2), (dRw, dRw2)):
+        assert torch.allclose(a, b, atol=1e-3, rtol=1e-4)

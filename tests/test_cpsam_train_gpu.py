@@ -151,3 +151,33 @@ def test_cpsam_runner_matches_cpu_reference(dev):
     assert _rel(yg.cpu(), yc) < 3e-2
     masks, _, _ = CellposeRunner(net=net, device=dev).eval(img)
     assert masks.shape == (1, 300, 280) and np.isfinite(yg.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_relpos_kernels_match_fp32_oracle(dev, B):
+    """relpos.hip (MFMA, hi/lo-split fp32 operands) vs the fp32 einsum oracle: rel_h / rel_w, dq + dq_rel
+    written as bf16 into a packed-dqkv q slot, and the gathered rel-pos table gradients."""
+    torch.manual_seed(1)
+    g, H, c = 32, 4, 64
+    N = g * g
+    qkv = (torch.randn(B, N, 3, H, c, device=dev) * 0.5).bfloat16()
+    q = qkv[:, :, 0]
+    Rh, Rw = torch.randn(g, g, c, device=dev) * 0.3, torch.randn(g, g, c, device=dev) * 0.3
+    rh, rw = vt.relpos_fwd(q, Rh, Rw)
+    rh_r, rw_r = vt.relpos_fwd_ref(q.cpu(), Rh.cpu(), Rw.cpu())
+    assert _rel(rh.cpu(), rh_r) < 1e-4 and _rel(rw.cpu(), rw_r) < 1e-4
+    drh, drw = torch.randn(B, H, N, g, device=dev), torch.randn(B, H, N, g, device=dev)
+    dq = torch.randn(B, N, H, c, device=dev)
+    dq0 = dq.clone()
+    dqkv = torch.zeros(B, N, 3, H, c, device=dev, dtype=torch.bfloat16)
+    ar = torch.arange(g, device=dev)
+    idx = (ar[:, None] - ar[None, :] + g - 1).long()
+    gh, gw = torch.full((2 * g - 1, c), 7.0, device=dev), torch.full((2 * g - 1, c), 7.0, device=dev)
+    vt.relpos_bwd_(q, Rh, Rw, drh, drw, dq, dqkv[:, :, 0], gh, gw, idx)
+    torch.cuda.synchronize()
+    dq_rel, dRh, dRw = vt.relpos_bwd_ref(q.cpu(), Rh.cpu(), Rw.cpu(), drh.cpu(), drw.cpu())
+    assert _rel(dqkv[:, :, 0].float().cpu(), dq0.cpu() + dq_rel) < 1e-2  # bf16 output
+    assert dqkv[:, :, 1:].abs().max() == 0  # k / v slots untouched
+    for got, dR in ((gh, dRh), (gw, dRw)):
+        ref = torch.zeros(2 * g - 1, c).index_add_(0, idx.cpu().reshape(-1), dR.reshape(-1, c))
+        assert _rel(got.cpu(), ref) < 1e-4
