@@ -21,6 +21,8 @@ def test_model_runner_e2e(tmp_path, monkeypatch):
     zoo = tmp_path / "zoo"
     write_unet2d_package(zoo / "tiny-unet", "tiny-unet", features=(8, 16, 32), test_shape=(1, 1, 96, 96),
                          torchscript=False)
+    write_unet2d_package(zoo / "tiny-onnx", "tiny-onnx", features=(8, 16, 32), test_shape=(1, 1, 96, 96),
+                         torchscript=False, state_dict=False, onnx=True)  # ONNX-only weights
     monkeypatch.setenv("BIOENGINE_MODEL_ZOO", str(zoo))
     monkeypatch.setenv("BIOENGINE_LOCAL_ARTIFACT_PATH", str(ROOT / "apps"))
     monkeypatch.setenv("BIOENGINE_REPLICA_MODE", "local")
@@ -44,7 +46,7 @@ def test_model_runner_e2e(tmp_path, monkeypatch):
         assert set(st["deployments"]) == {"EntryDeployment", "RuntimeDeployment"}
         app = await admin.get_service(st["service_ids"][0]["websocket_service_id"])
         found = await app.search_models(keywords=["unet"])
-        assert [m["model_id"] for m in found] == ["tiny-unet"]
+        assert sorted(m["model_id"] for m in found) == ["tiny-onnx", "tiny-unet"]
         rdf = await app.get_model_rdf(model_id="tiny-unet")
         assert rdf["inputs"][0]["id"] == "raw"
         doc = await app.get_model_documentation(model_id="tiny-unet")
@@ -66,6 +68,11 @@ def test_model_runner_e2e(tmp_path, monkeypatch):
         assert out2["probabilities"].shape == (1, 2, 80, 72)
         with pytest.raises(Exception):
             await app.infer(model_id="no-such-model", inputs=x)
+        # ONNX-only package: own graph executor (no onnxruntime), test + infer through the app
+        assert (await app.test(model_id="tiny-onnx"))["status"] == "passed"
+        xo = np.load(zoo / "tiny-onnx" / "test_input.npy")
+        outo = await app.infer(model_id="tiny-onnx", inputs=xo, weights_format="onnx")
+        assert np.abs(outo["probabilities"] - np.load(zoo / "tiny-onnx" / "test_output.npy")).max() < 1e-4
         await svc.stop_worker(blocking=True)
         await admin.disconnect()
 
