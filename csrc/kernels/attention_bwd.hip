@@ -52,6 +52,7 @@ struct BwdArgs {
   int B, H, N;
   float scale;
   int blocks_per_bh;
+  int write_delta;  // dq blocks store delta (two-launch path); the fused path gets it from attn_delta_kernel
 };
 
 __device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
@@ -98,11 +99,8 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t* p, bool ok) {
 }
 
 // ------------------------------------------------------------------ dQ (+ drel, delta)
-// 4-wave blocks are register-capped to 256 VGPRs so TWO waves share each SIMD (the unconstrained
-// build took 264 / 376 VGPRs -> one wave per SIMD, SQ_WAIT_ANY ~65 % of wave cycles in dkv).
 template <int NW, int BIAS>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 2 : 1, NW == 4 ? 2 : 1)))
-void attn_bwd_dq_kernel(BwdArgs a) {
+__device__ __forceinline__ void dq_body(const BwdArgs& a, int logical) {
   constexpr int NT = NW * 64;
   constexpr int CHUNKS = 2 * TT * (HD / 8);
   constexpr int CPT = (CHUNKS + NT - 1) / NT;
@@ -111,8 +109,6 @@ void attn_bwd_dq_kernel(BwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, ql = lane & 31;
-  const int total = a.blocks_per_bh * a.B * a.H;
-  const int logical = xcd_remap(blockIdx.x, total);
   const int bh = logical / a.blocks_per_bh, qb = logical % a.blocks_per_bh;
   const int b = bh / a.H, hh = bh % a.H;
   const int qi = qb * NW * 32 + wave * 32 + ql;
@@ -135,7 +131,7 @@ void attn_bwd_dq_kernel(BwdArgs a) {
     for (int j = 0; j < 8; ++j) dl += bf2f((uint16_t)df[ks][j]) * bf2f((uint16_t)of[j]);
   }
   dl += __shfl_xor(dl, 32, 64);
-  if (qv && h == 0) a.delta[(long long)bh * a.N + qi] = dl;
+  if (qv && h == 0 && a.write_delta) a.delta[(long long)bh * a.N + qi] = dl;
   const float lse2 = qv ? a.lse[(long long)bh * a.N + qi] * LOG2E : 0.f;
   const float c2 = a.scale * LOG2E;
 
@@ -260,8 +256,7 @@ void attn_bwd_dq_kernel(BwdArgs a) {
 
 // ------------------------------------------------------------------ dK, dV
 template <int NW, int BIAS>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 ? 2 : 1, NW == 4 ? 2 : 1)))
-void attn_bwd_dkv_kernel(BwdArgs a) {
+__device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical) {
   constexpr int NT = NW * 64;
   constexpr int QCH = 2 * TT * (HD / 8);       // Q + dO tile chunks (bf16 x 8)
   constexpr int WCH = BIAS ? TT * 32 / 4 : 0;   // rel_w tile chunks (fp32 x 4)
@@ -278,8 +273,6 @@ void attn_bwd_dkv_kernel(BwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, kl = lane & 31;
-  const int total = a.blocks_per_bh * a.B * a.H;
-  const int logical = xcd_remap(blockIdx.x, total);
   const int bh = logical / a.blocks_per_bh, kblk = logical % a.blocks_per_bh;
   const int b = bh / a.H, hh = bh % a.H;
   const int k0 = kblk * NW * 32 + wave * 32;
@@ -435,6 +428,66 @@ void attn_bwd_dkv_kernel(BwdArgs a) {
   }
 }
 
+// 4-wave blocks are register-capped to 256 VGPRs so TWO waves share each SIMD (the unconstrained
+// build took 264 / 376 VGPRs -> one wave per SIMD, SQ_WAIT_ANY ~65 % of wave cycles in dkv).
+#define BE_ATTN_BWD_WPE __attribute__((amdgpu_waves_per_eu(NW == 4 ? 2 : 1, NW == 4 ? 2 : 1)))
+
+template <int NW, int BIAS>
+__global__ __launch_bounds__(NW * 64) BE_ATTN_BWD_WPE void attn_bwd_dq_kernel(BwdArgs a) {
+  dq_body<NW, BIAS>(a, xcd_remap(blockIdx.x, a.blocks_per_bh * a.B * a.H));
+}
+
+template <int NW, int BIAS>
+__global__ __launch_bounds__(NW * 64) BE_ATTN_BWD_WPE void attn_bwd_dkv_kernel(BwdArgs a) {
+  dkv_body<NW, BIAS>(a, xcd_remap(blockIdx.x, a.blocks_per_bh * a.B * a.H));
+}
+
+// Small grids (batch 1: 16 heads x 1024 tokens = 256 + 256 two-wave blocks): the dq and dkv blocks
+// run as ONE launch (blocks [0, n) dq, [n, 2n) dkv) so both halves fill the 1024 SIMDs together;
+// delta = rowsum(dO * O) comes from attn_delta_kernel first.
+template <int NW, int BIAS>
+__global__ __launch_bounds__(NW * 64) BE_ATTN_BWD_WPE void attn_bwd_fused_kernel(BwdArgs a) {
+  const int n = a.blocks_per_bh * a.B * a.H;
+  if ((int)blockIdx.x < n)
+    dq_body<NW, BIAS>(a, xcd_remap(blockIdx.x, n));
+  else
+    dkv_body<NW, BIAS>(a, xcd_remap(blockIdx.x - n, n));
+}
+
+// delta[bh, q] = sum_c dO[b, q, h, c] O[b, q, h, c]: 8 lanes per row, 16-byte loads
+__global__ __launch_bounds__(256) void attn_delta_kernel(BwdArgs a) {
+  const long long row = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int part = threadIdx.x & 7;
+  const long long rows = (long long)a.B * a.H * a.N;
+  float acc = 0.f;
+  if (row < rows) {
+    const int bh = (int)(row / a.N), q = (int)(row % a.N);
+    const int b = bh / a.H, hh = bh % a.H;
+    const long long off = (long long)b * a.o_batch + (long long)hh * a.o_head + (long long)q * a.o_tok + part * 8;
+    const bf16x8 d = *reinterpret_cast<const bf16x8*>(a.dout + off);
+    const bf16x8 o = *reinterpret_cast<const bf16x8*>(a.o + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += bf2f((uint16_t)d[j]) * bf2f((uint16_t)o[j]);
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (row < rows && part == 0) a.delta[row] = acc;
+}
+
+template <int NW>
+void launch_fused(BwdArgs a, hipStream_t s) {
+  a.blocks_per_bh = (a.N + NW * 32 - 1) / (NW * 32);
+  const long long rows = (long long)a.B * a.H * a.N;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, s, a);
+  a.write_delta = 0;
+  const int grid = 2 * a.blocks_per_bh * a.B * a.H;
+  if (a.relh)
+    hipLaunchKernelGGL((attn_bwd_fused_kernel<NW, 1>), dim3(grid), dim3(NW * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((attn_bwd_fused_kernel<NW, 0>), dim3(grid), dim3(NW * 64), 0, s, a);
+}
+
 template <int NW>
 void launch_dq(BwdArgs a, hipStream_t s) {
   a.blocks_per_bh = (a.N + NW * 32 - 1) / (NW * 32);
@@ -481,11 +534,17 @@ int be_attn_bwd(const void* q, const void* k, const void* v, long long s_tok, lo
   a.lse = lse; a.delta = delta; a.relh = relh; a.relw = relw; a.Hg = Hg;
   a.dq = dq; a.drelh = drelh; a.drelw = drelw;
   a.dk = (bf16_t*)dk; a.dv = (bf16_t*)dv; a.d_tok = d_tok; a.d_head = d_head; a.d_batch = d_batch;
-  a.B = B; a.H = H; a.N = N; a.scale = scale;
-  if (nw == 0) {
-    // fill the 256 CUs: 4 waves per block when that still gives >= 512 blocks, else 2
-    const int blocks4 = ((N + 127) / 128) * B * H;
-    nw = blocks4 >= 512 ? 4 : 2;
+  a.B = B; a.H = H; a.N = N; a.scale = scale; a.write_delta = 1;
+  // fill the 256 CUs: 4 waves per block when that still gives >= 512 blocks, else 2
+  const int blocks4 = ((N + 127) / 128) * B * H;
+  if (nw == 0) nw = blocks4 >= 512 ? 4 : 2;
+  if (blocks4 < 512) {  // small grid: dq + dkv blocks in one launch (see attn_bwd_fused_kernel)
+    switch (nw) {
+      case 2: launch_fused<2>(a, stream); break;
+      case 4: launch_fused<4>(a, stream); break;
+      default: return -4;
+    }
+    return BE_CHECK_LAUNCH();
   }
   switch (nw) {
     case 2: launch_dq<2>(a, stream); break;
