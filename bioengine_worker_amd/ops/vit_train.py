@@ -29,7 +29,14 @@ def _rpb(rows: int, target_blocks: int = 512) -> int:
 
 
 def _colsum(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Column sums of [rows, C] (fp32), written into ``out`` when given (no extra copy)."""
+    """Column sums of [rows, C] (fp32), written into ``out`` when given (no extra copy).  On the GPU
+    the kernels' fp32 partials go through ``be_colsum`` (one small launch, ~3x faster than torch's
+    dim-0 reduction at these shapes)."""
+    if p.is_cuda and p.dtype == torch.float32 and p.dim() == 2 and p.is_contiguous():
+        o = torch.empty(p.shape[1], device=p.device, dtype=torch.float32) if out is None else out.view(-1)
+        if o.is_contiguous():
+            _native.call("be_colsum", _native.ptr(p), _native.ptr(o), p.shape[0], p.shape[1], _native.stream(p.device))
+            return o
     if out is None:
         return p.sum(0, dtype=torch.float32)
     return torch.sum(p, 0, dtype=torch.float32, out=out.view(-1))
