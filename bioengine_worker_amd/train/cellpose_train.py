@@ -59,6 +59,12 @@ class TrainConfig:
     # (tools/train_ddp_mode_ab.py): eager 5.86 vs graph 5.98 ms at 8 crops, 13.39 vs 13.44 ms at
     # 32 — the engine's launches already hide behind its kernels, so overlap wins.
     ddp_graph: bool = False
+    # CPSAM single-GPU graph: run each parameter group's AdamW inside the captured step on a side
+    # stream the moment its gradients are final (per-step lr / bias corrections read from a device
+    # buffer; same math as the flat update).  Measured slower on MI355X (profiles/r02/attn/README.md:
+    # batch 8 39.7 -> 41.4-41.8 ms, batch 1 15.3 -> 16.9-17.6 ms: the optimizer's HBM stream slows
+    # the backward kernels more than it hides), so the flat update after the replay stays the default.
+    cpsam_overlap_adamw: bool = False
 
 
 def lr_schedule(learning_rate: float, n_epochs: int) -> np.ndarray:
@@ -207,19 +213,48 @@ class CellposeTrainer:
         if self.net.rdrop > 0:
             keep = stochastic_depth_keep(x.shape[0], len(eng.blocks), self.net.rdrop, self.device, self.gen)
         with trace.span("train.fwd_bwd_cpsam", cuda=True):
+            fused_opt = False
             if self.cfg.graph and self.device.type == "cuda" and self.world == 1 and not self._cpsam_graph_failed:
                 loss = self._cpsam_graph_step(eng, x, lbl, keep)
+                fused_opt = getattr(self, "_adamw_in_graph", False)
             else:
                 loss = eng.loss_and_backward(x, lbl, keep,
                                              on_params_ready=self.ar.mark_ready if self.world > 1 else None)
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
+        if fused_opt:
+            return loss  # the update already ran inside the replayed graph
         with trace.span("train.adamw", cuda=True):
             mirror = eng.mirror if eng.mirror is not self.fp.flat else None
             train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
                                   weight_decay=self.cfg.weight_decay, grad_scale=gscale, p_bf16=mirror)
         return loss
+
+    def _adamw_group_cb(self, eng, side):
+        """on_params_ready callback used during capture: AdamW over the group's flat range on ``side``."""
+        from ..ops import _native
+
+        fp = self.fp
+        off = {id(p): o for p, o in zip(fp.params, fp.offsets)}
+        mirror = eng.mirror if eng.mirror is not fp.flat else None
+        cur = torch.cuda.current_stream(self.device)
+
+        def cb(params):
+            lo = min(off[id(p)] for p in params)
+            hi = max(off[id(p)] + (p.numel() + 3) // 4 * 4 for p in params)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                _native.call("be_adamw_flat_dev", _native.ptr(fp.flat[lo:]), _native.ptr(fp.grad[lo:]),
+                             _native.ptr(self.m[lo:]), _native.ptr(self.v[lo:]),
+                             _native.ptr(mirror[lo:] if mirror is not None else None), hi - lo,
+                             _native.ptr(self._hp), 0.9, 0.999, 1e-8, _native.stream(self.device))
+        return cb
+
+    def _set_hp(self, step: int) -> None:
+        b1, b2 = 0.9, 0.999
+        vals = [self.lr, float(self.cfg.weight_decay), 1.0 - b1 ** step, 1.0 - b2 ** step, 1.0]
+        self._hp.copy_(torch.tensor(vals, dtype=torch.float32))  # pageable source: staged before return
 
     def _cpsam_graph_step(self, eng, x, lbl, keep):
         """Replay the captured CPSAM fwd+bwd (~1.3k launches at ViT-L) on static buffers; the
@@ -236,18 +271,30 @@ class CellposeTrainer:
                     for _ in range(2):
                         eng.loss_and_backward(xs, ls, ks)
                 torch.cuda.current_stream(self.device).wait_stream(side)
+                fuse = bool(self.cfg.cpsam_overlap_adamw)
+                if fuse and not hasattr(self, "_hp"):
+                    self._hp = torch.zeros(5, device=self.device, dtype=torch.float32)
                 g = torch.cuda.CUDAGraph()
+                opt_side = torch.cuda.Stream(self.device)
                 with torch.cuda.graph(g):
-                    out = eng.loss_and_backward(xs, ls, ks)
+                    cur = torch.cuda.current_stream(self.device)
+                    cb = self._adamw_group_cb(eng, opt_side) if fuse else None
+                    out = eng.loss_and_backward(xs, ls, ks, on_params_ready=cb)
+                    if fuse:
+                        cur.wait_stream(opt_side)  # join the optimizer branch before the graph ends
+                self._adamw_in_graph = fuse
             except Exception as e:  # noqa: BLE001  (e.g. a library call that cannot be captured)
                 import logging
 
                 logging.getLogger("bioengine.train").warning("CPSAM graph capture failed (%s); running eagerly", e)
                 self._cpsam_graph_failed = True
+                self._adamw_in_graph = False
                 torch.cuda.synchronize(self.device)
                 return eng.loss_and_backward(x, lbl, keep)
             self._cpsam_graph = (key, g, xs, ls, ks, out)
         _, g, xs, ls, ks, out = self._cpsam_graph
+        if getattr(self, "_adamw_in_graph", False):
+            self._set_hp(self.step_count + 1)
         xs.copy_(x)
         ls.copy_(lbl)
         if keep is not None:
@@ -318,6 +365,7 @@ class CellposeTrainer:
                                     comm_dtype=torch.bfloat16 if self.cfg.comm_bf16 else None)
         self._graph = self._graph_io = None
         self._cpsam_graph = None
+        self._adamw_in_graph = False
         if self.world > 1:
             broadcast_params(self.fp, 0, group)
             for t in [self.m, self.v] + [b for b in self.net.buffers() if b.is_floating_point()]:

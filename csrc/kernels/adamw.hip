@@ -12,10 +12,15 @@
 
 namespace {
 
+// hp (optional): device copy of {lr, wd, bc1, bc2, gscale} overriding the by-value scalars, so the
+// update can live inside a captured HIP graph and still follow the host's LR schedule / step count.
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, bf16_t* __restrict__ pbf,
                                                     long long n, float lr, float b1, float b2, float eps, float wd,
-                                                    float bc1, float bc2, float gscale) {
+                                                    float bc1, float bc2, float gscale, const float* __restrict__ hp) {
+  if (hp) {
+    lr = hp[0]; wd = hp[1]; bc1 = hp[2]; bc2 = hp[3]; gscale = hp[4];
+  }
   const long long n4 = n / 4;
   const long long stride = (long long)gridDim.x * blockDim.x;
   const float step_size = lr / bc1;
@@ -86,7 +91,21 @@ int be_adamw_flat(float* p, const float* g, float* m, float* v, void* pbf, long 
   int blocks = (int)((n4 + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd, bc1, bc2,
-                     gscale);
+                     gscale, (const float*)nullptr);
+  return BE_CHECK_LAUNCH();
+}
+
+// Same update with {lr, wd, bc1, bc2, gscale} read from device memory (graph-capturable).  p/g/m/v/
+// pbf point at the START of the range (16-byte aligned for the float4 path), n elements.
+int be_adamw_flat_dev(float* p, const float* g, float* m, float* v, void* pbf, long long n, const float* hp, float b1,
+                      float b2, float eps, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long long n4 = (n + 3) / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks > 256) blocks = 256;  // a background stream: one block per CU, leave room for the backward
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, 0.f, b1, b2, eps, 0.f,
+                     1.f, 1.f, 1.f, hp);
   return BE_CHECK_LAUNCH();
 }
 

@@ -181,3 +181,31 @@ def test_relpos_kernels_match_fp32_oracle(dev, B):
     for got, dR in ((gh, dRh), (gw, dRw)):
         ref = torch.zeros(2 * g - 1, c).index_add_(0, idx.cpu().reshape(-1), dR.reshape(-1, c))
         assert _rel(got.cpu(), ref) < 1e-4
+
+
+def test_cpsam_adamw_overlapped_in_graph_matches_flat_update(dev):
+    """AdamW per parameter group inside the captured step (side stream, device-resident lr / bias
+    corrections) gives the same weights, moments and bf16 mirror as the flat update after it (not
+    bitwise: the rel-pos table gradients accumulate with fp32 atomics, and the bias corrections come
+    from the host in double instead of powf; a skipped group would show up as a ~1e-2 difference)."""
+    from bioengine_worker_amd.models.cpsam import CPSAM
+    from bioengine_worker_amd.train.cellpose_train import TrainConfig, build_trainer, synthetic_train_batch
+
+    trs = []
+    for fuse in (False, True):
+        cfg = TrainConfig(batch_size=2, bsize=256, lr=1e-4, weight_decay=1e-4, cpsam_overlap_adamw=fuse)
+        tr = build_trainer(cfg, dev, net=CPSAM(dim=256, depth=2, heads=4, bsize=256).randomize_(0))
+        tr._init_flat = tr.fp.flat.clone()
+        batch = synthetic_train_batch(2, 256, device=dev, seed=3)
+        for i in range(4):
+            tr.set_lr(1e-4 * (i + 1))  # the schedule must reach the in-graph update
+            tr.step(*batch)
+        torch.cuda.synchronize()
+        trs.append(tr)
+    a, b = trs
+    assert b._adamw_in_graph and not a._adamw_in_graph
+    upd = _rel(a.fp.flat, a._init_flat)  # how far 4 steps moved the weights
+    assert upd > 1e-3
+    # fused vs flat differ only by atomic-order / bias-correction rounding: far below one update
+    assert _rel(b.fp.flat, a.fp.flat) < 0.02 * upd, (_rel(b.fp.flat, a.fp.flat), upd)
+    assert _rel(b.m, a.m) < 0.05 and _rel(b._cpsam_engine(2).mirror.float(), a._cpsam_engine(2).mirror.float()) < 0.02 * upd + 1e-3
