@@ -257,16 +257,23 @@ def relpos_fwd_ref(q, Rh, Rw):
     return rh.contiguous(), rw.contiguous()
 
 
-def relpos_fwd(q, Rh, Rw):
-    """rel_h / rel_w on MFMA (``relpos.hip``) for the 32 x 32 grid / head_dim 64; torch otherwise."""
+def _rel_table_idx(g: int, device) -> torch.Tensor:
+    ar = torch.arange(g, device=device)
+    return (ar[:, None] - ar[None, :] + (g - 1)).long()
+
+
+def relpos_fwd(q, tab_h, tab_w):
+    """rel_h / rel_w from the [2g-1, c] rel-pos TABLES (get_rel_pos gather done inside the kernel) on
+    MFMA (``relpos.hip``) for the 32 x 32 grid / head_dim 64; torch oracle otherwise."""
     B, N, H, c = q.shape
-    g = Rh.shape[0]
+    g = (tab_h.shape[0] + 1) // 2
     if not (q.is_cuda and g == 32 and c == 64 and N == g * g and q.dtype == torch.bfloat16 and q.stride(-1) == 1):
-        return relpos_fwd_ref(q, Rh, Rw)
+        idx = _rel_table_idx(g, tab_h.device)
+        return relpos_fwd_ref(q, tab_h[idx], tab_w[idx])
     rh = torch.empty(B, H, N, g, device=q.device, dtype=torch.float32)
     rw = torch.empty_like(rh)
     _native.call("be_relpos_fwd", _native.ptr(q), q.stride(1), q.stride(2), q.stride(0),
-                 _native.ptr(Rh.float().contiguous()), _native.ptr(Rw.float().contiguous()), _native.ptr(rh),
+                 _native.ptr(tab_h.float().contiguous()), _native.ptr(tab_w.float().contiguous()), _native.ptr(rh),
                  _native.ptr(rw), B, H, g, c, _native.stream(q.device))
     return rh, rw
 
@@ -284,23 +291,24 @@ def relpos_bwd_ref(q, Rh, Rw, drh, drw):
     return dq.reshape(B, N, H, c), dRh, dRw
 
 
-def relpos_bwd_(q, Rh, Rw, drh, drw, dq, out_q, grad_rh, grad_rw, rel_idx):
-    """Fused backward of the rel-pos terms: ``out_q`` (bf16 view, e.g. the q slot of a packed dqkv
-    gradient) = dq + dq_rel; ``grad_rh`` / ``grad_rw`` (the [2g-1, c] table gradients) overwritten
-    with the gathered dRh / dRw (rel_idx [g, g] = y - k + g - 1).  ``dq`` (fp32) is clobbered."""
+def relpos_bwd_(q, tab_h, tab_w, drh, drw, dq, out_q, grad_rh, grad_rw, rel_idx):
+    """Fused backward of the rel-pos terms (tables ``tab_h`` / ``tab_w`` [2g-1, c]): ``out_q`` (bf16
+    view, e.g. the q slot of a packed dqkv gradient) = dq + dq_rel; ``grad_rh`` / ``grad_rw`` (the
+    table gradients) overwritten with the gathered dRh / dRw (rel_idx [g, g] = y - k + g - 1).
+    ``dq`` (fp32) is clobbered."""
     B, N, H, c = q.shape
-    g = Rh.shape[0]
+    g = rel_idx.shape[0]
     if q.is_cuda and g == 32 and c == 64 and N == g * g and q.stride(-1) == 1 and dq.stride(-1) == 1 \
             and out_q.stride(-1) == 1 and grad_rh.is_contiguous() and grad_rw.is_contiguous():
         grad_rh.zero_()
         grad_rw.zero_()
-        _native.call("be_relpos_bwd", _native.ptr(drh), _native.ptr(drw), _native.ptr(Rh.float().contiguous()),
-                     _native.ptr(Rw.float().contiguous()), _native.ptr(dq), dq.stride(1), dq.stride(2), dq.stride(0),
+        _native.call("be_relpos_bwd", _native.ptr(drh), _native.ptr(drw), _native.ptr(tab_h.float().contiguous()),
+                     _native.ptr(tab_w.float().contiguous()), _native.ptr(dq), dq.stride(1), dq.stride(2), dq.stride(0),
                      _native.ptr(out_q), out_q.stride(1), out_q.stride(2), out_q.stride(0), _native.ptr(q),
                      q.stride(1), q.stride(2), q.stride(0), _native.ptr(grad_rh), _native.ptr(grad_rw), B, H, g, c,
                      _native.stream(q.device))
         return
-    dq_rel, dRh, dRw = relpos_bwd_ref(q, Rh, Rw, drh, drw)
+    dq_rel, dRh, dRw = relpos_bwd_ref(q, tab_h[rel_idx], tab_w[rel_idx], drh, drw)
     out_q.copy_((dq.float() + dq_rel).to(out_q.dtype))
     for dR, out in ((dRh, grad_rh), (dRw, grad_rw)):
         out.zero_()

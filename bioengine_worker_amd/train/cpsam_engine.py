@@ -188,9 +188,13 @@ class CPSAMTrainEngine:
             kb = keep[:, i].contiguous() if keep is not None else None
             qkv = F.linear(h1, w["qkv_w"], w["qkv_b"]).view(B, N, 3, H, self.hd)
             q, k_, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-            Rh = get_rel_pos(g, g, p["rph"].detach()).float()
-            Rw = get_rel_pos(g, g, p["rpw"].detach()).float()
-            rel_h, rel_w = vt.relpos_fwd(q, Rh, Rw) if self.cuda else self._rel_terms(q, Rh, Rw)
+            if self.cuda:  # tables gathered inside relpos.hip (no get_rel_pos index kernels)
+                Rh, Rw = p["rph"].detach(), p["rpw"].detach()
+                rel_h, rel_w = vt.relpos_fwd(q, Rh, Rw)
+            else:
+                Rh = get_rel_pos(g, g, p["rph"].detach()).float()
+                Rw = get_rel_pos(g, g, p["rpw"].detach()).float()
+                rel_h, rel_w = self._rel_terms(q, Rh, Rw)
             a, lse = vt.attn_fwd(q, k_, v, self.scale, rel_h, rel_w)
             a2 = a.reshape(B * N, D)
             y = F.linear(a2, w["proj_w"], w["proj_b"])

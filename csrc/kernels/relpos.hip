@@ -55,14 +55,15 @@ __global__ __launch_bounds__(256) void relpos_fwd_kernel(const bf16_t* __restric
   const int pass = tile & 1, line = (tile >> 1) % G, bh = (tile >> 1) / G;
   const int b = bh / H, hh = bh % H;
   const bf16_t* qb = q + (long long)b * s_batch + (long long)hh * s_head;
-  const float* T = (pass ? Rw : Rh) + (long long)line * G * C;
+  // R[line][k] = table[line - k + G - 1] (get_rel_pos at q == k size): read the table directly
+  const float* T = (pass ? Rw : Rh) + (long long)(line - l32 + G - 1) * C;
   const int tokA = tok_of(pass, line, l32);
   f32x16 acc = zero16();
 #pragma unroll
   for (int ks = 0; ks < C / 16; ++ks) {
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(qb + (long long)tokA * s_tok + ks * 16 + h * 8);
     float tv[8];
-    const float4* tp = reinterpret_cast<const float4*>(T + l32 * C + ks * 16 + h * 8);
+    const float4* tp = reinterpret_cast<const float4*>(T + ks * 16 + h * 8);
     const float4 t0 = tp[0], t1 = tp[1];
     tv[0] = t0.x; tv[1] = t0.y; tv[2] = t0.z; tv[3] = t0.w; tv[4] = t1.x; tv[5] = t1.y; tv[6] = t1.z; tv[7] = t1.w;
     bf16x8 bhi, blo;
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(256) void relpos_bwd_dq_kernel(const float* __restr
   const int line = tile % G, bh = tile / G;
   const int b = bh / H, hh = bh % H;
   const float* d = (pass ? drw : drh) + (long long)bh * G * G * G;
-  const float* T = (pass ? Rw : Rh) + (long long)line * G * C;
+  const float* T = (pass ? Rw : Rh) + (long long)(line + G - 1) * C;  // row k: T - k * C
   const int tokA = tok_of(pass, line, l32);
   f32x16 acc[2] = {zero16(), zero16()};
 #pragma unroll
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256) void relpos_bwd_dq_kernel(const float* __restr
     for (int cb = 0; cb < 2; ++cb) {
       float bv[8];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) bv[jj] = T[(ks * 16 + h * 8 + jj) * C + cb * 32 + l32];
+      for (int jj = 0; jj < 8; ++jj) bv[jj] = T[-(ks * 16 + h * 8 + jj) * C + cb * 32 + l32];
       bf16x8 bhi, blo;
       split8(bv, bhi, blo);
       acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[cb], 0, 0, 0);
@@ -189,7 +190,8 @@ __global__ __launch_bounds__(256) void relpos_bwd_table_kernel(const float* __re
 
 extern "C" {
 
-// q: bf16 [B, N=1024, H, 64] view (element strides); Rh/Rw: fp32 [32, 32, 64]; rel_h/rel_w: fp32
+// q: bf16 [B, N=1024, H, 64] view (element strides); Rh/Rw: the fp32 rel-pos TABLES [63, 64]
+// (R[y][k] = table[y - k + 31], gathered in the kernels); rel_h/rel_w: fp32
 // [B, H, 1024, 32].  Grid side must be 32 and head_dim 64.
 int be_relpos_fwd(const void* q, long long s_tok, long long s_head, long long s_batch, const float* Rh, const float* Rw,
                   float* rel_h, float* rel_w, int B, int H, int g, int c, hipStream_t stream) {
@@ -200,7 +202,7 @@ int be_relpos_fwd(const void* q, long long s_tok, long long s_head, long long s_
   return BE_CHECK_LAUNCH();
 }
 
-// drh/drw: fp32 [B, H, 1024, 32]; dq: fp32 [B, N, H, 64] (strides), updated with the h term, then
+// drh/drw: fp32 [B, H, 1024, 32]; Rh/Rw: tables as above; dq: fp32 [B, N, H, 64] (strides), updated with the h term, then
 // (pass 2) the w term is added and the sum written as bf16 into out (strides o_*) when out != null.
 // q (for the table gradients): bf16 strides as in be_relpos_fwd; gRh / gRw: fp32 [2*32-1, 64],
 // zeroed by the caller.

@@ -162,18 +162,19 @@ def test_relpos_kernels_match_fp32_oracle(dev, B):
     N = g * g
     qkv = (torch.randn(B, N, 3, H, c, device=dev) * 0.5).bfloat16()
     q = qkv[:, :, 0]
-    Rh, Rw = torch.randn(g, g, c, device=dev) * 0.3, torch.randn(g, g, c, device=dev) * 0.3
-    rh, rw = vt.relpos_fwd(q, Rh, Rw)
+    ar = torch.arange(g, device=dev)
+    idx = (ar[:, None] - ar[None, :] + g - 1).long()
+    tab_h, tab_w = torch.randn(2 * g - 1, c, device=dev) * 0.3, torch.randn(2 * g - 1, c, device=dev) * 0.3
+    Rh, Rw = tab_h[idx], tab_w[idx]  # get_rel_pos at q == k size (the kernels gather it themselves)
+    rh, rw = vt.relpos_fwd(q, tab_h, tab_w)
     rh_r, rw_r = vt.relpos_fwd_ref(q.cpu(), Rh.cpu(), Rw.cpu())
     assert _rel(rh.cpu(), rh_r) < 1e-4 and _rel(rw.cpu(), rw_r) < 1e-4
     drh, drw = torch.randn(B, H, N, g, device=dev), torch.randn(B, H, N, g, device=dev)
     dq = torch.randn(B, N, H, c, device=dev)
     dq0 = dq.clone()
     dqkv = torch.zeros(B, N, 3, H, c, device=dev, dtype=torch.bfloat16)
-    ar = torch.arange(g, device=dev)
-    idx = (ar[:, None] - ar[None, :] + g - 1).long()
     gh, gw = torch.full((2 * g - 1, c), 7.0, device=dev), torch.full((2 * g - 1, c), 7.0, device=dev)
-    vt.relpos_bwd_(q, Rh, Rw, drh, drw, dq, dqkv[:, :, 0], gh, gw, idx)
+    vt.relpos_bwd_(q, tab_h, tab_w, drh, drw, dq, dqkv[:, :, 0], gh, gw, idx)
     torch.cuda.synchronize()
     dq_rel, dRh, dRw = vt.relpos_bwd_ref(q.cpu(), Rh.cpu(), Rw.cpu(), drh.cpu(), drw.cpu())
     assert _rel(dqkv[:, :, 0].float().cpu(), dq0.cpu() + dq_rel) < 1e-2  # bf16 output
