@@ -110,7 +110,13 @@ def ln_bwd(dh: torch.Tensor, x: torch.Tensor, stats: torch.Tensor, w: torch.Tens
                      _native.ptr(w.float().contiguous()), _native.ptr(f(r1)), _native.ptr(f(s1)), _native.ptr(f(r2)),
                      _native.ptr(f(s2)), int(rpn), _native.ptr(dx), _native.ptr(dxb), _native.ptr(pdw),
                      _native.ptr(pdb), _native.ptr(pcol), rows, C, rpb, _native.stream(dev))
-        return dx, dxb, _colsum(pdw, out_dw), _colsum(pdb, out_db), (_colsum(pcol, out_col) if want_col else None)
+        if out_dw is not None and out_db is not None and out_dw.is_contiguous() and out_db.is_contiguous():
+            _native.call("be_colsum2", _native.ptr(pdw), _native.ptr(out_dw), _native.ptr(pdb), _native.ptr(out_db),
+                         nblk, C, _native.stream(dev))  # dw and db partials in one launch
+            dw, db = out_dw.view(-1), out_db.view(-1)
+        else:
+            dw, db = _colsum(pdw, out_dw), _colsum(pdb, out_db)
+        return dx, dxb, dw, db, (_colsum(pcol, out_col) if want_col else None)
     xf = x.float().reshape(rows, C)
     d = dh.float().reshape(rows, C)
     mean, rstd = stats[:, 0:1], stats[:, 1:2]

@@ -201,9 +201,12 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const bf16_t* __restrict__ 
 // Column sums of the per-block partials [rows, C] fp32 -> out[C] (replaces a torch dim-0 reduction
 // that cost ~9 us per call, 9 per transformer block).  Block = 8 columns x 32 row lanes: every lane
 // issues its ~rows/32 loads back to back, one LDS step folds the 32 lanes.
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p, float* __restrict__ out, int rows,
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p0, float* __restrict__ out0,
+                                                     const float* __restrict__ p1, float* __restrict__ out1, int rows,
                                                      int C) {
   __shared__ float red[32][9];
+  const float* p = blockIdx.y ? p1 : p0;  // gridDim.y = 2: two partial matrices in one launch
+  float* out = blockIdx.y ? out1 : out0;
   const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c = blockIdx.x * 8 + cl;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -293,7 +296,14 @@ int be_scale_cast(const float* x, const float* rs, int rpn, void* y, float* pcol
 // out[C] = sum over rows of p [rows, C] (fp32)
 int be_colsum(const float* p, float* out, int rows, int C, hipStream_t s) {
   if (rows <= 0 || C <= 0) return -1;
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 7) / 8), dim3(256), 0, s, p, out, rows, C);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 7) / 8, 1), dim3(256), 0, s, p, out, p, out, rows, C);
+  return BE_CHECK_LAUNCH();
+}
+
+// two [rows, C] partial matrices reduced in one launch (e.g. LayerNorm dw and db)
+int be_colsum2(const float* p0, float* out0, const float* p1, float* out1, int rows, int C, hipStream_t s) {
+  if (rows <= 0 || C <= 0) return -1;
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 7) / 8, 2), dim3(256), 0, s, p0, out0, p1, out1, rows, C);
   return BE_CHECK_LAUNCH();
 }
 
