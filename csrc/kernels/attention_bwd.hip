@@ -314,20 +314,27 @@ __device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical) {
         if (qq < a.N)
           r = *reinterpret_cast<const u32x4*>(isd ? dbase + (long long)qq * a.o_tok + ch * 8
                                                   : qbase + (long long)qq * a.s_tok + ch * 8);
-      } else if (c < QCH + WCH) {
+      } else if (c < QCH + WCH) {  // rel_w, pre-scaled to log2 units
         const int cc = c - QCH;
         const int row = cc >> 3, c4 = cc & 7;
         const int qq = t * TT + row;
-        if (qq < a.N) r = *reinterpret_cast<const u32x4*>(a.relw + ((long long)bh * a.N + qq) * 32 + c4 * 4);
-      } else if (c < QCH + WCH + HCH) {
+        if (qq < a.N) {
+          const float4 f = *reinterpret_cast<const float4*>(a.relw + ((long long)bh * a.N + qq) * 32 + c4 * 4);
+          r[0] = __float_as_uint(f.x * LOG2E); r[1] = __float_as_uint(f.y * LOG2E);
+          r[2] = __float_as_uint(f.z * LOG2E); r[3] = __float_as_uint(f.w * LOG2E);
+        }
+      } else if (c < QCH + WCH + HCH) {  // rel_h of the block's grid rows minus the row's LSE (log2)
         const int qq = t * TT + (c - QCH - WCH);
         if (qq < a.N) {
           const float* hr = a.relh + ((long long)bh * a.N + qq) * a.Hg;
+          const float l2 = lrow[qq] * LOG2E;
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
             const int gr = kblk * NW + w;
-            r[w] = (w < NW && gr < a.Hg) ? __float_as_uint(hr[gr]) : 0u;
+            r[w] = __float_as_uint(((w < NW && gr < a.Hg) ? hr[gr] * LOG2E : 0.f) - l2);
           }
+        } else {  // padded query: P = 0
+          r[0] = r[1] = r[2] = r[3] = __float_as_uint(-INFINITY);
         }
       } else if (c < CHUNKS) {
         const int cc = c - QCH - WCH - HCH;
@@ -392,9 +399,9 @@ __device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qr = qb * 32 + 8 * (i >> 2) + 4 * h + (i & 3);  // query row in the tile
-        float x = s[i] * c2;
-        if (BIAS) x += (Hs[qr * 4 + wave] + Ws[qr * 32 + kl]) * LOG2E;
-        const float p = kv ? __builtin_amdgcn_exp2f(x - L2s[qr]) : 0.f;
+        // BIAS: Hs holds rel_h * log2e - lse * log2e, Ws rel_w * log2e (folded at staging time)
+        const float x = BIAS ? s[i] * c2 + (Hs[qr * 4 + wave] + Ws[qr * 32 + kl]) : s[i] * c2 - L2s[qr];
+        const float p = kv ? __builtin_amdgcn_exp2f(x) : 0.f;
         s[i] = p;
         dp[i] = p * (dp[i] - DLs[qr]);
       }
