@@ -306,8 +306,6 @@ def relpos_bwd_(q, tab_h, tab_w, drh, drw, dq, out_q, grad_rh, grad_rw, rel_idx)
     g = rel_idx.shape[0]
     if q.is_cuda and g == 32 and c == 64 and N == g * g and q.stride(-1) == 1 and dq.stride(-1) == 1 \
             and out_q.stride(-1) == 1 and grad_rh.is_contiguous() and grad_rw.is_contiguous():
-        grad_rh.zero_()
-        grad_rw.zero_()
         _native.call("be_relpos_bwd", _native.ptr(drh), _native.ptr(drw), _native.ptr(tab_h.float().contiguous()),
                      _native.ptr(tab_w.float().contiguous()), _native.ptr(dq), dq.stride(1), dq.stride(2), dq.stride(0),
                      _native.ptr(out_q), out_q.stride(1), out_q.stride(2), out_q.stride(0), _native.ptr(q),

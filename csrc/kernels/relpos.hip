@@ -86,7 +86,12 @@ __global__ __launch_bounds__(256) void relpos_bwd_dq_kernel(const float* __restr
                                                             const float* __restrict__ Rh, const float* __restrict__ Rw,
                                                             float* dq, long long q_tok, long long q_head,
                                                             long long q_batch, bf16_t* out_bf16, long long o_tok,
-                                                            long long o_head, long long o_batch, int pass, int B, int H) {
+                                                            long long o_head, long long o_batch, int pass, int B, int H,
+                                                            float* zero0, float* zero1) {
+  // pass 0, block 0 zeroes the table gradients the later table kernel accumulates into (saves two
+  // fill launches per transformer block)
+  if (zero0 && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < (2 * G - 1) * C; i += blockDim.x) { zero0[i] = 0.f; zero1[i] = 0.f; }
   const int lane = threadIdx.x & 63, h = lane >> 5, l32 = lane & 31;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);  // (bh, line)
   if (tile >= B * H * G) return;
@@ -135,7 +140,7 @@ __global__ __launch_bounds__(256) void relpos_bwd_dq_kernel(const float* __restr
 // ------------------------------------------------------------------ backward: rel-pos table gradients
 // Block = (pass, line, split); its 4 waves take (b, h) pairs split*4 + wave, += nsplit*4, accumulate
 // dT[line] [32 k x 64 c] in registers, reduce through LDS and add into the gathered table rows
-// line - k + G - 1 with global fp32 atomics (tables zeroed by the caller).
+// line - k + G - 1 with global fp32 atomics (tables zeroed by the pass-0 dq launch before it).
 __global__ __launch_bounds__(256) void relpos_bwd_table_kernel(const float* __restrict__ drh,
                                                                const float* __restrict__ drw,
                                                                const bf16_t* __restrict__ q, long long s_tok,
@@ -204,8 +209,8 @@ int be_relpos_fwd(const void* q, long long s_tok, long long s_head, long long s_
 
 // drh/drw: fp32 [B, H, 1024, 32]; Rh/Rw: tables as above; dq: fp32 [B, N, H, 64] (strides), updated with the h term, then
 // (pass 2) the w term is added and the sum written as bf16 into out (strides o_*) when out != null.
-// q (for the table gradients): bf16 strides as in be_relpos_fwd; gRh / gRw: fp32 [2*32-1, 64],
-// zeroed by the caller.
+// q (for the table gradients): bf16 strides as in be_relpos_fwd; gRh / gRw: fp32 [2*32-1, 64]
+// (overwritten: zeroed by the first dq launch, then accumulated by the table kernel).
 int be_relpos_bwd(const float* drh, const float* drw, const float* Rh, const float* Rw, float* dq, long long q_tok,
                   long long q_head, long long q_batch, void* out, long long o_tok, long long o_head, long long o_batch,
                   const void* q, long long s_tok, long long s_head, long long s_batch, float* gRh, float* gRw, int B,
@@ -214,7 +219,8 @@ int be_relpos_bwd(const float* drh, const float* drw, const float* Rh, const flo
   const int tiles = B * H * G;
   for (int pass = 0; pass < 2; ++pass) {
     hipLaunchKernelGGL(relpos_bwd_dq_kernel, dim3((tiles + 3) / 4), dim3(256), 0, stream, drh, drw, Rh, Rw, dq, q_tok,
-                       q_head, q_batch, pass ? (bf16_t*)out : (bf16_t*)nullptr, o_tok, o_head, o_batch, pass, B, H);
+                       q_head, q_batch, pass ? (bf16_t*)out : (bf16_t*)nullptr, o_tok, o_head, o_batch, pass, B, H,
+                       pass ? (float*)nullptr : gRh, pass ? (float*)nullptr : gRw);
     const int rc = BE_CHECK_LAUNCH();
     if (rc) return rc;
   }
