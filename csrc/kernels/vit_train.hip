@@ -156,6 +156,7 @@ __global__ __launch_bounds__(256) void rowcol_kernel(const bf16_t* __restrict__ 
     for (int j = 0; j < 8; ++j) { acc[n][j] = 0.f; bb[n][j] = 0.f; }
     if (bias && ch < C8) ld8f(bias + ch * 8, bb[n]);
   }
+#pragma unroll 4  // several rows' 16-byte loads in flight per thread (the loop was latency-bound)
   for (long long row = r0; row < r1; ++row) {
     const float sc = rs ? rs[row / rpn] : 1.f;
 #pragma unroll
