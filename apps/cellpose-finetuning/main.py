@@ -669,7 +669,7 @@ class CellposeFinetune:
         sid = normalize_session_id(session_id)
         st = read_status(session_dir(sid))
         uid = _user_id(context)
-        if st.get("user_id") and uid and st["user_id"] != uid:
+        if st.get("user_id") is not None and uid != st["user_id"]:  # no caller id -> refused too
             raise PermissionError(f"Session '{sid}' belongs to another user")
         t = self.tasks.get(sid)
         if t is not None and not t.done() and st.get("status_type") in ("completed", "failed", "stopped"):

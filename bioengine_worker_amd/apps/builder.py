@@ -137,7 +137,7 @@ class AppBuilder:
             from .requirements import _APP_PATHS
 
             _APP_PATHS.add(str(site))
-            sys.path.insert(0, str(site))
+            sys.path.append(str(site))  # appended: an app's wheels never shadow the worker's own modules
         mod_name = f"bioengine_app_{application_id.replace('-', '_')}_{Path(py).stem}"
         ns: dict[str, Any] = {"__name__": mod_name, "__file__": f"<{artifact_id}/{py}>", "__builtins__": __builtins__}
         ns.update({k: v for k, v in env_vars.items()})

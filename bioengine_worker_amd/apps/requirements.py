@@ -125,6 +125,28 @@ def resolve(requirements: list[str], extra_paths: list[str] | None = None) -> tu
     return ok, missing
 
 
+def invalid_requirements(requirements: list[str]) -> list[tuple[str, str]]:
+    """Entries that must never reach the pip command line: unparsable strings (pip would read
+    ``--target=/x``, ``-e path`` or ``--find-links=...`` as options) and direct-URL requirements
+    (``pkg @ https://...`` / ``file:///...sdist`` bypass ``--no-index`` and may run build code)."""
+    bad = []
+    for raw in requirements:
+        raw = (raw or "").strip()
+        if not raw or raw.startswith("#"):
+            continue
+        if raw.startswith("-"):
+            bad.append((raw, "pip options are not accepted as requirements"))
+            continue
+        try:
+            req = Requirement(raw)
+        except InvalidRequirement as e:
+            bad.append((raw, f"invalid requirement: {e}"))
+            continue
+        if req.url:
+            bad.append((raw, "direct-URL requirements are not installable offline from the wheelhouse"))
+    return bad
+
+
 def wheelhouses() -> list[str]:
     v = os.environ.get("BIOENGINE_WHEELHOUSE", "")
     return [p for p in v.split(os.pathsep) if p and Path(p).is_dir()]
@@ -176,13 +198,16 @@ def ensure(requirements: list[str], target: str | Path, wheel_dirs: list[str] | 
     :class:`MissingRequirementsError` listing everything that stays unsatisfied."""
     target = Path(target)
     pinned = update_requirements(list(requirements or []))
+    bad = invalid_requirements(pinned)
+    if bad:  # never hand these to pip: "--target=..." / "-e path" would be read as options
+        raise MissingRequirementsError(bad, "rejected before install")
     paths = [str(target)] if target.is_dir() else []
     _, missing = resolve(pinned, paths)
     installed: list[str] = []
     wheel_dirs = wheelhouses() if wheel_dirs is None else [w for w in wheel_dirs if Path(w).is_dir()]
     if missing and wheel_dirs:
         target.mkdir(parents=True, exist_ok=True)
-        reqs = [r for r, _ in missing]
+        reqs = [str(Requirement(r)) for r, _ in missing]
         # dependencies of the wheels are resolved against the worker environment + target below,
         # so pip installs only what was asked for (an index-free resolver cannot see site-packages
         # from a --target install)
@@ -190,7 +215,7 @@ def ensure(requirements: list[str], target: str | Path, wheel_dirs: list[str] | 
                "--no-cache-dir", "--target", str(target), "--upgrade"]
         for w in wheel_dirs:
             cmd += ["--find-links", w]
-        cmd += reqs
+        cmd += ["--"] + reqs
         log.info("installing %s from %s into %s", reqs, wheel_dirs, target)
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
         if p.returncode != 0:
@@ -209,7 +234,10 @@ def ensure(requirements: list[str], target: str | Path, wheel_dirs: list[str] | 
                   if not wheel_dirs else f"not satisfiable from the wheelhouse {wheel_dirs}")
         raise MissingRequirementsError(missing, detail)
     if paths and add_to_sys_path:  # in-process replicas import from the target too
+        # appended, not prepended: a package an app installs must never replace a module the worker
+        # (or another in-process app) already imports; process replicas get the target at the FRONT
+        # of their own PYTHONPATH instead (serve/replica.py), where it affects nobody else
         _APP_PATHS.add(paths[0])
         if paths[0] not in sys.path:
-            sys.path.insert(0, paths[0])
+            sys.path.append(paths[0])
     return {"pinned": pinned, "satisfied": True, "installed": installed, "target": paths[0] if paths else None}

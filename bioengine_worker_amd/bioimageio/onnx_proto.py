@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import struct
 from dataclasses import dataclass, field
+from pathlib import Path, PurePosixPath
 from typing import Any
 
 import numpy as np
@@ -294,19 +295,43 @@ def load_model(path) -> Model:
     return m
 
 
+def external_data_path(base_dir, location: str) -> Path:
+    """Resolve an initializer's ``external_data`` location inside the model directory.
+
+    Model packages are untrusted input: an absolute location or one with a ``..`` part could make
+    the loader read any file the worker can read (and echo it back through an Identity output), so
+    both are rejected, as is anything that resolves (symlinks included) outside ``base_dir``."""
+    if not isinstance(location, str) or not location or "\x00" in location:
+        raise ValueError("external data location must be a non-empty relative path")
+    norm = location.replace("\\", "/")
+    if norm.startswith("/") or PurePosixPath(norm).is_absolute() or (len(norm) > 1 and norm[1] == ":"):
+        raise ValueError(f"external data location '{location}' is absolute")
+    if any(part == ".." for part in PurePosixPath(norm).parts):
+        raise ValueError(f"external data location '{location}' leaves the model directory")
+    base = Path(base_dir or ".").resolve()
+    path = (base / norm).resolve()
+    if path != base and base not in path.parents:
+        raise ValueError(f"external data location '{location}' resolves outside the model directory")
+    if not path.is_file():
+        raise FileNotFoundError(f"external data file '{location}' not found next to the model")
+    return path
+
+
 def tensor_to_torch(t: Tensor, base_dir=None) -> torch.Tensor:
     """Materialise a TensorProto as a CPU torch tensor (copies out of the file buffer)."""
     dt = t.data_type
     shape = [int(d) for d in t.dims]
     n = int(np.prod(shape)) if shape else 1
     if t.external:
-        import os
-
-        loc = os.path.join(base_dir or ".", t.external["location"])
-        off, ln = int(t.external.get("offset", 0)), t.external.get("length")
+        loc = external_data_path(base_dir, t.external.get("location", ""))
+        size = loc.stat().st_size
+        off, ln = int(t.external.get("offset", 0) or 0), t.external.get("length")
+        ln = None if ln in (None, "") else int(ln)
+        if off < 0 or off > size or (ln is not None and (ln < 0 or off + ln > size)):
+            raise ValueError(f"external data of '{t.name}' (offset {off}, length {ln}) exceeds {loc.name} ({size} B)")
         with open(loc, "rb") as f:
             f.seek(off)
-            raw = f.read(int(ln) if ln else -1)
+            raw = f.read(ln if ln is not None else -1)
         t = Tensor(t.name, t.dims, dt, memoryview(raw))
     if t.raw is not None and len(t.raw):
         if dt == BFLOAT16:

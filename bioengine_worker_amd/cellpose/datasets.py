@@ -18,6 +18,7 @@ import io
 import json
 import logging
 import os
+import posixpath
 import re
 from pathlib import Path
 from typing import Any
@@ -51,8 +52,27 @@ def rel(p: str | Path) -> str:
     return str(p).replace("\\", "/").lstrip("/")
 
 
+def safe_rel(p: str | Path) -> str:
+    """:func:`rel` normalised, refusing any path that climbs out of its root (``..``).  Paths in a
+    user's metadata JSON are untrusted: without this a record could point training at another
+    session's files or make a download land outside the cache directory."""
+    r = posixpath.normpath(rel(p)) if rel(p) else ""
+    if r in ("", "."):
+        raise ValueError(f"empty artifact path: {p!r}")
+    if r == ".." or r.startswith("../") or "\x00" in r:
+        raise ValueError(f"artifact path escapes its root: {p!r}")
+    return r
+
+
 def local_path(root: Path, remote: str | Path) -> Path:
-    return Path(root) / rel(remote)
+    """Local cache location of an artifact file; must stay under ``root`` (symlinks included)."""
+    root = Path(root)
+    lp = root / safe_rel(remote)
+    base = root.resolve()
+    res = lp.resolve()
+    if res != base and base not in res.parents:
+        raise ValueError(f"artifact path escapes the cache directory: {remote!r}")
+    return lp
 
 
 def _glob_regex(pattern: str) -> re.Pattern:
@@ -259,11 +279,14 @@ def _record_path(value: Any, parent: Path) -> Path | None:
     v = value.strip().replace("\\", "/")
     if v.startswith(("http://", "https://")):
         return None
-    if v.startswith("/"):
-        return Path(v.lstrip("/"))
-    if "/" in v and not v.startswith("./"):
-        return Path(v)  # artifact-relative
-    return Path(rel(parent / v))  # relative to the metadata file's folder
+    try:
+        if v.startswith("/"):
+            return Path(safe_rel(v))
+        if "/" in v and not v.startswith("./"):
+            return Path(safe_rel(v))  # artifact-relative
+        return Path(safe_rel(parent / v))  # relative to the metadata file's folder
+    except ValueError:
+        return None  # a path that leaves the artifact is not a usable record
 
 
 def _record_pair(rec: dict, parent: Path) -> dict | None:
