@@ -451,13 +451,12 @@ class CellposeFinetune:
                 await self._prepare_data(sid, params, arrays)
             n_gpus = int(params.get("n_gpus") or 1)
             if n_gpus > 1:
-                from bioengine_worker_amd.serve.gang import run_gang
+                from bioengine_worker_amd.train.session import run_dp_session
 
                 write_status(d, message=f"Waiting for {n_gpus} GPUs (data-parallel gang)")
-                res = await run_gang("bioengine_worker_amd.train.session:train_session_rank",
-                                     {"session_dir": str(d), "params": params, "cpsam_arch": self.cpsam_arch},
-                                     world_size=n_gpus, gpus_per_rank=1, cpus_per_rank=1.0,
-                                     timeout_s=params.get("timeout_s"), name=f"train-{sid[-8:]}")
+                # a rank failure restarts a fresh gang at n_gpus - 1 from the last epoch checkpoint
+                res = await run_dp_session(d, params, n_gpus, self.cpsam_arch, max_restarts=params.get("max_restarts"),
+                                           name=f"train-{sid[-8:]}")
                 write_status(d, rank_weight_digests=[r.get("weights_sha256") for r in res])
             else:
                 from bioengine_worker_amd.train.session import train_session

@@ -21,7 +21,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import os
+
 from ..ops import conv as convops
+from ..ops import conv_pair as pairops
 from ..ops import style as styleops
 
 
@@ -273,6 +276,51 @@ class CPnetEngine:
         self.style_b = torch.cat(bs, 0).contiguous()
         self.style_s = torch.cat(ss, 0).contiguous()
         self.style_t = torch.cat(ts, 0).contiguous()
+        self.pair = self._build_pairs(net) if os.environ.get("BE_CPNET_PAIR", "1") != "0" else {}
+
+    # ------------------------------------------------------------------ fused half-blocks
+    def _build_pairs(self, net: CPnet) -> dict:
+        """Fused two-conv kernels (ops/conv_pair.py) for the 32/64-channel levels, where the
+        per-layer path is HBM bound.  Keys: ("down", n, 0|1) / ("up", i, 0|1)."""
+        nb = list(net.nbase)
+        if len(nb) < 3 or nb[1] != 32 or nb[2] != 64 or self.cin_pad != 8 or net.sz != 3:
+            return {}
+        pairs = {}
+
+        def spec(a: _FConv, b: _FConv, inmode="none", proj: _FConv | None = None, style_b=False):
+            bias = b.pc.bias if b.pc.bias is not None else torch.zeros(b.pc.cout, device=self.device)
+            if proj is not None and proj.pc.bias is not None:
+                bias = bias + proj.pc.bias
+            tb = None if style_b else pairops.fold_bias(b.shift, b.scale, a.pc.bias).contiguous()
+            return pairops.PairSpec(pa=a.pc, pb=b.pc, sa=a.scale, ta=a.shift, sb=b.scale, tb=tb,
+                                    bias=bias.float().contiguous(), inmode=inmode,
+                                    pp=None if proj is None else proj.pc, sp=None if proj is None else proj.scale,
+                                    tp=None if proj is None else proj.shift)
+
+        d0, d1 = self.down[0], self.down[1]
+        pairs[("down", 0, 0)] = spec(d0["c0"], d0["c1"], "none", proj=d0["proj"])
+        pairs[("down", 0, 1)] = spec(d0["c2"], d0["c3"])
+        pairs[("down", 1, 0)] = spec(d1["c0"], d1["c1"], "pool2")
+        pairs[("down", 1, 1)] = spec(d1["c2"], d1["c3"])
+        nup = len(self.up)
+        for i in (0, 1):
+            if i >= nup - 1:
+                continue
+            e = self.up[i]
+            pairs[("up", i, 0)] = spec(e["c0"], e["c1"], "up2", style_b=True)
+            pairs[("up", i, 1)] = spec(e["c2"], e["c3"], style_b=True)
+            # the per-image actB shifts come out of the stacked style GEMM: fold convA's bias into
+            # their constant term there (t + s * biasA), once, instead of per forward
+            for (ii, k, off, c) in self._feat_slices:
+                if ii == i and k in (1, 3):
+                    prev = e["c0"] if k == 1 else e["c2"]
+                    if prev.pc.bias is not None:
+                        self.style_t[off: off + c] += self.style_s[off: off + c] * prev.pc.bias[:c].to(self.device)
+        for key, sp in pairs.items():
+            has_x2 = key[0] == "up" and key[2] == 0
+            res = "none" if key == ("down", 0, 0) else ("up2" if has_x2 else "full")
+            assert sp.supports(has_x2, res), key
+        return pairs
 
     def _style_shifts(self, style: torch.Tensor) -> dict:
         st = style if self.style_on else torch.zeros_like(style)
@@ -288,9 +336,17 @@ class CPnetEngine:
     def forward(self, x: torch.Tensor):
         xd = []
         h = x
+        P = self.pair
         for n, e in enumerate(self.down):
             im = "pool2" if n > 0 else "none"
             src = x if n == 0 else xd[-1]
+            if ("down", n, 0) in P:
+                if n == 0:  # stem: projection computed inside the fused kernel (K concatenation)
+                    x1 = pairops.conv_pair(src, P[("down", 0, 0)])
+                else:
+                    x1 = pairops.conv_pair(src, P[("down", n, 0)], res=e["proj"](src, inmode=im), res_mode="full")
+                xd.append(pairops.conv_pair(x1, P[("down", n, 1)], res=x1, res_mode="full"))
+                continue
             proj = e["proj"](src, inmode=im)
             h = e["c0"](src, inmode=im)
             x1 = e["c1"](h, residual=proj)
@@ -305,6 +361,14 @@ class CPnetEngine:
             e = self.up[i]
             im = "none" if i == nup - 1 else "up2"
             y = xd[i] if i < nup - 1 else xd[-1]
+            if ("up", i, 0) in P:
+                # 1x1 projection commutes with nearest upsampling: run it at half resolution and
+                # let the fused kernel read it through an up2 residual
+                proj_lr = e["proj"](xcur)
+                x1 = pairops.conv_pair(xcur, P[("up", i, 0)], tb=shifts[(i, 1)], x2=y, res=proj_lr, res_mode="up2")
+                xcur = pairops.conv_pair(x1, P[("up", i, 1)], ta=shifts[(i, 2)], tb=shifts[(i, 3)], res=x1,
+                                         res_mode="full")
+                continue
             proj = e["proj"](xcur, inmode=im)
             h0 = e["c0"](xcur, inmode=im)
             x1 = e["c1"](h0, x2=y, shift=shifts[(i, 1)], residual=proj)

@@ -113,6 +113,10 @@ class GangManager:
                     e["HIP_VISIBLE_DEVICES"] = ",".join(map(str, ids))
                 else:
                     e["HIP_VISIBLE_DEVICES"] = ""
+                    # CPU ranks share the node's cores: one intra-op pool per rank sized to its share
+                    # (N ranks x all-cores pools oversubscribe and every collective waits on the slowest)
+                    if "OMP_NUM_THREADS" not in (env or {}):
+                        e["OMP_NUM_THREADS"] = str(max(1, int(self.resources.total_cpu // world)))
                 e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
                 err = open(work / f"rank{r}.err", "wb")
                 out = open(work / f"rank{r}.out", "wb")

@@ -102,6 +102,7 @@ class CellposeTrainer:
         self.m = torch.zeros_like(self.fp.flat)
         self.v = torch.zeros_like(self.fp.flat)
         self.step_count = 0
+        self.epoch = 0  # completed epochs (exact resume point)
         self.lr = cfg.lr
         self.gen = torch.Generator().manual_seed(cfg.seed * 1000 + rank)
         eng = cfg.engine
@@ -354,6 +355,21 @@ class CellposeTrainer:
         return {"loss": float(loss), "tp": tp, "fp": fp, "fn": fn, "tn": tn, "precision": prec, "recall": rec,
                 "f1": 2 * prec * rec / max(1e-12, prec + rec), "iou": tp / max(1, tp + fp + fn)}
 
+    def agree(self, loss, n_local: int, stop_local: bool = False) -> tuple[float, bool]:
+        """One tiny all-reduce per step: the GLOBAL mean loss (sample-weighted over ranks) and a
+        collective stop decision, so every rank leaves the loop after the same step (a rank that
+        left alone would strand the others in the next gradient all-reduce until the PG timeout).
+        Single process: (float(loss), stop_local)."""
+        if self.world == 1:
+            return float(loss), bool(stop_local)
+        dev = self.fp.flat.device
+        t = torch.stack([loss.detach().float().reshape(()) * float(n_local),
+                         torch.tensor(float(n_local), device=loss.device),
+                         torch.tensor(1.0 if stop_local else 0.0, device=loss.device)]).to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.ar.group)
+        vals = t.tolist()
+        return vals[0] / max(vals[1], 1e-12), vals[2] > 0
+
     def rebind(self, world_size: int, rank: int, group=None) -> None:
         """Adopt a new data-parallel world (elastic shrink, ``parallel/elastic.py``): rebuild the
         bucketed all-reduce for the new group and make every rank's weights, AdamW moments and BN
@@ -378,7 +394,7 @@ class CellposeTrainer:
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:
         return {"flat": self.fp.flat.detach().cpu(), "m": self.m.cpu(), "v": self.v.cpu(), "step": self.step_count,
-                "lr": self.lr, "rng": self.gen.get_state(), "cfg": asdict(self.cfg),
+                "epoch": self.epoch, "lr": self.lr, "rng": self.gen.get_state(), "cfg": asdict(self.cfg),
                 "buffers": {k: v.cpu() for k, v in self.net.named_buffers()}}
 
     def load_state_dict(self, sd: dict) -> None:
@@ -386,6 +402,7 @@ class CellposeTrainer:
         self.m.copy_(sd["m"].to(self.device))
         self.v.copy_(sd["v"].to(self.device))
         self.step_count = int(sd["step"])
+        self.epoch = int(sd.get("epoch", 0))
         self.lr = float(sd["lr"])
         self.gen.set_state(sd["rng"])
         bufs = dict(self.net.named_buffers())
@@ -489,19 +506,24 @@ def run_training(trainer: CellposeTrainer, train_imgs, train_lbls, n_epochs: int
         for k in range(nb):
             sl = perm[k * gb: (k + 1) * gb]
             mine = sl[trainer.rank::trainer.world] if trainer.world > 1 else sl
-            if len(mine) == 0:
-                mine = sl[:1]
             rsc = None
             if rescale and diams is not None:
                 rsc = [max(float(diams[int(i)]), 1e-3) / dmean for i in mine]
+            n_mine = len(mine)
+            if len(mine) == 0:  # fewer samples than ranks in the last batch: weight-0 filler
+                mine = sl[:1]
             loss = trainer.step(_take(train_imgs, mine), _take(train_lbls, mine), rsc)
-            lv = float(loss)
+            # stop marker read by rank 0 only, decided collectively with the global loss
+            stop_local = bool(stop_check()) if (stop_check is not None and trainer.rank == 0) else False
+            lv, stop = trainer.agree(loss, n_mine, stop_local)
             losses[ep] += lv * len(sl)
             if batch_callback is not None:
                 batch_callback(ep + 1, k, nb, lv, time.time() - t0, None)
-            if stop_check is not None and stop_check():
-                return {"train_losses": losses[: ep + 1].tolist(), "test_losses": test_losses[: ep + 1], "stopped": True}
+            if stop:
+                return {"train_losses": losses[: ep + 1].tolist(), "test_losses": test_losses[: ep + 1], "stopped": True,
+                        "epoch": ep}
         losses[ep] /= nimg
+        trainer.epoch = ep + 1
         metrics = None
         if test_imgs is not None and (ep == 0 or (ep + 1) % cfg.validation_interval == 0):
             metrics = trainer.validate(test_imgs, test_lbls)

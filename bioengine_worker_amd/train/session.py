@@ -160,10 +160,21 @@ def train_session(session_dir: str | Path, params: dict, device=None, rank: int 
         resume = params.get("resume_trainer_state")
         if resume and Path(resume).exists():
             trainer.load_state_dict(torch.load(resume, map_location="cpu", weights_only=True))
+        # "continue": the SAME session picks up after its last completed epoch (elastic restart of a
+        # data-parallel gang at a smaller world); otherwise a resumed state seeds a new session
+        start_epoch = trainer.epoch if (params.get("continue_session") and resume and Path(resume).exists()) else 0
+        trainer.epoch = start_epoch
         n_epochs = int(params.get("n_epochs", 10))
         hist = read_status(sdir)
         prev_losses = list(hist.get("inherited_train_losses") or [])
-        if lead:
+        if lead and start_epoch > 0:
+            st = read_status(sdir)
+            write_status(sdir, status_type="running", message=f"Training (resumed at epoch {start_epoch}, world {world})",
+                         world_size=world, train_losses=list(st.get("train_losses") or [])[:start_epoch + len(prev_losses)],
+                         test_losses=list(st.get("test_losses") or [])[:start_epoch + len(prev_losses)],
+                         test_metrics=list(st.get("test_metrics") or [])[:start_epoch])
+            log_info(sdir, f"resumed at epoch {start_epoch} with world {world}")
+        elif lead:
             write_status(sdir, status_type="running", message="Training", n_train=len(imgs), n_test=len(timgs),
                          total_epochs=n_epochs, start_time=hist.get("start_time") or now_iso(), world_size=world,
                          train_losses=prev_losses, test_losses=list(hist.get("inherited_test_losses") or []),
@@ -173,7 +184,14 @@ def train_session(session_dir: str | Path, params: dict, device=None, rank: int 
         t_last = [0.0]
         t_start = time.time()
 
+        fi = params.get("fault_injection") or {}
+        kill_at = int(fi.get("at_batch", -1)) if (fi.get("kill_rank") == rank and not params.get("continue_session")) else -1
+        nstep = [0]
+
         def on_batch(ep, k, nb, loss, el, _):
+            nstep[0] += 1
+            if nstep[0] == kill_at:  # test hook: this rank crashes like a lost GPU / OOM-killed process
+                os._exit(137)
             if lead and (time.time() - t_last[0] > 1.0 or k == nb - 1):
                 t_last[0] = time.time()
                 write_status(sdir, current_epoch=ep, current_batch=k + 1, total_batches=nb, elapsed_seconds=el,
@@ -191,7 +209,8 @@ def train_session(session_dir: str | Path, params: dict, device=None, rank: int 
             torch.save(trainer.state_dict(), sdir / "models" / "trainer_state.pt")
 
         out = run_training(trainer, tx, tl, n_epochs, vx, vl, batch_callback=on_batch, epoch_callback=on_epoch,
-                           stop_check=stop_file.exists, diams=diams, rescale=bool(params.get("rescale", False)))
+                           stop_check=stop_file.exists, diams=diams, rescale=bool(params.get("rescale", False)),
+                           start_epoch=start_epoch)
         digest = weights_digest(trainer)
         if not lead:
             return {"rank": rank, "weights_sha256": digest}
@@ -210,9 +229,75 @@ def train_session(session_dir: str | Path, params: dict, device=None, rank: int 
         return write_status(sdir, status_type="completed", message="Training completed", model_modified=True)
     except Exception as e:  # noqa: BLE001
         log.exception("training session %s failed", sdir.name)
+        if lead and world > 1 and _is_peer_failure(e):
+            # a collective failed because another rank died: the gang supervisor decides (elastic
+            # restart at world - 1, run_dp_session); do not mark the session failed
+            write_status(sdir, message=f"collective failed ({type(e).__name__}); waiting for the gang supervisor")
+            raise
         if lead:
             return write_status(sdir, status_type="failed", message=f"{type(e).__name__}: {e}")
         raise
+
+
+def _is_peer_failure(e: BaseException) -> bool:
+    import torch.distributed as dist
+
+    if isinstance(e, tuple(t for t in (getattr(dist, "DistBackendError", None), getattr(dist, "DistNetworkError", None))
+                          if t is not None)):
+        return True
+    msg = str(e).lower()
+    return any(k in msg for k in ("connection closed", "connection reset", "gloo", "nccl", "rccl", "broken pipe",
+                                  "peer", "timed out"))
+
+
+async def run_dp_session(session_dir: str | Path, params: dict, n_gpus: int, cpsam_arch: str = "vit_l",
+                         max_restarts: int | None = None, name: str | None = None, gpus_per_rank: int = 1) -> list:
+    """Data-parallel session as a gang (``serve/gang.py``) with elastic restart.
+
+    When a rank dies (process exit, signal, OOM kill) the gang supervisor tears the whole job down;
+    a FRESH gang of ``world - 1`` processes is then started from the session's last
+    ``models/trainer_state.pt`` (weights, AdamW moments, step, RNG, completed epochs) and continues
+    the same session -- never an exec of a process that used the GPU.  Per-rank batch stays fixed,
+    so the global batch shrinks with the world.  A user stop or an error the lead rank recorded is
+    not retried.  Returns the final gang's per-rank results."""
+    from ..serve.gang import GangError, run_gang
+
+    sdir = Path(session_dir)
+    world = int(n_gpus)
+    restarts = 0
+    max_restarts = max(0, world - 1) if max_restarts is None else int(max_restarts)
+    p = dict(params)
+    while True:
+        try:
+            return await run_gang("bioengine_worker_amd.train.session:train_session_rank",
+                                  {"session_dir": str(sdir), "params": p, "cpsam_arch": cpsam_arch},
+                                  world_size=world, gpus_per_rank=gpus_per_rank, cpus_per_rank=1.0,
+                                  timeout_s=p.get("timeout_s"), name=(name or "train") + (f"-r{restarts}" if restarts else ""))
+        except GangError as e:
+            st = read_status(sdir)
+            if (sdir / "stop").exists() or st.get("status_type") in ("failed", "stopped", "completed") \
+                    or world <= 1 or restarts >= max_restarts:
+                raise
+            ckpt = sdir / "models" / "trainer_state.pt"
+            restarts += 1
+            world -= 1
+            if ckpt.exists():
+                p["resume_trainer_state"] = str(ckpt)
+                p["continue_session"] = True
+            log.warning("session %s: gang failed (%s); elastic restart %d at world %d", sdir.name,
+                        str(e).splitlines()[0], restarts, world)
+            write_status(sdir, message=f"Rank failure; restarting at world {world} from "
+                                       f"{'epoch ' + str(_ckpt_epoch(ckpt)) if ckpt.exists() else 'the start'}",
+                         elastic_restarts=restarts, world_size=world,
+                         elastic_events=list(st.get("elastic_events") or []) + [
+                             {"time": now_iso(), "error": str(e).splitlines()[0][:300], "new_world": world}])
+
+
+def _ckpt_epoch(ckpt: Path) -> int:
+    try:
+        return int(torch.load(ckpt, map_location="cpu", weights_only=True).get("epoch", 0))
+    except Exception:  # noqa: BLE001
+        return 0
 
 
 def weights_digest(trainer) -> str:

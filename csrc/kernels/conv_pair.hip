@@ -1,0 +1,598 @@
+// Fused residual half-block of the Cellpose CPnet: two pre-activation 3x3 convs in ONE kernel, the
+// intermediate feature map never leaves LDS.
+//
+//   h   = relu( (convA( actA(inxform(x)) ) [+ x2]) * sB[c] + tB[n, c] )                tile + 1-px halo, LDS
+//   out = convB(h) + bias [+ projP( actP(x) )] [+ res | + up2(res)]                     bf16 NHWC
+//   actA(v) = relu(v * sA[c] + tA[n, c]),  actP(v) = v * sP[c] + tP[c]                  (eval BN / style folded)
+//
+// convA's bias is folded into tB on the host (tB' = tB + sB * biasA) and the projection's bias into
+// `bias`, so the kernel never reads them.
+//
+// One CPnet residual block is two of these: resdown = {proj+c0+c1, c2+c3(+x1)}, resup =
+// {c0+c1 (+skip, +up2(proj)), c2+c3(+x1)} (cellpose `resdown`/`resup`, reached by the reference
+// through cellpose==3.1.1.2, apps/model-runner/runtime_deployment.py:19).  The
+// per-layer kernel (conv2d_nhwc.hip) writes every intermediate to HBM and re-reads it; at the
+// 32/64-channel levels (224^2 / 112^2 tiles) those layers are memory bound, so keeping h on chip
+// removes most of their HBM traffic (profiles/r02/conv_roofline.md: 11.6 of 18.5 ms were there).
+//
+// MI355X design:
+//  * 512-thread workgroup, one per CU (LDS 113-137 KB), persistent over a CONTIGUOUS range of
+//    16x32 output tiles so neighbouring tiles (shared halo rows) run back to back on one CU / L2.
+//  * stage A computes h on the 18x34 tile+halo region (612 px = 39 MFMA pixel tiles in linear
+//    pixel order, 5 per wave) from a 20x36 input halo staged in LDS with actA applied on the way
+//    in; its epilogue applies actB (+ skip add) and writes h as bf16 over the (dead) input halo.
+//  * stage B is the 16x32 x CM implicit GEMM over h (tap-major K, chunks of 32 channels); the 1x1
+//    projection is one extra K step into the SAME accumulators (K concatenation); then residual +
+//    bias and a staged, 16-byte-coalesced NHWC store.
+//  * v_mfma_f32_16x16x32_bf16 with the weights as the A operand: each lane ends with 4 consecutive
+//    output channels of one pixel (8-byte LDS writes of h, 8-byte residual reads).
+//  * CM = 32: every weight panel stays resident in LDS for the whole launch; CM = 64: one weight
+//    chunk buffer, the next chunk's weights and the next A chunk's halo are prefetched into
+//    registers while the current chunk's MFMAs run ("issue early, write late").
+//  * pixel strides are 8 (mod 16) dwords, so ds_read_b128 fragment reads are conflict-free for any
+//    tap offset (same rule as conv2d_nhwc.hip).
+#include "common.h"
+
+namespace {
+
+constexpr int TW = 32, TH = 16, NW = 8, NT = NW * 64;
+constexpr int RW = TW + 2, RH = TH + 2, RPIX = RW * RH;  // h region 34 x 18 = 612 px
+constexpr int IW = TW + 4, IH = TH + 4, IPIX = IW * IH;  // A input halo 36 x 20 = 720 px
+constexpr int RPT = (RPIX + 15) / 16;                    // 39 pixel tiles of 16
+constexpr int APT = (RPT + NW - 1) / NW;                 // 5 per wave
+constexpr int KPB = 288;                                 // B K per 32-channel chunk (9 taps x 32)
+constexpr int WSTRB = KPB + 16;
+constexpr int PSTRP = 24;                                // proj region pixel stride (8 channels)
+constexpr int WSTRP = 48;
+
+struct PairArgs {
+  const bf16_t* x;   // [N, Hs, Ws, Cin]
+  const bf16_t* x2;  // [N, H, W, CM] skip added to convA's output (X2)
+  const float* sa; const float* ta; int ta_ns;  // actA: scale [Cin], shift [Cin] (ns 0) or [N, ns]
+  const float* sb; const float* tb; int tb_ns;  // actB (convA bias folded into tb)
+  const float* sp; const float* tp;             // actP (projection), shared
+  const bf16_t* wa;                             // [CM][NCA][KPA]
+  const bf16_t* wb;                             // [CM][CM/32][288]
+  const bf16_t* wp;                             // [CM][1][32]
+  const float* bias;                            // [CM] convB bias (+ projection bias)
+  const bf16_t* res;                            // [N, H, W, CM] or [N, H/2, W/2, CM] (RES = 2)
+  bf16_t* out;                                  // [N, H, W, CM]
+  int N, H, W, Hs, Ws, Cin;
+  int tiles_x, tiles_y;
+};
+
+template <int CK_, int CM_, int INMODE, bool X2, bool PROJ, int RES, int NCA>
+struct PC {
+  static constexpr int CK = CK_, CM = CM_;
+  static constexpr int KPA = ((9 * CK + 31) / 32) * 32;
+  static constexpr int KSA = KPA / 32;
+  static constexpr int WSTRA = KPA + 16;
+  static constexpr int PSTRI = CK == 8 ? 24 : CK + 16;
+  static constexpr int CGI = CK / 8;
+  static constexpr int PSTRM = CM + 16;
+  static constexpr int NCT = CM / 16;
+  static constexpr int NCB = CM / 32;
+  static constexpr bool RESW = CM == 32;  // every weight panel resident in LDS
+  static constexpr int HU = IPIX * CGI;   // 16-byte halo units per A chunk
+  static constexpr int HUPT = (HU + NT - 1) / NT;
+  static constexpr int WA_ELEMS = CM * WSTRA;
+  static constexpr int WB_ELEMS = CM * WSTRB;
+  static constexpr int WU = CM * KPB / 8;  // streaming: 16-byte units per weight chunk
+  static constexpr int WUPT = RESW ? 1 : (WU + NT - 1) / NT;
+  static constexpr int OUT_WAVE = 2 * TW * CM;
+  static constexpr int R_IN = IPIX * PSTRI, R_H = RPIX * PSTRM, R_OUT = NW * OUT_WAVE;
+  static constexpr int RREG0 = R_IN > R_H ? R_IN : R_H;
+  static constexpr int RREG = RREG0 > R_OUT ? RREG0 : R_OUT;
+  static constexpr int PREG = PROJ ? TH * TW * PSTRP : 0;
+  static constexpr int WREG = RESW ? NCA * WA_ELEMS + NCB * WB_ELEMS + (PROJ ? CM * WSTRP : 0) : WB_ELEMS;
+  static constexpr size_t LDS = (size_t)(RREG + PREG + WREG) * sizeof(bf16_t);
+  static constexpr int CPP = NCT * 2;  // 16-byte output chunks per pixel
+  static constexpr int OSH = CM == 32 ? 1 : 0;
+  static_assert(NT % CGI == 0, "a thread's channel group must not change across halo units");
+  static_assert(CK == 8 || (PSTRI / 2) % 16 == 8, "input pixel stride must be 8 (mod 16) dwords");
+  static_assert((PSTRM / 2) % 16 == 8, "h pixel stride must be 8 (mod 16) dwords");
+  static_assert((WSTRA / 2) % 16 == 8 && (WSTRB / 2) % 16 == 8, "weight row stride must be 8 (mod 16) dwords");
+  static_assert(!PROJ || (CK == 8 && NCA == 1 && RESW), "in-kernel projection only for the 8-channel stem");
+  static_assert(RESW || CK == 32, "streamed weight chunks assume equal A/B chunk geometry");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+struct TileXY {
+  int n, ty0, tx0;
+};
+
+__device__ __forceinline__ TileXY tile_xy(const PairArgs& a, int t) {
+  const int tpi = a.tiles_x * a.tiles_y;
+  TileXY r;
+  r.n = t / tpi;
+  const int q = t - r.n * tpi;
+  r.ty0 = (q / a.tiles_x) * TH;
+  r.tx0 = (q % a.tiles_x) * TW;
+  return r;
+}
+
+// ---- A input halo: global -> registers (raw, in-transform applied) --------------------------------
+template <typename C, int INMODE>
+__device__ __forceinline__ void issue_halo(const PairArgs& a, TileXY t, int ch, int tid, u32x4 (&hraw)[C::HUPT]) {
+  const int c0 = ch * C::CGI * 8;
+#pragma unroll
+  for (int i = 0; i < C::HUPT; ++i) {
+    const int u = tid + i * NT;
+    u32x4 r = (u32x4){0u, 0u, 0u, 0u};
+    if (u < C::HU) {
+      const int pix = u / C::CGI, cg = u % C::CGI;
+      const int gy = t.ty0 - 2 + pix / IW, gx = t.tx0 - 2 + pix % IW;
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+        const int c = c0 + cg * 8;
+        if (INMODE == 0) {
+          r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + gy) * a.Ws + gx) * a.Cin + c);
+        } else if (INMODE == 1) {
+          r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * a.Cin + c);
+        } else {
+          const bf16_t* base = a.x + (((size_t)t.n * a.Hs + 2 * gy) * a.Ws + 2 * gx) * a.Cin + c;
+          const u32x4 r0 = *reinterpret_cast<const u32x4*>(base);
+          const u32x4 r1 = *reinterpret_cast<const u32x4*>(base + a.Cin);
+          const u32x4 q0 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin);
+          const u32x4 q1 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin + a.Cin);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // max of bf16 values is exact in bf16
+            const float lo = fmaxf(fmaxf(lo_bf(r0[j]), lo_bf(r1[j])), fmaxf(lo_bf(q0[j]), lo_bf(q1[j])));
+            const float hi = fmaxf(fmaxf(hi_bf(r0[j]), hi_bf(r1[j])), fmaxf(hi_bf(q0[j]), hi_bf(q1[j])));
+            r[j] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+          }
+        }
+      }
+    }
+    hraw[i] = r;
+  }
+}
+
+__device__ __forceinline__ void load_aff8(const float* s, const float* t, int t_ns, int n, int c, float (&sc)[8],
+                                          float (&sh)[8]) {
+  const float4 s0 = *reinterpret_cast<const float4*>(s + c);
+  const float4 s1 = *reinterpret_cast<const float4*>(s + c + 4);
+  const float* tr = t + (size_t)n * t_ns + c;
+  const float4 t0 = *reinterpret_cast<const float4*>(tr);
+  const float4 t1 = *reinterpret_cast<const float4*>(tr + 4);
+  sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+  sh[0] = t0.x; sh[1] = t0.y; sh[2] = t0.z; sh[3] = t0.w; sh[4] = t1.x; sh[5] = t1.y; sh[6] = t1.z; sh[7] = t1.w;
+}
+
+// activated halo -> LDS (conv zero padding applies AFTER the activation); the stem also writes
+// actP of the centre pixels for the in-kernel projection
+template <typename C, bool PROJ>
+__device__ __forceinline__ void commit_halo(const PairArgs& a, TileXY t, int ch, int tid,
+                                            const u32x4 (&hraw)[C::HUPT], bf16_t* rin, bf16_t* preg) {
+  const int c = ch * C::CGI * 8 + (tid % C::CGI) * 8;
+  float sc[8], sh[8];
+  load_aff8(a.sa, a.ta, a.ta_ns, t.n, c, sc, sh);
+  float ps[8], pt[8];
+  if (PROJ) load_aff8(a.sp, a.tp, 0, 0, c, ps, pt);
+#pragma unroll
+  for (int i = 0; i < C::HUPT; ++i) {
+    const int u = tid + i * NT;
+    if (u >= C::HU) continue;
+    const int pix = u / C::CGI, cg = u % C::CGI;
+    const int iy = pix / IW, ix = pix % IW;
+    const int gy = t.ty0 - 2 + iy, gx = t.tx0 - 2 + ix;
+    const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(hraw[i][j]); v[2 * j + 1] = hi_bf(hraw[i][j]); }
+    u32x4 pk = (u32x4){0u, 0u, 0u, 0u};
+    if (in) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        pk[j] = relu_bf16x2(pack2bf(fmaf(v[2 * j], sc[2 * j], sh[2 * j]), fmaf(v[2 * j + 1], sc[2 * j + 1], sh[2 * j + 1])));
+    }
+    *reinterpret_cast<u32x4*>(rin + pix * C::PSTRI + cg * 8) = pk;
+    if (PROJ && iy >= 2 && iy < TH + 2 && ix >= 2 && ix < TW + 2) {
+      u32x4 pp = (u32x4){0u, 0u, 0u, 0u};
+      if (in) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          pp[j] = pack2bf(fmaf(v[2 * j], ps[2 * j], pt[2 * j]), fmaf(v[2 * j + 1], ps[2 * j + 1], pt[2 * j + 1]));
+      }
+      *reinterpret_cast<u32x4*>(preg + ((iy - 2) * TW + (ix - 2)) * PSTRP) = pp;
+    }
+  }
+}
+
+// ---- weights ---------------------------------------------------------------------------------
+// Streaming (CM = 64): stage s of a tile is A chunk s (s < NCA) or B chunk s - NCA; both are
+// [CM][288] panels of the packed [Cout][nchunk][288] layouts.
+template <typename C, int NCA>
+__device__ __forceinline__ void issue_w(const PairArgs& a, int s, int tid, u32x4 (&wraw)[C::WUPT]) {
+  const bf16_t* src;
+  int nch, ch;
+  if (s < NCA) { src = a.wa; nch = NCA; ch = s; } else { src = a.wb; nch = C::NCB; ch = s - NCA; }
+#pragma unroll
+  for (int i = 0; i < C::WUPT; ++i) {
+    const int u = tid + i * NT;
+    if (u < C::WU) {
+      const int r = u / (KPB / 8), k8 = u % (KPB / 8);
+      // 32-bit offsets off a uniform base (global_load ... saddr): loop-invariant 64-bit per-unit
+      // addresses kept live across tiles were what spilled
+      const uint32_t off = (uint32_t)((r * nch + ch) * KPB + k8 * 8);
+      wraw[i] = *reinterpret_cast<const u32x4*>(src + off);
+    }
+  }
+}
+
+template <typename C>
+__device__ __forceinline__ void commit_w(int tid, const u32x4 (&wraw)[C::WUPT], bf16_t* wl) {
+#pragma unroll
+  for (int i = 0; i < C::WUPT; ++i) {
+    const int u = tid + i * NT;
+    if (u < C::WU) {
+      const int r = u / (KPB / 8), k8 = u % (KPB / 8);
+      *reinterpret_cast<u32x4*>(wl + r * WSTRB + k8 * 8) = wraw[i];
+    }
+  }
+}
+
+// Resident (CM = 32): every panel copied once per workgroup: A chunks, B chunk(s), projection.
+template <typename C, bool PROJ, int NCA>
+__device__ __forceinline__ void load_resident(const PairArgs& a, int tid, bf16_t* wl) {
+  for (int u = tid; u < NCA * 32 * (C::KPA / 8); u += NT) {  // CM == 32 rows
+    const int ch = u / (32 * (C::KPA / 8)), q = u % (32 * (C::KPA / 8));
+    const int r = q / (C::KPA / 8), k8 = q % (C::KPA / 8);
+    *reinterpret_cast<u32x4*>(wl + ch * C::WA_ELEMS + r * C::WSTRA + k8 * 8) =
+        *reinterpret_cast<const u32x4*>(a.wa + ((size_t)r * NCA + ch) * C::KPA + k8 * 8);
+  }
+  bf16_t* wlb = wl + NCA * C::WA_ELEMS;
+  for (int u = tid; u < C::NCB * 32 * (KPB / 8); u += NT) {
+    const int ch = u / (32 * (KPB / 8)), q = u % (32 * (KPB / 8));
+    const int r = q / (KPB / 8), k8 = q % (KPB / 8);
+    *reinterpret_cast<u32x4*>(wlb + ch * C::WB_ELEMS + r * WSTRB + k8 * 8) =
+        *reinterpret_cast<const u32x4*>(a.wb + ((size_t)r * C::NCB + ch) * KPB + k8 * 8);
+  }
+  if (PROJ) {
+    bf16_t* wlp = wlb + C::NCB * C::WB_ELEMS;
+    for (int u = tid; u < 32 * 4; u += NT) {
+      const int r = u / 4, k8 = u % 4;
+      *reinterpret_cast<u32x4*>(wlp + r * WSTRP + k8 * 8) = *reinterpret_cast<const u32x4*>(a.wp + (size_t)r * 32 + k8 * 8);
+    }
+  }
+}
+
+// ---- stage A: h region (612 px, linear order) from the input halo ---------------------------------
+template <typename C>
+__device__ __forceinline__ void mma_a(f32x4 (&acc)[C::NCT][APT], const bf16_t* rin, const bf16_t* wl, int wave,
+                                      int lrow, int kq) {
+  int base[APT];
+#pragma unroll
+  for (int j = 0; j < APT; ++j) {
+    int p = (wave + j * NW) * 16 + lrow;
+    if (p >= RPIX) p = 0;  // padding pixels of the last MFMA tile: read valid data, discard later
+    base[j] = ((p / RW) * IW + (p % RW)) * C::PSTRI + (C::CK == 8 ? 0 : kq * 8);
+  }
+  auto frags = [&](int ks, bf16x8 (&af)[C::NCT], bf16x8 (&bf)[APT]) {
+    int off;
+    if constexpr (C::CK == 8) {  // 4 taps x 8 channels per K step; K padding (tap >= 9) has zero weights
+      int tap = ks * 4 + kq;
+      if (tap >= 9) tap = 0;
+      off = ((tap / 3) * IW + tap % 3) * C::PSTRI;
+    } else {
+      off = ((ks / 3) * IW + ks % 3) * C::PSTRI;
+    }
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct)
+      af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTRA + ks * 32 + kq * 8);
+#pragma unroll
+    for (int j = 0; j < APT; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(rin + base[j] + off);
+  };
+  if constexpr (C::NCT * APT <= 10) {  // registers to spare: explicit fragment double buffer
+    bf16x8 af[2][C::NCT], bf[2][APT];
+    frags(0, af[0], bf[0]);
+#pragma unroll
+    for (int ks = 0; ks < C::KSA; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < C::KSA) frags(ks + 1, af[cur ^ 1], bf[cur ^ 1]);
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct)
+#pragma unroll
+        for (int j = 0; j < APT; ++j)
+          acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bf[cur][j], acc[ct][j], 0, 0, 0);
+    }
+  } else {  // CM = 64: 80 accumulator VGPRs; single fragment set, the scheduler overlaps the reads
+#pragma unroll
+    for (int ks = 0; ks < C::KSA; ++ks) {
+      bf16x8 af[C::NCT], bf[APT];
+      frags(ks, af, bf);
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct)
+#pragma unroll
+        for (int j = 0; j < APT; ++j)
+          acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[j], acc[ct][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // keep later steps' ds_reads from being hoisted (spills)
+    }
+  }
+}
+
+// actB(+skip) of stage A's accumulators -> h (bf16) in LDS; zero outside the image
+template <typename C, bool X2>
+__device__ __forceinline__ void epi_a(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][APT], bf16_t* rh,
+                                      int wave, int lrow, int kq) {
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct) {
+    const int c = ct * 16 + kq * 4;
+    const float4 s = *reinterpret_cast<const float4*>(a.sb + c);
+    const float4 sh = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
+    u32x2 xv[APT];
+#pragma unroll
+    for (int j = 0; j < APT; ++j) {
+      xv[j] = (u32x2){0u, 0u};
+      const int p = (wave + j * NW) * 16 + lrow;
+      const int gy = t.ty0 - 1 + p / RW, gx = t.tx0 - 1 + p % RW;
+      if (X2 && p < RPIX && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+        xv[j] = *reinterpret_cast<const u32x2*>(a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * C::CM + c);
+    }
+#pragma unroll
+    for (int j = 0; j < APT; ++j) {
+      const int p = (wave + j * NW) * 16 + lrow;
+      if (p >= RPIX) continue;
+      const int gy = t.ty0 - 1 + p / RW, gx = t.tx0 - 1 + p % RW;
+      u32x2 st = (u32x2){0u, 0u};
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+        float v0 = acc[ct][j][0], v1 = acc[ct][j][1], v2 = acc[ct][j][2], v3 = acc[ct][j][3];
+        if (X2) {
+          v0 += lo_bf(xv[j][0]); v1 += hi_bf(xv[j][0]); v2 += lo_bf(xv[j][1]); v3 += hi_bf(xv[j][1]);
+        }
+        st[0] = relu_bf16x2(pack2bf(fmaf(v0, s.x, sh.x), fmaf(v1, s.y, sh.y)));
+        st[1] = relu_bf16x2(pack2bf(fmaf(v2, s.z, sh.z), fmaf(v3, s.w, sh.w)));
+      }
+      *reinterpret_cast<u32x2*>(rh + p * C::PSTRM + c) = st;
+    }
+  }
+}
+
+// ---- stage B: 16x32 output tile from h ----------------------------------------------------------
+template <typename C>
+__device__ __forceinline__ void mma_b(f32x4 (&acc)[C::NCT][4], const bf16_t* rh, const bf16_t* wl, int cb, int wave,
+                                      int lrow, int kq) {
+  int base[4];
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int oy = 2 * wave + (pt >> 1), ox = (pt & 1) * 16 + lrow;
+    base[pt] = (oy * RW + ox) * C::PSTRM + cb * 32 + kq * 8;
+  }
+  auto frags = [&](int ks, bf16x8 (&af)[C::NCT], bf16x8 (&bf)[4]) {
+    const int off = ((ks / 3) * RW + ks % 3) * C::PSTRM;
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct)
+      af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * WSTRB + ks * 32 + kq * 8);
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) bf[pt] = *reinterpret_cast<const bf16x8*>(rh + base[pt] + off);
+  };
+  bf16x8 af[2][C::NCT], bf[2][4];
+  frags(0, af[0], bf[0]);
+#pragma unroll
+  for (int ks = 0; ks < 9; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < 9) frags(ks + 1, af[cur ^ 1], bf[cur ^ 1]);
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct)
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+        acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bf[cur][pt], acc[ct][pt], 0, 0, 0);
+  }
+}
+
+// 1x1 projection of the stem (8 input channels = one 32-deep K step, k >= 8 zero weights)
+template <typename C>
+__device__ __forceinline__ void mma_p(f32x4 (&acc)[C::NCT][4], const bf16_t* preg, const bf16_t* wl, int wave, int lrow,
+                                      int kq) {
+  bf16x8 af[C::NCT], bf[4];
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct) af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * WSTRP + kq * 8);
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int oy = 2 * wave + (pt >> 1), ox = (pt & 1) * 16 + lrow;
+    bf[pt] = *reinterpret_cast<const bf16x8*>(preg + (oy * TW + ox) * PSTRP);
+  }
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct)
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+      acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[pt], acc[ct][pt], 0, 0, 0);
+}
+
+template <typename C>
+__device__ __forceinline__ int stage_off(int p, int co) {
+  return p * (C::NCT * 16) + ((co >> 3) ^ ((p >> C::OSH) & (C::CPP - 1))) * 8 + (co & 7);
+}
+
+// bias + residual, staged through LDS, 16-byte coalesced NHWC stores
+template <typename C, int RES>
+__device__ __forceinline__ void epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][4], bf16_t* stage, int wave,
+                                      int lrow, int kq) {
+  u32x2 rv[4][C::NCT];
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+    const bool ok = RES != 0 && py < a.H && px < a.W;
+    size_t pix = 0;
+    if (RES == 1) pix = ((size_t)t.n * a.H + py) * a.W + px;
+    if (RES == 2) pix = ((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1);
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct)
+      rv[pt][ct] = ok ? *reinterpret_cast<const u32x2*>(a.res + pix * C::CM + ct * 16 + kq * 4) : (u32x2){0u, 0u};
+  }
+  float4 bias[C::NCT];
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct) bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
+  bf16_t* ws = stage + wave * C::OUT_WAVE;
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int p = (pt >> 1) * TW + (pt & 1) * 16 + lrow;
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct) {
+      u32x2 st;
+      st[0] = pack2bf(acc[ct][pt][0] + bias[ct].x + lo_bf(rv[pt][ct][0]), acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]));
+      st[1] = pack2bf(acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]), acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]));
+      *reinterpret_cast<u32x2*>(ws + stage_off<C>(p, ct * 16 + kq * 4)) = st;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int lane = lrow + 16 * kq;
+#pragma unroll
+  for (int it = 0; it < 2 * TW * C::CPP / 64; ++it) {
+    const int q = it * 64 + lane;
+    const int p = q / C::CPP, c = q % C::CPP;
+    const int py = t.ty0 + 2 * wave + p / TW, px = t.tx0 + p % TW;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ws + stage_off<C>(p, c * 8));
+    if (py < a.H && px < a.W) *reinterpret_cast<u32x4*>(a.out + (((size_t)t.n * a.H + py) * a.W + px) * C::CM + c * 8) = v;
+  }
+}
+
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA>
+__global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
+  using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* R = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* P = R + C::RREG;
+  bf16_t* WL = P + C::PREG;
+  const int tid0 = threadIdx.x;
+  const int total = a.N * a.tiles_x * a.tiles_y;
+  // contiguous tile range per workgroup (tiles sharing halo rows run back to back on one CU)
+  const int t0 = (int)(((long long)blockIdx.x * total) / gridDim.x);
+  const int t1 = (int)(((long long)(blockIdx.x + 1) * total) / gridDim.x);
+  if (t0 >= t1) return;
+  if constexpr (C::RESW) load_resident<C, PROJ, NCA>(a, tid0, WL);
+
+  u32x4 hraw[C::HUPT];
+  u32x4 wraw[C::WUPT];
+  issue_halo<C, INMODE>(a, tile_xy(a, t0), 0, tid0, hraw);
+  if constexpr (!C::RESW) issue_w<C, NCA>(a, 0, tid0, wraw);
+
+  for (int t = t0; t < t1; ++t) {
+    // Opaque per-iteration copy of the thread id: without it LICM hoists every per-unit halo /
+    // weight / LDS address out of the tile loop and the CM = 64 variants spill (~100 B/lane).
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = tid >> 6, lrow = lane & 15, kq = lane >> 4;
+    const TileXY cur = tile_xy(a, t);
+    f32x4 acc_a[C::NCT][APT];
+#pragma unroll
+    for (int i = 0; i < C::NCT; ++i)
+#pragma unroll
+      for (int j = 0; j < APT; ++j) acc_a[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // ---- stage A: NCA input chunks ----
+#pragma unroll 1
+    for (int c = 0; c < NCA; ++c) {
+      __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
+      commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P);
+      if constexpr (!C::RESW) commit_w<C>(tid, wraw, WL);
+      __syncthreads();
+      if (c + 1 < NCA) issue_halo<C, INMODE>(a, cur, c + 1, tid, hraw);
+      else if (t + 1 < t1) issue_halo<C, INMODE>(a, tile_xy(a, t + 1), 0, tid, hraw);
+      if constexpr (!C::RESW) issue_w<C, NCA>(a, c + 1, tid, wraw);
+      mma_a<C>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
+    }
+    __syncthreads();  // every wave is done with the input halo and the A weights
+    epi_a<C, X2>(a, cur, acc_a, R, wave, lrow, kq);
+    // ---- stage B: CM/32 chunks of h ----
+    f32x4 acc_b[C::NCT][4];
+#pragma unroll
+    for (int i = 0; i < C::NCT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc_b[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cb = 0; cb < C::NCB; ++cb) {
+      if constexpr (!C::RESW) {
+        if (cb > 0) __syncthreads();  // previous chunk's weights consumed
+        commit_w<C>(tid, wraw, WL);
+        __syncthreads();
+        const int s = NCA + cb + 1;  // next stage: next B chunk or the next tile's A chunk 0
+        if (s < NCA + C::NCB) issue_w<C, NCA>(a, s, tid, wraw);
+        else if (t + 1 < t1) issue_w<C, NCA>(a, 0, tid, wraw);
+      } else {
+        __syncthreads();  // h complete
+      }
+      mma_b<C>(acc_b, R, C::RESW ? WL + NCA * C::WA_ELEMS + cb * C::WB_ELEMS : WL, cb, wave, lrow, kq);
+    }
+    if constexpr (PROJ) mma_p<C>(acc_b, P, WL + NCA * C::WA_ELEMS + C::NCB * C::WB_ELEMS, wave, lrow, kq);
+    __syncthreads();  // every wave is done reading h before the output staging overlays it
+    epi_b<C, RES>(a, cur, acc_b, R, wave, lrow, kq);
+  }
+}
+
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA>
+int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
+  using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
+  a.tiles_x = (a.W + TW - 1) / TW;
+  a.tiles_y = (a.H + TH - 1) / TH;
+  const int tiles = a.N * a.tiles_x * a.tiles_y;
+  int g = grid_cap > 0 ? grid_cap : 256;  // one 512-thread workgroup per CU
+  if (g > tiles) g = tiles;
+  if (g < 1) return 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA>), dim3(g), dim3(NT), C::LDS, s, a);
+  return BE_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+static int g_pair_grid = 0;  // tuning override (0 = one workgroup per CU)
+
+extern "C" {
+
+int be_conv_pair_set_grid(int blocks) {
+  g_pair_grid = blocks;
+  return 0;
+}
+
+// LDS bytes of one configuration (tests / tooling); -1 = unsupported configuration.
+int be_conv_pair_lds(int cin, int cm, int inmode, int x2, int proj, int res) {
+  (void)inmode; (void)x2; (void)res;
+  if (cm == 32 && cin == 8 && proj) return (int)PC<8, 32, 0, false, true, 0, 1>::LDS;
+  if (cm == 32 && cin == 32) return (int)PC<32, 32, 0, false, false, 1, 1>::LDS;
+  if (cm == 32 && cin == 64) return (int)PC<32, 32, 1, true, false, 2, 2>::LDS;
+  if (cm == 64) return (int)PC<32, 64, 0, false, false, 1, 2>::LDS;
+  return -1;
+}
+
+// Supported (cin, cm, inmode, x2, proj, res) configurations = the CPnet levels 0/1 half-blocks:
+//   (8,32,none,0,1,0)  stem: proj + c0 + c1          (32,32,none,0,0,full) c2 + c3 + x1 (down and up)
+//   (32,64,pool2,0,0,full) level-1 c0 + c1 + proj    (64,64,none,0,0,full) level-1 c2 + c3 + x1
+//   (128,64,up2,1,0,up2)  up level-1 c0 + c1 + skip + up2(proj)
+//   (64,32,up2,1,0,up2)   up level-0 c0 + c1 + skip + up2(proj)
+int be_conv_pair(const void* x, const void* x2, const float* sa, const float* ta, int ta_ns, const float* sb,
+                 const float* tb, int tb_ns, const float* sp, const float* tp, const void* wa, const void* wb,
+                 const void* wp, const float* bias, const void* res, void* out, int N, int H, int W, int Hs, int Ws,
+                 int Cin, int CM, int inmode, int proj, int resmode, hipStream_t stream) {
+  PairArgs a;
+  a.x = (const bf16_t*)x; a.x2 = (const bf16_t*)x2;
+  a.sa = sa; a.ta = ta; a.ta_ns = ta_ns; a.sb = sb; a.tb = tb; a.tb_ns = tb_ns; a.sp = sp; a.tp = tp;
+  a.wa = (const bf16_t*)wa; a.wb = (const bf16_t*)wb; a.wp = (const bf16_t*)wp; a.bias = bias;
+  a.res = (const bf16_t*)res; a.out = (bf16_t*)out;
+  a.N = N; a.H = H; a.W = W; a.Hs = Hs; a.Ws = Ws; a.Cin = Cin;
+  const bool hx2 = x2 != nullptr;
+  if (!sa || !ta || !sb || !tb || !wa || !wb || !bias || !out || !x) return -20;
+  if ((resmode != 0) != (res != nullptr)) return -21;
+  if (proj && (!sp || !tp || !wp)) return -22;
+  const int g = g_pair_grid;
+  if (CM == 32 && Cin == 8 && inmode == 0 && !hx2 && proj && resmode == 0)
+    return launch_pair<8, 32, 0, false, true, 0, 1>(a, g, stream);
+  if (CM == 32 && Cin == 32 && inmode == 0 && !hx2 && !proj && resmode == 1)
+    return launch_pair<32, 32, 0, false, false, 1, 1>(a, g, stream);
+  if (CM == 32 && Cin == 64 && inmode == 1 && hx2 && !proj && resmode == 2)
+    return launch_pair<32, 32, 1, true, false, 2, 2>(a, g, stream);
+  if (CM == 64 && Cin == 32 && inmode == 2 && !hx2 && !proj && resmode == 1)
+    return launch_pair<32, 64, 2, false, false, 1, 1>(a, g, stream);
+  if (CM == 64 && Cin == 64 && inmode == 0 && !hx2 && !proj && resmode == 1)
+    return launch_pair<32, 64, 0, false, false, 1, 2>(a, g, stream);
+  if (CM == 64 && Cin == 128 && inmode == 1 && hx2 && !proj && resmode == 2)
+    return launch_pair<32, 64, 1, true, false, 2, 4>(a, g, stream);
+  return -23;
+}
+
+}  // extern "C"
