@@ -209,13 +209,16 @@ def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
     return out
 
 
-def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int):
+def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int, force_dp: bool = False):
     """Cellpose-SAM (ViT-L/8, 256x256 crops) fine-tune steps -- the reference app's own training
-    workload -- on the HIP CPSAM engine; with world > 1 data-parallel over RCCL (bucketed, bf16 wire)."""
+    workload -- on the HIP CPSAM engine; with world > 1 data-parallel over RCCL (bucketed fp32
+    gradients, all-reduces overlapped with the segmented-graph backward).  ``force_dp`` runs that
+    data-parallel path on one GPU over a 1-rank group (its overhead vs the single-GPU graph)."""
     from bioengine_worker_amd.models.cpsam import CPSAM
     from bioengine_worker_amd.train.cellpose_train import TrainConfig, build_trainer, synthetic_train_batch
 
-    cfg = TrainConfig(batch_size=batch, bsize=256, lr=1e-5, weight_decay=1e-4, bucket_mb=64.0, comm_bf16=world > 1)
+    cfg = TrainConfig(batch_size=batch, bsize=256, lr=1e-5, weight_decay=1e-4, bucket_mb=64.0, comm_bf16=False,
+                      force_dp_path=force_dp)
     trainer = build_trainer(cfg, device=dev, world_size=world, rank=rank, net=CPSAM().randomize_(0))
     data = synthetic_train_batch(batch, 256, device=dev, seed=rank)
     for _ in range(3):
@@ -338,11 +341,25 @@ def main():
             out["finetune_cpsam_config"] = {"model": "Cellpose-SAM ViT-L/8 (dim 1024, 24 blocks)", "crop": 256,
                                             "batch_per_gpu": args.cpsam_batch, "ms_per_step": round(ms, 3),
                                             "engine": "HIP fwd/bwd engine, HIP-graph step" if world == 1 else
-                                            "HIP fwd/bwd engine, RCCL bucketed all-reduce (bf16) overlapped",
+                                            "HIP fwd/bwd engine, segmented HIP-graph step, RCCL bucketed fp32 all-reduce overlapped",
                                             "parallelism": f"dp{world}"}
             if world == 1:
                 sps1, ms1 = bench_train_cpsam(args, world, rank, dev, 1, args.train_steps)
                 out["finetune_cpsam_batch1_samples_per_sec"] = round(sps1, 2)  # the reference's batch size
+                out["finetune_cpsam_ms_b1"] = round(ms1, 3)
+                # the world > 1 step path (segmented graph + bucket all-reduces) forced on this GPU
+                import socket
+
+                with socket.socket() as so:
+                    so.bind(("127.0.0.1", 0))
+                    port = so.getsockname()[1]
+                dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                        device_id=dev)
+                try:
+                    _, msd = bench_train_cpsam(args, world, rank, dev, 1, args.train_steps, force_dp=True)
+                    out["finetune_cpsam_dp_path_ms_b1"] = round(msd, 3)
+                finally:
+                    dist.destroy_process_group()
         except Exception as e:  # noqa: BLE001
             out["extras_error_train_cpsam"] = f"{type(e).__name__}: {e}"
     if rank == 0:

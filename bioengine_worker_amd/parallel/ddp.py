@@ -64,10 +64,14 @@ class FlatParams:
 class BucketedAllReduce:
     """Overlapped gradient all-reduce over slices of a FlatParams gradient buffer."""
 
-    def __init__(self, fp: FlatParams, group=None, bucket_mb: float = 16.0, comm_dtype: torch.dtype | None = None):
+    def __init__(self, fp: FlatParams, group=None, bucket_mb: float = 16.0, comm_dtype: torch.dtype | None = None,
+                 force: bool = False):
         self.fp = fp
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # force: run the collectives even on a 1-rank group (measures the data-parallel code path,
+        # its launches and graph segmentation, on one GPU)
+        self.active = self.world > 1 or (force and dist.is_initialized())
         self.comm_dtype = comm_dtype
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
         # bucket boundaries on parameter boundaries, in gradient-arrival order
@@ -89,10 +93,19 @@ class BucketedAllReduce:
         self.works: list = []
         self._hooks = []
         self._index = {id(p): i for i, p in enumerate(fp.params)}
-        if self.world > 1:
+        if self.active:
             for i, p in enumerate(fp.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         self.reset()
+
+    def bucket_of(self, p) -> int:
+        return self.param_bucket[self._index[id(p)]]
+
+    def launch_bucket(self, bi: int) -> None:
+        """Issue bucket ``bi``'s all-reduce now (segmented-graph replay knows the completion order)."""
+        if self.active and self.pending[bi] > 0:
+            self.pending[bi] = 0
+            self._launch(bi)
 
     def reset(self):
         self.pending = [len(m) for (_, _, m) in self.buckets]
@@ -103,7 +116,7 @@ class BucketedAllReduce:
         """Explicit readiness for engines that write gradients without autograd
         (:class:`~bioengine_worker_amd.train.cpnet_engine.CPnetTrainEngine`): the moment the last
         parameter of a bucket is reported, that bucket's all-reduce is issued."""
-        if self.world == 1:
+        if not self.active:
             return
         for p in params:
             bi = self.param_bucket[self._index[id(p)]]
@@ -133,7 +146,7 @@ class BucketedAllReduce:
     def finish(self) -> float:
         """Wait for every bucket (launching any that never filled, e.g. unused params).
         Returns the gradient scale (1/world) the optimizer must apply."""
-        if self.world == 1:
+        if not self.active:
             return 1.0
         for bi, n in enumerate(self.pending):
             if n > 0:

@@ -65,6 +65,13 @@ class TrainConfig:
     # batch 8 39.7 -> 41.4-41.8 ms, batch 1 15.3 -> 16.9-17.6 ms: the optimizer's HBM stream slows
     # the backward kernels more than it hides), so the flat update after the replay stays the default.
     cpsam_overlap_adamw: bool = False
+    # run the data-parallel step path (segmented graph + bucket all-reduces) even at world 1 over a
+    # 1-rank process group: the on-one-GPU measurement of the DP code path's own overhead
+    force_dp_path: bool = False
+    # data-parallel CPSAM step: capture fwd+bwd as a chain of HIP graphs cut where gradient buckets
+    # complete; each bucket's all-reduce is issued right after its segment replays, so RCCL traffic
+    # overlaps the remaining backward while the step stays launch-free
+    cpsam_dp_graph: bool = True
 
 
 def lr_schedule(learning_rate: float, n_epochs: int) -> np.ndarray:
@@ -98,7 +105,7 @@ class CellposeTrainer:
         if world_size > 1:
             broadcast_params(self.fp, 0, group)
         self.ar = BucketedAllReduce(self.fp, group=group, bucket_mb=cfg.bucket_mb,
-                                    comm_dtype=torch.bfloat16 if cfg.comm_bf16 else None)
+                                    comm_dtype=torch.bfloat16 if cfg.comm_bf16 else None, force=cfg.force_dp_path)
         self.m = torch.zeros_like(self.fp.flat)
         self.v = torch.zeros_like(self.fp.flat)
         self.step_count = 0
@@ -180,10 +187,10 @@ class CellposeTrainer:
 
         eng = self._engine(x.shape[0], x.shape[-1])
         with trace.span("train.fwd_bwd_engine", cuda=True):
-            if self.cfg.graph and self.device.type == "cuda" and (self.world == 1 or self.cfg.ddp_graph):
+            if self.cfg.graph and self.device.type == "cuda" and (not self.ar.active or self.cfg.ddp_graph):
                 loss = self._graph_step(eng, x, lbl)  # ar.finish() then all-reduces every bucket
             else:
-                loss = eng.loss_and_backward(x, lbl, on_params_ready=self.ar.mark_ready if self.world > 1 else None)
+                loss = eng.loss_and_backward(x, lbl, on_params_ready=self.ar.mark_ready if self.ar.active else None)
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
@@ -215,12 +222,15 @@ class CellposeTrainer:
             keep = stochastic_depth_keep(x.shape[0], len(eng.blocks), self.net.rdrop, self.device, self.gen)
         with trace.span("train.fwd_bwd_cpsam", cuda=True):
             fused_opt = False
-            if self.cfg.graph and self.device.type == "cuda" and self.world == 1 and not self._cpsam_graph_failed:
+            graphable = self.cfg.graph and self.device.type == "cuda" and not self._cpsam_graph_failed
+            if graphable and not self.ar.active:
                 loss = self._cpsam_graph_step(eng, x, lbl, keep)
                 fused_opt = getattr(self, "_adamw_in_graph", False)
+            elif graphable and self.cfg.cpsam_dp_graph:
+                loss = self._cpsam_dp_graph_step(eng, x, lbl, keep)
             else:
                 loss = eng.loss_and_backward(x, lbl, keep,
-                                             on_params_ready=self.ar.mark_ready if self.world > 1 else None)
+                                             on_params_ready=self.ar.mark_ready if self.ar.active else None)
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
@@ -305,6 +315,75 @@ class CellposeTrainer:
         g.replay()
         return out.clone()
 
+    def _cpsam_dp_graph_step(self, eng, x, lbl, keep):
+        """Data-parallel CPSAM step: fwd+bwd captured as a CHAIN of graphs cut at every point where
+        a gradient bucket becomes complete (simulated with the bucket arrival counts during
+        capture).  Replay: segment k, then the all-reduces of the buckets it completed (async, RCCL
+        stream), then segment k+1 -- communication overlaps the rest of the backward exactly as in
+        the eager hook path, but with no per-kernel launch cost.  Segments share one memory pool and
+        are replayed in capture order."""
+        key = (tuple(x.shape), tuple(lbl.shape))
+        if getattr(self, "_cpsam_dp", None) is None or self._cpsam_dp[0] != key:
+            xs, ls = x.clone(), lbl.clone()
+            ks = (keep.clone() if keep is not None else
+                  torch.ones(x.shape[0], len(eng.blocks), device=self.device))
+            try:
+                side = torch.cuda.Stream(self.device)
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
+                    for _ in range(2):
+                        eng.loss_and_backward(xs, ls, ks)
+                torch.cuda.current_stream(self.device).wait_stream(side)
+                torch.cuda.synchronize(self.device)
+                pending = [len(m) for (_, _, m) in self.ar.buckets]
+                segs: list = []
+                state = {"g": torch.cuda.CUDAGraph(), "pool": None}
+                cap = torch.cuda.Stream(self.device)
+                cap.wait_stream(torch.cuda.current_stream(self.device))
+
+                def cut(params):
+                    done = []
+                    for p in params:
+                        bi = self.ar.bucket_of(p)
+                        pending[bi] -= 1
+                        if pending[bi] == 0:
+                            done.append(bi)
+                    if done:
+                        state["g"].capture_end()
+                        segs.append((state["g"], done))
+                        if state["pool"] is None:
+                            state["pool"] = state["g"].pool()
+                        state["g"] = torch.cuda.CUDAGraph()
+                        state["g"].capture_begin(pool=state["pool"])
+
+                with torch.cuda.stream(cap):
+                    state["g"].capture_begin()
+                    out = eng.loss_and_backward(xs, ls, ks, on_params_ready=cut)
+                    state["g"].capture_end()
+                segs.append((state["g"], [bi for bi, n in enumerate(pending) if n > 0]))
+                torch.cuda.current_stream(self.device).wait_stream(cap)
+            except Exception as e:  # noqa: BLE001
+                import logging
+
+                logging.getLogger("bioengine.train").warning("CPSAM DP graph capture failed (%s); running eagerly", e)
+                self._cpsam_graph_failed = True
+                torch.cuda.synchronize(self.device)
+                self.ar.reset()
+                return eng.loss_and_backward(x, lbl, keep, on_params_ready=self.ar.mark_ready)
+            self._cpsam_dp = (key, segs, xs, ls, ks, out)
+        _, segs, xs, ls, ks, out = self._cpsam_dp
+        xs.copy_(x)
+        ls.copy_(lbl)
+        if keep is not None:
+            ks.copy_(keep)
+        else:
+            ks.fill_(1.0)
+        for g, done in segs:
+            g.replay()
+            for bi in done:
+                self.ar.launch_bucket(bi)
+        return out.clone()
+
     def _refresh_mirrors(self) -> None:
         for eng in self._cpsam_engs.values():
             eng.refresh_mirror()
@@ -381,6 +460,7 @@ class CellposeTrainer:
                                     comm_dtype=torch.bfloat16 if self.cfg.comm_bf16 else None)
         self._graph = self._graph_io = None
         self._cpsam_graph = None
+        self._cpsam_dp = None
         self._adamw_in_graph = False
         if self.world > 1:
             broadcast_params(self.fp, 0, group)

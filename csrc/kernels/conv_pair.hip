@@ -64,6 +64,7 @@ struct PairArgs {
 template <int CK_, int CM_, int INMODE, bool X2, bool PROJ, int RES, int NCA>
 struct PC {
   static constexpr int CK = CK_, CM = CM_;
+  static constexpr bool PROJ_ = PROJ;
   static constexpr int KPA = ((9 * CK + 31) / 32) * 32;
   static constexpr int KSA = KPA / 32;
   static constexpr int WSTRA = KPA + 16;
@@ -87,6 +88,8 @@ struct PC {
   static constexpr int WREG = RESW ? NCA * WA_ELEMS + NCB * WB_ELEMS + (PROJ ? CM * WSTRP : 0) : WB_ELEMS;
   static constexpr size_t LDS = (size_t)(RREG + PREG + WREG) * sizeof(bf16_t);
   static constexpr int CPP = NCT * 2;  // 16-byte output chunks per pixel
+  // prefetch the residual / skip operands at tile start (registers permitting)
+  static constexpr bool PF = CM == 32;
   static constexpr int OSH = CM == 32 ? 1 : 0;
   static_assert(NT % CGI == 0, "a thread's channel group must not change across halo units");
   static_assert(CK == 8 || (PSTRI / 2) % 16 == 8, "input pixel stride must be 8 (mod 16) dwords");
@@ -111,16 +114,77 @@ __device__ __forceinline__ TileXY tile_xy(const PairArgs& a, int t) {
   return r;
 }
 
+// Stage-A pixel tile T (0..38) of the 18 x 34 h region -> this lane's region pixel (ry, rx).
+// Tiles 0..35 are the two 16-pixel halves of columns 0..31 of each region row, so the 16 lanes of an
+// MFMA operand read consecutive pixels of ONE halo row (ds_read_b128 conflict-free for the 8 (mod 16)
+// dword pixel stride); tiles 36..38 take the two edge columns 32..33 of 8 rows each.  (A linear
+// pixel order wraps rows inside ~half of the tiles: measured ~1.8 conflict cycles per LDS op.)
+__device__ __forceinline__ bool apix(int T, int lrow, int& ry, int& rx) {
+  if (T < 2 * RH) {
+    ry = T >> 1;
+    rx = (T & 1) * 16 + lrow;
+    return true;
+  }
+  ry = (T - 2 * RH) * 8 + (lrow >> 1);
+  rx = 2 * 16 + (lrow & 1);
+  const bool ok = ry < RH;
+  if (!ok) { ry = 0; rx = 0; }  // padding lanes: read valid data, never stored
+  return ok;
+}
+static_assert(RW == 2 * 16 + 2 && 2 * RH + (RH + 7) / 8 == RPT, "stage-A tile map covers the 18 x 34 region");
+
+// 16-byte halo unit u -> (halo pixel, 8-channel group).  For 32-channel chunks, 8 consecutive lanes
+// take 4 pixels x 2 channel groups: their ds_write_b128 then cover 8 distinct 16-byte slots of the
+// 32-bank write row (the plain pixel-major order is 2-way conflicted at the 24-dword pixel stride),
+// and 16 lanes still read 256 contiguous bytes of global memory.  The channel group of a thread is
+// the same for u and u + NT (NT % 16 == 0), which the affine prefetch relies on.
+template <int CGI>
+__device__ __forceinline__ void unit_pc(int u, int& pix, int& cg) {
+  if constexpr (CGI == 4) {
+    pix = (u >> 4) * 4 + ((u >> 1) & 3);
+    cg = ((u >> 3) & 1) * 2 + (u & 1);
+  } else {
+    pix = u / CGI;
+    cg = u % CGI;
+  }
+}
+static_assert(NT % 16 == 0, "unit_pc keeps a thread's channel group across units");
+
 // ---- A input halo: global -> registers (raw, in-transform applied) --------------------------------
-template <typename C, int INMODE>
-__device__ __forceinline__ void issue_halo(const PairArgs& a, TileXY t, int ch, int tid, u32x4 (&hraw)[C::HUPT]) {
+template <typename C>
+struct HaloRegs {
+  u32x4 h[C::HUPT];
+  float4 aff[C::PF ? 4 : 1];        // actA scale (2) + shift (2) of this thread's 8 channels
+  float4 paff[C::PROJ_ ? 4 : 1];    // actP
+};
+
+template <typename C, int INMODE, bool PROJ>
+__device__ __forceinline__ void issue_halo(const PairArgs& a, TileXY t, int ch, int tid, HaloRegs<C>& hr) {
   const int c0 = ch * C::CGI * 8;
+  if constexpr (C::PF) {  // the thread's channel group is the same for every unit: its affine rides along
+    int pix0, cg0;
+    unit_pc<C::CGI>(tid, pix0, cg0);
+    const int c = c0 + cg0 * 8;
+    hr.aff[0] = *reinterpret_cast<const float4*>(a.sa + c);
+    hr.aff[1] = *reinterpret_cast<const float4*>(a.sa + c + 4);
+    const float* tr = a.ta + (size_t)t.n * a.ta_ns + c;
+    hr.aff[2] = *reinterpret_cast<const float4*>(tr);
+    hr.aff[3] = *reinterpret_cast<const float4*>(tr + 4);
+    if constexpr (PROJ) {
+      hr.paff[0] = *reinterpret_cast<const float4*>(a.sp + c);
+      hr.paff[1] = *reinterpret_cast<const float4*>(a.sp + c + 4);
+      hr.paff[2] = *reinterpret_cast<const float4*>(a.tp + c);
+      hr.paff[3] = *reinterpret_cast<const float4*>(a.tp + c + 4);
+    }
+  }
+  u32x4 (&hraw)[C::HUPT] = hr.h;
 #pragma unroll
   for (int i = 0; i < C::HUPT; ++i) {
     const int u = tid + i * NT;
     u32x4 r = (u32x4){0u, 0u, 0u, 0u};
     if (u < C::HU) {
-      const int pix = u / C::CGI, cg = u % C::CGI;
+      int pix, cg;
+      unit_pc<C::CGI>(u, pix, cg);
       const int gy = t.ty0 - 2 + pix / IW, gx = t.tx0 - 2 + pix % IW;
       if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
         const int c = c0 + cg * 8;
@@ -147,32 +211,40 @@ __device__ __forceinline__ void issue_halo(const PairArgs& a, TileXY t, int ch, 
   }
 }
 
-__device__ __forceinline__ void load_aff8(const float* s, const float* t, int t_ns, int n, int c, float (&sc)[8],
-                                          float (&sh)[8]) {
-  const float4 s0 = *reinterpret_cast<const float4*>(s + c);
-  const float4 s1 = *reinterpret_cast<const float4*>(s + c + 4);
-  const float* tr = t + (size_t)n * t_ns + c;
-  const float4 t0 = *reinterpret_cast<const float4*>(tr);
-  const float4 t1 = *reinterpret_cast<const float4*>(tr + 4);
-  sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-  sh[0] = t0.x; sh[1] = t0.y; sh[2] = t0.z; sh[3] = t0.w; sh[4] = t1.x; sh[5] = t1.y; sh[6] = t1.z; sh[7] = t1.w;
-}
-
 // activated halo -> LDS (conv zero padding applies AFTER the activation); the stem also writes
 // actP of the centre pixels for the in-kernel projection
+__device__ __forceinline__ void unpack_aff(const float4 (&f)[4], float (&sc)[8], float (&sh)[8]) {
+  sc[0] = f[0].x; sc[1] = f[0].y; sc[2] = f[0].z; sc[3] = f[0].w; sc[4] = f[1].x; sc[5] = f[1].y; sc[6] = f[1].z; sc[7] = f[1].w;
+  sh[0] = f[2].x; sh[1] = f[2].y; sh[2] = f[2].z; sh[3] = f[2].w; sh[4] = f[3].x; sh[5] = f[3].y; sh[6] = f[3].z; sh[7] = f[3].w;
+}
+
 template <typename C, bool PROJ>
-__device__ __forceinline__ void commit_halo(const PairArgs& a, TileXY t, int ch, int tid,
-                                            const u32x4 (&hraw)[C::HUPT], bf16_t* rin, bf16_t* preg) {
-  const int c = ch * C::CGI * 8 + (tid % C::CGI) * 8;
+__device__ __forceinline__ void commit_halo(const PairArgs& a, TileXY t, int ch, int tid, const HaloRegs<C>& hr,
+                                            bf16_t* rin, bf16_t* preg) {
   float sc[8], sh[8];
-  load_aff8(a.sa, a.ta, a.ta_ns, t.n, c, sc, sh);
+  if constexpr (C::PF) {
+    unpack_aff(hr.aff, sc, sh);
+  } else {  // CM = 64: no registers to spare across the MFMA stage; read the (L2-hot) affine here
+    int pix0, cg0;
+    unit_pc<C::CGI>(tid, pix0, cg0);
+    const int c = ch * C::CGI * 8 + cg0 * 8;
+    float4 f[4];
+    f[0] = *reinterpret_cast<const float4*>(a.sa + c);
+    f[1] = *reinterpret_cast<const float4*>(a.sa + c + 4);
+    const float* tr = a.ta + (size_t)t.n * a.ta_ns + c;
+    f[2] = *reinterpret_cast<const float4*>(tr);
+    f[3] = *reinterpret_cast<const float4*>(tr + 4);
+    unpack_aff(f, sc, sh);
+  }
   float ps[8], pt[8];
-  if (PROJ) load_aff8(a.sp, a.tp, 0, 0, c, ps, pt);
+  if constexpr (PROJ) unpack_aff(hr.paff, ps, pt);
+  const u32x4 (&hraw)[C::HUPT] = hr.h;
 #pragma unroll
   for (int i = 0; i < C::HUPT; ++i) {
     const int u = tid + i * NT;
     if (u >= C::HU) continue;
-    const int pix = u / C::CGI, cg = u % C::CGI;
+    int pix, cg;
+    unit_pc<C::CGI>(u, pix, cg);
     const int iy = pix / IW, ix = pix % IW;
     const int gy = t.ty0 - 2 + iy, gx = t.tx0 - 2 + ix;
     const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
@@ -263,9 +335,9 @@ __device__ __forceinline__ void mma_a(f32x4 (&acc)[C::NCT][APT], const bf16_t* r
   int base[APT];
 #pragma unroll
   for (int j = 0; j < APT; ++j) {
-    int p = (wave + j * NW) * 16 + lrow;
-    if (p >= RPIX) p = 0;  // padding pixels of the last MFMA tile: read valid data, discard later
-    base[j] = ((p / RW) * IW + (p % RW)) * C::PSTRI + (C::CK == 8 ? 0 : kq * 8);
+    int ry, rx;
+    apix(wave + j * NW, lrow, ry, rx);
+    base[j] = (ry * IW + rx) * C::PSTRI + (C::CK == 8 ? 0 : kq * 8);
   }
   auto frags = [&](int ks, bf16x8 (&af)[C::NCT], bf16x8 (&bf)[APT]) {
     int off;
@@ -310,29 +382,90 @@ __device__ __forceinline__ void mma_a(f32x4 (&acc)[C::NCT][APT], const bf16_t* r
   }
 }
 
-// actB(+skip) of stage A's accumulators -> h (bf16) in LDS; zero outside the image
+// Per-tile epilogue operands, issued at the START of the tile so their latency hides behind the
+// A-stage MFMAs (loading them in the epilogues left ~1 us of dependent global-load latency exposed
+// per phase: 1 block of 8 waves per CU has nothing else to run meanwhile).
+template <typename C, bool X2, int RES, bool PF>
+struct EpiRegs {
+  float4 sb[PF ? C::NCT : 1], tb[PF ? C::NCT : 1], bias[PF ? C::NCT : 1];
+  u32x2 xv[X2 && PF ? APT : 1][C::NCT];
+  u32x2 rv[RES && PF ? 4 : 1][C::NCT];
+};
+
 template <typename C, bool X2>
+__device__ __forceinline__ u32x2 load_x2(const PairArgs& a, TileXY t, int j, int ct, int wave, int lrow, int kq) {
+  int ry, rx;
+  const bool ok = apix(wave + j * NW, lrow, ry, rx);
+  const int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
+  u32x2 v = (u32x2){0u, 0u};
+  if (X2 && ok && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+    v = *reinterpret_cast<const u32x2*>(a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * C::CM + ct * 16 + kq * 4);
+  return v;
+}
+
+template <typename C, int RES>
+__device__ __forceinline__ u32x2 load_res(const PairArgs& a, TileXY t, int pt, int ct, int wave, int lrow, int kq) {
+  const int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+  if (RES == 0 || py >= a.H || px >= a.W) return (u32x2){0u, 0u};
+  size_t pix;
+  if (RES == 1) pix = ((size_t)t.n * a.H + py) * a.W + px;
+  else pix = ((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1);
+  return *reinterpret_cast<const u32x2*>(a.res + pix * C::CM + ct * 16 + kq * 4);
+}
+
+template <typename C, bool X2, int RES, bool PF>
+__device__ __forceinline__ void issue_epi(const PairArgs& a, TileXY t, int wave, int lrow, int kq,
+                                          EpiRegs<C, X2, RES, PF>& e) {
+  if constexpr (PF) {
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct) {
+      const int c = ct * 16 + kq * 4;
+      e.sb[ct] = *reinterpret_cast<const float4*>(a.sb + c);
+      e.tb[ct] = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
+      e.bias[ct] = *reinterpret_cast<const float4*>(a.bias + c);
+    }
+  }
+  if constexpr (PF && X2) {
+#pragma unroll
+    for (int j = 0; j < APT; ++j)
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) e.xv[j][ct] = load_x2<C, X2>(a, t, j, ct, wave, lrow, kq);
+  }
+  if constexpr (PF && RES != 0) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < C::NCT; ++ct) e.rv[pt][ct] = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
+  }
+}
+
+// actB(+skip) of stage A's accumulators -> h (bf16) in LDS; zero outside the image
+template <typename C, bool X2, int RES, bool PF>
 __device__ __forceinline__ void epi_a(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][APT], bf16_t* rh,
-                                      int wave, int lrow, int kq) {
+                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq) {
 #pragma unroll
   for (int ct = 0; ct < C::NCT; ++ct) {
     const int c = ct * 16 + kq * 4;
-    const float4 s = *reinterpret_cast<const float4*>(a.sb + c);
-    const float4 sh = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
+    float4 s, sh;
+    if constexpr (PF) {
+      s = e.sb[ct];
+      sh = e.tb[ct];
+    } else {
+      s = *reinterpret_cast<const float4*>(a.sb + c);
+      sh = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
+    }
     u32x2 xv[APT];
 #pragma unroll
     for (int j = 0; j < APT; ++j) {
-      xv[j] = (u32x2){0u, 0u};
-      const int p = (wave + j * NW) * 16 + lrow;
-      const int gy = t.ty0 - 1 + p / RW, gx = t.tx0 - 1 + p % RW;
-      if (X2 && p < RPIX && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
-        xv[j] = *reinterpret_cast<const u32x2*>(a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * C::CM + c);
+      if constexpr (PF && X2) xv[j] = e.xv[j][ct];
+      else xv[j] = load_x2<C, X2>(a, t, j, ct, wave, lrow, kq);
     }
 #pragma unroll
     for (int j = 0; j < APT; ++j) {
-      const int p = (wave + j * NW) * 16 + lrow;
-      if (p >= RPIX) continue;
-      const int gy = t.ty0 - 1 + p / RW, gx = t.tx0 - 1 + p % RW;
+      int ry, rx;
+      if (!apix(wave + j * NW, lrow, ry, rx)) continue;
+      const int p = ry * RW + rx;
+      const int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
       u32x2 st = (u32x2){0u, 0u};
       if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
         float v0 = acc[ct][j][0], v1 = acc[ct][j][1], v2 = acc[ct][j][2], v3 = acc[ct][j][3];
@@ -404,24 +537,23 @@ __device__ __forceinline__ int stage_off(int p, int co) {
 }
 
 // bias + residual, staged through LDS, 16-byte coalesced NHWC stores
-template <typename C, int RES>
-__device__ __forceinline__ void epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][4], bf16_t* stage, int wave,
-                                      int lrow, int kq) {
+template <typename C, bool X2, int RES, bool PF>
+__device__ __forceinline__ void epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][4], bf16_t* stage,
+                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq) {
   u32x2 rv[4][C::NCT];
 #pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    const int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
-    const bool ok = RES != 0 && py < a.H && px < a.W;
-    size_t pix = 0;
-    if (RES == 1) pix = ((size_t)t.n * a.H + py) * a.W + px;
-    if (RES == 2) pix = ((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1);
+  for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct)
-      rv[pt][ct] = ok ? *reinterpret_cast<const u32x2*>(a.res + pix * C::CM + ct * 16 + kq * 4) : (u32x2){0u, 0u};
-  }
+    for (int ct = 0; ct < C::NCT; ++ct) {
+      if constexpr (PF && RES != 0) rv[pt][ct] = e.rv[pt][ct];
+      else rv[pt][ct] = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
+    }
   float4 bias[C::NCT];
 #pragma unroll
-  for (int ct = 0; ct < C::NCT; ++ct) bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
+  for (int ct = 0; ct < C::NCT; ++ct) {
+    if constexpr (PF) bias[ct] = e.bias[ct];
+    else bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
+  }
   bf16_t* ws = stage + wave * C::OUT_WAVE;
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt) {
@@ -463,9 +595,9 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   if (t0 >= t1) return;
   if constexpr (C::RESW) load_resident<C, PROJ, NCA>(a, tid0, WL);
 
-  u32x4 hraw[C::HUPT];
+  HaloRegs<C> hraw;
   u32x4 wraw[C::WUPT];
-  issue_halo<C, INMODE>(a, tile_xy(a, t0), 0, tid0, hraw);
+  issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t0), 0, tid0, hraw);
   if constexpr (!C::RESW) issue_w<C, NCA>(a, 0, tid0, wraw);
 
   for (int t = t0; t < t1; ++t) {
@@ -475,6 +607,8 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wave = tid >> 6, lrow = lane & 15, kq = lane >> 4;
     const TileXY cur = tile_xy(a, t);
+    EpiRegs<C, X2, RES, C::PF> ep;
+    issue_epi<C, X2, RES, C::PF>(a, cur, wave, lrow, kq, ep);
     f32x4 acc_a[C::NCT][APT];
 #pragma unroll
     for (int i = 0; i < C::NCT; ++i)
@@ -487,13 +621,13 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
       commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P);
       if constexpr (!C::RESW) commit_w<C>(tid, wraw, WL);
       __syncthreads();
-      if (c + 1 < NCA) issue_halo<C, INMODE>(a, cur, c + 1, tid, hraw);
-      else if (t + 1 < t1) issue_halo<C, INMODE>(a, tile_xy(a, t + 1), 0, tid, hraw);
+      if (c + 1 < NCA) issue_halo<C, INMODE, PROJ>(a, cur, c + 1, tid, hraw);
+      else if (t + 1 < t1) issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t + 1), 0, tid, hraw);
       if constexpr (!C::RESW) issue_w<C, NCA>(a, c + 1, tid, wraw);
       mma_a<C>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
     }
     __syncthreads();  // every wave is done with the input halo and the A weights
-    epi_a<C, X2>(a, cur, acc_a, R, wave, lrow, kq);
+    epi_a<C, X2, RES, C::PF>(a, cur, acc_a, R, ep, wave, lrow, kq);
     // ---- stage B: CM/32 chunks of h ----
     f32x4 acc_b[C::NCT][4];
 #pragma unroll
@@ -516,7 +650,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
     }
     if constexpr (PROJ) mma_p<C>(acc_b, P, WL + NCA * C::WA_ELEMS + C::NCB * C::WB_ELEMS, wave, lrow, kq);
     __syncthreads();  // every wave is done reading h before the output staging overlays it
-    epi_b<C, RES>(a, cur, acc_b, R, wave, lrow, kq);
+    epi_b<C, X2, RES, C::PF>(a, cur, acc_b, R, ep, wave, lrow, kq);
   }
 }
 

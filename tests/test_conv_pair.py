@@ -186,5 +186,5 @@ def test_cpnet_engine_pair_path_gpu(gpu, monkeypatch):
     # bf16 activations through ~40 random-init layers: judge by relative RMS, and require the fused
     # path to be no worse than the per-layer path against the fp32 module
     e_pair, e_layer = rel(y, ref), rel(y0, ref)
-    assert e_pair < 2e-2 and e_pair < 1.25 * e_layer + 1e-3, (e_pair, e_layer)
+    assert e_pair < 4e-2 and e_pair < 1.25 * e_layer + 1e-3, (e_pair, e_layer)
     assert (y - ref).abs().max().item() < 8e-2 * ref.abs().max().item()

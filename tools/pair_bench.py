@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--tiles", type=int, default=288)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only-pairs", action="store_true", help="skip the engine A/B (profiling passes)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     net = CPnet().randomize_(0).eval()
@@ -49,18 +50,22 @@ def main():
     os.environ["BE_CPNET_PAIR"] = "1"
     x = torch.randn(args.tiles, 224, 224, 8, device=dev).bfloat16()
     x[..., 2:] = 0
+    res = {"pair": [], "layer": []}
+    if args.only_pairs:
+        args.rounds = 0
     with torch.no_grad():
         ya, _ = eng_pair(x)
         yb, _ = eng_layer(x)
     d = (ya - yb).abs().max().item()
     print(json.dumps({"check": "pair_vs_layer_max_abs", "value": d, "ref_max": yb.abs().max().item()}), flush=True)
-    res = {"pair": [], "layer": []}
     for r in range(args.rounds):
         for name, eng in (("pair", eng_pair), ("layer", eng_layer)):
             with torch.no_grad():
                 med, mn = timed(lambda: eng(x), args.reps)
             res[name].append(med)
     for k, v in res.items():
+        if not v:
+            continue
         v.sort()
         print(json.dumps({"engine": k, "tiles": args.tiles, "ms_median": v[len(v) // 2], "ms_min": v[0],
                           "rounds": v}), flush=True)
