@@ -95,6 +95,9 @@ class CellImageSearch:
         self._tasks: dict[str, asyncio.Future] = {}
         self._session_dataset_map: dict[str, str] = {}
         self._lock = asyncio.Lock()
+        import threading
+
+        self._gpu_lock = threading.Lock()  # engine / index calls from the batch threads
 
     # ------------------------------------------------------------------ lifecycle
     async def async_init(self) -> None:
@@ -310,19 +313,76 @@ class CellImageSearch:
                              for s, t in list(self._tasks.items())]}
 
     async def _embed_query(self, image, plow, phigh) -> tuple[np.ndarray, np.ndarray]:
-        import torch
-
         from bioengine_worker_amd.search import reference as ref
-        from bioengine_worker_amd.search.preprocess import batch_to_dinov2
 
         img = ref.to_hwc(np.asarray(image))
+        rgb_f = asyncio.ensure_future(asyncio.to_thread(ref.to_rgb_uint8, img, None, plow, phigh))
+        emb = await self._embed_batch((img, float(plow), float(phigh)))
+        return emb, await rgb_f
+
+    # ------------------------------------------------------------------ batched serving path
+    # Concurrent search requests share ONE fp8 ViT-B/14 forward (up to 64 queries, the reference's
+    # embedding batch, embedder.py:59-95) and ONE index scan, instead of one forward + one scan each
+    # (the reference embeds and searches per request, main.py:1373-1418).  Two batches in flight:
+    # the next batch stacks/uploads while the current one computes.
+    @serve.batch(max_batch_size=64, batch_wait_timeout_s=0.002, max_concurrent_batches=2)
+    async def _embed_batch(self, reqs: list) -> list:
+        """reqs: [(image HWC ndarray, plow, phigh)] -> [embedding fp32 [D]]."""
+        import torch
+
+        from bioengine_worker_amd.search.preprocess import batch_to_dinov2
+
+        groups: dict = {}
+        for i, (img, pl, ph) in enumerate(reqs):
+            groups.setdefault((img.shape, img.dtype.str, pl, ph), []).append(i)
+        out = [None] * len(reqs)
 
         def run():
-            x = torch.from_numpy(np.ascontiguousarray(img)).to(self._worker.device)
-            t = batch_to_dinov2(x[None], None, plow, phigh)
-            return self._worker.engine.embed(t)[0].float().cpu().numpy(), ref.to_rgb_uint8(img, None, plow, phigh)
+            for (_, _, pl, ph), idxs in groups.items():
+                x = torch.from_numpy(np.ascontiguousarray(np.stack([reqs[i][0] for i in idxs])))
+                with self._gpu_lock:
+                    t = batch_to_dinov2(x.to(self._worker.device, non_blocking=True), None, pl, ph)
+                    e = self._worker.engine.embed(t).float().cpu().numpy()
+                for j, i in enumerate(idxs):
+                    out[i] = e[j]
+            return out
 
         return await asyncio.to_thread(run)
+
+    @schema_method
+    async def get_batch_stats(self) -> dict:
+        """Continuous-batching statistics of the query path (batches, requests, batch-size histogram,
+        mean queueing wait) for the embedding forward and the index scan."""
+        from bioengine_worker_amd.serve.batching import batch_stats
+
+        return {"embed": batch_stats(self, "_embed_batch") or {}, "search": batch_stats(self, "_search_batch") or {}}
+
+    @serve.batch(max_batch_size=64, batch_wait_timeout_s=0.001, max_concurrent_batches=2)
+    async def _search_batch(self, reqs: list) -> list:
+        """reqs: [(query fp32 [D], top_k)] -> [(scores [k], ids [k])]: one batched index search."""
+        kmax = max(int(k) for _, k in reqs)
+        q = np.stack([np.asarray(v, np.float32) for v, _ in reqs])
+
+        def run():
+            with self._gpu_lock:
+                return self._index.search(q, kmax)
+
+        S, I = await asyncio.to_thread(run)
+        return [(S[i, :k], I[i, :k]) for i, (_, k) in enumerate(reqs)]
+
+    def _thumb_b64(self, i: int) -> str:
+        """PNG/base64 of an indexed cell's thumbnail, cached (results repeat across queries; the
+        encode is the dominant per-result host cost)."""
+        cache = self.__dict__.setdefault("_thumb_cache", {})
+        v = cache.get(i)
+        if v is None:
+            from bioengine_worker_amd.search.ingestion import png_b64
+
+            v = png_b64(self._thumbnails[i])
+            if len(cache) >= 200_000:
+                cache.clear()
+            cache[i] = v
+        return v
 
     def _results(self, scores, ids) -> list:
         out = []
@@ -332,9 +392,7 @@ class CellImageSearch:
             meta = self._metadata_df.iloc[int(i)].to_dict() if self._metadata_df is not None and i < len(self._metadata_df) else {}
             thumb = ""
             if self._thumbnails is not None and i < len(self._thumbnails):
-                from bioengine_worker_amd.search.ingestion import png_b64
-
-                thumb = png_b64(self._thumbnails[int(i)])
+                thumb = self._thumb_b64(int(i))
             out.append({"rank": rank + 1, "score": float(s), "faiss_idx": int(i), **meta, "thumbnail_b64": thumb})
         return out
 
@@ -353,15 +411,20 @@ class CellImageSearch:
             q = np.asarray(embedding, np.float32)
             q = q / max(np.linalg.norm(q), 1e-9)
         else:
-            raw = _decode_image_b64(image_b64) if image_b64 is not None else np.asarray(image)
+            raw = (await asyncio.to_thread(_decode_image_b64, image_b64)) if image_b64 is not None else np.asarray(image)
             q, rgb = await self._embed_query(raw, plow, phigh)
-            from PIL import Image
 
-            from bioengine_worker_amd.search.ingestion import png_b64
+            def thumb():
+                from PIL import Image
 
-            qthumb = png_b64(np.asarray(Image.fromarray(rgb).resize((224, 224))))
-        S, I = await asyncio.to_thread(self._index.search, q[None], top_k)
-        return {"results": self._results(S[0], I[0]), "query_thumbnail_b64": qthumb,
+                from bioengine_worker_amd.search.ingestion import png_b64
+
+                return png_b64(np.asarray(Image.fromarray(rgb).resize((224, 224))))
+
+            qthumb = await asyncio.to_thread(thumb)
+        s_k, i_k = await self._search_batch((q, int(top_k)))
+        results = await asyncio.to_thread(self._results, s_k, i_k)  # metadata rows + thumbnails off the loop
+        return {"results": results, "query_thumbnail_b64": qthumb,
                 "elapsed_ms": round((time.time() - t0) * 1000, 1), "n_cells_searched": self._index.ntotal, "top_k": top_k}
 
     @schema_method

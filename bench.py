@@ -209,6 +209,45 @@ def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
     return out
 
 
+def bench_vit_embed(dev, batch: int = 64, steps: int = 20) -> float:
+    """DINOv2 ViT-B/14 embedding throughput, fp8 e4m3 GEMMs, batch 64 of 224x224 (the reference's
+    embedder batch and resolution, apps/cell-image-search/embedder.py:59-95; ~500 img/s/A100 fp16)."""
+    from bioengine_worker_amd.search.ingestion import default_engine_factory
+
+    eng = default_engine_factory(dev, "vitb14")
+    x = torch.randn(batch, 3, 224, 224, device=dev)
+    for _ in range(3):
+        eng.embed(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.embed(x)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    del eng
+    torch.cuda.empty_cache()
+    return batch / dt
+
+
+def bench_served_search(seconds: float = 4.0) -> dict:
+    """cell-image-search queries through the serving stack (tools/search_serve_bench.py)."""
+    import argparse as _ap
+    import asyncio
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import search_serve_bench
+
+    a = _ap.Namespace(concurrency=[1, 64], seconds=seconds, gpus=1, n_images=4, model="vitb14", max_ongoing=64,
+                      replica_mode="process")
+    out = {}
+    for r in asyncio.run(search_serve_bench.main_async(a)):
+        c = r["concurrency"]
+        out[f"search_served_qps_c{c}"] = r["qps"]
+        out[f"search_served_p50_ms_c{c}"] = r["p50_ms"]
+        out[f"search_served_p99_ms_c{c}"] = r["p99_ms"]
+    return out
+
+
 def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int, force_dp: bool = False):
     """Cellpose-SAM (ViT-L/8, 256x256 crops) fine-tune steps -- the reference app's own training
     workload -- on the HIP CPSAM engine; with world > 1 data-parallel over RCCL (bucketed fp32
@@ -324,6 +363,18 @@ def main():
                 out.update(bench_served(args.served_seconds))
             except Exception as e:  # noqa: BLE001
                 out["extras_error_served"] = f"{type(e).__name__}: {e}"
+        if rank == 0:
+            try:
+                out["vit_embed_imgs_per_s"] = round(bench_vit_embed(dev), 1)  # per GPU, batch 64, fp8
+                out["vit_embed_config"] = {"model": "DINOv2 ViT-B/14", "image": 224, "batch": 64,
+                                           "gemm_dtype": "fp8 e4m3", "baseline_img_s_A100_fp16": 500}
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_vit"] = f"{type(e).__name__}: {e}"
+        if world == 1 and not args.no_served:
+            try:
+                out.update(bench_served_search(args.served_seconds))
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_served_search"] = f"{type(e).__name__}: {e}"
         try:
             tdt = bench_train(args, world, rank, dev)
             out["finetune_samples_per_sec"] = round(args.train_batch * args.train_steps * world / tdt, 2)

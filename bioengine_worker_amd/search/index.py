@@ -4,8 +4,12 @@ Replaces the reference's FAISS indexes (apps/cell-image-search/index_manager.py:
 SURVEY.md K20) with an HBM-resident design: MI355X holds 288 GB, i.e. ~180 M 768-d bf16 vectors,
 so exact search is one bf16 GEMM (hipBLASLt) per query batch plus a top-k, streamed over
 fixed-size chunks.  Past ``ivf_threshold`` vectors an IVF layer (spherical k-means on the GPU,
-``nlist = clamp(sqrt(N), 64, 4096)``, ``nprobe = 64`` as in the reference) restricts each query to
-its closest lists.  Storage is plain ``.npy`` + JSON (no pickles).
+``nlist ~ 4 sqrt(N)``, ``nprobe = 64`` as in the reference) restricts each query to its closest
+lists, whose list-sorted bf16 slabs are scored EXACTLY by the HIP scan kernel
+(``csrc/kernels/ivf_scan.hip``) -- the reference needs 8-bit PQ codes at this size because it is
+CPU/DRAM bound; on one 288 GB GPU the full vectors fit, so recall is limited only by probing.  The
+compressed IVF-PQ tier (``search/ivfpq.py``) is kept for collections that do not fit.
+Storage is plain ``.npy`` + JSON (no pickles).
 
 Layout at ``<workspace>/cell_search/``: ``vectors.npy`` (fp16 [N, D]), ``index_info.json``,
 ``ivf_centroids.npy`` / ``ivf_assign.npy`` (IVF only), ``metadata.parquet``, ``thumbnails.npy``.
@@ -23,6 +27,14 @@ import torch
 CHUNK = 1 << 20  # database rows per GEMM chunk
 
 
+def _argmax_ip(x: torch.Tensor, cent: torch.Tensor, budget: int = 1 << 30) -> torch.Tensor:
+    """Nearest centroid by inner product, in row chunks sized so the [rows, nlist] score block stays
+    under ``budget`` elements (at 58 M x 30 k lists an unchunked product would be ~7 TB)."""
+    cent = cent.to(x.dtype)
+    rows = max(1, min(x.shape[0], budget // max(1, cent.shape[0])))
+    return torch.cat([(x[i:i + rows] @ cent.T).argmax(1) for i in range(0, x.shape[0], rows)])
+
+
 class VectorIndex:
     """Tiers (reference FlatIP / IVFFlat / IVFPQ): ``index_type="auto"`` keeps exact bf16 search up
     to ``ivf_threshold`` vectors, IVF-Flat above it and IVF-PQ (``search/ivfpq.py``, m=96 x 8 bit)
@@ -30,6 +42,7 @@ class VectorIndex:
 
     def __init__(self, dim: int = 768, device=None, ivf_threshold: int = 5_000_000, nprobe: int = 64,
                  index_type: str = "auto", ivfpq_threshold: int = 50_000_000, pq_m: int = 96, refine: int = 4):
+        self.lvecs: torch.Tensor | None = None
         self.dim = dim
         self.refine = refine  # IVF-PQ: re-rank refine*k PQ candidates with the stored vectors (0 = off)
         self.kind = index_type
@@ -63,12 +76,21 @@ class VectorIndex:
         self.vecs = torch.cat([self.vecs, x], 0)
         if self.pq is not None:
             self.pq.add(x.float())
-        elif self.kind == "ivfpq" or (self.kind == "auto" and self.ntotal >= self.ivfpq_threshold):
+        elif self.kind == "ivfpq" or (self.kind == "auto" and self.ntotal >= self.ivfpq_threshold
+                                       and not self._fits_hbm(self.ntotal)):
             self.train_ivfpq()
         elif self.centroids is not None:
             self._assign_new(x, self.ntotal - x.shape[0])
         elif self.kind == "ivf" or (self.kind == "auto" and self.ntotal >= self.ivf_threshold):
             self.train_ivf()
+
+    def _fits_hbm(self, n: int) -> bool:
+        """The exact-scan IVF tier keeps the vectors twice (id order + list-sorted): use it while
+        that fits in a third of this GPU's HBM (58 M x 768 bf16 x 2 = 178 GB of 288 GB: yes)."""
+        if self.device.type != "cuda":
+            return False
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        return 2 * n * self.dim * 2 <= 0.66 * total
 
     def train_ivfpq(self, nlist: int | None = None) -> None:
         from .ivfpq import IVFPQIndex, default_nlist
@@ -83,13 +105,17 @@ class VectorIndex:
 
     def train_ivf(self, nlist: int | None = None, iters: int = 10, seed: int = 0) -> None:
         n = self.ntotal
-        nlist = nlist or min(4096, max(64, int(math.sqrt(n))))
+        # ~4 sqrt(N) lists (the FAISS guideline the reference's IVF-PQ tier follows): at 58 M that is
+        # ~30 k lists of ~1.9 k vectors, so nprobe 64 scans ~120 k exact candidates per query
+        nlist = nlist or int(min(65536, max(64, 4 * math.sqrt(n))))
         g = torch.Generator(device="cpu").manual_seed(seed)
-        sample = self.vecs[torch.randperm(n, generator=g)[: min(n, 256 * nlist)].to(self.device)].float()
-        cent = sample[torch.randperm(sample.shape[0], generator=g)[:nlist].to(self.device)].clone()
+        # 64 points per list (FAISS trains IVF on 39-256 per list); scores in the storage dtype
+        sample = self.vecs[torch.randperm(n, generator=g)[: min(n, 64 * nlist)].to(self.device)]
+        samplef = sample.float()
+        cent = samplef[torch.randperm(sample.shape[0], generator=g)[:nlist].to(self.device)].clone()
         for _ in range(iters):  # spherical k-means
-            a = (sample @ cent.T).argmax(1)
-            new = torch.zeros_like(cent).index_add_(0, a, sample)
+            a = _argmax_ip(sample, cent)
+            new = torch.zeros_like(cent).index_add_(0, a, samplef)
             cnt = torch.bincount(a, minlength=nlist)
             empty = cnt == 0
             new[empty] = cent[empty]
@@ -99,18 +125,28 @@ class VectorIndex:
         self._assign_new(self.vecs, 0)
 
     def _assign_new(self, x: torch.Tensor, base: int) -> None:
-        a = torch.cat([(x[i:i + CHUNK] @ self.centroids.T).argmax(1) for i in range(0, x.shape[0], CHUNK)]).int()
+        a = _argmax_ip(x, self.centroids).int()
         self.assign = torch.cat([self.assign, a])
         order = torch.argsort(self.assign, stable=True)
         counts = torch.bincount(self.assign.long(), minlength=self.centroids.shape[0])
         self.sorted_ids = order  # vector ids grouped by list
         self.list_off = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0)])
-        self.lists = list(torch.split(order, counts.tolist()))
+        self.lists = None
+        # list-sorted copy of the vectors: every IVF list is one contiguous HBM slab that the exact
+        # scan kernel streams (be_ivf_scan_bf16); built chunk by chunk to bound the temporary
+        if self.device.type == "cuda" and self.dim % 128 == 0 and self.dim <= 1024:
+            lv = torch.empty_like(self.vecs)
+            for i in range(0, order.numel(), CHUNK):
+                lv[i:i + CHUNK] = self.vecs[order[i:i + CHUNK]]
+            self.lvecs = lv
+        else:
+            self.lvecs = None
 
     # ------------------------------------------------------------------ search
     @torch.no_grad()
-    def search(self, q, k: int = 20):
-        """q [Q, D] -> (scores [Q, k] fp32 numpy, ids [Q, k] int64 numpy; -1 = empty slot)."""
+    def search(self, q, k: int = 20, nprobe: int | None = None):
+        """q [Q, D] -> (scores [Q, k] fp32 numpy, ids [Q, k] int64 numpy; -1 = empty slot).
+        ``nprobe`` overrides the IVF probe count for this call."""
         q = torch.as_tensor(np.asarray(q, np.float32) if not torch.is_tensor(q) else q).to(self.device, self.dtype)
         if q.dim() == 1:
             q = q[None]
@@ -145,19 +181,20 @@ class VectorIndex:
                 best_s, j = torch.topk(best_s, min(k_eff, best_s.shape[1]), dim=1)
                 best_i = torch.gather(best_i, 1, j)
         else:
-            best_s, best_i = self._search_ivf(q, k_eff)
+            best_s, best_i = self._search_ivf(q, k_eff, nprobe=nprobe)
         S = np.full((Q, k), -np.inf, np.float32)
         I = np.full((Q, k), -1, np.int64)
         S[:, : best_s.shape[1]] = best_s.cpu().numpy()
         I[:, : best_i.shape[1]] = best_i.cpu().numpy()
         return S, I
 
-    def _search_ivf(self, q: torch.Tensor, k: int, q_chunk: int = 8):
+    def _search_ivf(self, q: torch.Tensor, k: int, q_chunk: int = 8, nprobe: int | None = None):
         """Batched IVF-Flat: every query's probed lists become one padded candidate row (list-sorted
-        vector ids, located through the list offsets), scored with one batched GEMM per query chunk
-        and reduced with a single top-k -- no per-query Python loop."""
+        vector ids, located through the list offsets).  GPU: the HIP scan kernel scores every
+        candidate exactly from the list-sorted bf16 slabs, then one top-k; CPU: one batched GEMM
+        per query chunk.  No per-query Python loop either way."""
         nl = self.centroids.shape[0]
-        probes = torch.topk((q @ self.centroids.T).float(), min(self.nprobe, nl), dim=1).indices
+        probes = torch.topk((q @ self.centroids.T).float(), min(nprobe or self.nprobe, nl), dim=1).indices
         sizes = (self.list_off[1:] - self.list_off[:-1])[probes]  # [Q, nprobe]
         cand_off = torch.cumsum(sizes, 1) - sizes
         stride = int(sizes.sum(1).max())
@@ -165,6 +202,20 @@ class VectorIndex:
         best_s = torch.full((Q, k), -float("inf"), device=self.device)
         best_i = torch.full((Q, k), -1, dtype=torch.long, device=self.device)
         if stride == 0:
+            return best_s, best_i
+        if getattr(self, "lvecs", None) is not None and self.lvecs.shape[0] == self.ntotal:
+            from ..ops import _native
+
+            out = torch.full((Q, stride), -float("inf"), dtype=torch.float32, device=self.device)
+            _native.call("be_ivf_scan_bf16", _native.ptr(q.float().contiguous()), _native.ptr(probes.int().contiguous()),
+                         _native.ptr(self.list_off), _native.ptr(cand_off.contiguous()), _native.ptr(self.lvecs), Q,
+                         probes.shape[1], self.dim, stride, _native.ptr(out), _native.stream(self.device))
+            ts, ti = torch.topk(out, min(k, stride), dim=1)
+            p = (torch.searchsorted(cand_off.contiguous(), ti.contiguous(), right=True) - 1).clamp(min=0)
+            rows = self.list_off[torch.gather(probes, 1, p)] + (ti - torch.gather(cand_off, 1, p))
+            ids = self.sorted_ids[rows.clamp(0, self.ntotal - 1)]
+            best_s[:, : ts.shape[1]] = ts
+            best_i[:, : ts.shape[1]] = torch.where(torch.isfinite(ts), ids, torch.full_like(ids, -1))
             return best_s, best_i
         slots = torch.arange(stride, device=self.device)
         for a in range(0, Q, q_chunk):

@@ -32,7 +32,9 @@ def _kmeans(x: torch.Tensor, k: int, iters: int, g: torch.Generator, spherical: 
     cent = x[torch.randperm(x.shape[0], generator=g)[:k].to(x.device)].clone()
     for _ in range(iters):
         if spherical:
-            a = (x @ cent.T).argmax(1)
+            from .index import _argmax_ip
+
+            a = _argmax_ip(x, cent)
         else:
             a = torch.cdist(x, cent).argmin(1)
         new = torch.zeros_like(cent).index_add_(0, a, x)
@@ -106,7 +108,9 @@ class IVFPQIndex:
         self.nlist = self.centroids.shape[0]
         self.list_off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
         ps = sample[:pq_sample]  # PQ codebooks: 256 centroids per sub-space need far fewer points
-        a = (ps @ self.centroids.T).argmax(1)
+        from .index import _argmax_ip
+
+        a = _argmax_ip(ps, self.centroids)
         self.codebooks = _pq_train(ps - self.centroids[a], self.m, pq_iters, g)
 
     def add(self, x, chunk: int = 1 << 18) -> None:
@@ -115,7 +119,9 @@ class IVFPQIndex:
         assigns, codes = [], []
         for i in range(0, x.shape[0], chunk):
             xc = x[i:i + chunk].to(self.device, torch.float32)
-            a = (xc @ self.centroids.T).argmax(1)
+            from .index import _argmax_ip
+
+            a = _argmax_ip(xc, self.centroids)
             codes.append(_pq_encode(xc - self.centroids[a], self.codebooks))
             assigns.append(a.int())
         self._assign = torch.cat([self._assign] + assigns)

@@ -119,6 +119,15 @@ def test_cell_image_search_app_e2e(tmp_path, monkeypatch):
         res = await app.search(image_b64=base64.b64encode(buf.getvalue()).decode(), top_k=5)
         assert len(res["results"]) == 5 and res["results"][0]["score"] >= res["results"][-1]["score"]
         assert res["results"][0]["thumbnail_b64"] and "compound" in res["results"][0]
+        # concurrent queries are served through one batched embedding forward + one index scan
+        b64 = base64.b64encode(buf.getvalue()).decode()
+        many = await asyncio.gather(*[app.search(image_b64=b64, top_k=3 + i % 3) for i in range(12)])
+        for i, r in enumerate(many):
+            assert len(r["results"]) == 3 + i % 3
+            assert r["results"][0]["faiss_idx"] == res["results"][0]["faiss_idx"]
+        bs = await app.get_batch_stats()
+        assert bs["embed"]["requests"] >= 13 and bs["embed"]["mean_batch"] > 1.0, bs
+        assert bs["search"]["requests"] >= 13 and bs["search"]["batches"] < bs["search"]["requests"], bs
         up = await app.get_umap_preview(n_samples=100)
         assert len(up["x"]) == stats["n_cells"] and up["method"] in ("pca", "umap")
         pq = await app.project_query_onto_umap(image_b64=base64.b64encode(buf.getvalue()).decode())
