@@ -14,6 +14,7 @@ reference's remote mode (any model-runner service on the hub).
 """
 from __future__ import annotations
 
+import asyncio
 import base64
 import io
 import json
@@ -150,8 +151,61 @@ class MitoAnalysisDeployment:
                 "image_shape": [H, W], "pixel_size_nm": pixel_size_nm, "model": self.model_id,
                 "processing_time_s": round(time.time() - t0, 2)}
 
+    def _data_root(self) -> Path:
+        return Path(os.environ.get("BIOENGINE_EM_DATA_ROOT") or Path(os.environ.get("HOME", ".")) / "em_data").resolve()
+
+    def _volume_spec(self, volume_npy_b64, volume_path, dataset_id, dataset_file, array, work: Path) -> dict:
+        """Where the ranks read the volume from (each reads only its z-slab): an uploaded ``.npy``
+        (written once to local disk, memory-mapped by the ranks), a ``.npy`` / ``.zarr`` path under
+        ``BIOENGINE_EM_DATA_ROOT``, or a zarr array of a BioEngine dataset (HTTP range reads,
+        reference ``bioengine/datasets/http_zarr_store.py``)."""
+        given = [x is not None for x in (volume_npy_b64, volume_path, dataset_id)]
+        if sum(given) != 1:
+            raise ValueError("give exactly one of volume_npy_b64, volume_path, dataset_id")
+        if volume_npy_b64 is not None:
+            vpath = work / "volume.npy"
+            vpath.write_bytes(base64.b64decode(volume_npy_b64))
+            return {"kind": "npy", "path": str(vpath)}
+        if volume_path is not None:
+            root = self._data_root()
+            p = (root / volume_path).resolve() if not Path(volume_path).is_absolute() else Path(volume_path).resolve()
+            if p != root and root not in p.parents:  # paths are caller input: never outside the data root
+                raise PermissionError(f"volume_path must lie under {root}")
+            if not p.exists():
+                raise FileNotFoundError(str(p))
+            kind = "zarr" if p.is_dir() else "npy"
+            return {"kind": kind, "path": str(p), "array": array or ""}
+        ds = getattr(self, "bioengine_datasets", None)
+        if ds is None or not getattr(ds, "data_server_url", None):
+            raise RuntimeError("no BioEngine datasets server is configured for this worker")
+        f = str(dataset_file or "")
+        if ".zarr" not in f:
+            raise ValueError("dataset_file must name a .zarr array")
+        rootf = f.split(".zarr")[0] + ".zarr"
+        inner = (f.split(".zarr", 1)[1].strip("/") or array or "")
+        return {"kind": "dataset", "url": f"{ds.data_server_url}/data/{dataset_id}/{rootf}", "array": inner,
+                "token": getattr(ds, "token", None)}
+
+    def _model3d_root(self, model_id_3d: str) -> str:
+        from bioengine_worker_amd.bioimageio.package import write_unet3d_package
+        from bioengine_worker_amd.bioimageio.zoo import list_local_models
+
+        local = list_local_models().get(model_id_3d)
+        if local is not None:
+            return str(local["dir"])
+        root = Path(os.environ.get("HOME", ".")) / "model_zoo" / model_id_3d
+        if not (root / "rdf.yaml").exists():
+            write_unet3d_package(root, model_id_3d, in_channels=1, out_channels=1)
+        return str(root)
+
     @schema_method
-    async def analyze_volume(self, volume_npy_b64: str = Field(..., description="3-D stack as base64 .npy bytes (Z,Y,X)."),
+    async def analyze_volume(self, volume_npy_b64: str | None = Field(None, description="3-D stack as base64 .npy bytes (Z,Y,X)."),
+                             volume_path: str | None = Field(None, description="A .npy file or .zarr directory under "
+                                                                               "BIOENGINE_EM_DATA_ROOT (no upload: every "
+                                                                               "GPU reads only its z-slab)."),
+                             dataset_id: str | None = Field(None, description="BioEngine dataset holding the volume."),
+                             dataset_file: str | None = Field(None, description="Zarr array in that dataset, e.g. 'em.zarr/raw'."),
+                             array: str | None = Field(None, description="Array path inside a zarr group."),
                              pixel_size_nm: float = Field(5.0, description="In-plane pixel size in nm."),
                              tile_size: int = Field(512, description="Tile edge length."),
                              overlap: int = Field(64, description="Tile overlap."),
@@ -163,53 +217,89 @@ class MitoAnalysisDeployment:
                              threshold: float = Field(0.5, description="Foreground probability threshold."),
                              input_is_probability: bool = Field(False, description="The volume already is a foreground "
                                                                                    "probability map (skip the model)."),
+                             split_touching: bool = Field(False, description="Separate touching mitochondria: the "
+                                                                             "reference post-processing (remove small, "
+                                                                             "closing, EDT, peaks, watershed) in 3-D, "
+                                                                             "sharded across the GPUs."),
+                             closing_radius: int = Field(4, description="Closing disk radius (split_touching)."),
+                             min_distance: int = Field(8, description="Peak min distance (split_touching)."),
+                             min_voxels: int = Field(300, description="Smallest instance kept (voxels)."),
+                             inference: str = Field("slice2d", description="'slice2d' (2-D tiles per slice) or "
+                                                                           "'tiled3d' (3-D tiles, 3-D U-Net, z-overlap blend)."),
+                             model_id_3d: str = Field("mito-unet3d", description="3-D model for inference='tiled3d'."),
+                             tile_z: int = Field(32, description="3-D tile depth."),
+                             overlap_z: int = Field(8, description="3-D tile z-overlap."),
                              ) -> dict:
-        """Slice-wise inference + 3-D connected instances (6-connectivity) with per-instance volume;
-        with ``n_gpus > 1`` the z-slabs run as one rank per GPU with globally consistent labels."""
+        """3-D mitochondria instances with per-instance volume.  With ``n_gpus > 1`` the z-slabs run
+        as one rank per GPU (each reads only its slab) with globally consistent labels."""
+        import shutil
         import tempfile
 
         import torch
 
         from bioengine_worker_amd.em import volume as vol
 
-        raw = base64.b64decode(volume_npy_b64)
-        if int(n_gpus or 1) > 1:
-            from bioengine_worker_amd.serve.gang import run_gang
+        if inference not in ("slice2d", "tiled3d"):
+            raise ValueError("inference must be 'slice2d' or 'tiled3d'")
+        if self._pipe is None and not input_is_probability:
+            raise RuntimeError("volume analysis needs the in-process pipeline (no model_runner_service)")
+        work = Path(tempfile.mkdtemp(prefix="em-vol-", dir=os.environ.get("TMPDIR")))
+        spec = await asyncio.to_thread(self._volume_spec, volume_npy_b64, volume_path, dataset_id, dataset_file, array, work)
+        model3d = None
+        if inference == "tiled3d" and not input_is_probability:
+            model3d = await asyncio.to_thread(self._model3d_root, model_id_3d)
+        t0 = time.time()
+        kw = {"volume": spec, "model_root": None if (input_is_probability or model3d) else str(self._pipe.root),
+              "model3d_root": model3d, "tile": tile_size, "overlap": overlap, "batch": self.tile_batch,
+              "threshold": float(threshold), "min_voxels": int(min_voxels), "split_touching": bool(split_touching),
+              "closing_radius": int(closing_radius), "min_distance": int(min_distance), "tile_z": int(tile_z),
+              "overlap_z": int(overlap_z)}
+        opath = work / "labels.npy"
+        try:
+            if int(n_gpus or 1) > 1:
+                from bioengine_worker_amd.serve.gang import run_gang
 
-            if self._pipe is None and not input_is_probability:
-                raise RuntimeError("multi-GPU volumes need the in-process pipeline (no model_runner_service)")
-            work = Path(tempfile.mkdtemp(prefix="em-vol-", dir=os.environ.get("TMPDIR")))
-            vpath, opath = work / "volume.npy", work / "labels.npy"
-            vpath.write_bytes(raw)
-            t0 = time.time()
-            res = await run_gang("bioengine_worker_amd.em.volume:gang_analyze_volume",
-                                 {"volume_path": str(vpath), "out_path": str(opath),
-                                  "model_root": None if input_is_probability else str(self._pipe.root),
-                                  "tile": tile_size, "overlap": overlap, "batch": self.tile_batch, "gather": gather,
-                                  "threshold": float(threshold)},
-                                 world_size=int(n_gpus), gpus_per_rank=1, name=f"em-{work.name[-8:]}")
-            out = dict(res[0])
-            out.update(ranks=[{k: r[k] for k in ("rank", "z_range", "timings_s", "gather_s", "total_s")} for r in res],
-                       n_gpus=int(n_gpus), gather=gather, processing_time_s=round(time.time() - t0, 2))
-            if return_labels and gather == "rank0":
-                out["labels_npy_b64"] = base64.b64encode(opath.read_bytes()).decode()
-            elif gather == "sharded":
-                out["label_shards"] = json.loads(Path(f"{opath}.manifest.json").read_text())
-            if gather != "sharded":
-                import shutil
+                res = await run_gang("bioengine_worker_amd.em.volume:gang_analyze_volume",
+                                     dict(kw, out_path=str(opath), gather=gather),
+                                     world_size=int(n_gpus), gpus_per_rank=1, name=f"em-{work.name[-8:]}")
+                out = dict(res[0])
+                out.update(ranks=[{k: r[k] for k in ("rank", "z_range", "timings_s", "gather_s", "total_s")} for r in res],
+                           n_gpus=int(n_gpus), gather=gather, processing_time_s=round(time.time() - t0, 2))
+                if return_labels and gather == "rank0":
+                    out["labels_npy_b64"] = base64.b64encode(opath.read_bytes()).decode()
+                elif gather == "sharded":
+                    out["label_shards"] = json.loads(Path(f"{opath}.manifest.json").read_text())
+            else:
+                def run_local():
+                    dev = self._pipe.device if self._pipe is not None else torch.device("cpu")
+                    src = vol.VolumeSource(spec)
+                    v = torch.from_numpy(src.read(0, src.shape[0]).astype(np.float32)).to(dev)
+                    p1, p99 = src.percentiles(dev)
+                    predict3d = None
+                    if model3d:
+                        from bioengine_worker_amd.bioimageio.runner import PredictionPipeline
 
+                        p3 = PredictionPipeline(model3d, device=dev)
+                        predict3d = lambda t: next(iter(p3.predict_tensors(t).values()))
+                    predict = vol.probability_identity if input_is_probability else self._predict_local
+                    r = vol.analyze_volume(v, predict, tile_size, overlap, self.tile_batch, threshold=float(threshold),
+                                           min_voxels=int(min_voxels), norm_range=(float(p1), float(p99)),
+                                           split_touching=bool(split_touching), closing_radius=int(closing_radius),
+                                           min_distance=int(min_distance), predict3d=predict3d, tile_z=int(tile_z),
+                                           overlap_z=int(overlap_z))
+                    labels = r.pop("labels_slab_t")
+                    if return_labels:
+                        b = io.BytesIO()
+                        np.save(b, labels.cpu().numpy())
+                        r["labels_npy_b64"] = base64.b64encode(b.getvalue()).decode()
+                    return r
+
+                out = await asyncio.to_thread(run_local)
+                out.update(split_touching=bool(split_touching), inference=inference,
+                           processing_time_s=round(time.time() - t0, 2))
+        finally:
+            if gather != "sharded" or int(n_gpus or 1) <= 1:
                 shutil.rmtree(work, ignore_errors=True)
-        else:
-            vol_np = np.load(io.BytesIO(raw), allow_pickle=False)
-            dev = self._pipe.device if self._pipe is not None else torch.device("cpu")
-            predict = vol.probability_identity if input_is_probability else self._predict_local
-            out = vol.analyze_volume(torch.from_numpy(vol_np.astype(np.float32)).to(dev), predict,
-                                     tile_size, overlap, self.tile_batch, threshold=float(threshold))
-            labels = out.pop("labels_slab_t")
-            if return_labels:
-                b = io.BytesIO()
-                np.save(b, labels.cpu().numpy())
-                out["labels_npy_b64"] = base64.b64encode(b.getvalue()).decode()
         out["pixel_size_nm"] = pixel_size_nm
-        out["model"] = self.model_id
+        out["model"] = model_id_3d if model3d else self.model_id
         return out

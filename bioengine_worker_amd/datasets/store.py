@@ -128,6 +128,39 @@ class HttpZarrStore:
         await self.client.aclose()
 
 
+class LocalZarrStore:
+    """Read-only zarr v3 store over a local directory (the same ``get`` contract as
+    :class:`HttpZarrStore`, so :func:`read_zarr_array` reads regions of local and served arrays)."""
+
+    read_only = True
+
+    def __init__(self, root: str):
+        from pathlib import Path
+
+        self.root = Path(root)
+
+    async def get(self, key: str, prototype=None, byte_range=None):
+        from pathlib import Path
+
+        p = (self.root / key.lstrip("/")).resolve()
+        if self.root.resolve() not in p.parents and p != self.root.resolve():
+            raise PermissionError(f"zarr key escapes the store: {key}")
+        if not p.is_file():
+            return None
+        data = p.read_bytes()
+        if byte_range is not None:
+            a, b = byte_range
+            data = data[a:b]
+        return data
+
+    async def close(self):
+        pass
+
+
+def zarr_shape(meta_raw: bytes) -> tuple[int, ...]:
+    return tuple(json.loads(meta_raw)["shape"])
+
+
 def _decode_chunk(raw: bytes, meta: dict, chunk_shape) -> np.ndarray:
     dtype = np.dtype(meta["data_type"]) if meta["data_type"] not in ("bool",) else np.dtype(bool)
     endian = "<"

@@ -326,15 +326,80 @@ def prob_to_instances(prob: torch.Tensor, threshold: float = 0.5, min_size: int 
     return watershed((-dist).cpu().numpy(), markers.cpu().numpy(), closed.cpu().numpy(), conn=1)
 
 
+def closing_per_slice(binary: torch.Tensor, r: int) -> torch.Tensor:
+    """Binary closing of every z-slice with a radius-``r`` disk (the reference's 2-D ``disk(4)``
+    structuring element applied slice by slice), [D, H, W] bool; GPU: ``be_morph_disk`` dilate + erode."""
+    if r <= 0:
+        return binary
+    D, H, W = binary.shape
+    if not binary.is_cuda:
+        from scipy import ndimage
+
+        yy, xx = np.mgrid[-r:r + 1, -r:r + 1]
+        disk = (yy ** 2 + xx ** 2) <= r ** 2
+        b = binary.cpu().numpy()
+        return torch.from_numpy(np.stack([ndimage.binary_closing(b[z], structure=disk) for z in range(D)]))
+    m8 = binary.to(torch.uint8).contiguous()
+    tmp, out = torch.empty_like(m8), torch.empty_like(m8)
+    st = _native.stream(binary.device)
+    _native.call("be_morph_disk", _native.ptr(m8), _native.ptr(tmp), D, H, W, r, 0, 0, st)
+    _native.call("be_morph_disk", _native.ptr(tmp), _native.ptr(out), D, H, W, r, 1, 0, st)
+    return out.bool()
+
+
+def peak_candidates3d(dist: torch.Tensor, closed: torch.Tensor, min_distance: int, z_lo: int, z_hi: int,
+                      z_global0: int, Z_global: int, floor: float) -> tuple[np.ndarray, np.ndarray]:
+    """Local-maximum candidates of :func:`peak_local_max3d` BEFORE the min-distance thinning, for a
+    z-window of a larger volume: ``dist``/``closed`` cover global slices [z_global0, z_global0 + D);
+    only candidates with local z in [z_lo, z_hi) are returned, as (global zyx [n, 3], values [n]) in
+    raster order.  The border exclusion uses the GLOBAL volume extent."""
+    D, H, W = dist.shape
+    b = min_distance
+    inner = torch.zeros_like(closed)
+    if Z_global > 2 * b and H > 2 * b and W > 2 * b:
+        za = max(0, b - z_global0)
+        zb = min(D, Z_global - b - z_global0)
+        if zb > za:
+            inner[za:zb, b:H - b, b:W - b] = True
+    lm = closed & inner
+    img = torch.where(lm, dist, torch.full_like(dist, -3.0e38))
+    mx = max_filter3d(img, min_distance)
+    cand = (img == mx) & (img > floor) & lm
+    cand[:z_lo] = False
+    cand[z_hi:] = False
+    zyx = cand.nonzero()
+    if zyx.shape[0] == 0:
+        return np.zeros((0, 3), np.int64), np.zeros(0, np.float32)
+    vals = img[zyx[:, 0], zyx[:, 1], zyx[:, 2]].float().cpu().numpy()
+    zyx = zyx.cpu().numpy().astype(np.int64)
+    zyx[:, 0] += z_global0
+    return zyx, vals
+
+
+def _stage(timings, name, t0, dev):
+    if timings is None:
+        return t0
+    import time
+
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    timings[name] = round(timings.get(name, 0.0) + (t - t0), 4)
+    return t
+
+
 def prob_to_instances_3d(mask: torch.Tensor, min_size: int = 300, closing_radius: int = 4, min_distance: int = 8,
-                         gpu_watershed: bool = True) -> tuple[torch.Tensor, int]:
+                         gpu_watershed: bool = True, timings: dict | None = None) -> tuple[torch.Tensor, int]:
     """Foreground volume [D, H, W] (bool, GPU) -> (int32 instance labels, count): the 3-D form of
     the reference post-processing -- remove components under ``min_size`` voxels (6-connected),
     binary closing with a disk per z-slice, 3-D EDT, 3-D peak_local_max, marker watershed on
     -EDT (6-connected) -- so touching objects are split instead of merged by plain CCL."""
+    import time
+
     from .volume import ccl3d
 
     dev = mask.device
+    t = time.perf_counter()
     roots = ccl3d(mask)
     flat = roots.reshape(-1).long()
     fg = flat >= 0
@@ -343,31 +408,23 @@ def prob_to_instances_3d(mask: torch.Tensor, min_size: int = 300, closing_radius
     keep = torch.zeros_like(flat, dtype=torch.bool)
     keep[fg] = cnt[flat[fg]] >= min_size
     binary = keep.reshape(mask.shape)
+    t = _stage(timings, "remove_small", t, dev)
     if not bool(binary.any()):
         return torch.zeros(mask.shape, dtype=torch.int32, device=dev), 0
     D, H, W = binary.shape
-    closed = binary
-    if closing_radius > 0 and not mask.is_cuda:
-        from scipy import ndimage
-
-        yy, xx = np.mgrid[-closing_radius:closing_radius + 1, -closing_radius:closing_radius + 1]
-        disk = (yy ** 2 + xx ** 2) <= closing_radius ** 2
-        b = binary.numpy()
-        closed = torch.from_numpy(np.stack([ndimage.binary_closing(b[z], structure=disk) for z in range(D)]))
-    elif closing_radius > 0:
-        m8 = binary.to(torch.uint8).contiguous()
-        tmp, out = torch.empty_like(m8), torch.empty_like(m8)
-        st = _native.stream(dev)
-        _native.call("be_morph_disk", _native.ptr(m8), _native.ptr(tmp), D, H, W, closing_radius, 0, 0, st)
-        _native.call("be_morph_disk", _native.ptr(tmp), _native.ptr(out), D, H, W, closing_radius, 1, 0, st)
-        closed = out.bool()
+    closed = closing_per_slice(binary, closing_radius)
+    t = _stage(timings, "closing", t, dev)
     dist = edt3d(closed)
+    t = _stage(timings, "edt3d", t, dev)
     peaks = peak_local_max3d(dist, closed, min_distance)
+    t = _stage(timings, "peaks", t, dev)
     markers = _markers_from_peaks(peaks, (D, H, W), dev)
+    t = _stage(timings, "markers", t, dev)
     if gpu_watershed and mask.is_cuda:
         labels = watershed_gpu(-dist, markers, closed)
     else:
         labels = torch.from_numpy(watershed((-dist).cpu().numpy(), markers.cpu().numpy(), closed.cpu().numpy(), conn=1)).to(dev)
+    _stage(timings, "watershed", t, dev)
     return labels, int(len(peaks))
 
 

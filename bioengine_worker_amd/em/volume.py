@@ -320,18 +320,137 @@ def split_instances_sharded(mask: torch.Tensor, group=None, min_size: int = 300,
     return mine[: mask.shape[0]].contiguous(), int(n.item())
 
 
+def exchange_halos(x: torch.Tensor, halo: int, group=None) -> tuple[torch.Tensor, int, int]:
+    """Point-to-point z-halo exchange between neighbouring slab ranks (RCCL send/recv over xGMI on
+    the GPU node, gloo on CPU): returns (``[below-halo | x | above-halo]``, slices received from the
+    rank below, slices received from the rank above).  Each neighbour sends min(halo, its depth)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1) or halo <= 0:
+        return x, 0, 0
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    depth = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    depths = [torch.zeros_like(depth) for _ in range(world)]
+    dist.all_gather(depths, depth, group=group)
+    depths = [int(d) for d in depths]
+    wire = torch.uint8 if x.dtype == torch.bool else x.dtype
+    xs = x.to(wire) if x.dtype == torch.bool else x
+    lo = min(halo, depths[rank - 1]) if rank > 0 else 0
+    hi = min(halo, depths[rank + 1]) if rank + 1 < world else 0
+    below = torch.empty((lo,) + tuple(x.shape[1:]), dtype=wire, device=x.device)
+    above = torch.empty((hi,) + tuple(x.shape[1:]), dtype=wire, device=x.device)
+    ops = []
+    g = (lambda r: r) if group is None else (lambda r: dist.get_global_rank(group, r))
+    if rank > 0:
+        ops.append(dist.P2POp(dist.isend, xs[: min(halo, x.shape[0])].contiguous(), g(rank - 1), group))
+        ops.append(dist.P2POp(dist.irecv, below, g(rank - 1), group))
+    if rank + 1 < world:
+        ops.append(dist.P2POp(dist.isend, xs[max(0, x.shape[0] - halo):].contiguous(), g(rank + 1), group))
+        ops.append(dist.P2POp(dist.irecv, above, g(rank + 1), group))
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    out = torch.cat([below, xs, above])
+    return (out.bool() if x.dtype == torch.bool else out), lo, hi
+
+
+def split_instances_halo(mask: torch.Tensor, group=None, min_size: int = 300, closing_radius: int = 4,
+                         min_distance: int = 8, halo: int | None = None,
+                         timings: dict | None = None) -> tuple[torch.Tensor, int]:
+    """Sharded form of :func:`mito.prob_to_instances_3d`: every rank post-processes ITS OWN z-slab
+    with a z-halo from its neighbours -- no rank ever holds the whole volume.
+
+    * remove-small: global 6-connected labels (:func:`label_sharded`) + all-reduced voxel counts --
+      exact;
+    * closing: per z-slice disk, slab-local -- exact;
+    * EDT / peak candidates / watershed on ``[halo | slab | halo]`` (P2P halo exchange): the EDT
+      inside the slab is exact wherever the nearest background lies within the halo, the
+      ``min_distance`` max-filter window needs ``min_distance`` more slices, so the default halo is
+      ``closing_radius + 2 * min_distance``;
+    * the greedy min-distance thinning (``ensure_spacing``) and the marker numbering are GLOBAL: the
+      ranks all-gather their (few) peak candidates, every rank thins the same global list and
+      numbers markers in global raster order, exactly like the single-process pipeline -- so labels
+      need no seam merge, a basin crossing a slab face carries the same marker id on both sides.
+    Returns (this rank's labels, number of instances)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return mito.prob_to_instances_3d(mask, min_size, closing_radius, min_distance, timings=timings)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = mask.device
+    halo = closing_radius + 2 * min_distance if halo is None else int(halo)
+    depth = torch.tensor([mask.shape[0]], dtype=torch.int64, device=dev)
+    depths = [torch.zeros_like(depth) for _ in range(world)]
+    dist.all_gather(depths, depth, group=group)
+    depths = [int(d) for d in depths]
+    z0 = sum(depths[:rank])
+    Zg = sum(depths)
+    # 1. remove small objects with GLOBAL component sizes
+    labels, n = label_sharded(mask, group)
+    cnt = torch.bincount(labels.reshape(-1).long(), minlength=n + 1)[: n + 1].to(torch.int64)
+    dist.all_reduce(cnt, group=group)
+    big = cnt >= min_size
+    big[0] = False
+    binary = big[labels.long()]
+    del labels
+    # 2. slice-wise closing (slab-local)
+    closed = mito.closing_per_slice(binary, closing_radius)
+    del binary
+    # 3. halo exchange, EDT and peak candidates of the core slices
+    ext, lo, hi = exchange_halos(closed, halo, group)
+    dmap = mito.edt3d(ext).to(dev)
+    core = dmap[lo: lo + mask.shape[0]]
+    floor = torch.tensor([float(core.min()) if core.numel() else 0.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(floor, op=dist.ReduceOp.MIN, group=group)
+    zyx, vals = mito.peak_candidates3d(dmap, ext, min_distance, lo, lo + mask.shape[0], z0 - lo, Zg,
+                                       float(floor.item()))
+    # 4. global candidate list -> global greedy thinning -> global raster-order marker ids
+    payload = torch.from_numpy(np.concatenate([zyx.astype(np.float64), vals[:, None].astype(np.float64)], 1)
+                               if len(zyx) else np.zeros((0, 4))).to(dev)
+    m = torch.tensor([payload.shape[0]], dtype=torch.int64, device=dev)
+    ms = [torch.zeros_like(m) for _ in range(world)]
+    dist.all_gather(ms, m, group=group)
+    mmax = max(1, max(int(v) for v in ms))
+    buf = torch.zeros(mmax, 4, dtype=torch.float64, device=dev)
+    buf[: payload.shape[0]] = payload
+    bufs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)
+    allc = torch.cat([bufs[r][: int(ms[r])] for r in range(world)]).cpu().numpy()  # raster order (slabs in z order)
+    if len(allc):
+        order = np.argsort(-allc[:, 3], kind="stable")  # = single process: stable sort of -value over raster order
+        peaks = mito.ensure_spacing(allc[order, :3].astype(np.int64), min_distance).astype(np.int64)
+    else:
+        peaks = np.zeros((0, 3), np.int64)
+    # 5. markers inside the extended slab, numbered by global raster order
+    markers = torch.zeros(ext.shape, dtype=torch.int32, device=dev)
+    if len(peaks):
+        pk = peaks[np.lexsort(peaks.T[::-1])]
+        ids = np.arange(1, len(pk) + 1, dtype=np.int32)
+        zl = pk[:, 0] - (z0 - lo)
+        sel = (zl >= 0) & (zl < ext.shape[0])
+        if sel.any():
+            loc = torch.from_numpy(np.stack([zl[sel], pk[sel, 1], pk[sel, 2]])).to(dev)
+            markers[tuple(loc)] = torch.from_numpy(ids[sel]).to(dev)
+    # 6. watershed on the extended slab, keep the core
+    if ext.is_cuda:
+        lab = mito.watershed_gpu(-dmap, markers, ext)
+    else:
+        lab = torch.from_numpy(mito.watershed((-dmap).cpu().numpy(), markers.cpu().numpy(), ext.cpu().numpy(), conn=1))
+    return lab[lo: lo + mask.shape[0]].to(dev).contiguous(), int(len(peaks))
+
+
 def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 64, batch: int = 8,
                    threshold: float = 0.5, min_voxels: int = 300, group=None, gather_labels: bool = False,
                    z_offset: int = 0, gather: str | None = None, timings: bool = False,
                    norm_range: tuple[float, float] | None = None, split_touching: bool = False,
-                   closing_radius: int = 4, min_distance: int = 8) -> dict:
+                   closing_radius: int = 4, min_distance: int = 8, predict3d=None, tile_z: int = 32,
+                   overlap_z: int = 8, core: tuple[int, int] | None = None, split_halo: int | None = None) -> dict:
     """Single-process (or per-rank) 3-D analysis.  With a process group, ``vol`` is this rank's
     z-slab and results are globally consistent.  ``gather="mask"`` / ``"labels"`` all-gathers the
     stitched foreground mask (uint8) / global instance labels of the whole volume onto every rank
     (``out["mask"]`` / ``out["labels_full"]``, device tensors); ``gather_labels`` returns this
     rank's slab labels as numpy.  ``split_touching`` replaces connected components by the 3-D
     reference post-processing (closing, EDT, peaks, marker watershed) so touching mitochondria
-    become separate instances (:func:`split_instances_sharded`)."""
+    become separate instances (sharded: :func:`split_instances_halo`, each rank on its own slab).
+    ``predict3d`` ([B, 1, tz, t, t] -> [B, C, tz, t, t], a 3-D U-Net) switches inference from
+    slice-wise 2-D tiles to 3-D tiles with z-overlap blending (:func:`infer_tiled_3d`); ``core``
+    = (lo, hi) crops this rank's slab out of a ``vol`` read with extra z-margin for that context
+    (overlap recompute instead of an input halo exchange)."""
     import time
 
     from ..search.preprocess import percentiles
@@ -356,18 +475,26 @@ def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 6
         p1, p99 = pr[0], pr[1]
     vn = ((v - p1) / (p99 - p1 + 1e-6)).clamp(0, 1)
     mark("normalize")
-    prob = slice_probabilities(vn, predict, tile, overlap, batch)
+    if predict3d is not None:
+        prob = infer_tiled_3d(vn, predict3d, tile=tile, tile_z=tile_z, overlap=overlap, overlap_z=overlap_z,
+                              batch=batch)[0]
+    else:
+        prob = slice_probabilities(vn if core is None else vn[core[0]:core[1]], predict, tile, overlap, batch)
+    if predict3d is not None and core is not None:
+        prob = prob[core[0]:core[1]]
     mark("inference")
-    mask = prob > threshold
+    mask = (prob > threshold).contiguous()
     del prob, vn, v
+    split_t: dict | None = {} if timings else None
     if split_touching:
-        labels, n = split_instances_sharded(mask, group, min_voxels, closing_radius, min_distance)
+        labels, n = split_instances_halo(mask, group, min_voxels, closing_radius, min_distance, split_halo,
+                                         timings=split_t)
     else:
         labels, n = label_sharded(mask, group)
     mark("label")
     stats = instance_stats(labels, n, z_offset, group)
     keep = stats["voxels"] >= min_voxels
-    out = {"n_instances": int(keep.sum()), "n_components": n, "volume_shape": list(vol.shape),
+    out = {"n_instances": int(keep.sum()), "n_components": n, "volume_shape": list(mask.shape),
            "instances": {k: vv[keep].tolist() for k, vv in stats.items()}}
     mark("stats")
     out["labels_slab_t"] = labels  # this rank's globally consistent slab labels (device tensor)
@@ -380,6 +507,8 @@ def analyze_volume(vol: torch.Tensor, predict, tile: int = 512, overlap: int = 6
     mark("gather")
     if timings:
         out["timings_s"] = {b[0]: round(b[1] - a[1], 4) for a, b in zip(marks, marks[1:])}
+        if split_t:
+            out["timings_s"]["split_stages"] = split_t
     return out
 
 
@@ -422,20 +551,103 @@ def gather_to_rank0(x: torch.Tensor, group=None) -> torch.Tensor | None:
     return out.bool() if x.dtype == torch.bool else out
 
 
+class VolumeSource:
+    """A [Z, Y, X] volume that every rank reads ONLY its z-range of:
+
+    * ``{"kind": "npy", "path": p}``      -- memory-mapped ``.npy`` (no full read anywhere);
+    * ``{"kind": "zarr", "path": p, "array": a}`` -- local zarr v3 directory, chunk reads;
+    * ``{"kind": "dataset", "url": u, "array": a, "token": t}`` -- zarr v3 served by the BioEngine
+      datasets server, HTTP range reads through :class:`~bioengine_worker_amd.datasets.store.HttpZarrStore`
+      (the reference's data plane, ``/root/reference/bioengine/datasets/http_zarr_store.py:31-245``).
+
+    A bare string is a ``.npy`` path (or a ``.zarr`` directory)."""
+
+    def __init__(self, spec):
+        if isinstance(spec, (str, bytes)) or hasattr(spec, "__fspath__"):
+            p = str(spec)
+            spec = {"kind": "zarr" if p.rstrip("/").endswith(".zarr") else "npy", "path": p}
+        self.spec = dict(spec)
+        self.kind = self.spec["kind"]
+        if self.kind == "npy":
+            self._mm = np.load(self.spec["path"], mmap_mode="r")
+            self.shape = tuple(self._mm.shape)
+        elif self.kind in ("zarr", "dataset"):
+            self._mm = None
+            meta = self._run(self._store().get(self._prefix() + "zarr.json"))
+            if meta is None:
+                raise FileNotFoundError(f"zarr array not found: {self.spec}")
+            from ..datasets.store import zarr_shape
+
+            self.shape = zarr_shape(meta)
+        else:
+            raise ValueError(f"unknown volume source kind {self.kind!r}")
+        if len(self.shape) != 3:
+            raise ValueError(f"expected a [Z, Y, X] volume, got shape {self.shape}")
+
+    def _prefix(self) -> str:
+        a = (self.spec.get("array") or "").strip("/")
+        return f"{a}/" if a else ""
+
+    def _store(self):
+        from ..datasets.store import HttpZarrStore, LocalZarrStore
+
+        if self.kind == "zarr":
+            return LocalZarrStore(self.spec["path"])
+        return HttpZarrStore(self.spec["url"], token=self.spec.get("token"))
+
+    @staticmethod
+    def _run(coro):
+        import asyncio
+
+        return asyncio.run(coro)
+
+    def read(self, z0: int, z1: int) -> np.ndarray:
+        z0, z1 = max(0, z0), min(self.shape[0], z1)
+        if self.kind == "npy":
+            return np.ascontiguousarray(self._mm[z0:z1])
+        from ..datasets.store import read_zarr_array
+
+        async def go():
+            st = self._store()
+            try:
+                return await read_zarr_array(st, self.spec.get("array") or "",
+                                             (slice(z0, z1), slice(0, self.shape[1]), slice(0, self.shape[2])))
+            finally:
+                await st.close()
+
+        return self._run(go())
+
+    def percentiles(self, device=None) -> tuple[torch.Tensor, torch.Tensor]:
+        """p1 / p99 of a deterministic sample, identical on every rank: the strided flat sample of
+        a memory-mapped ``.npy``; for zarr sources up to 16 evenly spaced z-slices, strided."""
+        if self.kind == "npy":
+            return volume_percentiles(self._mm, device)
+        Z = self.shape[0]
+        zs = sorted(set(int(round(z)) for z in np.linspace(0, Z - 1, min(16, Z))))
+        sl = np.stack([self.read(z, z + 1)[0] for z in zs])
+        return volume_percentiles(sl, device)
+
+
 def probability_identity(tiles: torch.Tensor) -> torch.Tensor:
     """``predict`` for inputs that are already foreground probabilities (normalised 0..1)."""
     return tiles
 
 
-def gang_analyze_volume(rank: int, world: int, volume_path: str, out_path: str, model_root: str | None,
+def gang_analyze_volume(rank: int, world: int, volume_path=None, out_path: str = "", model_root: str | None = None,
                         tile: int = 512,
                         overlap: int = 64, batch: int = 8, threshold: float = 0.5, min_voxels: int = 300,
-                        gather: str = "rank0") -> dict:
-    """Gang target (``serve/gang.py``): rank r memory-maps its z-slab of the ``.npy`` volume, runs
-    slice-wise tiled inference + 3-D labelling, and the ranks agree on global labels over the
-    process group (RCCL on the GPU node).  ``gather``: ``"rank0"`` stitches the label volume on
-    rank 0 and writes ``out_path`` (``.npy``); ``"sharded"`` leaves each slab where it was computed
-    and writes ``<out_path>.rank<r>.npy`` + the z offsets; ``"none"`` keeps only the statistics."""
+                        gather: str = "rank0", volume=None, split_touching: bool = False, closing_radius: int = 4,
+                        min_distance: int = 8, model3d_root: str | None = None, tile_z: int = 32,
+                        overlap_z: int = 8) -> dict:
+    """Gang target (``serve/gang.py``): rank r reads ONLY its z-slab of the volume (``volume``: a
+    :class:`VolumeSource` spec -- memory-mapped ``.npy``, local zarr, or a datasets-server zarr over
+    HTTP; ``volume_path``: a ``.npy`` path), runs tiled inference (slice-wise 2-D, or 3-D tiles with
+    a z-margin recomputed instead of exchanged when ``model3d_root`` is given) and labelling; the
+    ranks agree on global labels over the process group (RCCL on the GPU node).  ``split_touching``
+    runs the reference post-processing sharded (:func:`split_instances_halo`).  ``gather``:
+    ``"rank0"`` stitches the label volume on rank 0 and writes ``out_path`` (``.npy``);
+    ``"sharded"`` leaves each slab where it was computed and writes ``<out_path>.rank<r>.npy`` + the
+    z offsets; ``"none"`` keeps only the statistics."""
     import json
     import time
 
@@ -444,17 +656,27 @@ def gang_analyze_volume(rank: int, world: int, volume_path: str, out_path: str, 
     group = None
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
     t0 = time.perf_counter()
-    vol = np.load(volume_path, mmap_mode="r")
-    z0, z1 = slab_bounds(vol.shape[0], rank, world)
-    slab = torch.from_numpy(np.ascontiguousarray(vol[z0:z1])).to(dev)
-    if model_root:
+    src = VolumeSource(volume if volume is not None else volume_path)
+    Z = src.shape[0]
+    z0, z1 = slab_bounds(Z, rank, world)
+    predict, predict3d, core, margin = probability_identity, None, None, 0
+    if model3d_root:
+        pipe3 = PredictionPipeline(model3d_root, device=dev)
+        predict3d = lambda t: next(iter(pipe3.predict_tensors(t).values()))
+        margin = max(overlap_z, tile_z // 2)
+    elif model_root:
         pipe = PredictionPipeline(model_root, device=dev)
         predict = lambda t: next(iter(pipe.predict_tensors(t).values()))
-    else:  # the volume already is a probability map (e.g. from an earlier pass): identity "model"
-        predict = probability_identity
-    p1, p99 = volume_percentiles(vol, dev)  # identical on every rank and to the single-GPU path
+    # else: the volume already is a probability map (e.g. from an earlier pass): identity "model"
+    za, zb = max(0, z0 - margin), min(Z, z1 + margin)
+    slab = torch.from_numpy(src.read(za, zb)).to(dev)
+    if margin:
+        core = (z0 - za, z0 - za + (z1 - z0))
+    p1, p99 = src.percentiles(dev)  # identical on every rank and to the single-GPU path
     res = analyze_volume(slab, predict, tile, overlap, batch, threshold, min_voxels, group=group, z_offset=z0,
-                         timings=True, norm_range=(float(p1), float(p99)))
+                         timings=True, norm_range=(float(p1), float(p99)), split_touching=split_touching,
+                         closing_radius=closing_radius, min_distance=min_distance, predict3d=predict3d,
+                         tile_z=tile_z, overlap_z=overlap_z, core=core)
     t_an = time.perf_counter()
     out = {"rank": rank, "z_range": [z0, z1], "n_instances": res["n_instances"], "timings_s": res["timings_s"]}
     if gather == "rank0":
@@ -465,12 +687,13 @@ def gang_analyze_volume(rank: int, world: int, volume_path: str, out_path: str, 
         np.save(f"{out_path}.rank{rank}.npy", res["labels_slab_t"].cpu().numpy())
         if rank == 0:
             with open(f"{out_path}.manifest.json", "w") as f:
-                json.dump({"world": world, "z_ranges": [list(slab_bounds(vol.shape[0], r, world)) for r in range(world)],
+                json.dump({"world": world, "z_ranges": [list(slab_bounds(Z, r, world)) for r in range(world)],
                            "files": [f"{out_path}.rank{r}.npy" for r in range(world)]}, f)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     out["gather_s"] = round(time.perf_counter() - t_an, 4)
     out["total_s"] = round(time.perf_counter() - t0, 4)
     if rank == 0:
-        out.update(n_components=res["n_components"], volume_shape=list(vol.shape), instances=res["instances"])
+        out.update(n_components=res["n_components"], volume_shape=list(src.shape), instances=res["instances"],
+                   split_touching=bool(split_touching), inference="tiled3d" if predict3d is not None else "slice2d")
     return out

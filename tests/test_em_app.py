@@ -20,6 +20,7 @@ def test_em_app_e2e(tmp_path, monkeypatch):
     monkeypatch.setenv("BIOENGINE_REPLICA_MODE", "local")
     monkeypatch.setenv("HOME", str(tmp_path / "home"))
     monkeypatch.delenv("BIOENGINE_MODEL_ZOO", raising=False)
+    monkeypatch.setenv("BIOENGINE_EM_DATA_ROOT", str(tmp_path / "emdata"))
     reset_local_hubs()
 
     async def main():
@@ -74,6 +75,29 @@ def test_em_app_e2e(tmp_path, monkeypatch):
                                       threshold=float(thr), input_is_probability=True)
         parts = [np.load(f) for f in rs["label_shards"]["files"]]
         assert np.array_equal(np.concatenate(parts), l1)
+        # volumes referenced by path (each rank reads only its slab): .npy memmap and local zarr,
+        # touching objects split by the sharded 3-D watershed == the single-process split
+        from bioengine_worker_amd.datasets.store import write_zarr_array
+
+        data = tmp_path / "emdata"
+        data.mkdir()
+        zz, yy, xx = np.mgrid[0:40, 0:48, 0:48]
+        touching = np.zeros((40, 48, 48), np.float32)
+        for c in ((12, 20, 20), (21, 20, 22), (28, 30, 30), (20, 34, 12)):
+            touching = np.maximum(touching, (((zz - c[0]) ** 2 + (yy - c[1]) ** 2 + (xx - c[2]) ** 2) < 36).astype(np.float32))
+        np.save(data / "vol.npy", (touching * 255).astype(np.uint8))
+        write_zarr_array(str(data / "vol.zarr"), (touching * 255).astype(np.uint8), chunks=(8, 24, 24))
+        kw = dict(tile_size=64, overlap=16, input_is_probability=True, split_touching=True, closing_radius=1,
+                  min_distance=3, min_voxels=20, return_labels=True)
+        ref = await app.analyze_volume(volume_path="vol.npy", **kw)
+        lref = np.load(io.BytesIO(base64.b64decode(ref["labels_npy_b64"])))
+        assert ref["split_touching"] and ref["n_components"] >= 4  # the touching pair became two
+        for src in ("vol.npy", "vol.zarr"):
+            r2 = await app.analyze_volume(volume_path=src, n_gpus=2, gather="rank0", **kw)
+            l2 = np.load(io.BytesIO(base64.b64decode(r2["labels_npy_b64"])))
+            assert np.array_equal(l2, lref), src
+        with pytest.raises(Exception):
+            await app.analyze_volume(volume_path="../../etc/passwd", input_is_probability=True)
         await svc.stop_worker(blocking=True)
         await admin.disconnect()
 
