@@ -27,6 +27,14 @@ import torch
 CHUNK = 1 << 20  # database rows per GEMM chunk
 
 
+def _scores(q: torch.Tensor, v: torch.Tensor) -> torch.Tensor:
+    """q [Q, D] x v [n, D] -> fp32 [Q, n].  bf16 GEMMs keep fp32 outputs (``mm.dtype``): bf16-rounded
+    scores (8 mantissa bits, ~0.004 near 1.0) tie near-duplicate neighbours and scramble the top-k."""
+    if q.is_cuda and q.dtype == torch.bfloat16:
+        return torch.mm(q, v.T, out_dtype=torch.float32)
+    return (q @ v.T).float()
+
+
 def _argmax_ip(x: torch.Tensor, cent: torch.Tensor, budget: int = 1 << 30) -> torch.Tensor:
     """Nearest centroid by inner product, in row chunks sized so the [rows, nlist] score block stays
     under ``budget`` elements (at 58 M x 30 k lists an unchunked product would be ~7 TB)."""
@@ -174,7 +182,7 @@ class VectorIndex:
             best_s = torch.full((Q, 0), -float("inf"), device=self.device)
             best_i = torch.empty(Q, 0, dtype=torch.long, device=self.device)
             for i in range(0, self.ntotal, CHUNK):
-                s = (q @ self.vecs[i:i + CHUNK].T).float()
+                s = _scores(q, self.vecs[i:i + CHUNK])
                 ts, ti = torch.topk(s, min(k_eff, s.shape[1]), dim=1)
                 best_s = torch.cat([best_s, ts], 1)
                 best_i = torch.cat([best_i, ti + i], 1)

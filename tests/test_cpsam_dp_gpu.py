@@ -14,7 +14,7 @@ def test_cpsam_segmented_dp_graph_matches_single_gpu_graph(gpu):
     from bioengine_worker_amd.train.cellpose_train import CellposeTrainer, TrainConfig
 
     def net():
-        m = new_net("cpsam", dict(CPSAM_ARCHS["tiny"], bsize=64))
+        m = new_net("cpsam", dict(CPSAM_ARCHS["tiny"], bsize=256))  # rel-pos attention: 32 x 32 token grid
         torch.manual_seed(0)
         for p in m.parameters():
             p.data.normal_(0, 0.05) if p.dim() > 1 else p.data.normal_(0, 0.01)
@@ -22,7 +22,7 @@ def test_cpsam_segmented_dp_graph_matches_single_gpu_graph(gpu):
         return m
 
     g = torch.Generator().manual_seed(3)
-    B, S = 2, 64
+    B, S = 2, 256
     xs = [torch.randn(B, 3, S, S, generator=g).to(gpu) for _ in range(4)]
     ls = []
     for _ in range(4):

@@ -81,7 +81,15 @@ def main():
         q = torch.nn.functional.normalize(x[qidx].float() + 0.02 * torch.randn(64, a.dim, device=dev, generator=gq), dim=1)
         flat = VectorIndex(dim=a.dim, device=dev, index_type="flat")
         flat.vecs = x
-        gt = flat.search(q, a.k)[1]
+        # ground truth in fp32 (fp32 query x bf16 vectors upcast per chunk): exact up to fp32 rounding
+        gs, gi = [], []
+        for i in range(0, n, 1 << 20):
+            sc = q @ x[i:i + (1 << 20)].float().T
+            ts, ti = torch.topk(sc, a.k, dim=1)
+            gs.append(ts)
+            gi.append(ti + i)
+        ts, j = torch.topk(torch.cat(gs, 1), a.k, dim=1)
+        gt = torch.gather(torch.cat(gi, 1), 1, j).cpu().numpy()
         for name, fn in (("flat_q1", lambda: flat.search(q[:1], a.k)), ("flat_q64", lambda: flat.search(q, a.k))):
             fn()
             p50, p95 = timeit(fn, a.reps)
