@@ -82,6 +82,7 @@ async def _main():
     from .replica import builtin_gpu_check
 
     inflight = faults.InflightTable()
+    nonlocal_state = {"health_ok": 0}
 
     async def handle_call(rid, method, args, kwargs, model_id, deadline=None):
         # never cancelled in the child: the entry stays until the user code returns
@@ -102,6 +103,11 @@ async def _main():
                     res = fn()
                     if inspect.isawaitable(res):
                         res = await res
+                nonlocal_state["health_ok"] += 1
+                if nonlocal_state["health_ok"] in (1, 3):  # lazy async_init has built the app by now
+                    from ..runtime.gcpolicy import refreeze
+
+                    refreeze()
             else:
                 faults.point(f"replica_entry.{method}")
                 fn = getattr(obj, method)
@@ -172,6 +178,9 @@ async def _main():
             try:
                 obj = await asyncio.to_thread(_construct, ctx, cls, args, kwargs)
                 ctx.servable_object = obj
+                from ..runtime.gcpolicy import serving_gc
+
+                serving_gc()  # app constructed: freeze startup objects out of the GC scans
                 await asyncio.to_thread(send_frames, conn, lock, ("ready", True, None))
             except BaseException as e:  # noqa: BLE001
                 traceback.print_exc()

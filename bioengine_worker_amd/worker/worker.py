@@ -185,6 +185,9 @@ class BioEngineWorker:
         await self.apps_manager.deploy_startup_applications(self.startup_applications, self._admin_context)
         await self._register_service()
         self.is_ready.set()
+        from ..runtime.gcpolicy import serving_gc
+
+        serving_gc()  # router / bridge / hub share this loop: keep gen-2 GC pauses out of request latency
         self._monitor_task = asyncio.ensure_future(self._monitor())
         self.log.info(f"BioEngine worker ready: service '{self.full_service_id}' on {self.server_url}")
         if blocking:
