@@ -206,6 +206,7 @@ def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
         out[f"served_imgs_per_sec_c{c}"] = r["imgs_per_s"]
         out[f"served_p50_ms_c{c}"] = r["p50_ms"]
         out[f"served_p95_ms_c{c}"] = r["p95_ms"]
+        out[f"served_p99_ms_c{c}"] = r["p99_ms"]
     return out
 
 
