@@ -183,7 +183,7 @@ class EntryDeployment:
     @schema_method
     async def test(self, model_id: str = Field(..., description="Model id."),
                    stage: Optional[bool] = Field(False, description="Staged version."),
-                   additional_requirements: Optional[List[str]] = Field(None, description="Extra packages (ignored offline)."),
+                   additional_requirements: Optional[List[str]] = Field(None, description="Extra pip requirements for the test; installed from the local wheelhouse, test run in an isolated task."),
                    skip_cache: Optional[bool] = Field(False, description="Re-download and re-test."),
                    publish_test_report: Optional[bool] = Field(False, description="Upload the report to the artifact.")) -> Dict:
         """Run the package's test (test inputs -> outputs) on the GPU runtime; reports are cached

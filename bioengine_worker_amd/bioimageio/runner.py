@@ -180,6 +180,51 @@ class PredictionPipeline:
     def predict(self, inputs, blocksize: int | None = None) -> dict[str, np.ndarray]:
         return {k: v.cpu().numpy() for k, v in self.predict_tensors(inputs, blocksize).items()}
 
+    def batchable(self, blocksize: int | None = None) -> bool:
+        """Whether :meth:`predict_many` can run several requests as one forward: a single-input
+        model with a leading batch axis, predicted whole (tiled requests batch their tiles already)."""
+        blocksize = blocksize if blocksize is not None else self.blocksize
+        return blocksize is None and len(self.inputs) == 1 and self.inputs[0].axes[0].type == "batch"
+
+    def predict_many(self, samples: list, blocksize: int | None = None) -> list[dict[str, np.ndarray]]:
+        """Predict several requests of this model.  Each request is pre- and post-processed on its
+        own (per-sample statistics stay per request); requests whose padded inputs have the same
+        shape are concatenated along the batch axis and run as ONE forward.  Falls back to one
+        :meth:`predict` per request when the model is not :meth:`batchable`."""
+        if len(samples) == 1 or not self.batchable(blocksize):
+            return [self.predict(s, blocksize) for s in samples]
+        spec = self.inputs[0]
+        prepped = []  # (padded input, original lengths, processed inputs)
+        for s in samples:
+            x = self._as_sample(s)
+            proc = {spec.id: processing.apply_chain(x[spec.id].float(), spec.preprocessing, spec.axis_ids, x)}
+            orig = {(spec.id, ax.id): proc[spec.id].shape[i] for i, ax in enumerate(spec.axes)}
+            xp, _ = self._pad_to_valid(spec, proc[spec.id])
+            prepped.append((xp, orig, proc))
+        groups: dict[tuple, list[int]] = {}
+        for i, (xp, _, _) in enumerate(prepped):
+            groups.setdefault(tuple(xp.shape), []).append(i)
+        results: list = [None] * len(samples)
+        for idx in groups.values():
+            xb = torch.cat([prepped[i][0] for i in idx], 0)
+            ys = self._forward([xb])
+            sizes = [prepped[i][0].shape[0] for i in idx]
+            parts = [torch.split(y, sizes, 0) for y in ys]
+            for j, i in enumerate(idx):
+                _, orig, proc = prepped[i]
+                res = {}
+                for spec_o, yp in zip(self.outputs, parts):
+                    y = yp[j]
+                    sl = []
+                    for a, ax in enumerate(spec_o.axes):
+                        L = self._out_len(spec_o, ax, orig) if ax.type == "space" else -1
+                        sl.append(slice(0, L) if 0 < L <= y.shape[a] else slice(None))
+                    y = y[tuple(sl)]
+                    y = processing.apply_chain(y, spec_o.postprocessing, spec_o.axis_ids, {**proc, **{spec_o.id: y}})
+                    res[spec_o.id] = y.cpu().numpy()
+                results[i] = res
+        return results
+
     def predict_tensors(self, inputs, blocksize: int | None = None) -> dict[str, torch.Tensor]:
         """Like :meth:`predict` but keeps the outputs on the device (used by in-process pipelines)."""
         sample = self._as_sample(inputs)

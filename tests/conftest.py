@@ -37,3 +37,23 @@ def gpu():
     assert torch.cuda.is_available()
     _native.hip()  # must load: GPU tests never run on a silent fallback
     return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def wheelhouse(tmp_path_factory):
+    """A local wheelhouse holding ``bioengine-testdep==0.1.0`` (module ``bioengine_testdep``,
+    ``VALUE = "wheel-ok"``), built offline with ``pip wheel --no-index``."""
+    import subprocess
+    import textwrap
+
+    src = tmp_path_factory.mktemp("pkgsrc")
+    (src / "bioengine_testdep.py").write_text('VALUE = "wheel-ok"\n')
+    (src / "setup.py").write_text(textwrap.dedent("""
+        from setuptools import setup
+        setup(name="bioengine-testdep", version="0.1.0", py_modules=["bioengine_testdep"])
+    """))
+    wh = tmp_path_factory.mktemp("wheelhouse")
+    subprocess.run([sys.executable, "-m", "pip", "wheel", "--no-index", "--no-deps", "--no-build-isolation",
+                    "--disable-pip-version-check", "-w", str(wh), str(src)], check=True, capture_output=True, timeout=300)
+    assert list(wh.glob("bioengine_testdep-0.1.0-*.whl"))
+    return wh

@@ -4,9 +4,7 @@ into the app's ``site-packages``, and ``DEPLOY_FAILED`` naming what cannot be sa
 
 The wheel is built here from a two-line package with ``pip wheel --no-index`` (no network)."""
 import asyncio
-import subprocess
 import sys
-import textwrap
 from pathlib import Path
 
 import pytest
@@ -43,21 +41,6 @@ class DepApp:
 
         return bioengine_testdep.VALUE
 '''
-
-
-@pytest.fixture(scope="module")
-def wheelhouse(tmp_path_factory):
-    src = tmp_path_factory.mktemp("pkgsrc")
-    (src / "bioengine_testdep.py").write_text('VALUE = "wheel-ok"\n')
-    (src / "setup.py").write_text(textwrap.dedent("""
-        from setuptools import setup
-        setup(name="bioengine-testdep", version="0.1.0", py_modules=["bioengine_testdep"])
-    """))
-    wh = tmp_path_factory.mktemp("wheelhouse")
-    subprocess.run([sys.executable, "-m", "pip", "wheel", "--no-index", "--no-deps", "--no-build-isolation",
-                    "--disable-pip-version-check", "-w", str(wh), str(src)], check=True, capture_output=True, timeout=300)
-    assert list(wh.glob("bioengine_testdep-0.1.0-*.whl"))
-    return wh
 
 
 @pytest.mark.unit
