@@ -37,6 +37,7 @@ import torch
 import torch.nn.functional as F
 
 from ..models.cpsam import CPSAM, get_rel_pos
+from ..ops import gemm
 from ..ops import vit_train as vt
 from ..parallel.ddp import FlatParams
 
@@ -177,7 +178,7 @@ class CPSAMTrainEngine:
             x = torch.cat([x, x.new_zeros(B, 3 - x.shape[1], *x.shape[2:])], 1)
         W = self._W
         patches = x.to(self.cdt).reshape(B, 3, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B * N, 3 * ps * ps)
-        t = F.linear(patches, W(self.pe[0]).reshape(D, -1), W(self.pe[1]))
+        t = gemm.linear(patches, W(self.pe[0]).reshape(D, -1), W(self.pe[1]))
         t = (t.view(B, N, D) + W(self.pos).reshape(1, N, D)).reshape(B * N, D).contiguous()
         saved = {"patches": patches, "keep": keep, "blocks": []}
         nl = len(self.blocks)
@@ -186,7 +187,7 @@ class CPSAMTrainEngine:
         for i, b in enumerate(self.blocks):
             w, p = b.w, b.p
             kb = keep[:, i].contiguous() if keep is not None else None
-            qkv = F.linear(h1, w["qkv_w"], w["qkv_b"]).view(B, N, 3, H, self.hd)
+            qkv = gemm.linear(h1, w["qkv_w"], w["qkv_b"]).view(B, N, 3, H, self.hd)
             q, k_, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             if self.cuda:  # tables gathered inside relpos.hip (no get_rel_pos index kernels)
                 Rh, Rw = p["rph"].detach(), p["rpw"].detach()
@@ -197,11 +198,10 @@ class CPSAMTrainEngine:
                 rel_h, rel_w = self._rel_terms(q, Rh, Rw)
             a, lse = vt.attn_fwd(q, k_, v, self.scale, rel_h, rel_w)
             a2 = a.reshape(B * N, D)
-            y = F.linear(a2, w["proj_w"], w["proj_b"])
+            y = gemm.linear(a2, w["proj_w"], w["proj_b"])
             t_mid, h2, st2 = vt.ln_fwd(t, p["n2w"], p["n2b"], y=y, rs=kb, rpn=N, eps=self.eps)
-            f = F.linear(h2, w["l1_w"])
-            gg = vt.gelu_fwd(f, p["l1_b"])
-            m = F.linear(gg, w["l2_w"], w["l2_b"])
+            gg, f = gemm.linear_gelu(h2, w["l1_w"], w["l1_b"])  # f: pre-activation (epilogue aux output)
+            m = gemm.linear(gg, w["l2_w"], w["l2_b"])
             if save:
                 saved["blocks"].append(dict(t_in=t, st1=st1, h1=h1, qkv=qkv, rel_h=rel_h, rel_w=rel_w, Rh=Rh, Rw=Rw,
                                             a=a, lse=lse, t_mid=t_mid, st2=st2, h2=h2, f=f, g=gg, keep=kb))
@@ -211,13 +211,13 @@ class CPSAMTrainEngine:
             else:
                 t = self._residual(t_mid, m, kb)
         # neck: 1x1 conv (GEMM) -> LN2d -> 3x3 conv -> LN2d -> readout -> pixel shuffle
-        n0 = F.linear(t, W(self.neck[0].weight).reshape(256, D))
+        n0 = gemm.linear(t, W(self.neck[0].weight).reshape(256, D))
         _, n1, sn1 = vt.ln_fwd(n0, self.neck[1].weight, self.neck[1].bias, eps=self.eps)
         n1i = n1.view(B, g, g, 256).permute(0, 3, 1, 2)  # NCHW view of NHWC memory (channels_last)
         n2 = F.conv2d(n1i, W(self.neck[2].weight), padding=1)
         n2r = n2.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
         _, n3, sn3 = vt.ln_fwd(n2r, self.neck[3].weight, self.neck[3].bias, eps=self.eps)
-        o = F.linear(n3, W(self.outc.weight).reshape(self.outc.weight.shape[0], 256), W(self.outc.bias))
+        o = gemm.linear(n3, W(self.outc.weight).reshape(self.outc.weight.shape[0], 256), W(self.outc.bias))
         yout = o.view(B, g, g, self.nout, ps, ps).permute(0, 3, 1, 4, 2, 5).reshape(B, self.nout, g * ps, g * ps)
         if save:
             saved.update(t_last=t, n0=n0, n1=n1, n1i=n1i, sn1=sn1, n2r=n2r, sn3=sn3, n3=n3)
@@ -245,8 +245,8 @@ class CPSAMTrainEngine:
         do = dyout.to(cd).reshape(B, self.nout, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B * N, -1).contiguous()
         outw = W(self.outc.weight).reshape(self.outc.weight.shape[0], 256)
         torch.sum(do, 0, dtype=torch.float32, out=self.outc.bias.grad)
-        _wgrad(do, s["n3"], self.outc.weight.grad)
-        dn3 = torch.mm(do, outw)
+        gemm.wgrad(do, s["n3"], self.outc.weight.grad)
+        dn3 = gemm.mm(do, outw)
         _, dn2, _, _, _ = vt.ln_bwd(dn3, s["n2r"], s["sn3"], self.neck[3].weight, want_dx=False, want_dxb=True,
                                     out_dw=self.neck[3].weight.grad, out_db=self.neck[3].bias.grad)
         dn2i = dn2.view(B, g, g, 256).permute(0, 3, 1, 2)
@@ -258,8 +258,8 @@ class CPSAMTrainEngine:
         _, dn0, _, _, _ = vt.ln_bwd(dn1, s["n0"], s["sn1"], self.neck[1].weight, want_dx=False, want_dxb=True,
                                     out_dw=self.neck[1].weight.grad, out_db=self.neck[1].bias.grad)
         n0w = W(self.neck[0].weight).reshape(256, D)
-        _wgrad(dn0, s["t_last"], self.neck[0].weight.grad)
-        G = torch.mm(dn0, n0w).float()  # d t_out of the last block (fp32 residual-stream gradient)
+        gemm.wgrad(dn0, s["t_last"], self.neck[0].weight.grad)
+        G = gemm.mm(dn0, n0w).float()  # d t_out of the last block (fp32 residual-stream gradient)
         ready([self.outc.weight, self.outc.bias, self.neck[3].weight, self.neck[3].bias, self.neck[2].weight,
                self.neck[1].weight, self.neck[1].bias, self.neck[0].weight])
         for i in range(len(self.blocks) - 1, -1, -1):
@@ -268,7 +268,7 @@ class CPSAMTrainEngine:
         # patch embedding + position embedding
         torch.sum(G.view(B, N * D), 0, out=self.pos.grad.view(-1))
         Gb, _ = vt.scale_cast(G, dtype=cd, out_col=self.pe[1].grad)
-        _wgrad(Gb, s["patches"], self.pe[0].grad)
+        gemm.wgrad(Gb, s["patches"], self.pe[0].grad)
         ready([self.pos, self.pe[0], self.pe[1]])
         self._saved = None
 
@@ -278,17 +278,17 @@ class CPSAMTrainEngine:
         kb = s["keep"]
         # MLP: t_out = t_mid + k m
         dm, _ = vt.scale_cast(G, kb, N, dtype=self.cdt, out_col=p["l2_b"].grad)
-        _wgrad(dm, s["g"], p["l2_w"].grad)
-        dg = torch.mm(dm, w["l2_w"])
-        df, _ = vt.gelu_bwd(dg, s["f"], p["l1_b"], out_db=p["l1_b"].grad)
-        _wgrad(df, s["h2"], p["l1_w"].grad)
-        dh2 = torch.mm(df, w["l1_w"])
+        gemm.wgrad(dm, s["g"], p["l2_w"].grad)
+        # lin2 dgrad with the GELU backward and lin1's bias gradient in the GEMM epilogue
+        df = gemm.mm_dgelu(dm, w["l2_w"], s["f"], out_db=p["l1_b"].grad)
+        gemm.wgrad(df, s["h2"], p["l1_w"].grad)
+        dh2 = gemm.mm(df, w["l1_w"])
         dt_mid, _, _, _, _ = vt.ln_bwd(dh2, s["t_mid"], s["st2"], p["n2w"], r1=G, out_dw=p["n2w"].grad,
                                        out_db=p["n2b"].grad)
         # attention: t_mid = t_in + k y
         dy, _ = vt.scale_cast(dt_mid, kb, N, dtype=self.cdt, out_col=p["proj_b"].grad)
-        _wgrad(dy, s["a"].reshape(B * N, D), p["proj_w"].grad)
-        da = torch.mm(dy, w["proj_w"]).view(B, N, H, hd)
+        gemm.wgrad(dy, s["a"].reshape(B * N, D), p["proj_w"].grad)
+        da = gemm.mm(dy, w["proj_w"]).view(B, N, H, hd)
         qkv = s["qkv"]
         dqkv = torch.empty(B, N, 3, H, hd, device=G.device, dtype=self.cdt)
         dq, _, _, drh, drw = vt.attn_bwd(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], s["a"], da, s["lse"], self.scale,
@@ -303,8 +303,8 @@ class CPSAMTrainEngine:
             self._table_grad(dRw, p["rpw"].grad)
         dqkv2 = dqkv.view(B * N, 3 * D)
         torch.sum(dqkv2, 0, dtype=torch.float32, out=p["qkv_b"].grad)
-        _wgrad(dqkv2, s["h1"], p["qkv_w"].grad)
-        dh1 = torch.mm(dqkv2, w["qkv_w"])
+        gemm.wgrad(dqkv2, s["h1"], p["qkv_w"].grad)
+        dh1 = gemm.mm(dqkv2, w["qkv_w"])
         dt_in, _, _, _, _ = vt.ln_bwd(dh1, s["t_in"], s["st1"], p["n1w"], r1=dt_mid, out_dw=p["n1w"].grad,
                                       out_db=p["n1b"].grad)
         return dt_in
