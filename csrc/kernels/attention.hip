@@ -12,7 +12,8 @@
 //  * V^T fragments come from ds_read_b64_tr_b16 transposed reads of a row-major V tile; K and V LDS
 //    tiles are XOR-swizzled per 16-byte chunk (conflict-free transposed reads, spread b128 row reads).
 //  * K/V tiles of 64 keys are register-staged: the next tile's global loads are in flight while the
-//    current tile's MFMAs run (T14 "issue early / write late"), one LDS image per tile.
+//    current tile's MFMAs run (T14 "issue early / write late") and land in the second of two LDS
+//    images, so each tile costs one barrier.
 //  * block = NW waves x 32 queries of one (batch, head); the linear block id is XCD-remapped so the
 //    blocks sharing a (batch, head)'s K/V stream run on one XCD's L2.
 #include "common.h"
@@ -53,13 +54,22 @@ __device__ __forceinline__ int v_off(int row, int ch) { return row * HD + ((ch ^
 // BIAS: 0 none, 1 generic decomposed rel-pos (per-key gathers), 2 the SAM 32-wide grid: a 32-key
 // block is exactly one grid row, so a lane's 16 key columns are fixed (rel_w in registers) and the
 // row term is one value per block.
+//
+// Per-tile VALU budget (the loop is VALU-issue bound at head_dim 64: 16 MFMAs of 32 cycles vs 32
+// scores per lane): the rel_w term and the score scale are one FMA per score, the rel_h term is
+// applied to the two block maxima and to the exponent offsets instead of to every score, the
+// key-range mask runs only on a ragged last tile, and the O / l rescale is skipped (wave-uniform
+// branch) when no query's running maximum grew -- exact, alpha would be 1.  K/V tiles are double
+// buffered in LDS: one barrier per tile, the next tile's global loads in flight under the MFMAs and
+// written to the other buffer after them.
 template <int NW, int BIAS>
 __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
   constexpr int CHUNKS = 2 * KT * (HD / 8);        // K + V tile, 16-byte chunks
   constexpr int CPT = (CHUNKS + NT - 1) / NT;      // chunks per thread
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[KT * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[KT * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KT * HD];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KT * HD];
+  constexpr float LOG2E = 1.4426950408889634f;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -78,32 +88,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
   const bf16_t* qbase = a.q + (long long)b * a.s_batch + (long long)hh * a.s_head;
   const bf16_t* kbase = a.k + (long long)b * a.s_batch + (long long)hh * a.s_head;
   const bf16_t* vbase = a.v + (long long)b * a.s_batch + (long long)hh * a.s_head;
-
-  // Q^T fragments (B operand of S^T = K Q^T): 4 k-steps of 16 head dims.
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    u32x4 r = *reinterpret_cast<const u32x4*>(qbase + (long long)qc * a.s_tok + ks * 16 + h * 8);
-    if (qi >= a.N) r = (u32x4){0u, 0u, 0u, 0u};
-    qf[ks] = *reinterpret_cast<bf16x8*>(&r);
-  }
-  const float c2 = a.scale * 1.4426950408889634f;  // scores -> log2 domain
-  const float* rh = nullptr;
-  const float* rw = nullptr;
-  float rwr[16];
-  if (BIAS) {
-    rh = a.relh + ((long long)bh * a.N + qc) * a.Hg;
-    rw = a.relw + ((long long)bh * a.N + qc) * a.Wg;
-  }
-  if (BIAS == 2) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) rwr[i] = rw[8 * (i >> 2) + 4 * h + (i & 3)] * 1.4426950408889634f;
-  }
-
-  f32x16 oacc[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
-  float m = -INFINITY, l = 0.f;
 
   const int ntiles = (a.N + KT - 1) / KT;
   u32x4 stage[CPT];
@@ -125,7 +109,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
       stage[i] = r;
     }
   };
-  auto commit = [&]() {
+  auto commit = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int c = tid + i * NT;
@@ -134,71 +118,131 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
         const int cc = c - isv * (CHUNKS / 2);
         const int row = cc >> 3, ch = cc & 7;
         if (isv)
-          *reinterpret_cast<u32x4*>(Vs + v_off(row, ch)) = stage[i];
+          *reinterpret_cast<u32x4*>(&Vs[buf][v_off(row, ch)]) = stage[i];
         else
-          *reinterpret_cast<u32x4*>(Ks + k_off(row, ch)) = stage[i];
+          *reinterpret_cast<u32x4*>(&Ks[buf][k_off(row, ch)]) = stage[i];
       }
     }
   };
-
   issue(0);
-  for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();  // previous tile fully consumed
-    commit();
-    __syncthreads();
-    if (t + 1 < ntiles) issue(t + 1);
 
-    // ---- S^T = K Q^T for the two 32-key blocks
-    f32x16 s[2];
+  // Q^T fragments (B operand of S^T = K Q^T): 4 k-steps of 16 head dims.
+  bf16x8 qf[4];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+  for (int ks = 0; ks < 4; ++ks) {
+    u32x4 r = *reinterpret_cast<const u32x4*>(qbase + (long long)qc * a.s_tok + ks * 16 + h * 8);
+    if (qi >= a.N) r = (u32x4){0u, 0u, 0u, 0u};
+    qf[ks] = *reinterpret_cast<bf16x8*>(&r);
+  }
+  const float c2 = a.scale * LOG2E;  // scores -> log2 domain
+  const float* rh = nullptr;
+  const float* rw = nullptr;
+  float rwr[16];
+  if (BIAS) {
+    rh = a.relh + ((long long)bh * a.N + qc) * a.Hg;
+    rw = a.relw + ((long long)bh * a.N + qc) * a.Wg;
+  }
+  float rh_cur[2] = {0.f, 0.f};
+  if (BIAS == 2) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
-      const int row = kb * 32 + ql;
+    for (int i = 0; i < 16; ++i) rwr[i] = rw[8 * (i >> 2) + 4 * h + (i & 3)] * LOG2E;
+    rh_cur[0] = rh[0];
+    rh_cur[1] = rh[min(1, a.Hg - 1)];
+  }
+
+  f32x16 oacc[2];
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k_off(row, 2 * ks + h));
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
-      }
+  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  commit(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) issue(t + 1);
+    float rh_next[2] = {0.f, 0.f};
+    if (BIAS == 2) {  // the next tile's row terms (clamped), in flight under this tile's work
+      rh_next[0] = rh[min(2 * t + 2, a.Hg - 1)];
+      rh_next[1] = rh[min(2 * t + 3, a.Hg - 1)];
     }
-    // ---- online softmax (lane = query; keys: kb*32 + 8(i>>2) + 4h + (i&3))
-    float mt = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      float rhv = 0.f;
-      if (BIAS == 2) rhv = rh[min(2 * t + kb, a.Hg - 1)] * 1.4426950408889634f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = t * KT + kb * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
-        float x = s[kb][i] * c2;
-        if (BIAS == 2) {
-          x += rhv + rwr[i];
-        } else if (BIAS == 1) {
-          const int kc = min(key, a.N - 1);
-          const int kh = kc / a.Wg, kw = kc - kh * a.Wg;
-          x += (rh[kh] + rw[kw]) * 1.4426950408889634f;
-        }
-        x = key < a.N ? x : -INFINITY;
-        s[kb][i] = x;
-        mt = fmaxf(mt, x);
-      }
-    }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
-    m = mn;
-    float rs = 0.f;
+    const bf16_t* Kc = Ks[cur];
+    const bf16_t* Vc = Vs[cur];
+
+    // ---- S^T = K Q^T for the two 32-key blocks: all 8 K fragments requested before the MFMAs
+    // so the reads' latency is paid once per tile, not once per MFMA
+    bf16x8 kf[2][4];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        kf[kb][ks] = *reinterpret_cast<const bf16x8*>(Kc + k_off(kb * 32 + ql, 2 * ks + h));
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], zero16, 0, 0, 0);
+#pragma unroll
+      for (int ks = 1; ks < 4; ++ks) s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][ks], qf[ks], s[kb], 0, 0, 0);
+    }
+    // ---- online softmax (lane = query; keys: kb*32 + 8(i>>2) + 4h + (i&3)), log2 domain
+    float rhv[2] = {0.f, 0.f};
+    if (BIAS == 2) {
+      rhv[0] = rh_cur[0] * LOG2E;
+      rhv[1] = rh_cur[1] * LOG2E;
+    }
+    float mt = -INFINITY;
+    const bool ragged = (t + 1) * KT > a.N;  // wave-uniform
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float mk = -INFINITY;
+#pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[kb][i] - mn);
+        float x;
+        if (BIAS == 2) {
+          x = __builtin_fmaf(s[kb][i], c2, rwr[i]);
+        } else if (BIAS == 1) {
+          const int key = t * KT + kb * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+          const int kc = min(key, a.N - 1);
+          const int kh = kc / a.Wg, kw = kc - kh * a.Wg;
+          x = __builtin_fmaf(s[kb][i], c2, (rh[kh] + rw[kw]) * LOG2E);
+        } else {
+          x = s[kb][i] * c2;
+        }
+        s[kb][i] = x;
+      }
+      if (ragged) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = t * KT + kb * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
+          s[kb][i] = key < a.N ? s[kb][i] : -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mk = fmaxf(mk, s[kb][i]);
+      mt = fmaxf(mt, mk + rhv[kb]);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    if (__any(mt > m)) {  // some query's maximum grew: rescale (others get alpha = 1 exactly)
+      const float mn = fmaxf(m, mt);
+      const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const float off = m - rhv[kb];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(s[kb][i] - off);
         s[kb][i] = p;
         rs += p;
       }
-    l = l * alpha + rs;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+    }
+    l += rs;
 
     // ---- O^T += V^T P^T
 #pragma unroll
@@ -218,15 +262,19 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
           const int ch = db * 4 + 2 * g1 + (pp >> 1);
           const int row0 = kb * 32 + 16 * st + 4 * h + qq;
           const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(Vs + v_off(row0, ch) + 4 * (pp & 1)));
+              (__attribute__((address_space(3))) s16x4*)(Vc + v_off(row0, ch) + 4 * (pp & 1)));
           const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(Vs + v_off(row0 + 8, ch) + 4 * (pp & 1)));
+              (__attribute__((address_space(3))) s16x4*)(Vc + v_off(row0 + 8, ch) + 4 * (pp & 1)));
           bf16x8 vf;
           vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
           vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
           oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
         }
       }
+    if (t + 1 < ntiles) commit(cur ^ 1);
+    rh_cur[0] = rh_next[0];
+    rh_cur[1] = rh_next[1];
+    __syncthreads();
   }
 
   // ---- epilogue: O = O^T / l  (lane = query, d = db*32 + 8(i>>2) + 4h + (i&3))

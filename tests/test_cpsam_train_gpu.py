@@ -25,10 +25,12 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("N,bias", [(1024, True), (1056, True), (257, False)])
-def test_attn_bwd_matches_reference(dev, N, bias):
+# (B, H) = (2, 3): small grids -> the fused dq + dkv launch; (8, 8) / (16, 32): the two-launch path
+@pytest.mark.parametrize("N,bias,B,H", [(1024, True, 2, 3), (1056, True, 2, 3), (257, False, 2, 3),
+                                        (1024, True, 8, 8), (1056, True, 8, 8), (257, False, 16, 32)])
+def test_attn_bwd_matches_reference(dev, N, bias, B, H):
     torch.manual_seed(0)
-    B, H, D = 2, 3, 64
+    D = 64
     qkv = (torch.randn(B, N, 3, H, D, device=dev) * 0.5).bfloat16()
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
     rh = rw = None
@@ -44,6 +46,7 @@ def test_attn_bwd_matches_reference(dev, N, bias):
     c = lambda t: None if t is None else t.cpu()
     o_r, lse_r = vt.attn_fwd(c(q).float(), c(k).float(), c(v).float(), scale, c(rh), c(rw))
     assert _rel(lse.cpu(), lse_r) < 1e-3
+    assert _rel(o.cpu(), o_r) < 1e-2, _rel(o.cpu(), o_r)
     dq_r, dk_r, dv_r, drh_r, drw_r = vt.attn_bwd(c(q).float(), c(k).float(), c(v).float(), c(o).float(),
                                                 c(do).float(), lse_r, scale, c(rh), c(rw))
     for name, a, r in (("dq", dq, dq_r), ("dk", dk, dk_r), ("dv", dv, dv_r)):

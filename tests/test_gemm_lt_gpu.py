@@ -8,6 +8,11 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _lt_on(monkeypatch):
+    monkeypatch.setenv("BE_LT", "1")  # the tuned-hipBLASLt path is opt-in (ops/gemm.py enabled())
+
+
 def _rel(a, b):
     a, b = a.float(), b.float()
     return float((a - b).norm() / b.norm().clamp_min(1e-12))

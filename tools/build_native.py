@@ -54,7 +54,9 @@ HIP_FLAGS = [
 ]
 # Per-source extra flags.  clahe: OpenCV bit parity needs separately rounded fp32 products; hipcc's
 # default contraction fuses them into FMAs even under `#pragma clang fp contract(off)`.
-PER_SOURCE_FLAGS = {"clahe": ["-ffp-contract=off"]}
+# attention: MFMA accumulators in arch VGPRs (the default AGPR form moved every S / O tile through
+# v_accvgpr_read/write around the softmax: 192 moves per KV tile); forward 0.085 -> 0.076 ms at B=8.
+PER_SOURCE_FLAGS = {"clahe": ["-ffp-contract=off"], "attention": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread", "-I", str(CSRC / "runtime")]
 
 
