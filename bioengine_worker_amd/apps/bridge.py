@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import time
 import uuid
 
@@ -45,6 +46,10 @@ class AppServiceBridge:
         self.client = None
         self.service_id: str | None = None
         self.rtc_service_id: str | None = None
+        # WebRTC: deploy-time ICE servers (else fetched, else hypha-rpc's defaults) and the live
+        # peer connections get_num_pcs reports (reference proxy_deployment.py:599-732, 767-791)
+        self.ice_servers = built.metadata.get("ice_servers")
+        self.peer_connections: dict[str, dict] = {}
         self.registered = False
         self.calls = 0
         self.errors = 0
@@ -99,7 +104,53 @@ class AppServiceBridge:
         return self.active / max(1, self.max_ongoing)
 
     async def get_num_pcs(self, context=None) -> int:
-        return 0
+        return len(self.peer_connections)
+
+    # ------------------------------------------------------------------ WebRTC
+    ICE_SERVERS_URL = "https://hypha.aicell.io/turn-server/services/coturn/get_rtc_ice_servers"
+
+    async def fetch_ice_servers(self, url: str | None = None, timeout: float = 30.0) -> list | None:
+        """ICE servers for the RTC service: the deploy-time list if one was given, else the TURN
+        endpoint's list (``BIOENGINE_ICE_SERVERS_URL`` overrides the URL), else None so hypha-rpc uses
+        its built-in defaults.  Fetch failures are logged, never raised."""
+        if self.ice_servers is not None:
+            return self.ice_servers
+        url = url or os.environ.get("BIOENGINE_ICE_SERVERS_URL") or self.ICE_SERVERS_URL
+        try:
+            import httpx
+
+            async with httpx.AsyncClient(timeout=timeout) as client:
+                r = await client.get(url)
+                r.raise_for_status()
+                servers = r.json()
+            if not isinstance(servers, list) or not all(isinstance(e, dict) and "urls" in e for e in servers):
+                raise ValueError(f"unexpected ICE server payload: {str(servers)[:200]}")
+            return servers
+        except Exception as e:  # noqa: BLE001
+            self.log.warning(f"ICE server fetch for '{self.application_id}' failed ({type(e).__name__}: {e}); "
+                             "using the RTC library's defaults")
+            return None
+
+    async def on_webrtc_init(self, peer_connection) -> None:
+        """hypha-rpc ``on_init`` hook: track the connection until it reports closed / failed."""
+        cid = uuid.uuid4().hex
+        self.peer_connections[cid] = {"created_at": time.time(), "state": "new"}
+
+        def on_state_change():
+            state = getattr(peer_connection, "connectionState", None)
+            ent = self.peer_connections.get(cid)
+            if ent is None:
+                return
+            ent["state"] = state
+            if state in ("closed", "failed"):
+                self.peer_connections.pop(cid, None)
+            self.log.info(f"WebRTC connection {cid[:8]} of '{self.application_id}' -> {state} "
+                          f"({len(self.peer_connections)} active)")
+
+        try:
+            peer_connection.on("connectionstatechange")(on_state_change)
+        except Exception as e:  # noqa: BLE001  (not an event emitter: keep counting it)
+            self.log.warning(f"WebRTC connection {cid[:8]}: no state events ({e})")
 
     async def get_rtc_service_id(self, context=None):
         return self.rtc_service_id
@@ -136,7 +187,11 @@ class AppServiceBridge:
             from hypha_rpc import register_rtc_service  # type: ignore
 
             rtc_id = f"{self.application_id}-rtc"
-            await register_rtc_service(self.client, rtc_id, {"visibility": "public"})
+            rtc_cfg = {"visibility": "public", "on_init": self.on_webrtc_init}
+            ice = await self.fetch_ice_servers()
+            if ice:
+                rtc_cfg["ice_servers"] = ice
+            await register_rtc_service(self.client, rtc_id, rtc_cfg)
             self.rtc_service_id = f"{self.service_id.split(':')[0]}:{rtc_id}"
         except Exception:
             self.rtc_service_id = None

@@ -241,6 +241,7 @@ class AppsManager:
                 application_kwargs = application_kwargs if application_kwargs is not None else prev.get("application_kwargs")
                 application_env_vars = application_env_vars if application_env_vars is not None else prev.get("application_env_vars_raw")
                 authorized_users = authorized_users if authorized_users is not None else prev.get("authorized_users_param")
+                ice_servers = ice_servers if ice_servers is not None else prev.get("ice_servers")
                 started_at = prev.get("started_at")
                 await self._undeploy(aid)
             else:
