@@ -277,6 +277,11 @@ class CPnetEngine:
         self.style_s = torch.cat(ss, 0).contiguous()
         self.style_t = torch.cat(ts, 0).contiguous()
         self.pair = self._build_pairs(net) if os.environ.get("BE_CPNET_PAIR", "1") != "0" else {}
+        # output layer fused into the last half-block's epilogue (ops/conv_pair.py HeadSpec)
+        self.head = None
+        if ("up", 0, 1) in self.pair and self.out.relu and self.nout <= 16 and os.environ.get("BE_CPNET_HEAD", "1") != "0":
+            self.head = pairops.HeadSpec.build(self.out.scale, self.out.shift, net.output[-1].weight.to(d),
+                                               None if net.output[-1].bias is None else net.output[-1].bias.to(d))
 
     # ------------------------------------------------------------------ fused half-blocks
     def _build_pairs(self, net: CPnet) -> dict:
@@ -366,6 +371,10 @@ class CPnetEngine:
                 # let the fused kernel read it through an up2 residual
                 proj_lr = e["proj"](xcur)
                 x1 = pairops.conv_pair(xcur, P[("up", i, 0)], tb=shifts[(i, 1)], x2=y, res=proj_lr, res_mode="up2")
+                if i == 0 and self.head is not None:
+                    y = pairops.conv_pair_head(x1, P[("up", 0, 1)], self.head, ta=shifts[(0, 2)], tb=shifts[(0, 3)],
+                                               res=x1)
+                    return y, style
                 xcur = pairops.conv_pair(x1, P[("up", i, 1)], ta=shifts[(i, 2)], tb=shifts[(i, 3)], res=x1,
                                          res_mode="full")
                 continue

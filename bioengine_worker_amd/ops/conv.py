@@ -174,7 +174,8 @@ def choose_nw(pc: PackedConv, H: int, W: int, inmode: str = "none", has_x2: bool
     """Measured on MI355X (tools/conv_sweep2.py, profiles/conv_sweep.md): the persistent
     small-channel variants (tco <= 32) prefer 8 waves (more halo reuse per weight fetch); the
     64-channel variants prefer 4 waves (two blocks/CU hide the barrier) except when the halo loader
-    does the 2x2 max-pool (8 waves amortise the 4x wider input read).  The skip-add (x2) 64-channel
+    does the 2x2 max-pool at <= 28x28 output (8 waves amortise the 4x wider input read; measured
+    again in round 3, profiles/r03/conv_deep_ab.md: at 56x56 the 4-wave tiles are 11 % faster).  The skip-add (x2) 64-channel
     variant only fits without spills at 4 waves."""
     key = (pc.ks, pc.cin_pad, pc.cout, inmode)
     if key in NW_POLICY:
@@ -185,8 +186,8 @@ def choose_nw(pc: PackedConv, H: int, W: int, inmode: str = "none", has_x2: bool
         return 8
     if has_x2:
         return 4
-    if inmode == "pool2" and pc.ks == 3:
-        return 8
+    if inmode == "pool2" and pc.ks == 3 and H * W <= 28 * 28:
+        return 8  # 8 waves amortise the 4x wider pooled input read (56x56 and up: 4 waves, conv_deep_ab)
     return 4
 
 

@@ -166,3 +166,76 @@ def conv_pair(x: torch.Tensor, spec: PairSpec, *, ta=None, tb=None, x2=None, res
         RESMODES[res_mode], _native.stream(x.device),
     )
     return out
+
+
+@dataclass
+class HeadSpec:
+    """The network's output layer (``relu(v * s + t)`` then a 1x1 conv with bias; eval BN folded)
+    fused into the epilogue of the final 32-channel half-block (kernel ``be_conv_pair_head``).
+    ``wh``: bf16 [16, 32], rows = output channels (zero past ``nh``), k axis permuted to the
+    accumulator layout (lane group kq holds channels 4kq..4kq+3 and 16+4kq..16+4kq+3)."""
+
+    s: torch.Tensor
+    t: torch.Tensor
+    w: torch.Tensor      # fp32 [nh, 32] original weights (reference path)
+    b: torch.Tensor      # fp32 [16] bias, zero padded
+    nh: int
+    wh: torch.Tensor | None = None
+
+    @staticmethod
+    def k_order() -> list[int]:
+        return [(kq * 4 + j) if j < 4 else (16 + kq * 4 + j - 4) for kq in range(4) for j in range(8)]
+
+    @classmethod
+    def build(cls, scale: torch.Tensor, shift: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None):
+        nh, cin = weight.shape[0], weight.shape[1]
+        assert cin <= 32 and nh <= 16 and weight.shape[2:] == (1, 1)
+        dev = weight.device
+        w = torch.zeros(nh, 32, device=dev)
+        w[:, :cin] = weight.detach().float().reshape(nh, cin)
+        b = torch.zeros(16, device=dev)
+        if bias is not None:
+            b[:nh] = bias.detach().float()
+        s = torch.zeros(32, device=dev)
+        t = torch.zeros(32, device=dev)
+        s[: scale.numel()] = scale.float()
+        t[: shift.numel()] = shift.float()
+        wp = torch.zeros(16, 32, device=dev)
+        wp[:nh] = w[:, cls.k_order()]
+        return cls(s=s.contiguous(), t=t.contiguous(), w=w, b=b.contiguous(), nh=nh,
+                   wh=wp.to(torch.bfloat16).contiguous())
+
+
+def head_ref(xout: torch.Tensor, head: HeadSpec) -> torch.Tensor:
+    """fp32 oracle of the fused head from the block output ``xout`` (NHWC bf16): the activated input is
+    rounded to bf16 as the kernel's MFMA operand is."""
+    a = torch.relu(xout.float() * head.s.to(xout.device) + head.t.to(xout.device))
+    w = head.w.to(a.device)
+    if xout.dtype == torch.bfloat16:  # the GPU path's rounding points (CPU fp32 runs stay fp32)
+        a = a.to(torch.bfloat16).float()
+        w = w.to(torch.bfloat16).float()
+    y = torch.einsum("nhwc,oc->nohw", a, w) + head.b[: head.nh].to(a.device).view(1, -1, 1, 1)
+    return y.contiguous()
+
+
+def conv_pair_head(x: torch.Tensor, spec: PairSpec, head: HeadSpec, *, ta=None, tb=None, res=None) -> torch.Tensor:
+    """Final up half-block (32 -> 32 channels, ``+ res`` at full resolution) with the output layer fused:
+    returns fp32 NCHW [N, nh, H, W]; the block's own 32-channel output never reaches HBM."""
+    ta = spec.ta if ta is None else ta
+    tb = spec.tb if tb is None else tb
+    assert ta is not None and tb is not None and res is not None
+    if not x.is_cuda:
+        return head_ref(conv_pair_ref(x, spec, ta=ta, tb=tb, res=res, res_mode="full"), head)
+    N, H, W, Cin = x.shape
+    assert spec.cin == 32 and spec.cm == 32 and spec.inmode == "none" and spec.pp is None, "head fusion: 32->32 only"
+    assert x.dtype == torch.bfloat16 and x.is_contiguous() and Cin == 32
+    assert res.shape == (N, H, W, 32) and res.dtype == torch.bfloat16 and res.is_contiguous()
+    hout = torch.empty(N, head.nh, H, W, device=x.device, dtype=torch.float32)
+    _native.call(
+        "be_conv_pair_head",
+        _native.ptr(x), _native.ptr(spec.sa), _native.ptr(ta), _affine_stride(ta, N, Cin), _native.ptr(spec.sb),
+        _native.ptr(tb), _affine_stride(tb, N, 32), _native.ptr(spec.pa.wp), _native.ptr(spec.pb.wp),
+        _native.ptr(spec.bias), _native.ptr(res), _native.ptr(head.s), _native.ptr(head.t), _native.ptr(head.wh),
+        _native.ptr(head.b), _native.ptr(hout), head.nh, N, H, W, _native.stream(x.device),
+    )
+    return hout

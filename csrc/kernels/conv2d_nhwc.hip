@@ -39,7 +39,13 @@
 #define CONV_EXP 0
 #endif
 #ifndef CONV_SCHED_BARRIER
-#define CONV_SCHED_BARRIER 0
+#define CONV_SCHED_BARRIER 1  // per-K-step scheduling fence: deep 3x3 layers 6.03 -> 5.78 ms/step (profiles/r03/conv_deep_ab.md)
+#endif
+// Output-channel-major block order for the one-tile-per-block kernel: the Cout/TCO blocks of one
+// pixel tile are consecutive block ids, so the second..last of them find the tile's halo in L2
+// instead of re-reading it from HBM once per output-channel tile.
+#ifndef CONV_CO_MAJOR
+#define CONV_CO_MAJOR 0
 #endif
 
 namespace {
@@ -481,11 +487,11 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : CONV_KERNEL_WPE) void conv2d_nhwc
   const int lrow = lane & 15;
   const int kq = lane >> 4;
   const int tiles_per_img = a.tiles_x * a.tiles_y;
-  const int tile = blockIdx.x;
+  const int tile = CONV_CO_MAJOR ? blockIdx.y : blockIdx.x;
   const int n = tile / tiles_per_img;
   const int ty0 = ((tile % tiles_per_img) / a.tiles_x) * C::TH;
   const int tx0 = ((tile % tiles_per_img) % a.tiles_x) * TW;
-  const int co0 = blockIdx.y * TCO;
+  const int co0 = (CONV_CO_MAJOR ? blockIdx.x : blockIdx.y) * TCO;
   f32x4 acc[C::NCT][4];
 #pragma unroll
   for (int i = 0; i < C::NCT; ++i)
@@ -524,7 +530,9 @@ int launch(ConvArgs a, hipStream_t s) {
   const int cot = (a.Cout + TCO - 1) / TCO;
   // persistent blocks: ~4 resident workgroups per CU across the cout tiles (256 CUs)
   if constexpr (TCO > 32) {  // non-persistent variant: one block per tile
-    hipLaunchKernelGGL((conv2d_nhwc_kernel<KS, CK, TCO, INMODE, X2, NW>), dim3(tiles, cot), dim3(C::NT), C::LDS, s, a);
+    if (CONV_CO_MAJOR && tiles > 65535) return -13;
+    hipLaunchKernelGGL((conv2d_nhwc_kernel<KS, CK, TCO, INMODE, X2, NW>), CONV_CO_MAJOR ? dim3(cot, tiles) : dim3(tiles, cot),
+                       dim3(C::NT), C::LDS, s, a);
     return BE_CHECK_LAUNCH();
   } else {
   int gx = (256 * 4 * (NW == 4 ? 2 : 1)) / cot;

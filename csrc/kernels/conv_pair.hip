@@ -57,6 +57,13 @@ struct PairArgs {
   const float* bias;                            // [CM] convB bias (+ projection bias)
   const bf16_t* res;                            // [N, H, W, CM] or [N, H/2, W/2, CM] (RES = 2)
   bf16_t* out;                                  // [N, H, W, CM]
+  // HEAD (final up half-block only): the network's output conv fused into the epilogue,
+  //   y = Wh relu(bf16(out) * sH + tH) + bH  -> fp32 NCHW [N, nh, H, W]; `out` is never written
+  const float* sh; const float* th;             // [CM] head pre-activation (eval BN folded)
+  const bf16_t* wh;                             // [16][32] bf16, k order permuted to the accumulator layout
+  const float* bh;                              // [16] head bias (zero padded)
+  float* hout;                                  // [N, nh, H, W]
+  int nh;
   int N, H, W, Hs, Ws, Cin;
   int tiles_x, tiles_y;
 };
@@ -580,7 +587,64 @@ __device__ __forceinline__ void epi_b(const PairArgs& a, TileXY t, const f32x4 (
   }
 }
 
-template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA>
+// HEAD epilogue (CM = 32): out = bf16(acc + bias + res) as the per-layer path would store it, then the
+// output layer's pre-activation and 1x1 conv as ONE 16x16x32 MFMA per 16 pixels straight from the
+// registers: this lane's B fragment is its 8 channels {4kq..4kq+3, 16+4kq..16+4kq+3} of pixel lrow
+// (the host packs Wh's k axis in that order), so the 32-channel map never goes to HBM and the
+// separate head launch (a full re-read of it) disappears.  Lane (lrow, kq) ends with output
+// channels 4kq..4kq+3 of pixel lrow; rows >= nh are zero-weight padding.
+struct HeadRegs {
+  float4 s[2], t[2];
+  bf16x8 w;
+  float4 b;
+};
+
+__device__ __forceinline__ void load_head(const PairArgs& a, int lrow, int kq, HeadRegs& hr) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    hr.s[ct] = *reinterpret_cast<const float4*>(a.sh + ct * 16 + kq * 4);
+    hr.t[ct] = *reinterpret_cast<const float4*>(a.th + ct * 16 + kq * 4);
+  }
+  hr.w = *reinterpret_cast<const bf16x8*>(a.wh + lrow * 32 + kq * 8);
+  hr.b = *reinterpret_cast<const float4*>(a.bh + kq * 4);
+}
+
+template <typename C, bool X2, int RES, bool PF>
+__device__ __forceinline__ void epi_head(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][4],
+                                         const EpiRegs<C, X2, RES, PF>& e, const HeadRegs& hr, int wave, int lrow,
+                                         int kq) {
+  static_assert(C::NCT == 2, "head fusion is for the 32-channel level");
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    u32x4 bw;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      u32x2 rv;
+      if constexpr (PF && RES != 0) rv = e.rv[pt][ct];
+      else rv = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
+      float4 bias;
+      if constexpr (PF) bias = e.bias[ct];
+      else bias = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
+      const uint32_t o0 = pack2bf(acc[ct][pt][0] + bias.x + lo_bf(rv[0]), acc[ct][pt][1] + bias.y + hi_bf(rv[0]));
+      const uint32_t o1 = pack2bf(acc[ct][pt][2] + bias.z + lo_bf(rv[1]), acc[ct][pt][3] + bias.w + hi_bf(rv[1]));
+      bw[2 * ct] = relu_bf16x2(pack2bf(fmaf(lo_bf(o0), hr.s[ct].x, hr.t[ct].x), fmaf(hi_bf(o0), hr.s[ct].y, hr.t[ct].y)));
+      bw[2 * ct + 1] = relu_bf16x2(pack2bf(fmaf(lo_bf(o1), hr.s[ct].z, hr.t[ct].z), fmaf(hi_bf(o1), hr.s[ct].w, hr.t[ct].w)));
+    }
+    const f32x4 y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hr.w, *reinterpret_cast<const bf16x8*>(&bw), zero, 0, 0, 0);
+    const int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+    if (py < a.H && px < a.W) {
+      const float bb[4] = {hr.b.x, hr.b.y, hr.b.z, hr.b.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = kq * 4 + i;
+        if (co < a.nh) a.hout[(((size_t)t.n * a.nh + co) * a.H + py) * a.W + px] = y[i] + bb[i];
+      }
+    }
+  }
+}
+
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false>
 __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -595,6 +659,8 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   if (t0 >= t1) return;
   if constexpr (C::RESW) load_resident<C, PROJ, NCA>(a, tid0, WL);
 
+  HeadRegs hr;
+  if constexpr (HEAD) load_head(a, tid0 & 15, (tid0 & 63) >> 4, hr);
   HaloRegs<C> hraw;
   u32x4 wraw[C::WUPT];
   issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t0), 0, tid0, hraw);
@@ -649,12 +715,16 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
       mma_b<C>(acc_b, R, C::RESW ? WL + NCA * C::WA_ELEMS + cb * C::WB_ELEMS : WL, cb, wave, lrow, kq);
     }
     if constexpr (PROJ) mma_p<C>(acc_b, P, WL + NCA * C::WA_ELEMS + C::NCB * C::WB_ELEMS, wave, lrow, kq);
-    __syncthreads();  // every wave is done reading h before the output staging overlays it
-    epi_b<C, X2, RES, C::PF>(a, cur, acc_b, R, ep, wave, lrow, kq);
+    if constexpr (HEAD) {
+      epi_head<C, X2, RES, C::PF>(a, cur, acc_b, ep, hr, wave, lrow, kq);  // registers only: no LDS staging
+    } else {
+      __syncthreads();  // every wave is done reading h before the output staging overlays it
+      epi_b<C, X2, RES, C::PF>(a, cur, acc_b, R, ep, wave, lrow, kq);
+    }
   }
 }
 
-template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA>
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false>
 int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   a.tiles_x = (a.W + TW - 1) / TW;
@@ -665,11 +735,11 @@ int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
   if (g < 1) return 0;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA>), dim3(g), dim3(NT), C::LDS, s, a);
+  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD>), dim3(g), dim3(NT), C::LDS, s, a);
   return BE_CHECK_LAUNCH();
 }
 
@@ -709,6 +779,7 @@ int be_conv_pair(const void* x, const void* x2, const float* sa, const float* ta
   a.wa = (const bf16_t*)wa; a.wb = (const bf16_t*)wb; a.wp = (const bf16_t*)wp; a.bias = bias;
   a.res = (const bf16_t*)res; a.out = (bf16_t*)out;
   a.N = N; a.H = H; a.W = W; a.Hs = Hs; a.Ws = Ws; a.Cin = Cin;
+  a.sh = a.th = a.bh = nullptr; a.wh = nullptr; a.hout = nullptr; a.nh = 0;
   const bool hx2 = x2 != nullptr;
   if (!sa || !ta || !sb || !tb || !wa || !wb || !bias || !out || !x) return -20;
   if ((resmode != 0) != (res != nullptr)) return -21;
@@ -727,6 +798,24 @@ int be_conv_pair(const void* x, const void* x2, const float* sa, const float* ta
   if (CM == 64 && Cin == 128 && inmode == 1 && hx2 && !proj && resmode == 2)
     return launch_pair<32, 64, 1, true, false, 2, 4>(a, g, stream);
   return -23;
+}
+
+// The final up half-block (32 -> 32 channels, + x1) with the network's output layer fused into its
+// epilogue (see epi_head): writes hout fp32 NCHW [N, nh, H, W] (nh <= 16), never `out`.
+int be_conv_pair_head(const void* x, const float* sa, const float* ta, int ta_ns, const float* sb, const float* tb,
+                      int tb_ns, const void* wa, const void* wb, const float* bias, const void* res, const float* sh,
+                      const float* th, const void* wh, const float* bh, float* hout, int nh, int N, int H, int W,
+                      hipStream_t stream) {
+  if (!x || !sa || !ta || !sb || !tb || !wa || !wb || !bias || !res || !sh || !th || !wh || !bh || !hout) return -20;
+  if (nh < 1 || nh > 16) return -24;
+  PairArgs a;
+  a.x = (const bf16_t*)x; a.x2 = nullptr;
+  a.sa = sa; a.ta = ta; a.ta_ns = ta_ns; a.sb = sb; a.tb = tb; a.tb_ns = tb_ns; a.sp = nullptr; a.tp = nullptr;
+  a.wa = (const bf16_t*)wa; a.wb = (const bf16_t*)wb; a.wp = nullptr; a.bias = bias;
+  a.res = (const bf16_t*)res; a.out = nullptr;
+  a.sh = sh; a.th = th; a.wh = (const bf16_t*)wh; a.bh = bh; a.hout = hout; a.nh = nh;
+  a.N = N; a.H = H; a.W = W; a.Hs = H; a.Ws = W; a.Cin = 32;
+  return launch_pair<32, 32, 0, false, false, 1, 1, true>(a, g_pair_grid, stream);
 }
 
 }  // extern "C"

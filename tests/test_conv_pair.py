@@ -188,3 +188,28 @@ def test_cpnet_engine_pair_path_gpu(gpu, monkeypatch):
     e_pair, e_layer = rel(y, ref), rel(y0, ref)
     assert e_pair < 4e-2 and e_pair < 1.25 * e_layer + 1e-3, (e_pair, e_layer)
     assert (y - ref).abs().max().item() < 8e-2 * ref.abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw", [(48, 64), (30, 44)])
+@pytest.mark.parametrize("nh", [3, 16])
+def test_conv_pair_head_matches_reference(gpu, hw, nh):
+    """Final half-block with the output layer fused into its epilogue (be_conv_pair_head) vs the fp32
+    oracle of the same op (conv_pair_ref -> head_ref), per-image shifts as in the engine."""
+    H, W = hw
+    case = (32, 32, "none", False, False, "full", True, True)
+    spec, raw = _spec(32, 32, "none", False, seed=6)
+    x, _, r, ta, tb_raw = _inputs(case, 3, H, W, seed=7)
+    tb = cp.fold_bias(tb_raw, spec.sb, raw[1])
+    g = torch.Generator().manual_seed(8)
+    head = cp.HeadSpec.build(1 + 0.1 * torch.randn(32, generator=g), 0.1 * torch.randn(32, generator=g),
+                             torch.randn(nh, 32, 1, 1, generator=g) / 32 ** 0.5, 0.1 * torch.randn(nh, generator=g))
+    ref = cp.head_ref(cp.conv_pair_ref(x, spec, ta=ta, tb=tb, res=r, res_mode="full"), head)
+    d = lambda t: None if t is None else t.to(gpu)
+    gspec = cp.PairSpec(pa=spec.pa.to(gpu), pb=spec.pb.to(gpu), sa=d(spec.sa), ta=d(spec.ta), sb=d(spec.sb),
+                        tb=d(spec.tb), bias=d(spec.bias), inmode="none")
+    ghead = cp.HeadSpec(s=d(head.s), t=d(head.t), w=d(head.w), b=d(head.b), nh=nh, wh=d(head.wh))
+    out = cp.conv_pair_head(d(x), gspec, ghead, ta=d(ta), tb=d(tb), res=d(r)).cpu()
+    assert out.shape == (3, nh, H, W) and torch.isfinite(out).all()
+    err = (out - ref).abs().max().item()
+    assert err < 1.5e-2 * max(1.0, ref.abs().max().item()), err
