@@ -308,6 +308,14 @@ class CellposeRunner:
             m.record_stream(main)
         return torch.cat(masks), torch.cat(ys), torch.cat(styles)
 
+    def stream(self, p: EvalParams | None = None) -> "_EvalStream":
+        """Cross-batch pipeline for a stream of batches (continuous serving / offline throughput):
+        ``submit(images)`` queues batch i's network on the current stream, then runs mask recovery of
+        batch i-1 on a second HIP stream (so its latency-bound kernels and host syncs overlap batch
+        i's convs) and returns batch i-1's ``(masks, flows, styles)`` (None for the first batch);
+        ``flush()`` returns the last batch's.  Same per-batch results as :meth:`eval`."""
+        return _EvalStream(self, p or EvalParams())
+
     def _normalize(self, x):
         if self.device.type == "cuda":
             from .gpu import normalize99
@@ -391,3 +399,47 @@ def synthetic_cells(B: int, H: int = 512, W: int = 512, nchan: int = 2, ncells: 
     out += 0.05 * rng.standard_normal(out.shape).astype(np.float32)
     out = np.clip(out, 0, None)
     return (out / out.max() * 4000).astype(np.uint16)
+
+
+class _EvalStream:
+    """See :meth:`CellposeRunner.stream` (GPU only; a CPU runner evaluates each batch directly)."""
+
+    def __init__(self, runner: CellposeRunner, p: EvalParams):
+        self.r, self.p = runner, p
+        self.pending = None
+        self.cuda = runner.device.type == "cuda" and p.compute_masks
+        if self.cuda:
+            if getattr(runner, "_mask_stream", None) is None:
+                runner._mask_stream = torch.cuda.Stream(runner.device)
+            self.side = runner._mask_stream
+
+    @torch.no_grad()
+    def submit(self, images):
+        if not self.cuda:
+            return self.r.eval(images, self.p)
+        x = as_batch(images, self.r.nchan, self.r.device)  # device tensors only: no shared pinned staging
+        y, style, rescale = self.r._net_stage(x, self.p)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.r.device))
+        prev, self.pending = self.pending, (y, style, rescale, ev)
+        return self._finish(prev) if prev is not None else None
+
+    def _finish(self, item):
+        y, style, rescale, ev = item
+        main = torch.cuda.current_stream(self.r.device)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(ev)
+            y.record_stream(self.side)
+            with trace.span("cellpose.masks", cuda=True, images=y.shape[0]):
+                m = self.r.compute_masks(y, self.p, rescale)
+        done = torch.cuda.Event()
+        done.record(self.side)
+        main.wait_event(done)  # consumers on the main stream see finished masks
+        m.record_stream(main)
+        return m, y, style
+
+    def flush(self):
+        if self.pending is None:
+            return None
+        prev, self.pending = self.pending, None
+        return self._finish(prev)

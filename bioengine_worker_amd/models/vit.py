@@ -230,8 +230,10 @@ class ViTEngine:
 
     def _blocks_fp8(self, t: torch.Tensor, B: int, N: int) -> torch.Tensor:
         """fp8 encoder blocks: LayerNorms emit e4m3 + per-token scales straight into the qkv / fc1
-        GEMMs; the attention output is re-quantised per token for proj, and fc1's output goes through
-        GELU + per-token quantisation in one pass for fc2."""
+        GEMMs; the attention output is re-quantised per token for proj.  fc1 -> fc2: with the HIP GEMM
+        the GELU and an MX-fp8 quantisation (E8M0 scale per 32 outputs) run in fc1's epilogue and the
+        block scales go into fc2's MFMA scale operand; with hipBLASLt, GELU + per-token quantisation
+        run as one pass between the two library GEMMs."""
         cfg, blocks = self.cfg, self.blocks
         D, Hh = cfg.embed_dim, cfg.num_heads
         hq = add_layernorm_fp8(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"], cfg.eps)
@@ -240,7 +242,10 @@ class ViTEngine:
             a = flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]).view(B, N, D)
             y = b["proj_q"](a)
             h2q = add_layernorm_fp8(t, y, b["g1"], b["n2w"], b["n2b"], cfg.eps)
-            m = b["fc2_q"](quantize_rows(b["fc1_q"](h2q), gelu=True))
+            if b["fc1_q"].gemm == "hip":  # GELU + MX-fp8 in fc1's epilogue, block scales into fc2's MFMA
+                m = b["fc2_q"](b["fc1_q"](h2q, mx_out=True))
+            else:
+                m = b["fc2_q"](quantize_rows(b["fc1_q"](h2q), gelu=True))
             if i + 1 < len(blocks):
                 hq = add_layernorm_fp8(t, m, b["g2"], blocks[i + 1]["n1w"], blocks[i + 1]["n1b"], cfg.eps)
         return add_layernorm(t, m, blocks[-1]["g2"], self.nw, self.nb, cfg.eps)

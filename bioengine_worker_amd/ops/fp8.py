@@ -95,6 +95,73 @@ def linear_fp8(xq: torch.Tensor, sx: torch.Tensor, wq: torch.Tensor, sw: torch.T
     return y
 
 
+MX_BLOCK = 32
+
+
+def mx_quantize_ref(x: torch.Tensor, gelu: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
+    """[..., K] -> MX-fp8 (e4m3fn [..., K], E8M0 uint8 [..., K/32]): one power-of-two scale 2^e per 32
+    consecutive elements of a row, the smallest with amax / 2^e <= 448 (byte = e + 127).  ``gelu``:
+    quantise the exact GELU of x (fp32) -- what the fused fc1 epilogue does."""
+    xf = x.float()
+    if gelu:
+        xf = F.gelu(xf)
+    K = xf.shape[-1]
+    assert K % MX_BLOCK == 0
+    blk = xf.reshape(*xf.shape[:-1], K // MX_BLOCK, MX_BLOCK)
+    amax = blk.abs().amax(-1)
+    e = torch.where(amax > 0, torch.ceil(torch.log2(amax / FP8_MAX)), torch.full_like(amax, -127.0))
+    e = torch.where((amax > 0) & (amax * torch.exp2(-e) > FP8_MAX), e + 1, e).clamp(-127, 127)
+    q = (blk * torch.exp2(-e)[..., None]).clamp(-FP8_MAX, FP8_MAX).to(FP8_DTYPE).reshape(xf.shape)
+    return q, (e + 127).to(torch.uint8)
+
+
+def mx_dequant_ref(q: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    K = q.shape[-1]
+    blk = q.float().reshape(*q.shape[:-1], K // MX_BLOCK, MX_BLOCK)
+    return (blk * torch.exp2(s.float() - 127.0)[..., None]).reshape(q.shape)
+
+
+def linear_fp8_mx(x: tuple, wq: torch.Tensor, sw: torch.Tensor, bias: torch.Tensor | None = None,
+                  gelu: bool = False, mx_out: bool = False):
+    """fp8 GEMM whose input ``x = (xq, scales)`` carries either per-row fp32 scales ``[M]`` or MX block
+    scales (uint8 E8M0 ``[M, K/32]``, applied inside ``v_mfma_scale_f32_16x16x128_f8f6f4``).
+    ``mx_out`` (requires ``gelu``): the epilogue applies GELU and writes MX-fp8 ``(yq, ys)`` for the
+    next GEMM instead of bf16 -- fc1 -> fc2 of a ViT MLP with no bf16 activation and no quantisation
+    pass in between (``be_gemm_fp8_mx``)."""
+    xq, xs = x
+    mx_in = xs.dtype == torch.uint8
+    assert not mx_out or gelu, "MX output is the fused GELU epilogue"
+    if not xq.is_cuda:
+        xf = mx_dequant_ref(xq, xs) if mx_in else xq.float() * xs.float()[..., None]
+        y = torch.matmul(xf, wq.float().t()) * sw.float()
+        if bias is not None:
+            y = y + bias.float()
+        if mx_out:
+            return mx_quantize_ref(y, gelu=True)
+        return (F.gelu(y) if gelu else y).to(torch.bfloat16)
+    K = xq.shape[-1]
+    N = wq.shape[0]
+    M = xq.numel() // K
+    assert xq.dtype == FP8_DTYPE and wq.dtype == FP8_DTYPE and wq.shape[1] == K and xq.is_contiguous()
+    assert K % 128 == 0 and N % (MX_BLOCK if mx_out else 4) == 0
+    if mx_in:
+        assert xs.shape[-1] == K // MX_BLOCK and xs.numel() == M * (K // MX_BLOCK) and xs.is_contiguous()
+    else:
+        assert xs.numel() == M
+    b = bias.float().contiguous() if bias is not None else None
+    y = yq = ys = None
+    if mx_out:
+        yq = torch.empty(*xq.shape[:-1], N, dtype=FP8_DTYPE, device=xq.device)
+        ys = torch.empty(*xq.shape[:-1], N // MX_BLOCK, dtype=torch.uint8, device=xq.device)
+    else:
+        y = torch.empty(*xq.shape[:-1], N, dtype=torch.bfloat16, device=xq.device)
+    _native.call("be_gemm_fp8_mx", _native.ptr(xq), None if mx_in else _native.ptr(xs.float().contiguous()),
+                 _native.ptr(xs) if mx_in else None, _native.ptr(wq), _native.ptr(sw.float().contiguous()),
+                 _native.ptr(b), _native.ptr(y), _native.ptr(yq), _native.ptr(ys), M, N, K,
+                 2 if mx_out else int(bool(gelu)), _native.stream(xq.device))
+    return (yq, ys) if mx_out else y
+
+
 def add_layernorm_fp8(x: torch.Tensor, y: torch.Tensor | None, gamma: torch.Tensor | None, w: torch.Tensor,
                       b: torch.Tensor, eps: float = 1e-6) -> tuple[torch.Tensor, torch.Tensor]:
     """``x <- x + gamma * y`` (in place) and returns ``quantize_rows(LN(x) * w + b)`` — the fused
@@ -149,8 +216,15 @@ class Fp8Linear:
             self.bias = self.bias.to(device)
         return self
 
-    def __call__(self, x, gelu: bool = False) -> torch.Tensor:
-        """x: bf16 activations, or an already-quantised ``(xq, sx)`` pair (``add_layernorm_fp8``)."""
+    def __call__(self, x, gelu: bool = False, mx_out: bool = False):
+        """x: bf16 activations, or an already-quantised ``(xq, sx)`` pair (``add_layernorm_fp8``), or
+        an MX pair ``(xq, uint8 block scales)`` (``mx_out`` of the previous layer; HIP GEMM only).
+        ``mx_out``: GELU + MX-fp8 output ``(yq, ys)`` straight from the epilogue (HIP GEMM only)."""
+        if mx_out or (isinstance(x, tuple) and x[1].dtype == torch.uint8):
+            if self.gemm != "hip" and x[0].is_cuda:
+                raise ValueError("MX-fp8 activations need Fp8Linear(gemm='hip')")
+            return linear_fp8_mx(x if isinstance(x, tuple) else quantize_rows(x), self.wq, self.sw, self.bias,
+                                 gelu=gelu or mx_out, mx_out=mx_out)
         xq, sx = x if isinstance(x, tuple) else quantize_rows(x)
         if xq.is_cuda and self.gemm == "hipblaslt":
             y = linear_fp8_hipblaslt(xq, sx, self.wq, self.sw, self.bias)

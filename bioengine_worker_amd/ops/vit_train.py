@@ -18,14 +18,19 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import _native
 
 
-def _rpb(rows: int, target_blocks: int = 512) -> int:
-    return max(4, -(-rows // target_blocks))
+_ROWCOL_BLOCKS = int(os.environ.get("BE_ROWCOL_BLOCKS", "512"))
+
+
+def _rpb(rows: int, target_blocks: int | None = None) -> int:
+    return max(4, -(-rows // (target_blocks or _ROWCOL_BLOCKS)))
 
 
 def _colsum(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -63,14 +63,21 @@ __device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ g, long l
   }
 }
 
-// Fragment of a 16x128 (rows x k-bytes) slab for v_mfma_scale_f32_16x16x128_f8f6f4:
-// lane l holds row (l & 15), k-bytes [32*(l>>4), +32) as two swizzled 16-byte chunks.
+// Fragment of a 16x128 (rows x k-bytes) slab for v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds row
+// (l & 15) as two swizzled 16-byte chunks.  FP8_KLAYOUT 0: k-bytes [32 (l>>4), +32); 1: [16 (l>>4), +16)
+// and [64 + 16 (l>>4), +16).  Any layout shared by A and B gives the same plain GEMM; with block
+// scales the instruction's own K order decides which elements a 32-block scale covers
+// (tools/mx_scale_probe.py).
+#ifndef FP8_KLAYOUT
+#define FP8_KLAYOUT 1  // the instruction's own K order: a 32-block scale covers memory K [32b, 32b+32) (mx_scale_probe)
+#endif
 __device__ __forceinline__ i32x8 read_frag(const uint8_t* lds_tile, int row, int lane) {
-  const int c0 = 2 * (lane >> 4);
+  const int c0 = FP8_KLAYOUT ? (lane >> 4) : 2 * (lane >> 4);
+  const int c1 = FP8_KLAYOUT ? c0 + 4 : c0 + 1;
   const int sw = frag_swz(row);
   const uint8_t* base = lds_tile + row * 128;
   const u32x4 lo = *reinterpret_cast<const u32x4*>(base + ((c0 ^ sw) << 4));
-  const u32x4 hi = *reinterpret_cast<const u32x4*>(base + (((c0 + 1) ^ sw) << 4));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(base + ((c1 ^ sw) << 4));
   i32x8 f;
   f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
   f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
@@ -95,11 +102,17 @@ __device__ __forceinline__ float gelu_erf(float x) {
 
 // Block tile BM x BN = (WAVES_M * 16 * TM) x (WAVES_N * 16 * TN); each wave owns TM x TN MFMA tiles.
 // PRIO: s_setprio(1) around the MFMA cluster (cdna_hip_programming.md T5).
-template <int TM, int TN, int WAVES_M, int WAVES_N, int EPI, bool PRIO = false>  // EPI 0: scale + bias, 1: + GELU(erf)
+// EPI 0: scale + bias -> bf16, 1: + GELU(erf) -> bf16, 2: + GELU -> MX-fp8 (e4m3 + one E8M0 scale per
+// 32 consecutive outputs of a row, written to Yq / Ys): the next GEMM consumes it with XS = true.
+// XS: X carries E8M0 block scales (one per row and 32-element K block, Xs [M, K/32]) that go into the
+// MFMA's scale operand (scale_b: the lane's row / K block is exactly its fragment's 32 bytes), instead
+// of a per-row fp32 scale in the epilogue.
+template <int TM, int TN, int WAVES_M, int WAVES_N, int EPI, bool PRIO = false, bool XS = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ W, const float* __restrict__ sx,
     const float* __restrict__ sw, const float* __restrict__ bias, bf16_t* __restrict__ Y, int M, int N, int K,
-    int tiles_n) {
+    int tiles_n, const uint8_t* __restrict__ Xs = nullptr, uint8_t* __restrict__ Yq = nullptr,
+    uint8_t* __restrict__ Ys = nullptr) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int BM = WAVES_M * 16 * TM, BN = WAVES_N * 16 * TN;
   constexpr int XB = BM * BK, BUF = (BM + BN) * BK;
@@ -118,6 +131,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
     for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
+  const int kb32 = K / 32;
+  int xsc[XS ? TM : 1], xsn[XS ? TM : 1];  // this lane's X block scales (current / next K step)
+  auto load_xs = [&](int kt, int (&dst)[XS ? TM : 1]) {
+    if constexpr (XS) {
+#pragma unroll
+      for (int b = 0; b < TM; ++b) {
+        const int m = min(m0 + wm + b * 16 + (lane & 15), M - 1);
+        dst[b] = Xs[(long long)m * kb32 + kt * 4 + (lane >> 4)];
+      }
+    }
+  };
+  load_xs(0, xsc);
   stage_tile<BM, NW>(X, K, m0, M, 0, smem, wave, lane);
   stage_tile<BN, NW>(W, K, n0, N, 0, smem + XB, wave, lane);
   for (int kt = 0; kt < nk; ++kt) {
@@ -126,7 +151,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
       uint8_t* nxt = smem + ((kt + 1) & 1) * BUF;
       stage_tile<BM, NW>(X, K, m0, M, (kt + 1) * BK, nxt, wave, lane);
       stage_tile<BN, NW>(W, K, n0, N, (kt + 1) * BK, nxt + XB, wave, lane);
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(LOADS));  // tile kt landed; tile kt+1 stays in flight
+      if constexpr (XS) {
+        load_xs(kt + 1, xsn);  // issued after the DMA: the counted wait below then also covers it
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(LOADS + TM));
+      } else {
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(LOADS));  // tile kt landed; tile kt+1 stays in flight
+      }
     } else {
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
     }
@@ -143,11 +173,65 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
 #pragma unroll
       for (int b = 0; b < TM; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(aw, bx[b], acc[a][b], 0, 0, 0, E8M0_ONE, 0,
-                                                                     E8M0_ONE);
+                                                                     XS ? xsc[b] : E8M0_ONE);
     }
     if (PRIO) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // WAR: the next iteration restages the buffer read here
+    if constexpr (XS) {
+#pragma unroll
+      for (int b = 0; b < TM; ++b) xsc[b] = xsn[b];
+    }
+  }
+  if constexpr (EPI == 2) {
+    // GELU -> MX-fp8: a 32-output block of row m is tiles a, a+1 (16 columns each) x the 4 lane
+    // groups sharing lane & 15 x 4 values; amax over it = lane-local max of 8 + two xor shuffles.
+    static_assert(TN % 2 == 0, "MX blocks pair 16-column tiles");
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+      const int m = m0 + wm + b * 16 + (lane & 15);
+      const float s_m = XS ? 1.f : sx[min(m, M - 1)];
+#pragma unroll
+      for (int a = 0; a < TN; a += 2) {
+        float v[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int n = min(n0 + wn + (a + h) * 16 + 4 * (lane >> 4), N - 4);
+          const float4 swv = *reinterpret_cast<const float4*>(sw + n);
+          float4 bv = {0.f, 0.f, 0.f, 0.f};
+          if (bias) bv = *reinterpret_cast<const float4*>(bias + n);
+          v[h][0] = gelu_erf(acc[a + h][b][0] * s_m * swv.x + bv.x);
+          v[h][1] = gelu_erf(acc[a + h][b][1] * s_m * swv.y + bv.y);
+          v[h][2] = gelu_erf(acc[a + h][b][2] * s_m * swv.z + bv.z);
+          v[h][3] = gelu_erf(acc[a + h][b][3] * s_m * swv.w + bv.w);
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(v[h][i]));
+        amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        // smallest power of two 2^e with amax / 2^e <= 448 (E8M0 byte e + 127)
+        int e = amax > 0.f ? (int)ceilf(__log2f(amax * (1.f / 448.f))) : -127;
+        if (e > 0 && amax * __builtin_ldexpf(1.f, -e) > 448.f) ++e;  // log2 rounding guard
+        e = max(-127, min(127, e));
+        const float inv = __builtin_ldexpf(1.f, -e);
+        const int nb = n0 + wn + a * 16;  // first column of the 32-block
+        if (m < M && nb < N) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[h][0] * inv, -448.f), 448.f),
+                                                    fminf(fmaxf(v[h][1] * inv, -448.f), 448.f), 0, false);
+            w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[h][2] * inv, -448.f), 448.f),
+                                                fminf(fmaxf(v[h][3] * inv, -448.f), 448.f), w, true);
+            *reinterpret_cast<uint32_t*>(Yq + (long long)m * N + nb + h * 16 + 4 * (lane >> 4)) = (uint32_t)w;
+          }
+          if ((lane >> 4) == 0) Ys[(long long)m * (N / 32) + nb / 32] = (uint8_t)(e + 127);
+        }
+      }
+    }
+    return;
   }
 
   // epilogue: acc[a][b][i] = C[m = wm + 16b + (lane&15)][n = wn + 16a + 4(lane>>4) + i]
@@ -155,7 +239,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
   for (int b = 0; b < TM; ++b) {
     const int m = m0 + wm + b * 16 + (lane & 15);
     if (m >= M) continue;
-    const float s_m = sx[m];
+    const float s_m = XS ? 1.f : sx[m];
 #pragma unroll
     for (int a = 0; a < TN; ++a) {
       const int n = n0 + wn + a * 16 + 4 * (lane >> 4);
@@ -267,6 +351,42 @@ int be_gemm_fp8(const void* xq, const void* wq, const float* sx, const float* sw
     case 6: return launch_gemm<2, 4, 4, 2, true>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     default: return -2;
   }
+}
+
+// MX-fp8 variants of be_gemm_fp8 (tile by shape as cfg 0 picks it, 4 or 6):
+//   xs != null: X carries E8M0 block scales xs [M, K/32] (sx unused); else per-row fp32 sx.
+//   epi 0 / 1: y bf16 [M, N] (GELU for 1);  epi 2: GELU -> yq e4m3 [M, N] + ys E8M0 [M, N/32] (N % 32 == 0).
+int be_gemm_fp8_mx(const void* xq, const float* sx, const void* xs, const void* wq, const float* sw,
+                   const float* bias, void* y, void* yq, void* ys, int M, int N, int K, int epi, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 4 != 0) return -1;
+  if (epi == 2 && (N % 32 != 0 || !yq || !ys)) return -3;
+  if (epi != 2 && !y) return -3;
+  if (!xs && !sx) return -4;
+  const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  const bool big = K >= 2048 && t256 >= 256;
+  const uint8_t* X = (const uint8_t*)xq;
+  const uint8_t* Wt = (const uint8_t*)wq;
+  const uint8_t* Xs = (const uint8_t*)xs;
+  bf16_t* Y = (bf16_t*)y;
+  uint8_t* Yq = (uint8_t*)yq;
+  uint8_t* Ys = (uint8_t*)ys;
+#define MXL(TM, TN, WM, WN, PR, EP, XSV)                                                                     \
+  {                                                                                                          \
+    constexpr int BM = WM * 16 * TM, BN = WN * 16 * TN;                                                      \
+    const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;                                      \
+    hipLaunchKernelGGL((gemm_fp8_kernel<TM, TN, WM, WN, EP, PR, XSV>), dim3((unsigned)(tiles_m * tiles_n)),   \
+                       dim3(64 * WM * WN), 0, s, X, Wt, sx, sw, bias, Y, M, N, K, tiles_n, Xs, Yq, Ys);      \
+  }
+#define MXE(TM, TN, WM, WN, PR, XSV) \
+  if (epi == 2) MXL(TM, TN, WM, WN, PR, 2, XSV) else if (epi == 1) MXL(TM, TN, WM, WN, PR, 1, XSV) else MXL(TM, TN, WM, WN, PR, 0, XSV)
+  if (xs) {  // block-scaled X: 128x128 tiles only (the 256x256 tile's scale registers spill)
+    MXE(2, 4, 4, 2, true, true)
+  } else {
+    if (big) MXE(8, 4, 2, 4, false, false) else MXE(2, 4, 4, 2, true, false)
+  }
+#undef MXE
+#undef MXL
+  return BE_CHECK_LAUNCH();
 }
 
 // x bf16 [rows, K] -> q e4m3fn [rows, K] + scale float [rows]; K % 8 == 0, K <= 4096.

@@ -132,9 +132,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   if (pcol) flush(ac, pcol);
 }
 
-__device__ __forceinline__ float gelu_f(float t) { return 0.5f * t * (1.f + erff(t * 0.70710678118654752f)); }
+// erf(x) by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16 outputs' 2^-9 step):
+// one v_rcp, one v_exp and a few FMAs, branch-free, where the library erff takes range branches that
+// diverge inside a wave (these passes stream [tokens, 4 * dim] activations and were VALU-heavy).
+// e = exp(-x^2) is returned too: the GELU derivative reuses it.
+__device__ __forceinline__ float erf_as(float x, float& e) {
+  const float z = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  e = __expf(-z * z);
+  return copysignf(1.f - p * e, x);
+}
+__device__ __forceinline__ float gelu_f(float t) {
+  float e;
+  return 0.5f * t * (1.f + erf_as(t * 0.70710678118654752f, e));
+}
 __device__ __forceinline__ float gelu_d(float t) {
-  return 0.5f * (1.f + erff(t * 0.70710678118654752f)) + t * 0.3989422804014327f * __expf(-0.5f * t * t);
+  float e;  // exp(-t^2 / 2) from the erf evaluation
+  const float er = erf_as(t * 0.70710678118654752f, e);
+  return 0.5f * (1.f + er) + t * 0.3989422804014327f * e;
 }
 
 // elementwise kernels with column partials: a block owns `rpb` rows and all columns; thread t owns

@@ -143,3 +143,48 @@ def test_vit_engine_fp8_gpu_embedding_close(gpu):
     out = ViTEngine(net, gpu, precision="fp8").embed(x.to(gpu))
     cos = torch.nn.functional.cosine_similarity(out, ref, dim=1)
     assert cos.min() > 0.99, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(16448, 3072, 768), (300, 768, 3072), (129, 256, 256)])
+def test_gemm_fp8_mx_epilogue_and_block_scaled_input(gpu, M, N, K):
+    """fc1 -> fc2 with MX-fp8 in between (be_gemm_fp8_mx): the GELU + E8M0-block quantisation epilogue
+    vs the PyTorch reference of the same math, then the block-scaled-input GEMM vs its reference on the
+    SAME quantised operands (scales into the MFMA scale operand)."""
+    from bioengine_worker_amd.ops.fp8 import linear_fp8_mx, mx_dequant_ref, mx_quantize_ref
+
+    g = torch.Generator().manual_seed(M + N)
+    x = (torch.randn(M, K, generator=g) + torch.arange(K) / K).bfloat16()
+    w1 = torch.randn(N, K, generator=g) * K ** -0.5 + torch.arange(N)[:, None] / (10 * N)
+    w2 = torch.randn(K, N, generator=g) * N ** -0.5
+    l1, l2 = Fp8Linear(w1, torch.randn(N, generator=g) * 0.1), Fp8Linear(w2, torch.randn(K, generator=g) * 0.1)
+    xq, sx = quantize_rows_ref(x)
+    pre = (xq.float() * sx[:, None]) @ l1.wq.float().t() * l1.sw + l1.bias
+    l1.to(gpu)
+    l2.to(gpu)
+    yq, ys = linear_fp8_mx((xq.to(gpu), sx.to(gpu)), l1.wq, l1.sw, l1.bias, gelu=True, mx_out=True)
+    yq, ys = yq.cpu(), ys.cpu()
+    assert ys.dtype == torch.uint8 and ys.shape == (M, N // 32)
+    qr, sr = mx_quantize_ref(pre, gelu=True)
+    # scales: identical except where a block's amax sits on a power-of-two boundary (fp32 order)
+    assert (ys.int() - sr.int()).abs().max() <= 1 and (ys != sr).float().mean() < 1e-3
+    deq, deq_r = mx_dequant_ref(yq, ys), mx_dequant_ref(qr, sr)
+    ref1 = torch.nn.functional.gelu(pre)
+    assert ((deq - ref1).norm() / ref1.norm()).item() < 0.05
+    assert ((deq - deq_r).norm() / deq_r.norm()).item() < 0.02
+    # block-scaled input GEMM on the kernel's own MX output
+    y2 = linear_fp8_mx((yq.to(gpu), ys.to(gpu)), l2.wq, l2.sw, l2.bias).float().cpu()
+    ref2 = deq @ l2.wq.cpu().float().t() * l2.sw.cpu() + l2.bias.cpu()
+    err = (y2 - ref2).abs().max().item()
+    assert err <= 1e-2 * ref2.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.gpu
+def test_vit_engine_fp8_hip_mx_embedding_close(gpu):
+    """The HIP fp8 path (MX-fp8 between fc1 and fc2) against the bf16 engine, end to end."""
+    net = ViT(ViTConfig.dinov2("vitb14")).randomize_(0).eval()
+    x = torch.randn(4, 3, 224, 224)
+    ref = ViTEngine(net, gpu).embed(x.to(gpu))
+    out = ViTEngine(net, gpu, precision="fp8", fp8_gemm="hip").embed(x.to(gpu))
+    cos = torch.nn.functional.cosine_similarity(out, ref, dim=1)
+    assert cos.min() > 0.99, cos

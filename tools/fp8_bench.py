@@ -77,6 +77,7 @@ def main():
         embs[prec] = eng.embed(x)
         del eng
     out["fp8_vs_bf16_cos_min"] = round(F.cosine_similarity(embs["fp8"], embs["bf16"], dim=1).min().item(), 5)
+    out["fp8hip_vs_bf16_cos_min"] = round(F.cosine_similarity(embs["fp8hip"], embs["bf16"], dim=1).min().item(), 5)
     out["reference_a100_fp16_imgs_per_s"] = 500.0
     print(json.dumps(out), flush=True)
 
