@@ -182,6 +182,7 @@ class CellposeFinetune:
         self._lock = asyncio.Lock()
         self._weights: dict[str, str] = {}
         self._gpu_lock = threading.Lock()
+        self._mask_lock = threading.Lock()  # mask recovery of one batch overlaps the next batch's network
 
     # ------------------------------------------------------------------ models
     def _device(self):
@@ -280,19 +281,21 @@ class CellposeFinetune:
 
                 with trace.span("app.stack", images=len(idxs)):
                     batch = self._stage_batch([reqs[i][1] for i in idxs], runner)
-                with self._gpu_lock:
-                    if torch.is_tensor(batch) and batch.is_cuda:  # H2D issued on the copy stream
-                        torch.cuda.current_stream(batch.device).wait_stream(self._h2d_stream)
-                        batch.record_stream(torch.cuda.current_stream(batch.device))
-                    with trace.span("app.eval", images=len(idxs)):
-                        m, f, _ = runner.eval(batch, **prm)
-                    if m.is_cuda:
-                        # uint16 masks (cellpose's dtype when labels fit): low 16 bits + an overflow
-                        # flag, so the copy-back needs a single host sync
-                        m16 = m.to(torch.int16)
-                        over = (m > 65535).any().reshape(1)
-                        ev = torch.cuda.Event()
-                        ev.record()
+                if torch.is_tensor(batch) and batch.is_cuda:  # H2D issued on the copy stream
+                    torch.cuda.current_stream(batch.device).wait_stream(self._h2d_stream)
+                    batch.record_stream(torch.cuda.current_stream(batch.device))
+                with trace.span("app.eval", images=len(idxs)):
+                    if hasattr(runner, "eval_locked"):
+                        # network under the GPU lock, mask recovery under its own lock on a second
+                        # stream: the other in-flight batch's network overlaps this batch's masks
+                        m, f, _, ev = runner.eval_locked(batch, self._gpu_lock, self._mask_lock, **prm)
+                    else:
+                        with self._gpu_lock:
+                            m, f, _ = runner.eval(batch, **prm)
+                            ev = None
+                            if m.is_cuda:
+                                ev = torch.cuda.Event()
+                                ev.record()
                 with trace.span("app.d2h", images=len(idxs)):
                     if not m.is_cuda:
                         return m.numpy(), (f.numpy() if flows_needed else None)
@@ -301,6 +304,10 @@ class CellposeFinetune:
                     st = self._d2h_stream
                     with torch.cuda.stream(st):
                         st.wait_event(ev)
+                        # uint16 masks (cellpose's dtype when labels fit): low 16 bits + an overflow
+                        # flag, so the copy-back needs a single host sync
+                        m16 = m.to(torch.int16)
+                        over = (m > 65535).any().reshape(1)
                         mh = torch.empty(m.shape, dtype=torch.int16, pin_memory=True)
                         oh = torch.empty(1, dtype=torch.bool, pin_memory=True)
                         mh.copy_(m16, non_blocking=True)

@@ -308,6 +308,46 @@ class CellposeRunner:
             m.record_stream(main)
         return torch.cat(masks), torch.cat(ys), torch.cat(styles)
 
+    @torch.no_grad()
+    def eval_locked(self, images, net_lock, mask_lock, p: EvalParams | None = None, **kw):
+        """:meth:`eval` for concurrent callers (serving threads): the network stage runs under
+        ``net_lock`` on the caller's stream, mask recovery under ``mask_lock`` on the runner's second
+        stream -- so one batch's mask recovery overlaps the next batch's network (the cross-batch
+        overlap of :meth:`stream`, for batches that arrive on different threads).  Returns
+        ``(masks, flows, styles, ready)``: ``ready`` is a HIP event recorded after the masks (None
+        off the GPU path) -- wait on it on a copy stream rather than on the caller's stream, which may
+        already hold the next batch's network."""
+        p = p or EvalParams()
+        for k, v in kw.items():
+            setattr(p, k, v)
+        if self.device.type != "cuda" or not p.compute_masks:
+            with net_lock:
+                m, y, st = self.eval(images, p)
+                ev = None
+                if self.device.type == "cuda":
+                    ev = torch.cuda.Event()
+                    ev.record()
+                return m, y, st, ev
+        with net_lock:
+            # no shared pinned staging buffer here: the previous batch's H2D may still be reading it
+            x = as_batch(images, self.nchan, self.device)
+            y, style, rescale = self._net_stage(x, p)
+            main = torch.cuda.current_stream(self.device)
+            ev = torch.cuda.Event()
+            ev.record(main)
+        with mask_lock:
+            if getattr(self, "_mask_stream", None) is None:
+                self._mask_stream = torch.cuda.Stream(self.device)
+            side = self._mask_stream
+            with torch.cuda.stream(side):
+                side.wait_event(ev)
+                y.record_stream(side)
+                with trace.span("cellpose.masks", cuda=True, images=y.shape[0]):
+                    m = self.compute_masks(y, p, rescale)
+            done = torch.cuda.Event()
+            done.record(side)
+        return m, y, style, done
+
     def stream(self, p: EvalParams | None = None) -> "_EvalStream":
         """Cross-batch pipeline for a stream of batches (continuous serving / offline throughput):
         ``submit(images)`` queues batch i's network on the current stream, then runs mask recovery of

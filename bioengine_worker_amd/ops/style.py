@@ -25,11 +25,11 @@ def nhwc_channel_sum(x: torch.Tensor, square: bool = False) -> torch.Tensor:
         xf = x.float().reshape(N, HW, C)
         return (xf * xf if square else xf).sum(1)
     assert x.dtype == torch.bfloat16 and x.is_contiguous()
-    out = torch.zeros(N, C, device=x.device, dtype=torch.float32)
     split = max(1, min(64, HW // 256))
-    _native.call("be_nhwc_channel_sum", _native.ptr(x), _native.ptr(out), N, HW, C, split, int(square),
+    part = torch.empty(N, split, C, device=x.device, dtype=torch.float32)
+    _native.call("be_nhwc_channel_sum", _native.ptr(x), _native.ptr(part), N, HW, C, split, int(square),
                  _native.stream(x.device))
-    return out
+    return part.sum(1) if split > 1 else part.view(N, C)  # fixed-order reduction: run-to-run identical
 
 
 def make_style(x: torch.Tensor) -> torch.Tensor:

@@ -44,6 +44,9 @@
 // Output-channel-major block order for the one-tile-per-block kernel: the Cout/TCO blocks of one
 // pixel tile are consecutive block ids, so the second..last of them find the tile's halo in L2
 // instead of re-reading it from HBM once per output-channel tile.
+#ifndef CONV_RES_PREFETCH
+#define CONV_RES_PREFETCH 0  // 1: +32 VGPRs on a kernel already at the 256 cap -> 131 spills (not used)
+#endif
 #ifndef CONV_CO_MAJOR
 #define CONV_CO_MAJOR 0
 #endif
@@ -279,9 +282,27 @@ __device__ __forceinline__ int stage_off(int p, int co) {
 }
 
 template <typename C>
+__device__ __forceinline__ void load_res_regs(const ConvArgs& a, int n, int ty0, int tx0, int co0, int wave, int lrow,
+                                              int kq, u32x2 (&rv)[4][C::NCT]) {
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int py = ty0 + 2 * wave + (pt >> 1);
+    const int px = tx0 + (pt & 1) * 16 + lrow;
+    const bool ok = a.res && py < a.H && px < a.W;
+    const size_t pix = ((size_t)n * a.H + py) * a.W + px;
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct) {
+      const int co = co0 + ct * 16 + kq * 4;
+      rv[pt][ct] = (ok && co < a.Cout) ? *reinterpret_cast<const u32x2*>(a.res + pix * a.Cout + co) : (u32x2){0u, 0u};
+    }
+  }
+}
+
+// rvp: residual registers loaded earlier (load_res_regs), or null to load them here
+template <typename C>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT][4], const float4 (&bias)[C::NCT],
                                          int n, int ty0, int tx0, int co0, int wave, int lrow, int kq,
-                                         bf16_t* stage) {
+                                         bf16_t* stage, const u32x2 (*rvp)[C::NCT] = nullptr) {
   if (a.out_f32_nchw) {
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
@@ -305,19 +326,13 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
     return;
   }
   u32x2 rv[4][C::NCT];
-  if (a.res) {
+  if (rvp) {
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt) {
-      const int py = ty0 + 2 * wave + (pt >> 1);
-      const int px = tx0 + (pt & 1) * 16 + lrow;
-      const bool ok = py < a.H && px < a.W;
-      const size_t pix = ((size_t)n * a.H + py) * a.W + px;
+    for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct) {
-        const int co = co0 + ct * 16 + kq * 4;
-        rv[pt][ct] = (ok && co < a.Cout) ? *reinterpret_cast<const u32x2*>(a.res + pix * a.Cout + co) : (u32x2){0u, 0u};
-      }
-    }
+      for (int ct = 0; ct < C::NCT; ++ct) rv[pt][ct] = rvp[pt][ct];
+  } else if (a.res) {
+    load_res_regs<C>(a, n, ty0, tx0, co0, wave, lrow, kq, rv);
   } else {
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt)
@@ -503,6 +518,10 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : CONV_KERNEL_WPE) void conv2d_nhwc
   float4 aff[4] = {make_float4(1.f, 1.f, 1.f, 1.f), make_float4(1.f, 1.f, 1.f, 1.f), make_float4(0.f, 0.f, 0.f, 0.f),
                    make_float4(0.f, 0.f, 0.f, 0.f)};
   issue_chunk<C, KS, INMODE, X2>(a, n, ty0, tx0, co0, 0, tid, hraw, h2raw, wraw, aff, true);
+  // residual operand fetched at tile start: its latency hides behind the K loop (the registers are
+  // free -- occupancy here is set by LDS, two blocks per CU); it was exposed at the epilogue
+  u32x2 rv[4][C::NCT];
+  if (CONV_RES_PREFETCH) load_res_regs<C>(a, n, ty0, tx0, co0, wave, lrow, kq, rv);
   for (int ch = 0; ch < a.nchunk; ++ch) {
     if (ch > 0) __syncthreads();
     commit_chunk<C, KS, X2>(a, ty0, tx0, tid, hraw, h2raw, wraw, aff, hl, wl, true);
@@ -518,7 +537,7 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : CONV_KERNEL_WPE) void conv2d_nhwc
     __syncthreads();
     stage = hl;
   }
-  epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq, stage);
+  epilogue<C>(a, acc, bias, n, ty0, tx0, co0, wave, lrow, kq, stage, CONV_RES_PREFETCH ? rv : nullptr);
 }
 
 template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>

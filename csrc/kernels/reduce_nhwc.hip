@@ -45,12 +45,16 @@ __global__ __launch_bounds__(256) void nhwc_channel_sum_kernel(const bf16_t* __r
     const int g = c / 8, j = c % 8;
     float s = 0.f;
     for (int q = 0; q < PG; ++q) s += red[(q * C8 + g) * 8 + j];
-    atomicAdd(out + (size_t)n * C + c, s);
+    // one partial per (image, pixel split): out is [N, split, C], summed in a fixed order by the
+    // caller -- float atomics here made the style vector (and, through bf16 rounding flips in the
+    // decoder, the flows) differ run to run
+    out[((size_t)n * gridDim.y + sb) * C + c] = s;
   }
 }
 
 }  // namespace
 
+// out: [N, split, C] per-split partial sums (every element written; the caller reduces over split)
 extern "C" int be_nhwc_channel_sum(const void* x, float* out, int N, int HW, int C, int split, int square,
                                    hipStream_t s) {
   if (C % 8 != 0 || C > 2048) return -1;

@@ -251,3 +251,45 @@ def test_sparse_diffusion_bit_identical_to_dense(gpu):
     torch.cuda.synchronize()
     assert dense.abs().sum() > 0
     assert torch.equal(dense, sparse)
+
+
+@pytest.mark.gpu
+def test_cross_batch_stream_and_locked_eval_match_eval(gpu):
+    """CellposeRunner.stream (net of batch i+1 over masks of batch i on a second stream) and
+    eval_locked from two threads (the served path) give eval()'s masks and flows.  eval() itself is
+    not bitwise repeatable: the style reduction's float atomics move style by ~1e-8, which flips a
+    few bf16 roundings downstream (two eval() calls of the same batch differ by up to ~0.04 in single
+    flow pixels, tools/debug_stream.py) -- so flows are compared by relative RMS."""
+    import threading
+
+    from bioengine_worker_amd.cellpose.pipeline import CellposeRunner, synthetic_cells
+
+    r = CellposeRunner(device=gpu, seed=1)
+    batches = [torch.from_numpy(synthetic_cells(3, 256, 256, ncells=25, seed=s)).to(gpu) for s in range(4)]
+    ref_out = [r.eval(b) for b in batches]
+    st = r.stream()
+    got = [st.submit(b) for b in batches] + [st.flush()]
+    assert got[0] is None
+    def same(m, f, mr, fr):
+        rel = ((f - fr).norm() / fr.norm()).item()
+        assert rel < 2e-3, rel
+        assert (m != mr).float().mean().item() < 1e-3
+
+    for (m, f, s), (mr, fr, sr) in zip(got[1:], ref_out):
+        same(m, f, mr, fr)
+    net_lock, mask_lock = threading.Lock(), threading.Lock()
+    res = [None] * len(batches)
+
+    def work(i):
+        m, f, _, ev = r.eval_locked(batches[i], net_lock, mask_lock)
+        ev.synchronize()
+        res[i] = (m.clone(), f.clone())
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(batches))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    for (m, f), (mr, fr, _) in zip(res, ref_out):
+        same(m, f, mr, fr)
