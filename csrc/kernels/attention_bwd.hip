@@ -17,9 +17,10 @@
 //    rows sit in registers for the whole kernel); the query tiles stream through LDS.  dV^T += dO^T P
 //    and dK^T += Q^T dS with P / dS straight from the accumulators, dO^T / Q^T read transposed.
 //
-// Tiles are XOR-swizzled per 16-byte chunk (v_off: conflict-free transposed reads), and the next
-// tile's global loads are register-staged while the current tile's MFMAs run.  Block ids are
-// XCD-remapped so the blocks that stream the same (batch, head) K/V or Q/dO rows share an L2.
+// Tiles are XOR-swizzled per 16-byte chunk (v_off: conflict-free transposed reads) and stream
+// HBM -> LDS by LDS-DMA two tiles ahead of the MFMAs (three LDS stages, counted vmcnt across raw
+// barriers).  Block ids are XCD-remapped so the blocks that stream the same (batch, head) K/V or
+// Q/dO rows share an L2.
 #include "common.h"
 
 namespace {
@@ -29,6 +30,30 @@ constexpr int TT = 64;   // streamed rows per LDS tile (keys in the dq kernel, q
 constexpr float LOG2E = 1.4426950408889634f;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+// s_waitcnt immediate waiting for vmcnt <= n only (gfx9 encoding, as in gemm_fp8.hip)
+constexpr int waitcnt_vm(int n) { return (n & 0xf) | (0x7 << 4) | (0xf << 8) | ((n >> 4) << 14); }
+
+// HBM -> LDS DMA (global_load_lds_dword / _dwordx4) in inline asm.  Through the builtin the compiler
+// treats every later ds_read of the (single) LDS array as aliasing the newest DMA and puts a
+// vmcnt(0) in front of it, which drains the prefetch this pipeline keeps in flight; these waits are
+// explicit below.  lds is the wave-uniform LDS byte address of lane 0's destination (lane i writes
+// at lds + i * size); M0 is saved and restored around the instruction.
+template <int SIZE>
+__device__ __forceinline__ void glds(const void* src, uint32_t lds) {
+  unsigned keep;
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  if constexpr (SIZE == 16)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(lds_u8*)(p);
+}
 
 struct BwdArgs {
   const bf16_t* q;
@@ -61,9 +86,15 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
   return r;
 }
 
-// chunk swizzles (16-byte chunks, 8 per 128-byte row); same layouts as attention.hip
+// chunk swizzles (16-byte chunks, 8 per 128-byte row).  k_off: conflict-free 16-row b128 row reads.
+// v_off, for tiles read BOTH as rows (b128, 16 lanes = 16 rows at one chunk) and transposed
+// (read_tr: 4 rows x 4 chunks per 32 lanes): with m = row >> 1, bit 2 of the XOR is m & 1 (rows r and
+// r + 2 of a transposed group land in different 4-chunk halves) and bits 0-1 are m >> 1, so the 8
+// even (odd) rows of a 16-row group get 8 distinct chunk slots.  (attention.hip's v_off, XOR 4 (m & 1)
+// only, is 4-way conflicted on row reads: SQ_LDS_BANK_CONFLICT in profiles/r03/cpsam/attn_pmc.md.)
 __device__ __forceinline__ int k_off(int row, int ch) { return row * HD + ((ch ^ ((row >> 1) & 7)) << 3); }
-__device__ __forceinline__ int v_off(int row, int ch) { return row * HD + ((ch ^ (((row >> 1) & 1) << 2)) << 3); }
+__device__ __forceinline__ int v_swz(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int v_off(int row, int ch) { return row * HD + ((ch ^ v_swz(row)) << 3); }
 
 // Transposed A operand X^T [32 head dims (db) x 16 rows (rb*32 + 16 st ...)] of a v_off-laid tile;
 // the k order matches the B operand built from an accumulator by pack_b() below.
@@ -98,16 +129,30 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16_t* p, bool ok) {
   return *reinterpret_cast<bf16x8*>(&r);
 }
 
-// ------------------------------------------------------------------ dQ (+ drel, delta)
+// LDS bytes per block (three pipeline stages).  dq: K | V tile + the tile's two rel_h grid rows per
+// query.  dkv: see dkv_body.
 template <int NW, int BIAS>
-__device__ __forceinline__ void dq_body(const BwdArgs& a, int logical) {
-  constexpr int NT = NW * 64;
-  constexpr int CHUNKS = 2 * TT * (HD / 8);
-  constexpr int CPT = (CHUNKS + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[TT * HD];  // v_off: row reads + transposed reads
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[TT * HD];  // k_off: row reads
+constexpr int dq_lds() {
+  return 3 * (2 * TT * HD * 2 + (BIAS ? NW * 64 * 4 : 0));
+}
+template <int NW, int BIAS>
+constexpr int dkv_lds() {
+  return 3 * (2 * TT * HD * 2 + (BIAS ? TT * 32 * 4 + NW * TT * 4 : 0) + 2 * TT * 4);
+}
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// ------------------------------------------------------------------ dQ (+ drel, delta)
+// The K / V tiles go HBM -> LDS by global_load_lds through three stages (the dkv pipeline below);
+// the tile's two rel_h grid rows per query ride along as one dword DMA per wave, so the loop has no
+// register loads left (an in-loop global load would make the compiler drain the DMAs with vmcnt(0)).
+template <int NW, int BIAS>
+__device__ __forceinline__ void dq_body(const BwdArgs& a, int logical, uint8_t* smem) {
+  constexpr int TB = TT * HD * 2;
+  constexpr int OFF_R = 2 * TB;  // rel_h: [wave][kb][32 queries]
+  constexpr int STAGE = OFF_R + (BIAS ? NW * 64 * 4 : 0);
+  constexpr int LOADS = 16 / NW + (BIAS ? 1 : 0);  // DMA instructions per wave and tile
+  static_assert(3 * STAGE <= dq_lds<NW, BIAS>(), "LDS size");
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, ql = lane & 31;
   const int bh = logical / a.blocks_per_bh, qb = logical % a.blocks_per_bh;
   const int b = bh / a.H, hh = bh % a.H;
@@ -135,60 +180,54 @@ __device__ __forceinline__ void dq_body(const BwdArgs& a, int logical) {
   const float lse2 = qv ? a.lse[(long long)bh * a.N + qi] * LOG2E : 0.f;
   const float c2 = a.scale * LOG2E;
 
-  const float* rh = nullptr;
+  const float* rhq = BIAS ? a.relh + ((long long)bh * a.N + qc) * a.Hg : nullptr;
   float rwr[16], drw[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { rwr[i] = 0.f; drw[i] = 0.f; }
   if (BIAS) {
-    rh = a.relh + ((long long)bh * a.N + qc) * a.Hg;
     const float* rw = a.relw + ((long long)bh * a.N + qc) * 32;
 #pragma unroll
     for (int i = 0; i < 16; ++i) rwr[i] = rw[8 * (i >> 2) + 4 * h + (i & 3)] * LOG2E;
   }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // register loads land before the (compiler-invisible) DMAs
 
   f32x16 dqa[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dqa[0][i] = 0.f; dqa[1][i] = 0.f; }
 
   const int ntiles = (a.N + TT - 1) / TT;
-  u32x4 stage[CPT];
   auto issue = [&](int t) {
+    uint8_t* st = smem + (t % 3) * STAGE;
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + i * NT;
-      u32x4 r = (u32x4){0u, 0u, 0u, 0u};
-      if (c < CHUNKS) {
-        const int isv = c >= CHUNKS / 2;
-        const int cc = c - isv * (CHUNKS / 2);
-        const int row = cc >> 3, ch = cc & 7;
-        const int key = t * TT + row;
-        if (key < a.N) r = *reinterpret_cast<const u32x4*>((isv ? vbase : kbase) + (long long)key * a.s_tok + ch * 8);
-      }
-      stage[i] = r;
+    for (int j = 0; j < 16 / NW; ++j) {
+      const int g = j * NW + wave;  // wave-uniform: 1 KiB = 8 key rows of K (g < 8) or V
+      const int row = (g & 7) * 8 + (lane >> 3);
+      const int key = min(t * TT + row, a.N - 1);  // padded keys: any finite row, P = 0 below
+      // source chunk = the swizzle's inverse at the lane-linear LDS slot (both are involutions)
+      const int ch = g < 8 ? (lane & 7) ^ v_swz(row) : (lane & 7) ^ ((row >> 1) & 7);
+      const bf16_t* src = (g < 8 ? kbase : vbase) + (long long)key * a.s_tok + ch * 8;
+      glds<16>(src, lds_addr(st + (g < 8 ? 0 : TB) + (g & 7) * 1024));
     }
-  };
-  auto commit = [&]() {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + i * NT;
-      if (c < CHUNKS) {
-        const int isv = c >= CHUNKS / 2;
-        const int cc = c - isv * (CHUNKS / 2);
-        const int row = cc >> 3, ch = cc & 7;
-        if (isv)
-          *reinterpret_cast<u32x4*>(Vs + k_off(row, ch)) = stage[i];
-        else
-          *reinterpret_cast<u32x4*>(Ks + v_off(row, ch)) = stage[i];
-      }
-    }
+    if (BIAS)  // lanes 0-31: grid row 2t, 32-63: row 2t+1, of this wave's 32 queries
+      glds<4>(rhq + min(2 * t + h, a.Hg - 1), lds_addr(st + OFF_R + wave * 256));
   };
 
   issue(0);
+  if (ntiles > 1) issue(1);
   for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();
-    commit();
-    __syncthreads();
-    if (t + 1 < ntiles) issue(t + 1);
+    // tile t landed (tile t+1 may stay in flight).  The drel_h stores of earlier tiles also count in
+    // vmcnt; waiting for <= LOADS outstanding is safe whatever order they retire in.
+    if (t + 1 < ntiles)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < ntiles) issue(t + 2);
+    const uint8_t* st = smem + (t % 3) * STAGE;
+    const bf16_t* Ks = reinterpret_cast<const bf16_t*>(st);
+    const bf16_t* Vs = reinterpret_cast<const bf16_t*>(st + TB);
+    const float* Rh = reinterpret_cast<const float*>(st + OFF_R) + wave * 64;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       f32x16 s, dp;
@@ -203,7 +242,7 @@ __device__ __forceinline__ void dq_body(const BwdArgs& a, int logical) {
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[ks], dp, 0, 0, 0);
       }
       const int krow = 2 * t + kb;  // grid row of this 32-key block (BIAS: Wg == 32)
-      const float rhv = BIAS ? rh[min(krow, a.Hg - 1)] * LOG2E : 0.f;
+      const float rhv = BIAS ? Rh[kb * 32 + ql] * LOG2E : 0.f;
       float dsum = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -220,11 +259,11 @@ __device__ __forceinline__ void dq_body(const BwdArgs& a, int logical) {
         if (qv && h == 0 && krow < a.Hg) a.drelh[((long long)bh * a.N + qi) * a.Hg + krow] = dsum;
       }
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8 pf = pack_b(s, st);
+      for (int st2 = 0; st2 < 2; ++st2) {
+        const bf16x8 pf = pack_b(s, st2);
 #pragma unroll
         for (int db = 0; db < 2; ++db)
-          dqa[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Ks, lane, kb, st, db), pf, dqa[db], 0, 0, 0);
+          dqa[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Ks, lane, kb, st2, db), pf, dqa[db], 0, 0, 0);
       }
     }
   }
@@ -255,37 +294,44 @@ __device__ __forceinline__ void dq_body(const BwdArgs& a, int logical) {
 }
 
 // ------------------------------------------------------------------ dK, dV
+// The query tiles go HBM -> LDS with global_load_lds (no staging VGPRs, no ds_write pass) through
+// THREE LDS stages: tile t+2's DMA is issued right after the barrier that opens tile t and stays in
+// flight across the next barrier (counted vmcnt, raw s_barrier).  The register-staged version of
+// this kernel waited for tile t+1's loads at the top of every tile: SQ_WAIT_ANY 62 % of its wave
+// cycles; with the DMA pipeline 25 % and 0.58x the wave cycles (profiles/r03/cpsam/attn_pmc.md).
+// The LDS image is raw: rel_w / rel_h / lse stay in natural-log units and are combined at read time.
+// Stage = Q 8K | dO 8K | rel_w 8K | rel_h NW x 256 B | lse 256 B | delta 256 B; three stages of the
+// 4-wave bias kernel = 76.5 KiB: two blocks per CU.
 template <int NW, int BIAS>
-__device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical) {
-  constexpr int NT = NW * 64;
-  constexpr int QCH = 2 * TT * (HD / 8);       // Q + dO tile chunks (bf16 x 8)
-  constexpr int WCH = BIAS ? TT * 32 / 4 : 0;   // rel_w tile chunks (fp32 x 4)
-  constexpr int HCH = BIAS ? TT : 0;             // rel_h: the block's NW grid rows, one chunk per query
-  constexpr int SCH = TT / 4 * 2;               // lse2 + delta chunks
-  constexpr int CHUNKS = QCH + WCH + HCH + SCH;
-  constexpr int CPT = (CHUNKS + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[TT * HD];
-  __shared__ __attribute__((aligned(16))) bf16_t Ds[TT * HD];
-  __shared__ __attribute__((aligned(16))) float Ws[BIAS ? TT * 32 : 4];
-  __shared__ __attribute__((aligned(16))) float Hs[BIAS ? TT * 4 : 4];
-  __shared__ __attribute__((aligned(16))) float L2s[TT];
-  __shared__ __attribute__((aligned(16))) float DLs[TT];
+__device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical, uint8_t* smem) {
+  constexpr int QB = TT * HD * 2;
+  constexpr int WB = BIAS ? TT * 32 * 4 : 0;
+  constexpr int HB = BIAS ? NW * TT * 4 : 0;
+  constexpr int OFF_D = QB, OFF_W = 2 * QB, OFF_H = OFF_W + WB, OFF_L = OFF_H + HB, OFF_DL = OFF_L + TT * 4;
+  constexpr int STAGE = OFF_DL + TT * 4;
+  constexpr int GROUPS = BIAS ? 24 : 16;  // 1 KiB wave-instructions: Q 8, dO 8, rel_w 8
+  static_assert(GROUPS % NW == 0, "row groups must split evenly over waves");
+  // per-wave DMA instructions per tile: GROUPS / NW (+ one rel_h row, + lse / delta on waves 0 / 1);
+  // the counted wait uses the smallest count (a wave with more waits a little longer, never too short)
+  constexpr int LOADS_MIN = GROUPS / NW + (BIAS ? 1 : 0) + (NW > 2 ? 0 : 1);
+  static_assert(3 * STAGE <= dkv_lds<NW, BIAS>(), "LDS size");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  (void)tid;
   const int h = lane >> 5, kl = lane & 31;
   const int bh = logical / a.blocks_per_bh, kblk = logical % a.blocks_per_bh;
   const int b = bh / a.H, hh = bh % a.H;
-  const int k0 = kblk * NW * 32 + wave * 32;
-  const int kj = k0 + kl;
+  const int kj = kblk * NW * 32 + wave * 32 + kl;
   const bool kv = kj < a.N;
   const int kc = min(kj, a.N - 1);
-  // BIAS: this wave's 32 keys are one grid row (Wg == 32), row kblk * NW + wave; key col = kl
 
   const long long kvoff = (long long)b * a.s_batch + (long long)hh * a.s_head;
   const bf16_t* qbase = a.q + kvoff;
   const bf16_t* dbase = a.dout + (long long)b * a.o_batch + (long long)hh * a.o_head;
   const float* lrow = a.lse + (long long)bh * a.N;
   const float* drow = a.delta + (long long)bh * a.N;
+  const float* hbase = BIAS ? a.relh + (long long)bh * a.N * a.Hg + min(kblk * NW + wave, a.Hg - 1) : nullptr;
+  const float* wbase = BIAS ? a.relw + (long long)bh * a.N * 32 : nullptr;
 
   bf16x8 kf[4], vf[4];
 #pragma unroll
@@ -293,6 +339,9 @@ __device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical) {
     kf[ks] = load_frag(a.k + kvoff + (long long)kc * a.s_tok + ks * 16 + h * 8, kv);
     vf[ks] = load_frag(a.v + kvoff + (long long)kc * a.s_tok + ks * 16 + h * 8, kv);
   }
+  // K / V rows land before the DMA pipeline starts: the compiler does not see the asm DMAs, and a
+  // first use of kf / vf inside the loop would make it wait vmcnt(0) there on every tile
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
   const float c2 = a.scale * LOG2E;
 
   f32x16 dva[2], dka[2];
@@ -300,119 +349,102 @@ __device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical) {
   for (int i = 0; i < 16; ++i) { dva[0][i] = 0.f; dva[1][i] = 0.f; dka[0][i] = 0.f; dka[1][i] = 0.f; }
 
   const int ntiles = (a.N + TT - 1) / TT;
-  u32x4 stage[CPT];
   auto issue = [&](int t) {
+    uint8_t* st = smem + (t % 3) * STAGE;
+    const int q0 = t * TT;
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + i * NT;
-      u32x4 r = (u32x4){0u, 0u, 0u, 0u};
-      if (c < QCH) {
-        const int isd = c >= QCH / 2;
-        const int cc = c - isd * (QCH / 2);
-        const int row = cc >> 3, ch = cc & 7;
-        const int qq = t * TT + row;
-        if (qq < a.N)
-          r = *reinterpret_cast<const u32x4*>(isd ? dbase + (long long)qq * a.o_tok + ch * 8
-                                                  : qbase + (long long)qq * a.s_tok + ch * 8);
-      } else if (c < QCH + WCH) {  // rel_w, pre-scaled to log2 units
-        const int cc = c - QCH;
-        const int row = cc >> 3, c4 = cc & 7;
-        const int qq = t * TT + row;
-        if (qq < a.N) {
-          const float4 f = *reinterpret_cast<const float4*>(a.relw + ((long long)bh * a.N + qq) * 32 + c4 * 4);
-          r[0] = __float_as_uint(f.x * LOG2E); r[1] = __float_as_uint(f.y * LOG2E);
-          r[2] = __float_as_uint(f.z * LOG2E); r[3] = __float_as_uint(f.w * LOG2E);
-        }
-      } else if (c < QCH + WCH + HCH) {  // rel_h of the block's grid rows minus the row's LSE (log2)
-        const int qq = t * TT + (c - QCH - WCH);
-        if (qq < a.N) {
-          const float* hr = a.relh + ((long long)bh * a.N + qq) * a.Hg;
-          const float l2 = lrow[qq] * LOG2E;
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const int gr = kblk * NW + w;
-            r[w] = __float_as_uint(((w < NW && gr < a.Hg) ? hr[gr] * LOG2E : 0.f) - l2);
-          }
-        } else {  // padded query: P = 0
-          r[0] = r[1] = r[2] = r[3] = __float_as_uint(-INFINITY);
-        }
-      } else if (c < CHUNKS) {
-        const int cc = c - QCH - WCH - HCH;
-        const int isd = cc >= TT / 4;
-        const int q4 = (cc - isd * (TT / 4)) * 4;
-        float f[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int qq = t * TT + q4 + j;
-          // lse of a padded query = +inf -> P = 0; delta 0
-          f[j] = qq < a.N ? (isd ? drow[qq] : lrow[qq] * LOG2E) : (isd ? 0.f : INFINITY);
-        }
-        r[0] = __float_as_uint(f[0]); r[1] = __float_as_uint(f[1]);
-        r[2] = __float_as_uint(f[2]); r[3] = __float_as_uint(f[3]);
+    for (int j = 0; j < GROUPS / NW; ++j) {
+      const int g = j * NW + wave;  // wave-uniform
+      const int row = (g & 7) * 8 + (lane >> 3);
+      const int qc = min(q0 + row, a.N - 1);  // padded queries: any finite row, P = 0 below
+      const void* src;
+      if (!BIAS || g < 16) {  // Q / dO rows, v_off swizzle applied on the source chunk (involution)
+        const int ch = (lane & 7) ^ v_swz(row);
+        src = g < 8 ? (const void*)(qbase + (long long)qc * a.s_tok + ch * 8)
+                    : (const void*)(dbase + (long long)qc * a.o_tok + ch * 8);
+      } else {
+        src = (const void*)(wbase + (long long)qc * 32 + (lane & 7) * 4);
       }
-      stage[i] = r;
+      const int off = g < 8 ? 0 : (g < 16 ? OFF_D : OFF_W);
+      glds<16>(src, lds_addr(st + off + (g & 7) * 1024));
     }
-  };
-  auto commit = [&]() {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int c = tid + i * NT;
-      if (c < QCH) {
-        const int isd = c >= QCH / 2;
-        const int cc = c - isd * (QCH / 2);
-        const int row = cc >> 3, ch = cc & 7;
-        *reinterpret_cast<u32x4*>((isd ? Ds : Qs) + v_off(row, ch)) = stage[i];
-      } else if (c < QCH + WCH) {
-        const int cc = c - QCH;
-        *reinterpret_cast<u32x4*>(Ws + cc * 4) = stage[i];
-      } else if (c < QCH + WCH + HCH) {
-        const int cc = c - QCH - WCH;
-        *reinterpret_cast<u32x4*>(Hs + cc * 4) = stage[i];
-      } else if (c < CHUNKS) {
-        const int cc = c - QCH - WCH - HCH;
-        const int isd = cc >= TT / 4;
-        const int q4 = (cc - isd * (TT / 4)) * 4;
-        *reinterpret_cast<u32x4*>((isd ? DLs : L2s) + q4) = stage[i];
-      }
-    }
+    const int qc = min(q0 + lane, a.N - 1);
+    if (BIAS)
+      glds<4>(hbase + (long long)qc * a.Hg, lds_addr(st + OFF_H + wave * TT * 4));
+    if (wave < 2)
+      glds<4>((wave == 0 ? lrow : drow) + qc, lds_addr(st + (wave == 0 ? OFF_L : OFF_DL)));
   };
 
   issue(0);
+  if (ntiles > 1) issue(1);
   for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();
-    commit();
-    __syncthreads();
-    if (t + 1 < ntiles) issue(t + 1);
-#pragma unroll 1  // one 32-query half at a time: keeps dkv<4, 1> at 254 VGPRs without spills
+    // tile t landed; tile t+1 stays in flight
+    if (t + 1 < ntiles)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS_MIN) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's part of tile t is in LDS; every wave is done with t-1
+    if (t + 2 < ntiles) issue(t + 2);  // into tile t-1's stage
+    const uint8_t* st = smem + (t % 3) * STAGE;
+    const bf16_t* Qc = reinterpret_cast<const bf16_t*>(st);
+    const bf16_t* Dc = reinterpret_cast<const bf16_t*>(st + OFF_D);
+    const float* Wc = reinterpret_cast<const float*>(st + OFF_W);
+    const float* Hc = reinterpret_cast<const float*>(st + OFF_H) + wave * TT;
+    const float* Lc = reinterpret_cast<const float*>(st + OFF_L);
+    const float* DLc = reinterpret_cast<const float*>(st + OFF_DL);
+    const int qlim = a.N - t * TT;  // queries >= qlim in this tile are padding
+#pragma unroll 1
     for (int qb = 0; qb < 2; ++qb) {
       f32x16 s, dp;
 #pragma unroll
       for (int i = 0; i < 16; ++i) { s[i] = 0.f; dp[i] = 0.f; }
+      // LDS reads of this lane's 16 queries' lse / delta / rel_h / rel_w, all issued ahead of the
+      // S / dP MFMAs (sched_barrier) so their latency hides under the matrix work
+      float4 lv[4], dlv[4], hv[4];
+      float wv[16];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int qr0 = qb * 32 + 8 * g4 + 4 * h;
+        lv[g4] = *reinterpret_cast<const float4*>(Lc + qr0);
+        dlv[g4] = *reinterpret_cast<const float4*>(DLc + qr0);
+        hv[g4] = BIAS ? *reinterpret_cast<const float4*>(Hc + qr0) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wv[4 * g4 + j] = BIAS ? Wc[(qr0 + j) * 32 + kl] : 0.f;
+      }
       const int row = qb * 32 + kl;
+      bf16x8 qa[4], da[4];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(Qs + v_off(row, 2 * ks + h));
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(Ds + v_off(row, 2 * ks + h));
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[ks], dp, 0, 0, 0);
+        qa[ks] = *reinterpret_cast<const bf16x8*>(Qc + v_off(row, 2 * ks + h));
+        da[ks] = *reinterpret_cast<const bf16x8*>(Dc + v_off(row, 2 * ks + h));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[ks], kf[ks], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[ks], vf[ks], dp, 0, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int qr = qb * 32 + 8 * (i >> 2) + 4 * h + (i & 3);  // query row in the tile
-        // BIAS: Hs holds rel_h * log2e - lse * log2e, Ws rel_w * log2e (folded at staging time)
-        const float x = BIAS ? s[i] * c2 + (Hs[qr * 4 + wave] + Ws[qr * 32 + kl]) : s[i] * c2 - L2s[qr];
-        const float p = kv ? __builtin_amdgcn_exp2f(x) : 0.f;
+        const int g4 = i >> 2, j = i & 3;
+        const int qr = qb * 32 + 8 * g4 + 4 * h + j;
+        const float l = j == 0 ? lv[g4].x : j == 1 ? lv[g4].y : j == 2 ? lv[g4].z : lv[g4].w;
+        const float d = j == 0 ? dlv[g4].x : j == 1 ? dlv[g4].y : j == 2 ? dlv[g4].z : dlv[g4].w;
+        const float hr = j == 0 ? hv[g4].x : j == 1 ? hv[g4].y : j == 2 ? hv[g4].z : hv[g4].w;
+        const float bz = ((BIAS ? hr + wv[i] : 0.f) - l) * LOG2E;
+        const float p = (kv && qr < qlim) ? __builtin_amdgcn_exp2f(__builtin_fmaf(s[i], c2, bz)) : 0.f;
         s[i] = p;
-        dp[i] = p * (dp[i] - DLs[qr]);
+        dp[i] = p * (dp[i] - d);
       }
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8 pf = pack_b(s, st);
-        const bf16x8 dsf = pack_b(dp, st);
+      for (int st2 = 0; st2 < 2; ++st2) {
+        const bf16x8 pf = pack_b(s, st2);
+        const bf16x8 dsf = pack_b(dp, st2);
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
-          dva[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Ds, lane, qb, st, db), pf, dva[db], 0, 0, 0);
-          dka[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Qs, lane, qb, st, db), dsf, dka[db], 0, 0, 0);
+          dva[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Dc, lane, qb, st2, db), pf, dva[db], 0, 0, 0);
+          dka[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(read_tr(Qc, lane, qb, st2, db), dsf, dka[db], 0, 0, 0);
         }
       }
     }
@@ -441,24 +473,29 @@ __device__ __forceinline__ void dkv_body(const BwdArgs& a, int logical) {
 
 template <int NW, int BIAS>
 __global__ __launch_bounds__(NW * 64) BE_ATTN_BWD_WPE void attn_bwd_dq_kernel(BwdArgs a) {
-  dq_body<NW, BIAS>(a, xcd_remap(blockIdx.x, a.blocks_per_bh * a.B * a.H));
+  __shared__ __attribute__((aligned(16))) uint8_t smem[dq_lds<NW, BIAS>()];  // the only LDS object
+  dq_body<NW, BIAS>(a, xcd_remap(blockIdx.x, a.blocks_per_bh * a.B * a.H), smem);
 }
 
 template <int NW, int BIAS>
 __global__ __launch_bounds__(NW * 64) BE_ATTN_BWD_WPE void attn_bwd_dkv_kernel(BwdArgs a) {
-  dkv_body<NW, BIAS>(a, xcd_remap(blockIdx.x, a.blocks_per_bh * a.B * a.H));
+  __shared__ __attribute__((aligned(16))) uint8_t smem[dkv_lds<NW, BIAS>()];
+  dkv_body<NW, BIAS>(a, xcd_remap(blockIdx.x, a.blocks_per_bh * a.B * a.H), smem);
 }
 
 // Small grids (batch 1: 16 heads x 1024 tokens = 256 + 256 two-wave blocks): the dq and dkv blocks
 // run as ONE launch (blocks [0, n) dq, [n, 2n) dkv) so both halves fill the 1024 SIMDs together;
-// delta = rowsum(dO * O) comes from attn_delta_kernel first.
+// delta = rowsum(dO * O) comes from attn_delta_kernel first.  One LDS array serves either body.
 template <int NW, int BIAS>
 __global__ __launch_bounds__(NW * 64) BE_ATTN_BWD_WPE void attn_bwd_fused_kernel(BwdArgs a) {
+  constexpr int L = dq_lds<NW, BIAS>() > dkv_lds<NW, BIAS>() ? dq_lds<NW, BIAS>() : dkv_lds<NW, BIAS>();
+  __shared__ __attribute__((aligned(16))) uint8_t smem[L];
   const int n = a.blocks_per_bh * a.B * a.H;
-  if ((int)blockIdx.x < n)
-    dq_body<NW, BIAS>(a, xcd_remap(blockIdx.x, n));
-  else
-    dkv_body<NW, BIAS>(a, xcd_remap(blockIdx.x - n, n));
+  if ((int)blockIdx.x < n) {
+    dq_body<NW, BIAS>(a, xcd_remap(blockIdx.x, n), smem);
+  } else {
+    dkv_body<NW, BIAS>(a, xcd_remap(blockIdx.x - n, n), smem);
+  }
 }
 
 // delta[bh, q] = sum_c dO[b, q, h, c] O[b, q, h, c]: 8 lanes per row, 16-byte loads
