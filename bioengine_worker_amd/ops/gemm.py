@@ -46,9 +46,12 @@ def enabled(t: torch.Tensor) -> bool:
 
 
 def _workspace(dev: torch.device) -> torch.Tensor:
-    w = _ws.get(dev.index)
+    """One workspace per (device, stream): GEMMs on two streams (the CPSAM engine's side-stream
+    weight gradients) must not share scratch."""
+    key = (dev.index, torch.cuda.current_stream(dev).stream_id)
+    w = _ws.get(key)
     if w is None:
-        w = _ws[dev.index] = torch.empty(_WS_BYTES, dtype=torch.uint8, device=dev)
+        w = _ws[key] = torch.empty(_WS_BYTES, dtype=torch.uint8, device=dev)
     return w
 
 

@@ -33,6 +33,8 @@ reference, so the same engine code is checked against autograd in the CPU suite.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -92,10 +94,22 @@ class _Blk:
 class CPSAMTrainEngine:
     """Forward + backward of :class:`CPSAM` at a fixed batch shape ``[B, 3, bsize, bsize]``."""
 
-    def __init__(self, net: CPSAM, fp: FlatParams, B: int, device, eps: float = 1e-6):
+
+    def __init__(self, net: CPSAM, fp: FlatParams, B: int, device, eps: float = 1e-6,
+                 side_wgrad: bool | None = None):
         self.net, self.fp, self.B = net, fp, int(B)
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
+        # Optional: weight-gradient GEMMs (and bias column sums) on a second stream, off the dgrad
+        # critical path (fork/join are stream waits, so the step stays graph-capturable).  Measured
+        # slower on MI355X at both batch sizes (profiles/r03/cpsam/side_wgrad_ab.jsonl: batch 1 12.47
+        # -> 13.74 ms, batch 8 33.74 -> 35.01 ms: two GEMMs sharing the CUs run longer than they
+        # overlap), so it is off unless asked for (side_wgrad=True / BE_CPSAM_SIDE_WGRAD=1).
+        if side_wgrad is None and os.environ.get("BE_CPSAM_SIDE_WGRAD", "") in ("0", "1"):
+            side_wgrad = os.environ["BE_CPSAM_SIDE_WGRAD"] == "1"  # A/B override
+        self._side_wgrad = side_wgrad
+        self._side: torch.cuda.Stream | None = None
+        self._side_keep: list = []
         self.cdt = torch.bfloat16 if self.cuda else torch.float32
         self.eps = eps
         e = net.encoder
@@ -162,6 +176,28 @@ class CPSAMTrainEngine:
         qx = q5.permute(2, 0, 1, 3, 4).reshape(g, B * g * H, c)            # x, (b y h), c
         dRw = torch.bmm(bw.transpose(1, 2), qx)
         return (dq_h + dq_w).reshape(B, self.N, H, c), dRh, dRw
+
+    def _use_side(self) -> bool:
+        if not self.cuda:
+            return False
+        return bool(self._side_wgrad)
+
+    def _off_path(self, fn, *keep: torch.Tensor) -> None:
+        """Run ``fn`` (weight-gradient work) on the side stream after everything queued so far on the
+        current stream; the operands stay referenced until :meth:`_join_side`, so the allocator
+        cannot hand their memory to later main-stream work while the side stream still reads it."""
+        if self._side is None:
+            fn()
+            return
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            fn()
+        self._side_keep.extend(keep)
+
+    def _join_side(self) -> None:
+        if self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._side_keep.clear()
 
     def _table_grad(self, dR: torch.Tensor, out: torch.Tensor) -> None:
         out.zero_()
@@ -236,7 +272,17 @@ class CPSAMTrainEngine:
     def backward(self, dyout: torch.Tensor, on_params_ready=None) -> None:
         """dyout [B, nout, S, S] -> parameter gradients written into ``fp.grad`` (overwritten).
         ``on_params_ready(params)`` fires as each group's gradients are final (DDP bucket launch)."""
-        ready = on_params_ready or (lambda ps: None)
+        if self._use_side():
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+        else:
+            self._side = None
+        if on_params_ready is None:
+            ready = lambda ps: None  # noqa: E731
+        else:
+            def ready(ps):  # a bucket's consumer reads these gradients on the main stream
+                self._join_side()
+                on_params_ready(ps)
         s = self._saved
         B, ps, g, D, N, H, hd = self.B, self.ps, self.g, self.D, self.N, self.H, self.hd
         W = self._W
@@ -269,6 +315,7 @@ class CPSAMTrainEngine:
         torch.sum(G.view(B, N * D), 0, out=self.pos.grad.view(-1))
         Gb, _ = vt.scale_cast(G, dtype=cd, out_col=self.pe[1].grad)
         gemm.wgrad(Gb, s["patches"], self.pe[0].grad)
+        self._join_side()
         ready([self.pos, self.pe[0], self.pe[1]])
         self._saved = None
 
@@ -278,16 +325,16 @@ class CPSAMTrainEngine:
         kb = s["keep"]
         # MLP: t_out = t_mid + k m
         dm, _ = vt.scale_cast(G, kb, N, dtype=self.cdt, out_col=p["l2_b"].grad)
-        gemm.wgrad(dm, s["g"], p["l2_w"].grad)
+        self._off_path(lambda: gemm.wgrad(dm, s["g"], p["l2_w"].grad), dm)
         # lin2 dgrad with the GELU backward and lin1's bias gradient in the GEMM epilogue
         df = gemm.mm_dgelu(dm, w["l2_w"], s["f"], out_db=p["l1_b"].grad)
-        gemm.wgrad(df, s["h2"], p["l1_w"].grad)
+        self._off_path(lambda: gemm.wgrad(df, s["h2"], p["l1_w"].grad), df)
         dh2 = gemm.mm(df, w["l1_w"])
         dt_mid, _, _, _, _ = vt.ln_bwd(dh2, s["t_mid"], s["st2"], p["n2w"], r1=G, out_dw=p["n2w"].grad,
                                        out_db=p["n2b"].grad)
         # attention: t_mid = t_in + k y
         dy, _ = vt.scale_cast(dt_mid, kb, N, dtype=self.cdt, out_col=p["proj_b"].grad)
-        gemm.wgrad(dy, s["a"].reshape(B * N, D), p["proj_w"].grad)
+        self._off_path(lambda: gemm.wgrad(dy, s["a"].reshape(B * N, D), p["proj_w"].grad), dy)
         da = gemm.mm(dy, w["proj_w"]).view(B, N, H, hd)
         qkv = s["qkv"]
         dqkv = torch.empty(B, N, 3, H, hd, device=G.device, dtype=self.cdt)
@@ -302,8 +349,11 @@ class CPSAMTrainEngine:
             self._table_grad(dRh, p["rph"].grad)
             self._table_grad(dRw, p["rpw"].grad)
         dqkv2 = dqkv.view(B * N, 3 * D)
-        torch.sum(dqkv2, 0, dtype=torch.float32, out=p["qkv_b"].grad)
-        gemm.wgrad(dqkv2, s["h1"], p["qkv_w"].grad)
+        def qkv_grads():
+            torch.sum(dqkv2, 0, dtype=torch.float32, out=p["qkv_b"].grad)
+            gemm.wgrad(dqkv2, s["h1"], p["qkv_w"].grad)
+
+        self._off_path(qkv_grads, dqkv2)
         dh1 = gemm.mm(dqkv2, w["qkv_w"])
         dt_in, _, _, _, _ = vt.ln_bwd(dh1, s["t_in"], s["st1"], p["n1w"], r1=dt_mid, out_dw=p["n1w"].grad,
                                       out_db=p["n1b"].grad)

@@ -87,7 +87,8 @@ def test_layernorm_gelu_cast_kernels(dev):
     assert torch.equal(yb.cpu(), yb_r) and _rel(col.cpu(), col_r) < 1e-5
 
 
-def test_cpsam_engine_matches_fp32_autograd(dev):
+@pytest.mark.parametrize("side_wgrad", [False, True])
+def test_cpsam_engine_matches_fp32_autograd(dev, side_wgrad):
     from bioengine_worker_amd.models.cpsam import CPSAM
     from bioengine_worker_amd.ops import train_ops
     from bioengine_worker_amd.parallel.ddp import FlatParams
@@ -107,7 +108,7 @@ def test_cpsam_engine_matches_fp32_autograd(dev):
     loss_r.backward()
     net = net.to(dev)
     fp = FlatParams(net, dev)
-    eng = CPSAMTrainEngine(net, fp, B, dev)
+    eng = CPSAMTrainEngine(net, fp, B, dev, side_wgrad=side_wgrad)
     loss = eng.loss_and_backward(x, lbl, keep)
     torch.cuda.synchronize()
     assert abs(float(loss) - float(loss_r)) < 2e-2 * abs(float(loss_r))
