@@ -33,10 +33,60 @@ def _rpb(rows: int, target_blocks: int | None = None) -> int:
     return max(4, -(-rows // (target_blocks or _ROWCOL_BLOCKS)))
 
 
+class ColsumDeferral:
+    """Collects the fp32 partial -> ``out`` column reductions of the backward kernels and runs them
+    all in :meth:`flush` (``be_colsum_batched``: one launch per 48 reductions instead of one each).
+    Only reductions with a caller-supplied ``out`` (gradient views read after the backward) are
+    deferred; the partials stay referenced until the flush."""
+
+    def __init__(self):
+        self.items: list[tuple[torch.Tensor, torch.Tensor]] = []
+
+    def add(self, p: torch.Tensor, out: torch.Tensor) -> None:
+        self.items.append((p, out))
+
+    def flush(self) -> None:
+        if not self.items:
+            return
+        desc = torch.tensor([[p.data_ptr(), o.data_ptr(), p.shape[0], p.shape[1]] for p, o in self.items],
+                            dtype=torch.int64)
+        dev = self.items[0][0].device
+        _native.call("be_colsum_batched", desc.data_ptr(), len(self.items), _native.stream(dev))
+        self.items.clear()
+
+
+_DEFER: ColsumDeferral | None = None
+
+
+class defer_colsums:
+    """``with defer_colsums() as d: ...; d.flush()`` -- see :class:`ColsumDeferral` (GPU only; the
+    flush also runs on exit)."""
+
+    def __enter__(self) -> ColsumDeferral:
+        global _DEFER
+        self._prev, _DEFER = _DEFER, ColsumDeferral()
+        return _DEFER
+
+    def __exit__(self, *exc) -> None:
+        global _DEFER
+        d, _DEFER = _DEFER, self._prev
+        if exc[0] is None:
+            d.flush()
+
+
+def _deferrable(p: torch.Tensor, out: torch.Tensor | None) -> bool:
+    return (_DEFER is not None and out is not None and p.is_cuda and p.dtype == torch.float32 and p.dim() == 2
+            and p.is_contiguous() and out.is_contiguous() and out.dtype == torch.float32
+            and out.numel() == p.shape[1])
+
+
 def _colsum(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """Column sums of [rows, C] (fp32), written into ``out`` when given (no extra copy).  On the GPU
     the kernels' fp32 partials go through ``be_colsum`` (one small launch, ~3x faster than torch's
-    dim-0 reduction at these shapes)."""
+    dim-0 reduction at these shapes), or are deferred to a batched launch (:class:`defer_colsums`)."""
+    if _deferrable(p, out):
+        _DEFER.add(p, out)
+        return out.view(-1)
     if p.is_cuda and p.dtype == torch.float32 and p.dim() == 2 and p.is_contiguous():
         o = torch.empty(p.shape[1], device=p.device, dtype=torch.float32) if out is None else out.view(-1)
         if o.is_contiguous():
@@ -45,6 +95,27 @@ def _colsum(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     if out is None:
         return p.sum(0, dtype=torch.float32)
     return torch.sum(p, 0, dtype=torch.float32, out=out.view(-1))
+
+
+def colsum_bf16(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out (fp32 [C]) = column sums of x [rows, C] (bf16 on GPU: per-64-row fp32 partials by
+    ``be_colpart_bf16``, then the (deferrable) partial reduction)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and C % 8 == 0:
+        part = torch.empty(-(-rows // 64), C, device=x.device, dtype=torch.float32)
+        _native.call("be_colpart_bf16", _native.ptr(x), _native.ptr(part), rows, C, _native.stream(x.device))
+        return _colsum(part, out)
+    return torch.sum(x.reshape(rows, C), 0, dtype=torch.float32, out=out.view(-1))
+
+
+def sum_slabs(ws: torch.Tensor, out: torch.Tensor) -> None:
+    """out = ws.sum(0) for fp32 split-K slabs ws [S, ...] (one vectorised pass on the GPU)."""
+    n = out.numel()
+    if ws.is_cuda and ws.is_contiguous() and out.is_contiguous() and n % 4 == 0 and ws.numel() == ws.shape[0] * n:
+        _native.call("be_sum_slabs", _native.ptr(ws), _native.ptr(out), ws.shape[0], n, _native.stream(ws.device))
+    else:
+        torch.sum(ws, 0, out=out.view(ws.shape[1:]))
 
 
 def _rowscale(rs: torch.Tensor | None, rows: int, rpn: int):
@@ -115,7 +186,9 @@ def ln_bwd(dh: torch.Tensor, x: torch.Tensor, stats: torch.Tensor, w: torch.Tens
                      _native.ptr(w.float().contiguous()), _native.ptr(f(r1)), _native.ptr(f(s1)), _native.ptr(f(r2)),
                      _native.ptr(f(s2)), int(rpn), _native.ptr(dx), _native.ptr(dxb), _native.ptr(pdw),
                      _native.ptr(pdb), _native.ptr(pcol), rows, C, rpb, _native.stream(dev))
-        if out_dw is not None and out_db is not None and out_dw.is_contiguous() and out_db.is_contiguous():
+        if _deferrable(pdw, out_dw) and _deferrable(pdb, out_db):
+            dw, db = _colsum(pdw, out_dw), _colsum(pdb, out_db)
+        elif out_dw is not None and out_db is not None and out_dw.is_contiguous() and out_db.is_contiguous():
             _native.call("be_colsum2", _native.ptr(pdw), _native.ptr(out_dw), _native.ptr(pdb), _native.ptr(out_db),
                          nblk, C, _native.stream(dev))  # dw and db partials in one launch
             dw, db = out_dw.view(-1), out_db.view(-1)

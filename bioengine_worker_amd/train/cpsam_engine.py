@@ -74,7 +74,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> None:
         # proj 57.8 -> 37.7 us, qkv 87.6 -> 74.6 us; the 4096-wide fc1 / fc2 outputs gain nothing)
         ws = torch.empty(4, n, k, device=dy.device, dtype=torch.float32)
         torch.bmm(dy.reshape(4, m // 4, n).transpose(1, 2), x.reshape(4, m // 4, k), out_dtype=torch.float32, out=ws)
-        torch.sum(ws, 0, out=out2)
+        vt.sum_slabs(ws, out2)
     elif _MM_MODE == 2:
         torch.mm(dy.t(), x, out_dtype=torch.float32, out=out2)
     elif _MM_MODE == 1:
@@ -272,6 +272,13 @@ class CPSAMTrainEngine:
     def backward(self, dyout: torch.Tensor, on_params_ready=None) -> None:
         """dyout [B, nout, S, S] -> parameter gradients written into ``fp.grad`` (overwritten).
         ``on_params_ready(params)`` fires as each group's gradients are final (DDP bucket launch)."""
+        if self.cuda:  # LayerNorm / bias column reductions batched into a few launches
+            with vt.defer_colsums() as dc:
+                self._backward(dyout, on_params_ready, dc)
+        else:
+            self._backward(dyout, on_params_ready, None)
+
+    def _backward(self, dyout: torch.Tensor, on_params_ready, dc) -> None:
         if self._use_side():
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
@@ -281,6 +288,8 @@ class CPSAMTrainEngine:
             ready = lambda ps: None  # noqa: E731
         else:
             def ready(ps):  # a bucket's consumer reads these gradients on the main stream
+                if dc is not None:
+                    dc.flush()
                 self._join_side()
                 on_params_ready(ps)
         s = self._saved
@@ -290,7 +299,7 @@ class CPSAMTrainEngine:
         # pixel unshuffle of the output gradient -> [B*N, nout*ps*ps]
         do = dyout.to(cd).reshape(B, self.nout, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B * N, -1).contiguous()
         outw = W(self.outc.weight).reshape(self.outc.weight.shape[0], 256)
-        torch.sum(do, 0, dtype=torch.float32, out=self.outc.bias.grad)
+        vt.colsum_bf16(do, self.outc.bias.grad)
         gemm.wgrad(do, s["n3"], self.outc.weight.grad)
         dn3 = gemm.mm(do, outw)
         _, dn2, _, _, _ = vt.ln_bwd(dn3, s["n2r"], s["sn3"], self.neck[3].weight, want_dx=False, want_dxb=True,
@@ -312,7 +321,7 @@ class CPSAMTrainEngine:
             G = self._block_bwd(self.blocks[i], s["blocks"][i], G)
             ready(list(self.blocks[i].p.values()))
         # patch embedding + position embedding
-        torch.sum(G.view(B, N * D), 0, out=self.pos.grad.view(-1))
+        vt._colsum(G.view(B, N * D), self.pos.grad.view(-1))
         Gb, _ = vt.scale_cast(G, dtype=cd, out_col=self.pe[1].grad)
         gemm.wgrad(Gb, s["patches"], self.pe[0].grad)
         self._join_side()
@@ -350,7 +359,7 @@ class CPSAMTrainEngine:
             self._table_grad(dRw, p["rpw"].grad)
         dqkv2 = dqkv.view(B * N, 3 * D)
         def qkv_grads():
-            torch.sum(dqkv2, 0, dtype=torch.float32, out=p["qkv_b"].grad)
+            vt.colsum_bf16(dqkv2, p["qkv_b"].grad)
             gemm.wgrad(dqkv2, s["h1"], p["qkv_w"].grad)
 
         self._off_path(qkv_grads, dqkv2)

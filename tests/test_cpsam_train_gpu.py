@@ -214,3 +214,27 @@ def test_cpsam_adamw_overlapped_in_graph_matches_flat_update(dev):
     # fused vs flat differ only by atomic-order / bias-correction rounding: far below one update
     assert _rel(b.fp.flat, a.fp.flat) < 0.02 * upd, (_rel(b.fp.flat, a.fp.flat), upd)
     assert _rel(b.m, a.m) < 0.05 and _rel(b._cpsam_engine(2).mirror.float(), a._cpsam_engine(2).mirror.float()) < 0.02 * upd + 1e-3
+
+
+def test_batched_colsums_bf16_partials_and_slab_sums(dev):
+    """Deferred (batched) column reductions, bf16 column partials and split-K slab sums vs torch."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    shapes = [(512, 1024), (16, 4096), (3, 3072), (64, 192), (8, 8)] * 12  # 60 > one 48-entry launch
+    parts = [torch.randn(r, c, generator=g).to(dev) for r, c in shapes]
+    outs = [torch.full((c,), float("nan"), device=dev) for _, c in shapes]
+    with vt.defer_colsums() as d:
+        for p, o in zip(parts, outs):
+            vt._colsum(p, o)
+        assert len(d.items) == len(shapes)  # nothing launched before the flush
+    torch.cuda.synchronize()
+    for p, o in zip(parts, outs):
+        torch.testing.assert_close(o, p.sum(0), rtol=1e-5, atol=1e-4)
+    for rows, C in ((8192, 3072), (1000, 192), (1, 8)):
+        x = torch.randn(rows, C, generator=g).to(dev).bfloat16()
+        out = torch.empty(C, device=dev)
+        vt.colsum_bf16(x, out)
+        torch.testing.assert_close(out, x.float().sum(0), rtol=1e-4, atol=1e-2)
+    ws = torch.randn(4, 1024, 3072, generator=g).to(dev)
+    out = torch.empty(1024, 3072, device=dev)
+    vt.sum_slabs(ws, out)
+    torch.testing.assert_close(out, ws.sum(0), rtol=1e-5, atol=1e-5)
