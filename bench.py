@@ -398,7 +398,7 @@ def main():
             try:
                 out["vit_embed_imgs_per_s"] = round(bench_vit_embed(dev), 1)  # per GPU, batch 64, fp8
                 out["vit_embed_config"] = {"model": "DINOv2 ViT-B/14", "image": 224, "batch": 64,
-                                           "gemm_dtype": "fp8 e4m3", "baseline_img_s_A100_fp16": 500}
+                                           "gemm_dtype": "fp8 e4m3", "gemm": "HIP be_gemm_fp8 (block-scaled MFMA, MX-fp8 activations)", "baseline_img_s_A100_fp16": 500}
             except Exception as e:  # noqa: BLE001
                 out["extras_error_vit"] = f"{type(e).__name__}: {e}"
         if world == 1 and not args.no_served:

@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.fp8 import Fp8Linear, add_layernorm_fp8, quantize_rows
-from ..ops.transformer import add_layernorm, attention_ref, bias_gelu_, flash_attention
+from ..ops.transformer import add_layernorm, attention_ref, bias_gelu_, flash_attention, flash_attention_mx
 
 
 @dataclass
@@ -157,7 +157,7 @@ class ViT(nn.Module):
 class ViTEngine:
     """bf16 HIP inference engine for a :class:`ViT` (see module docstring)."""
 
-    def __init__(self, net: ViT, device, img_size: int = 224, precision: str = "bf16", fp8_gemm: str = "hipblaslt"):
+    def __init__(self, net: ViT, device, img_size: int = 224, precision: str = "bf16", fp8_gemm: str = "hip"):
         if precision not in ("bf16", "fp8"):
             raise ValueError(f"precision must be 'bf16' or 'fp8', got {precision!r}")
         self.precision = precision
@@ -230,7 +230,8 @@ class ViTEngine:
 
     def _blocks_fp8(self, t: torch.Tensor, B: int, N: int) -> torch.Tensor:
         """fp8 encoder blocks: LayerNorms emit e4m3 + per-token scales straight into the qkv / fc1
-        GEMMs; the attention output is re-quantised per token for proj.  fc1 -> fc2: with the HIP GEMM
+        GEMMs; the attention output is re-quantised per token for proj (hipBLASLt) or leaves the
+        attention kernel as MX-fp8 for proj's block-scaled MFMA (HIP GEMM).  fc1 -> fc2: with the HIP GEMM
         the GELU and an MX-fp8 quantisation (E8M0 scale per 32 outputs) run in fc1's epilogue and the
         block scales go into fc2's MFMA scale operand; with hipBLASLt, GELU + per-token quantisation
         run as one pass between the two library GEMMs."""
@@ -239,8 +240,12 @@ class ViTEngine:
         hq = add_layernorm_fp8(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"], cfg.eps)
         for i, b in enumerate(blocks):
             qkv = b["qkv_q"](hq).view(B, N, 3, Hh, D // Hh)
-            a = flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]).view(B, N, D)
-            y = b["proj_q"](a)
+            if b["proj_q"].gemm == "hip":  # attention epilogue -> MX-fp8 -> proj's MFMA scale operand
+                aq, as_ = flash_attention_mx(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2])
+                y = b["proj_q"]((aq.view(B * N, D), as_)).view(B, N, D)
+            else:
+                a = flash_attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]).view(B, N, D)
+                y = b["proj_q"](a)
             h2q = add_layernorm_fp8(t, y, b["g1"], b["n2w"], b["n2b"], cfg.eps)
             if b["fc1_q"].gemm == "hip":  # GELU + MX-fp8 in fc1's epilogue, block scales into fc2's MFMA
                 m = b["fc2_q"](b["fc1_q"](h2q, mx_out=True))

@@ -110,6 +110,29 @@ def flash_attention(q, k, v, scale: float | None = None, rel_h=None, rel_w=None)
     return attention_ref(q, k, v, scale, rel_h, rel_w).to(q.dtype).contiguous()
 
 
+def flash_attention_mx(q, k, v, scale: float | None = None):
+    """Multi-head attention with an MX-fp8 output for the next fp8 GEMM: returns (oq e4m3fn [B, N, H*64],
+    os E8M0 uint8 [B*N, H*2]) -- one power-of-two scale per 32 head dims, quantised from the fp32
+    accumulator in the kernel's epilogue (no bf16 output, no separate quantisation pass).  CPU: the
+    PyTorch reference (fp32 attention, then ``mx_quantize_ref``)."""
+    from .fp8 import FP8_DTYPE, mx_quantize_ref
+
+    B, N, H, D = q.shape
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not q.is_cuda:
+        o = attention_ref(q, k, v, scale).float().reshape(B, N, H * D)
+        oq, os_ = mx_quantize_ref(o)
+        return oq, os_.reshape(B * N, H * D // 32)
+    if not _strides_ok(q, k, v):
+        raise ValueError("flash_attention_mx needs bf16 q/k/v with head_dim 64 and identical strides")
+    oq = torch.empty(B, N, H * D, device=q.device, dtype=FP8_DTYPE)
+    os_ = torch.empty(B * N, H * D // 32, device=q.device, dtype=torch.uint8)
+    sb, st, sh = q.stride(0), q.stride(1), q.stride(2)
+    _native.call("be_attn_fwd_mx", _native.ptr(q), _native.ptr(k), _native.ptr(v), st, sh, sb, _native.ptr(oq),
+                 _native.ptr(os_), B, H, N, D, float(scale), _native.stream(q.device))
+    return oq, os_
+
+
 # ------------------------------------------------------------------ layer norm / residual
 
 def add_layernorm_ref(x, y, gamma, w, b, eps: float = 1e-6):

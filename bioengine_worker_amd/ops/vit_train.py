@@ -98,12 +98,12 @@ def _colsum(p: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
 
 
 def colsum_bf16(x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-    """out (fp32 [C]) = column sums of x [rows, C] (bf16 on GPU: per-64-row fp32 partials by
-    ``be_colpart_bf16``, then the (deferrable) partial reduction)."""
+    """out (fp32 [C]) = column sums of x [rows, C] (bf16 on GPU: per-16-row fp32 partials by
+    ``be_colpart_bf16``, 16 rows each, then the (deferrable) partial reduction)."""
     C = x.shape[-1]
     rows = x.numel() // C
     if x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and C % 8 == 0:
-        part = torch.empty(-(-rows // 64), C, device=x.device, dtype=torch.float32)
+        part = torch.empty(-(-rows // 16), C, device=x.device, dtype=torch.float32)
         _native.call("be_colpart_bf16", _native.ptr(x), _native.ptr(part), rows, C, _native.stream(x.device))
         return _colsum(part, out)
     return torch.sum(x.reshape(rows, C), 0, dtype=torch.float32, out=out.view(-1))

@@ -39,6 +39,9 @@ struct AttnArgs {
   int B, H, N;
   float scale;
   int qblocks;         // ceil(N / (32 * NW))
+  uint8_t* oq;         // optional MX-fp8 output instead of o: e4m3 with o's strides (bytes) ...
+  uint8_t* os;         // ... + E8M0 scales [B * N, H * 2] (one per 32 head dims), the block-scaled
+                       // input of the next fp8 GEMM (gemm_fp8.hip, XS) with no quantisation pass
 };
 
 __device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
@@ -279,6 +282,35 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd_kernel(AttnArgs a) {
 
   // ---- epilogue: O = O^T / l  (lane = query, d = db*32 + 8(i>>2) + 4h + (i&3))
   const float lt = l + __shfl_xor(l, 32, 64);
+  if (a.oq) {  // MX-fp8: block db = head dims [32 db, +32) = this lane's 16 values + the partner lane's
+    const float inv = 1.f / lt;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      float amax = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) amax = fmaxf(amax, fabsf(oacc[db][i] * inv));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      // smallest power of two 2^e with amax / 2^e <= 448 (E8M0 byte e + 127), as gemm_fp8.hip EPI 2
+      int e = amax > 0.f ? (int)ceilf(__log2f(amax * (1.f / 448.f))) : -127;
+      if (e > 0 && amax * __builtin_ldexpf(1.f, -e) > 448.f) ++e;
+      e = max(-127, min(127, e));
+      const float sc = inv * __builtin_ldexpf(1.f, -e);
+      if (qi < a.N) {
+        uint8_t* oqb = a.oq + (long long)b * a.o_batch + (long long)hh * a.o_head + (long long)qi * a.o_tok + db * 32;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(oacc[db][4 * g + 0] * sc, -448.f), 448.f),
+                                                  fminf(fmaxf(oacc[db][4 * g + 1] * sc, -448.f), 448.f), 0, false);
+          w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(oacc[db][4 * g + 2] * sc, -448.f), 448.f),
+                                              fminf(fmaxf(oacc[db][4 * g + 3] * sc, -448.f), 448.f), w, true);
+          *reinterpret_cast<uint32_t*>(oqb + 8 * g + 4 * h) = (uint32_t)w;
+        }
+        if (h == 0) a.os[((long long)b * a.N + qi) * (2 * a.H) + 2 * hh + db] = (uint8_t)(e + 127);
+      }
+    }
+    if (qi < a.N && a.lse && h == 0) a.lse[(long long)bh * a.N + qi] = (m + __log2f(lt)) * 0.6931471805599453f;
+    return;
+  }
   if (qi < a.N) {
     const float inv = 1.f / lt;
     bf16_t* ob = a.o + (long long)b * a.o_batch + (long long)hh * a.o_head + (long long)qi * a.o_tok;
@@ -308,27 +340,9 @@ int launch_nw(AttnArgs a, hipStream_t s) {
   return BE_CHECK_LAUNCH();
 }
 
-}  // namespace
-
-extern "C" {
-
-// q/k/v: bf16 with element strides (token, head, batch) shared by the three (e.g. a packed
-// [B, N, 3, H, 64] qkv buffer); o: bf16 with its own strides.  head_dim must be 64.
 // nw = 0 picks the waves per block (2, 3 or 4 x 32 queries) that least overpads N.
-int be_attn_fwd(const void* q, const void* k, const void* v, long long s_tok, long long s_head, long long s_batch,
-                void* o, long long o_tok, long long o_head, long long o_batch, float* lse, const float* relh,
-                const float* relw, int Hg, int Wg, int B, int H, int N, int head_dim, float scale, int nw,
-                hipStream_t stream) {
-  if (head_dim != HD) return -1;
-  if (N <= 0 || B <= 0 || H <= 0) return 0;
-  if ((relh == nullptr) != (relw == nullptr)) return -2;
-  if (relh && (Hg <= 0 || Wg <= 0 || Hg * Wg != N)) return -3;
-  AttnArgs a;
-  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
-  a.s_tok = s_tok; a.s_head = s_head; a.s_batch = s_batch;
-  a.o = (bf16_t*)o; a.o_tok = o_tok; a.o_head = o_head; a.o_batch = o_batch;
-  a.lse = lse; a.relh = relh; a.relw = relw; a.Hg = Hg; a.Wg = Wg;
-  a.B = B; a.H = H; a.N = N; a.scale = scale;
+int attn_dispatch(AttnArgs a, int nw, hipStream_t stream) {
+  const int N = a.N;
   if (nw == 0) {
     const int slices = (N + 31) / 32;
     int best = 4, waste = 1 << 30;
@@ -345,6 +359,47 @@ int be_attn_fwd(const void* q, const void* k, const void* v, long long s_tok, lo
     case 8: return launch_nw<8>(a, stream);
   }
   return -4;
+}
+
+}  // namespace
+
+extern "C" {
+
+// q/k/v: bf16 with element strides (token, head, batch) shared by the three (e.g. a packed
+// [B, N, 3, H, 64] qkv buffer); o: bf16 with its own strides.  head_dim must be 64.
+// nw = 0 picks the waves per block (2, 3 or 4 x 32 queries) that least overpads N.
+// be_attn_fwd with an MX-fp8 output: oq e4m3 [B, N, H, 64] contiguous + os E8M0 [B * N, H * 2].
+int be_attn_fwd_mx(const void* q, const void* k, const void* v, long long s_tok, long long s_head, long long s_batch,
+                   void* oq, void* os, int B, int H, int N, int head_dim, float scale, hipStream_t stream) {
+  if (head_dim != HD) return -1;
+  if (N <= 0 || B <= 0 || H <= 0) return 0;
+  if (!oq || !os) return -2;
+  AttnArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.s_tok = s_tok; a.s_head = s_head; a.s_batch = s_batch;
+  a.o = nullptr; a.o_tok = (long long)H * HD; a.o_head = HD; a.o_batch = (long long)N * H * HD;
+  a.lse = nullptr; a.relh = nullptr; a.relw = nullptr; a.Hg = 0; a.Wg = 0;
+  a.B = B; a.H = H; a.N = N; a.scale = scale;
+  a.oq = (uint8_t*)oq; a.os = (uint8_t*)os;
+  return attn_dispatch(a, 0, stream);
+}
+
+int be_attn_fwd(const void* q, const void* k, const void* v, long long s_tok, long long s_head, long long s_batch,
+                void* o, long long o_tok, long long o_head, long long o_batch, float* lse, const float* relh,
+                const float* relw, int Hg, int Wg, int B, int H, int N, int head_dim, float scale, int nw,
+                hipStream_t stream) {
+  if (head_dim != HD) return -1;
+  if (N <= 0 || B <= 0 || H <= 0) return 0;
+  if ((relh == nullptr) != (relw == nullptr)) return -2;
+  if (relh && (Hg <= 0 || Wg <= 0 || Hg * Wg != N)) return -3;
+  AttnArgs a;
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v;
+  a.s_tok = s_tok; a.s_head = s_head; a.s_batch = s_batch;
+  a.o = (bf16_t*)o; a.o_tok = o_tok; a.o_head = o_head; a.o_batch = o_batch;
+  a.lse = lse; a.relh = relh; a.relw = relw; a.Hg = Hg; a.Wg = Wg;
+  a.B = B; a.H = H; a.N = N; a.scale = scale;
+  a.oq = nullptr; a.os = nullptr;
+  return attn_dispatch(a, nw, stream);
 }
 
 }  // extern "C"

@@ -118,7 +118,11 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
   constexpr int XB = BM * BK, BUF = (BM + BN) * BK;
   constexpr int LOADS = (BM + BN) / 8 / NW;  // glds per thread per K-step
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "row groups must split evenly over waves");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];  // the only LDS object (rule 4a)
+  // XS: one dword (a row's 4 E8M0 bytes of the K step) per lane; every wave issues XSL DMAs so the
+  // counted waits stay uniform; lanes past BM reload rows modulo BM into a spare tail (harmless)
+  constexpr int XSL = XS ? (BM + 64 * NW - 1) / (64 * NW) : 0;
+  constexpr int SCB = XSL * NW * 64 * 4;            // LDS bytes per K step of scales
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF + 2 * SCB];  // the only LDS object (rule 4a)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
@@ -130,39 +134,69 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
 #pragma unroll
     for (int b = 0; b < TM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Epilogue operands (per-channel scales, bias, per-token scales) loaded once, before the K loop:
+  // they are in registers when the epilogue runs, so its stores never sit behind a load.  (Loaded
+  // inside the epilogue, every 8-byte store was followed by the next column's scale load and an
+  // s_waitcnt vmcnt(0) that also waited for the store's write acknowledgement: TM x TN serial
+  // store + load round trips per tile.)
+  // The 256x256 tile (TM * TN = 32) has no registers to spare across its K loop: it loads them all
+  // together at the start of the epilogue instead (one exposed round trip, not TM x TN).
+  constexpr bool EARLY_EPI_LOADS = TM * TN <= 16;
+  float4 swv[TN], bvv[TN];
+  float sxv[TM];
+  auto load_epi = [&]() {
+#pragma unroll
+    for (int a = 0; a < TN; ++a) {
+      const int n = min(n0 + wn + a * 16 + 4 * (lane >> 4), N - 4);
+      swv[a] = *reinterpret_cast<const float4*>(sw + n);
+      bvv[a] = bias ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int b = 0; b < TM; ++b) sxv[b] = XS ? 1.f : sx[min(m0 + wm + b * 16 + (lane & 15), M - 1)];
+  };
+  if constexpr (EARLY_EPI_LOADS) load_epi();
+
   const int nk = K / BK;
   const int kb32 = K / 32;
-  int xsc[XS ? TM : 1], xsn[XS ? TM : 1];  // this lane's X block scales (current / next K step)
-  auto load_xs = [&](int kt, int (&dst)[XS ? TM : 1]) {
+  // XS: the X block scales of each K step ride along with its tile: dword LDS-DMAs stage the BM
+  // rows x 4 E8M0 bytes next to the tile, and each lane reads its (row, 32-block)
+  // byte after the barrier like a fragment.  (Held in registers, the scales loaded for step kt+1
+  // had to be copied into the set step kt+2 reads, and that copy compiled to an s_waitcnt
+  // vmcnt(0) that drained the next tile's DMA every K step.)
+  auto stage_xs = [&](int kt, uint8_t* dst) {
     if constexpr (XS) {
 #pragma unroll
-      for (int b = 0; b < TM; ++b) {
-        const int m = min(m0 + wm + b * 16 + (lane & 15), M - 1);
-        dst[b] = Xs[(long long)m * kb32 + kt * 4 + (lane >> 4)];
+      for (int i = 0; i < XSL; ++i) {
+        const int r = ((i * NW + wave) * 64 + lane) % BM;  // row whose 4 scale bytes this lane moves
+        const int m = min(m0 + r, M - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(Xs + (long long)m * kb32 + kt * 4),
+                                         (lds_void*)(dst + (i * NW + wave) * 256), 4, 0, 0);
       }
     }
   };
-  load_xs(0, xsc);
   stage_tile<BM, NW>(X, K, m0, M, 0, smem, wave, lane);
   stage_tile<BN, NW>(W, K, n0, N, 0, smem + XB, wave, lane);
+  stage_xs(0, smem + 2 * BUF);
   for (int kt = 0; kt < nk; ++kt) {
     const uint8_t* buf = smem + (kt & 1) * BUF;
     if (kt + 1 < nk) {
       uint8_t* nxt = smem + ((kt + 1) & 1) * BUF;
       stage_tile<BM, NW>(X, K, m0, M, (kt + 1) * BK, nxt, wave, lane);
       stage_tile<BN, NW>(W, K, n0, N, (kt + 1) * BK, nxt + XB, wave, lane);
-      if constexpr (XS) {
-        load_xs(kt + 1, xsn);  // issued after the DMA: the counted wait below then also covers it
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm(LOADS + TM));
-      } else {
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm(LOADS));  // tile kt landed; tile kt+1 stays in flight
-      }
+      stage_xs(kt + 1, smem + 2 * BUF + ((kt + 1) & 1) * SCB);
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(LOADS + XSL));  // step kt landed; step kt+1 stays in flight
     } else {
       __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
     }
     __builtin_amdgcn_s_barrier();
     const uint8_t* xt = buf;
     const uint8_t* wt = buf + XB;
+    int xsc[XS ? TM : 1];
+    if constexpr (XS) {
+      const uint8_t* sc = smem + 2 * BUF + (kt & 1) * SCB;
+#pragma unroll
+      for (int b = 0; b < TM; ++b) xsc[b] = sc[(wm + b * 16 + (lane & 15)) * 4 + (lane >> 4)];
+    }
     i32x8 bx[TM];
 #pragma unroll
     for (int b = 0; b < TM; ++b) bx[b] = read_frag(xt, wm + b * 16 + (lane & 15), lane);
@@ -178,11 +212,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
     if (PRIO) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // WAR: the next iteration restages the buffer read here
-    if constexpr (XS) {
-#pragma unroll
-      for (int b = 0; b < TM; ++b) xsc[b] = xsn[b];
-    }
   }
+  // One unconditional wait for the hoisted epilogue operands: a wait the compiler places inside the
+  // guarded (m < M, n < N) store blocks does not carry across their joins, so it would re-wait
+  // (vmcnt(0), i.e. for every earlier store's acknowledgement too) before each of them.
+  if constexpr (!EARLY_EPI_LOADS) load_epi();
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
   if constexpr (EPI == 2) {
     // GELU -> MX-fp8: a 32-output block of row m is tiles a, a+1 (16 columns each) x the 4 lane
     // groups sharing lane & 15 x 4 values; amax over it = lane-local max of 8 + two xor shuffles.
@@ -190,20 +225,17 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
 #pragma unroll
     for (int b = 0; b < TM; ++b) {
       const int m = m0 + wm + b * 16 + (lane & 15);
-      const float s_m = XS ? 1.f : sx[min(m, M - 1)];
+      const float s_m = sxv[b];
 #pragma unroll
       for (int a = 0; a < TN; a += 2) {
         float v[2][4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int n = min(n0 + wn + (a + h) * 16 + 4 * (lane >> 4), N - 4);
-          const float4 swv = *reinterpret_cast<const float4*>(sw + n);
-          float4 bv = {0.f, 0.f, 0.f, 0.f};
-          if (bias) bv = *reinterpret_cast<const float4*>(bias + n);
-          v[h][0] = gelu_erf(acc[a + h][b][0] * s_m * swv.x + bv.x);
-          v[h][1] = gelu_erf(acc[a + h][b][1] * s_m * swv.y + bv.y);
-          v[h][2] = gelu_erf(acc[a + h][b][2] * s_m * swv.z + bv.z);
-          v[h][3] = gelu_erf(acc[a + h][b][3] * s_m * swv.w + bv.w);
+          const float4 sv = swv[a + h], bv = bvv[a + h];
+          v[h][0] = gelu_erf(acc[a + h][b][0] * s_m * sv.x + bv.x);
+          v[h][1] = gelu_erf(acc[a + h][b][1] * s_m * sv.y + bv.y);
+          v[h][2] = gelu_erf(acc[a + h][b][2] * s_m * sv.z + bv.z);
+          v[h][3] = gelu_erf(acc[a + h][b][3] * s_m * sv.w + bv.w);
         }
         float amax = 0.f;
 #pragma unroll
@@ -239,18 +271,16 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_fp8_kernel(
   for (int b = 0; b < TM; ++b) {
     const int m = m0 + wm + b * 16 + (lane & 15);
     if (m >= M) continue;
-    const float s_m = XS ? 1.f : sx[m];
+    const float s_m = sxv[b];
 #pragma unroll
     for (int a = 0; a < TN; ++a) {
       const int n = n0 + wn + a * 16 + 4 * (lane >> 4);
       if (n >= N) continue;
-      const float4 swv = *reinterpret_cast<const float4*>(sw + n);
-      float4 bv = {0.f, 0.f, 0.f, 0.f};
-      if (bias) bv = *reinterpret_cast<const float4*>(bias + n);
-      float v0 = acc[a][b][0] * s_m * swv.x + bv.x;
-      float v1 = acc[a][b][1] * s_m * swv.y + bv.y;
-      float v2 = acc[a][b][2] * s_m * swv.z + bv.z;
-      float v3 = acc[a][b][3] * s_m * swv.w + bv.w;
+      const float4 sv = swv[a], bv = bvv[a];
+      float v0 = acc[a][b][0] * s_m * sv.x + bv.x;
+      float v1 = acc[a][b][1] * s_m * sv.y + bv.y;
+      float v2 = acc[a][b][2] * s_m * sv.z + bv.z;
+      float v3 = acc[a][b][3] * s_m * sv.w + bv.w;
       if (EPI == 1) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3); }
       u32x2 o;
       o[0] = pack2bf(v0, v1);
@@ -327,6 +357,16 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restric
 
 extern "C" {
 
+// Tile by shape, measured on the ViT-B/14 batch-64 shapes (profiles/r03/fp8/fp8_bench_s23.jsonl, per-config
+// TF/s): 256x256 for long K (fc2: 1552 vs 1393 TF/s for 128x128, even at 195 tiles on 256 CUs) and for
+// narrow N (proj: 851 vs 826) as long as the grid is at least half full; otherwise 128x128 on 8
+// waves, 64x32 per wave with the GELU epilogue (fc1: 986 vs 962), 32x64 without (qkv: 1023 vs 1018).
+static int pick_cfg(int M, int N, int K, int epi) {
+  const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  if ((K >= 2048 || N <= 1024) && t256 >= 128) return 4;
+  return epi == 0 ? 6 : 5;
+}
+
 // Y[M,N] bf16 = epi(Xq[M,K] e4m3 . Wq[N,K]^T e4m3 * sx[M] * sw[N] + bias[N]); epi 0 = none, 1 = GELU.
 // K % 128 == 0, N % 4 == 0; any M.  cfg selects the block tile (0 = by shape):
 //   1: 128x128 (4 waves, 64x64 each)   2: 256x128 (8 waves)   3: 128x256 (8 waves)
@@ -336,11 +376,7 @@ extern "C" {
 int be_gemm_fp8(const void* xq, const void* wq, const float* sx, const float* sw, const float* bias, void* y, int M,
                 int N, int K, int epi, int cfg, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || K % BK != 0 || N % 4 != 0) return -1;
-  if (cfg == 0) {  // measured (profiles/r02/fp8_gemm_bench_r02.md): 256x256 only pays for long K on a full
-                   // grid; otherwise 128x128 on 8 waves (+10-15 % over 4 waves at K = 768; 16 waves: no gain)
-    const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    cfg = (K >= 2048 && t256 >= 256) ? 4 : 6;
-  }
+  if (cfg == 0) cfg = pick_cfg(M, N, K, epi);
   switch (cfg) {
     case 1: return launch_gemm<4, 4, 2, 2, true>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
     case 2: return launch_gemm<4, 4, 4, 2>(xq, wq, sx, sw, bias, y, M, N, K, epi, s);
@@ -353,7 +389,7 @@ int be_gemm_fp8(const void* xq, const void* wq, const float* sx, const float* sw
   }
 }
 
-// MX-fp8 variants of be_gemm_fp8 (tile by shape as cfg 0 picks it, 4 or 6):
+// MX-fp8 variants of be_gemm_fp8 (tile by shape: pick_cfg):
 //   xs != null: X carries E8M0 block scales xs [M, K/32] (sx unused); else per-row fp32 sx.
 //   epi 0 / 1: y bf16 [M, N] (GELU for 1);  epi 2: GELU -> yq e4m3 [M, N] + ys E8M0 [M, N/32] (N % 32 == 0).
 int be_gemm_fp8_mx(const void* xq, const float* sx, const void* xs, const void* wq, const float* sw,
@@ -362,8 +398,7 @@ int be_gemm_fp8_mx(const void* xq, const float* sx, const void* xs, const void* 
   if (epi == 2 && (N % 32 != 0 || !yq || !ys)) return -3;
   if (epi != 2 && !y) return -3;
   if (!xs && !sx) return -4;
-  const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
-  const bool big = K >= 2048 && t256 >= 256;
+  const int cfg = pick_cfg(M, N, K, epi);
   const uint8_t* X = (const uint8_t*)xq;
   const uint8_t* Wt = (const uint8_t*)wq;
   const uint8_t* Xs = (const uint8_t*)xs;
@@ -379,10 +414,13 @@ int be_gemm_fp8_mx(const void* xq, const float* sx, const void* xs, const void* 
   }
 #define MXE(TM, TN, WM, WN, PR, XSV) \
   if (epi == 2) MXL(TM, TN, WM, WN, PR, 2, XSV) else if (epi == 1) MXL(TM, TN, WM, WN, PR, 1, XSV) else MXL(TM, TN, WM, WN, PR, 0, XSV)
-  if (xs) {  // block-scaled X: 128x128 tiles only (the 256x256 tile's scale registers spill)
-    MXE(2, 4, 4, 2, true, true)
+  // block-scaled X: the scales come from LDS per K step (stage_xs), so the 256x256 tile takes them too
+  if (cfg == 4) {
+    if (xs) MXE(8, 4, 2, 4, false, true) else MXE(8, 4, 2, 4, false, false)
+  } else if (cfg == 5) {
+    if (xs) MXE(4, 2, 2, 4, true, true) else MXE(4, 2, 2, 4, true, false)
   } else {
-    if (big) MXE(8, 4, 2, 4, false, false) else MXE(2, 4, 4, 2, true, false)
+    if (xs) MXE(2, 4, 4, 2, true, true) else MXE(2, 4, 4, 2, true, false)
   }
 #undef MXE
 #undef MXL

@@ -121,6 +121,16 @@ __global__ __launch_bounds__(256) void relpos_bwd_dq_kernel(const float* __restr
       acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[cb], 0, 0, 0);
     }
   }
+  // all 32 dq reads issued before any store: a read after a store would wait (vmcnt) for the
+  // store's acknowledgement too, serialising 32 store + load round trips per lane
+  float dqv[16][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int tok = tok_of(pass, line, 8 * (i >> 2) + 4 * h + (i & 3));
+    const float* dr = dq + (long long)b * q_batch + (long long)tok * q_tok + (long long)hh * q_head;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) dqv[i][cb] = dr[cb * 32 + l32];
+  }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int tok = tok_of(pass, line, 8 * (i >> 2) + 4 * h + (i & 3));
@@ -128,7 +138,7 @@ __global__ __launch_bounds__(256) void relpos_bwd_dq_kernel(const float* __restr
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const int c = cb * 32 + l32;
-      const float v = dr[c] + acc[cb][i];
+      const float v = dqv[i][cb] + acc[cb][i];
       if (out_bf16)
         out_bf16[(long long)b * o_batch + (long long)tok * o_tok + (long long)hh * o_head + c] = f2bf(v);
       else

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
 // matrices per step (LayerNorm dw/db, bias gradients); each reduced by its own launch costs a
 // kernel boundary (~5 us at batch 1) for a few us of work.  The descriptors travel by value in the
 // kernarg segment; blocks are laid out entry after entry (start[] prefix sums, scanned by the
-// block's scalar unit) and reduce exactly like colsum_kernel (same summation order, same result).
+// block's scalar unit); fixed summation order (deterministic).
 constexpr int COLSUM_BATCH = 48;
 struct ColsumBatch {
   int n;
@@ -267,45 +267,42 @@ struct ColsumBatch {
 };
 
 __global__ __launch_bounds__(256) void colsum_batched_kernel(const ColsumBatch b) {
-  __shared__ float red[32][9];
+  // block = 64 columns x 4 row-waves: every wave-load is one contiguous 256-byte row segment
+  __shared__ float red[4][64];
   const int blk = blockIdx.x;
   int e = 0;
   while (e + 1 < b.n && blk >= b.start[e + 1]) ++e;
   const float* __restrict__ p = b.p[e];
   const int rows = b.rows[e], C = b.C[e];
-  const int cl = threadIdx.x & 7, rl = threadIdx.x >> 3;
-  const int c = (blk - b.start[e]) * 8 + cl;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blk - b.start[e]) * 64 + lane;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (c < C) {
-    int r = rl;
-    for (; r + 96 < rows; r += 128) {
+    int r = w;
+    for (; r + 12 < rows; r += 16) {
       a0 += p[(long long)r * C + c];
-      a1 += p[(long long)(r + 32) * C + c];
-      a2 += p[(long long)(r + 64) * C + c];
-      a3 += p[(long long)(r + 96) * C + c];
+      a1 += p[(long long)(r + 4) * C + c];
+      a2 += p[(long long)(r + 8) * C + c];
+      a3 += p[(long long)(r + 12) * C + c];
     }
-    for (; r < rows; r += 32) a0 += p[(long long)r * C + c];
+    for (; r < rows; r += 4) a0 += p[(long long)r * C + c];
   }
-  red[rl][cl] = (a0 + a1) + (a2 + a3);
+  red[w][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
-  if (rl == 0 && c < C) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) t += red[i][cl];
-    b.o[e][c] = t;
-  }
+  if (w == 0 && c < C) b.o[e][c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-// Column partial sums of a bf16 [rows, C] matrix: block (x, y) sums rows [64 y, 64 y + 64) of columns
-// [1024 x, +1024) (8 per thread, one 16-byte load per row) into part[y, :] (fp32); the [ceil(rows/64), C]
+// Column partial sums of a bf16 [rows, C] matrix: block (x, y) sums rows [16 y, 16 y + 16) of columns
+// [1024 x, +1024) (8 per thread, 16-byte loads, 8 rows in flight) into part[y, :] (fp32); the [ceil(rows/16), C]
 // partials then go through a colsum (batched with the others).  Replaces torch's bf16 dim-0 reduction
 // of the packed dqkv gradient (the qkv bias gradient), which ran at ~2.3 TB/s.
 __global__ __launch_bounds__(128) void colpart_bf16_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
                                                            int rows, int C) {
   const int c = (blockIdx.x * 128 + threadIdx.x) * 8;
   if (c >= C) return;
-  const int r0 = blockIdx.y * 64, r1 = min(rows, r0 + 64);
+  const int r0 = blockIdx.y * 16, r1 = min(rows, r0 + 16);
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
   for (int r = r0; r < r1; ++r) {
     const u32x4 v = *reinterpret_cast<const u32x4*>(x + (long long)r * C + c);
 #pragma unroll
@@ -400,10 +397,10 @@ int be_colsum(const float* p, float* out, int rows, int C, hipStream_t s) {
   return BE_CHECK_LAUNCH();
 }
 
-// part [ceil(rows / 64), C] fp32 = per-64-row column sums of x bf16 [rows, C]; C % 8 == 0.
+// part [ceil(rows / 16), C] fp32 = per-16-row column sums of x bf16 [rows, C]; C % 8 == 0.
 int be_colpart_bf16(const void* x, float* part, int rows, int C, hipStream_t s) {
   if (rows <= 0 || C <= 0 || C % 8 != 0) return -1;
-  hipLaunchKernelGGL(colpart_bf16_kernel, dim3((unsigned)((C / 8 + 127) / 128), (unsigned)((rows + 63) / 64)), dim3(128),
+  hipLaunchKernelGGL(colpart_bf16_kernel, dim3((unsigned)((C / 8 + 127) / 128), (unsigned)((rows + 15) / 16)), dim3(128),
                      0, s, (const bf16_t*)x, part, rows, C);
   return BE_CHECK_LAUNCH();
 }
@@ -432,7 +429,7 @@ int be_colsum_batched(const long long* desc, int n, hipStream_t s) {
       b.C[i] = (int)d[3];
       if (!b.p[i] || !b.o[i] || b.rows[i] <= 0 || b.C[i] <= 0) return -2;
       b.start[i] = blocks;
-      blocks += (b.C[i] + 7) / 8;
+      blocks += (b.C[i] + 63) / 64;
     }
     b.start[b.n] = blocks;
     hipLaunchKernelGGL(colsum_batched_kernel, dim3((unsigned)blocks), dim3(256), 0, s, b);

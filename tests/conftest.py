@@ -28,6 +28,23 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
+@pytest.fixture(autouse=True)
+def _isolate_app_installs():
+    """Apps deployed in-process append their pip ``--target`` directory to ``sys.path``
+    (``apps/requirements.py``); undo that after each test so one test's wheelhouse installs (e.g.
+    ``bioengine_testdep``) are not importable in the next one."""
+    before = list(sys.path)
+    mods = set(sys.modules)
+    yield
+    from bioengine_worker_amd.apps import requirements as _req
+
+    for p in [p for p in sys.path if p not in before]:
+        sys.path.remove(p)
+        _req._APP_PATHS.discard(p)
+    for m in [m for m in sys.modules if m not in mods and m.startswith("bioengine_testdep")]:
+        del sys.modules[m]
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch

@@ -30,12 +30,13 @@ def test_fp8_linear_cpu_close_to_fp32():
     assert err < 0.05, err
 
 
-def test_vit_engine_fp8_cpu_embedding_close():
+@pytest.mark.parametrize("fp8_gemm", ["hipblaslt", "hip"])
+def test_vit_engine_fp8_cpu_embedding_close(fp8_gemm):
     cfg = ViTConfig(embed_dim=128, depth=2, num_heads=2, img_size=70)
     net = ViT(cfg).randomize_(0).eval()
     x = torch.randn(2, 3, 56, 56)
     ref = net(x)
-    out = ViTEngine(net, "cpu", img_size=56, precision="fp8").embed(x, normalize=False)
+    out = ViTEngine(net, "cpu", img_size=56, precision="fp8", fp8_gemm=fp8_gemm).embed(x, normalize=False)
     cos = torch.nn.functional.cosine_similarity(out, ref.float(), dim=1)
     assert cos.min() > 0.98, cos
     with pytest.raises(ValueError):
@@ -188,3 +189,27 @@ def test_vit_engine_fp8_hip_mx_embedding_close(gpu):
     out = ViTEngine(net, gpu, precision="fp8", fp8_gemm="hip").embed(x.to(gpu))
     cos = torch.nn.functional.cosine_similarity(out, ref, dim=1)
     assert cos.min() > 0.99, cos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N,H", [(2, 257, 12), (1, 100, 2)])
+def test_attention_mx_fp8_output_matches_reference(gpu, B, N, H):
+    """Attention epilogue -> MX-fp8 (E8M0 per 32 head dims) vs the fp32 attention quantised by the
+    PyTorch MX reference: the same block scales (up to a rounding-boundary flip) and dequantised
+    values within one e4m3 step of the block."""
+    from bioengine_worker_amd.ops.fp8 import mx_dequant_ref, mx_quantize_ref
+    from bioengine_worker_amd.ops.transformer import attention_ref, flash_attention_mx
+
+    g = torch.Generator().manual_seed(7)
+    qkv = (torch.randn(B, N, 3, H, 64, generator=g) * 1.5).to(gpu).bfloat16()
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    oq, os_ = flash_attention_mx(q, k, v)
+    torch.cuda.synchronize()
+    ref = attention_ref(q.float(), k.float(), v.float(), 64 ** -0.5).reshape(B * N, H * 64)
+    rq, rs = mx_quantize_ref(ref)
+    assert os_.shape == rs.shape and oq.shape == (B, N, H * 64)
+    assert (os_.cpu().int() - rs.cpu().int()).abs().max().item() <= 1
+    assert (os_.cpu() == rs.cpu()).float().mean().item() > 0.99
+    deq = mx_dequant_ref(oq.reshape(B * N, H * 64), os_).cpu()
+    step = torch.exp2(os_.cpu().float() - 127.0).repeat_interleave(32, dim=1) * 32  # e4m3 step at the block max
+    assert ((deq - ref.cpu()).abs() <= step).all()
