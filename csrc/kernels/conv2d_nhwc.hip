@@ -31,6 +31,8 @@
 //    the tap offsets into ds_read immediates instead of holding ~50 swizzled addresses in VGPRs.
 //    The previous +8 padding measured ~4 conflict cycles per LDS instruction
 //    (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS; profiles/conv_pmc_swizzled.txt shows 0 after the fix).
+#include <cstdlib>
+
 #include "common.h"
 
 // Tuning experiments only (tools/build_native.py --variant): 1 = no halo loads, 2 = no output
@@ -71,7 +73,24 @@ struct ConvArgs {
   int out_f32_nchw;
   int tiles_x, tiles_y;
   int persist_blocks;  // 0 = auto
+  int cot;             // output-channel blocks (block order 2)
+  int order;           // conv2d_nhwc_kernel block order: 0 tile-major, 2 XCD-grouped co-major (1-D grid)
 };
+
+// Block order of the one-block-per-tile kernel.  Tile-major (grid x = tile, y = cout block) sends
+// the cot blocks that read one input halo through the GPU ~`tiles` blocks apart: by the time the
+// second one runs, the halo has left the XCD's 4 MiB L2 and comes back from the Infinity Cache
+// (the deep 3x3 layers moved ~2.2 GB per 32-image batch through L2 -> LDS at ~7 TB/s).  Order 2
+// numbers blocks so that each XCD works through a contiguous range of (tile, cout block) pairs,
+// cout block fastest: a tile's cot blocks run back to back on one XCD and share its L2 copy of the
+// halo, and the layer's weights stay L2-resident on every XCD.  BE_CONV_ORDER overrides (A/B).
+static int conv_block_order() {
+  static int o = [] {
+    const char* e = getenv("BE_CONV_ORDER");
+    return e ? atoi(e) : 2;
+  }();
+  return o;
+}
 
 template <int KS, int CK, int TCO, int INMODE, bool X2, int NW>
 struct Cfg {
@@ -502,11 +521,19 @@ __global__ __launch_bounds__(NW * 64, X2 ? 1 : CONV_KERNEL_WPE) void conv2d_nhwc
   const int lrow = lane & 15;
   const int kq = lane >> 4;
   const int tiles_per_img = a.tiles_x * a.tiles_y;
-  const int tile = CONV_CO_MAJOR ? blockIdx.y : blockIdx.x;
+  int tile, cob;
+  if (a.order == 2) {
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    tile = lid / a.cot;
+    cob = lid % a.cot;
+  } else {
+    tile = CONV_CO_MAJOR ? blockIdx.y : blockIdx.x;
+    cob = CONV_CO_MAJOR ? blockIdx.x : blockIdx.y;
+  }
   const int n = tile / tiles_per_img;
   const int ty0 = ((tile % tiles_per_img) / a.tiles_x) * C::TH;
   const int tx0 = ((tile % tiles_per_img) % a.tiles_x) * TW;
-  const int co0 = (CONV_CO_MAJOR ? blockIdx.x : blockIdx.y) * TCO;
+  const int co0 = cob * TCO;
   f32x4 acc[C::NCT][4];
 #pragma unroll
   for (int i = 0; i < C::NCT; ++i)
@@ -549,6 +576,14 @@ int launch(ConvArgs a, hipStream_t s) {
   const int cot = (a.Cout + TCO - 1) / TCO;
   // persistent blocks: ~4 resident workgroups per CU across the cout tiles (256 CUs)
   if constexpr (TCO > 32) {  // non-persistent variant: one block per tile
+    a.cot = cot;
+    a.order = conv_block_order();
+    if (a.order == 2 && (long long)tiles * cot < (1LL << 31)) {
+      hipLaunchKernelGGL((conv2d_nhwc_kernel<KS, CK, TCO, INMODE, X2, NW>), dim3((unsigned)(tiles * cot)), dim3(C::NT),
+                         C::LDS, s, a);
+      return BE_CHECK_LAUNCH();
+    }
+    a.order = 0;
     if (CONV_CO_MAJOR && tiles > 65535) return -13;
     hipLaunchKernelGGL((conv2d_nhwc_kernel<KS, CK, TCO, INMODE, X2, NW>), CONV_CO_MAJOR ? dim3(cot, tiles) : dim3(tiles, cot),
                        dim3(C::NT), C::LDS, s, a);
