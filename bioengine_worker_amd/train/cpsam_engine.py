@@ -68,7 +68,16 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> None:
             except Exception:  # noqa: BLE001
                 continue
     m, n, k = dy.shape[0], dy.shape[1], x.shape[1]
-    if _MM_MODE == 2 and m >= 4096 and m % 4 == 0 and n * k <= 3072 * 1024:
+    # the 4096-wide fc1 / fc2 weight gradients: hipBLASLt runs them as one 128x128 tile per CU (256
+    # tiles, K = 8192 each); split-K 2 + the vectorised slab sum measured 34.42 -> 33.37 ms per batch-8
+    # step (profiles/r03/cpsam/wgrad_split_wide_ab.txt; split 4: 33.45).  BE_WGRAD_SPLIT_WIDE=0 turns it off.
+    wide_split = int(os.environ.get("BE_WGRAD_SPLIT_WIDE", "2"))
+    if _MM_MODE == 2 and wide_split > 1 and m >= 4096 and m % wide_split == 0 and n * k > 3072 * 1024:
+        ws = torch.empty(wide_split, n, k, device=dy.device, dtype=torch.float32)
+        torch.bmm(dy.reshape(wide_split, m // wide_split, n).transpose(1, 2), x.reshape(wide_split, m // wide_split, k),
+                  out_dtype=torch.float32, out=ws)
+        vt.sum_slabs(ws, out2)
+    elif _MM_MODE == 2 and m >= 4096 and m % 4 == 0 and n * k <= 3072 * 1024:
         # split-K: the [n, k] output is <= 192 hipBLASLt 128x128 tiles, under one per CU, so the
         # m = B*N reduction runs as 4 batched slices + an fp32 sum (profiles/r02/attn/wgrad.jsonl:
         # proj 57.8 -> 37.7 us, qkv 87.6 -> 74.6 us; the 4096-wide fc1 / fc2 outputs gain nothing)
