@@ -43,6 +43,9 @@ from ..ops import gemm
 from ..ops import vit_train as vt
 from ..parallel.ddp import FlatParams
 
+#: smallest token count m at which the <= 192-tile weight gradients run split-K 4 (A/B knob; at batch 1,
+#: m = 1024, splitting measured slower: 11.39-11.74 vs 11.91-12.02 ms, profiles/r03/cpsam/wgrad_split_b1_ab.txt)
+_SPLIT_MIN_M = int(os.environ.get("BE_WGRAD_SPLIT_MIN_M", "4096"))
 _MM_MODE: int | None = None  # 2: mm(out_dtype=fp32, out=grad view), 1: mm(out_dtype=fp32) + copy, 0: bf16 mm + copy
 
 
@@ -77,7 +80,7 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor) -> None:
         torch.bmm(dy.reshape(wide_split, m // wide_split, n).transpose(1, 2), x.reshape(wide_split, m // wide_split, k),
                   out_dtype=torch.float32, out=ws)
         vt.sum_slabs(ws, out2)
-    elif _MM_MODE == 2 and m >= 4096 and m % 4 == 0 and n * k <= 3072 * 1024:
+    elif _MM_MODE == 2 and m >= _SPLIT_MIN_M and m % 4 == 0 and n * k <= 3072 * 1024:
         # split-K: the [n, k] output is <= 192 hipBLASLt 128x128 tiles, under one per CU, so the
         # m = B*N reduction runs as 4 batched slices + an fp32 sum (profiles/r02/attn/wgrad.jsonl:
         # proj 57.8 -> 37.7 us, qkv 87.6 -> 74.6 us; the 4096-wide fc1 / fc2 outputs gain nothing)

@@ -238,3 +238,20 @@ def test_batched_colsums_bf16_partials_and_slab_sums(dev):
     out = torch.empty(1024, 3072, device=dev)
     vt.sum_slabs(ws, out)
     torch.testing.assert_close(out, ws.sum(0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,k", [(4096, 1024), (1024, 4096), (3072, 1024), (1024, 1024)])
+def test_wgrad_split_paths_match_fp32(dev, n, k):
+    """Weight-gradient GEMM paths at the batch-8 token count (split-K 2 for the 4096-wide shapes,
+    split-K 4 for the <= 192-tile ones, slab sums on the HIP kernel) vs an fp32 matmul."""
+    from bioengine_worker_amd.train.cpsam_engine import _wgrad
+
+    g = torch.Generator().manual_seed(11)
+    m = 8192
+    dy = torch.randn(m, n, generator=g).to(dev).bfloat16()
+    x = torch.randn(m, k, generator=g).to(dev).bfloat16()
+    out = torch.full((n, k), float("nan"), device=dev)
+    _wgrad(dy, x, out)
+    ref = dy.float().t() @ x.float()
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < 1e-4
