@@ -13,6 +13,8 @@
 //
 // Column sums are never done with atomics: each block owns a row range and writes one partial row
 // [nblocks, C]; the caller reduces the partials (deterministic, and tiny next to the GEMMs).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -327,6 +329,39 @@ __global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict_
   reinterpret_cast<float4*>(out)[i] = t;
 }
 
+// g = gelu(f + bias) as a flat streaming pass (no column sums to keep): every thread converts U
+// independent 8-element chunks, all U 16-byte loads issued before the first store; bias read per
+// chunk (L2 / L1 resident).  The row-blocked rowcol form streamed at ~3.5 TB/s.
+template <int U>
+__global__ __launch_bounds__(256) void gelu_fwd_flat_kernel(const bf16_t* __restrict__ f, const float* __restrict__ bias,
+                                                            bf16_t* __restrict__ g, long long n8, int C8) {
+  const long long base = ((long long)blockIdx.x * U) * 256 + threadIdx.x;
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * 256;
+    if (i < n8) v[u] = *reinterpret_cast<const u32x4*>(f + i * 8);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * 256;
+    if (i >= n8) continue;
+    float bb[8];
+    if (bias) ld8f(bias + (i % C8) * 8, bb);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bb[j] = 0.f;
+    }
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[2 * j] = gelu_f(lo_bf(v[u][j]) + bb[2 * j]);
+      o[2 * j + 1] = gelu_f(hi_bf(v[u][j]) + bb[2 * j + 1]);
+    }
+    st8(g + i * 8, o);
+  }
+}
+
 template <int MODE>
 int launch_rowcol(const bf16_t* a, const bf16_t* f, const float* xf, const float* bias, const float* rs, int rpn,
                   bf16_t* out, float* pcol, long long rows, int C, int rpb, hipStream_t s) {
@@ -374,6 +409,17 @@ int be_ln_bwd(const void* dh, const void* x, const float* stats, const float* w,
 
 // g = gelu(f + bias) (exact erf GELU), bf16 [rows, C].
 int be_gelu_fwd(const void* f, const float* bias, void* g, long long rows, int C, int rpb, hipStream_t s) {
+  static const int flat = [] {
+    const char* e = getenv("BE_GELU_FWD_FLAT");
+    return e ? atoi(e) : 1;
+  }();
+  if (flat && C % 8 == 0) {
+    const long long n8 = rows * (C / 8);
+    constexpr int U = 4;
+    hipLaunchKernelGGL(gelu_fwd_flat_kernel<U>, dim3((unsigned)((n8 + 256 * U - 1) / (256 * U))), dim3(256), 0, s,
+                       (const bf16_t*)f, bias, (bf16_t*)g, n8, C / 8);
+    return BE_CHECK_LAUNCH();
+  }
   return launch_rowcol<0>(nullptr, (const bf16_t*)f, nullptr, bias, nullptr, 1, (bf16_t*)g, nullptr, rows, C, rpb, s);
 }
 
