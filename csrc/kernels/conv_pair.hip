@@ -31,6 +31,8 @@
 //    registers while the current chunk's MFMAs run ("issue early, write late").
 //  * pixel strides are 8 (mod 16) dwords, so ds_read_b128 fragment reads are conflict-free for any
 //    tap offset (same rule as conv2d_nhwc.hip).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -745,7 +747,11 @@ int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
 
 }  // namespace
 
-static int g_pair_grid = 0;  // tuning override (0 = one workgroup per CU)
+// tuning override (0 = one workgroup per CU); BE_PAIR_GRID sets it for A/B runs
+static int g_pair_grid = [] {
+  const char* e = getenv("BE_PAIR_GRID");
+  return e ? atoi(e) : 0;
+}();
 
 extern "C" {
 
