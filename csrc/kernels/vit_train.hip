@@ -61,22 +61,41 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   for (int k = 0; k < NV; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) { aw[k][j] = 0.f; ab[k][j] = 0.f; ac[k][j] = 0.f; }
+  // LN weight: loaded once, not per row
+  float ww[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < C) ld8f(w + c, ww[k]);
+  }
   for (long long row = r0 + wave; row < r1e; row += 4) {
+    // every load of the row (incl. the residual-gradient terms) issued before its first store: a load
+    // behind a store could only be waited for with vmcnt(0), which also waits for the store's ack
     const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    const float sc1 = r1 ? (s1 ? s1[row / rpn] : 1.f) : 0.f;
+    const float sc2 = r2 ? (s2 ? s2[row / rpn] : 1.f) : 0.f;
+    float t1[NV][8], t2[NV][8];
     float g[NV][8], xh[NV][8];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 8;
       if (c < C) {
-        float d[8], xv[8], ww[8];
+        if (r1) ld8f(r1 + row * C + c, t1[k]);
+        if (r2) ld8f(r2 + row * C + c, t2[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < C) {
+        float d[8], xv[8];
         ld8(dh + row * C + c, d);
         ld8(x + row * C + c, xv);
-        ld8f(w + c, ww);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[k][j] = (xv[j] - mean) * rstd;
-          g[k][j] = d[j] * ww[j];
+          g[k][j] = d[j] * ww[k][j];
           sg += g[k][j];
           sgx += g[k][j] * xh[k][j];
           aw[k][j] += d[j] * xh[k][j];
@@ -86,8 +105,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     }
     sg = wave_sum(sg) / C;
     sgx = wave_sum(sgx) / C;
-    const float sc1 = r1 ? (s1 ? s1[row / rpn] : 1.f) : 0.f;
-    const float sc2 = r2 ? (s2 ? s2[row / rpn] : 1.f) : 0.f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 8;
@@ -96,16 +113,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - sg - xh[k][j] * sgx);
         if (r1) {
-          float t[8];
-          ld8f(r1 + row * C + c, t);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += sc1 * t[j];
+          for (int j = 0; j < 8; ++j) o[j] += sc1 * t1[k][j];
         }
         if (r2) {
-          float t[8];
-          ld8f(r2 + row * C + c, t);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += sc2 * t[j];
+          for (int j = 0; j < 8; ++j) o[j] += sc2 * t2[k][j];
         }
         if (dx) st8f(dx + row * C + c, o);
         if (dxb) st8(dxb + row * C + c, o);
