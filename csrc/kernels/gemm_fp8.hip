@@ -23,6 +23,14 @@
 //   bf16 runs along N (the row-major output's contiguous axis).
 // * Block -> tile mapping is XCD-aware (common.h xcd_remap): consecutive tiles of one M-panel run
 //   on one XCD and share its L2 copy of the activation panel.
+// * MX-fp8 activations (XS): E8M0 scales per row and 32-wide K block go into the MFMA's scale
+//   operand; each K step's [rows][4] scale bytes ride along with the tile (dword LDS-DMA) and are read
+//   after the barrier like a fragment.  Producers: this kernel's EPI 2 (fc1: GELU + block
+//   quantisation) and the attention epilogue (attention.hip, oq / os) for proj.
+// * Nothing in the main loop waits on an ordinary global load: the epilogue operands (channel
+//   scales, bias, row scales) are loaded before the K loop (or all at once at its end for the
+//   256x256 tile) behind one unconditional wait, so no store waits for another round trip.
+// * Default GEMM of Fp8Linear (ops/fp8.py); tile choice: pick_cfg.
 #include "common.h"
 
 namespace {
