@@ -59,6 +59,10 @@ def _upsert_registry(ws: str, entry: dict) -> None:
     _save_registry(ws, reg)
 
 
+def _is_npy_b64(s: str) -> bool:
+    return s[:8] == base64.b64encode(b"\x93NUMPY")[:8].decode()
+
+
 def _decode_image_b64(s: str) -> np.ndarray:
     data = base64.b64decode(s)
     if data[:6] == b"\x93NUMPY":
@@ -140,9 +144,21 @@ class CellImageSearch:
 
         try:
             self._index, self._metadata_df, self._index_info, self._thumbnails = await asyncio.to_thread(load)
-            return True
         except FileNotFoundError:
             return False
+        await asyncio.to_thread(self._prepare_results_tables)
+        return True
+
+    def _prepare_results_tables(self) -> None:
+        """Per-result lookups for the serving path: metadata as plain per-column Python lists
+        (no pandas row access per result) and the base64 PNG thumbnails encoded at ingestion."""
+        from bioengine_worker_amd.search.ingestion import index_dir, read_thumbnails_b64
+
+        df = self._metadata_df
+        self._meta_cols = [(c, df[c].tolist()) for c in df.columns] if df is not None else []
+        self._meta_n = len(df) if df is not None else 0
+        n = len(self._thumbnails) if self._thumbnails is not None else 0
+        self._thumbs_b64 = read_thumbnails_b64(index_dir(self._workspace_dir), n) if n else None
 
     async def _start_dataset_ingestion(self, ds: dict) -> str:
         from bioengine_worker_amd.search import ingestion as ing
@@ -355,7 +371,8 @@ class CellImageSearch:
         mean queueing wait) for the embedding forward and the index scan."""
         from bioengine_worker_amd.serve.batching import batch_stats
 
-        return {"embed": batch_stats(self, "_embed_batch") or {}, "search": batch_stats(self, "_search_batch") or {}}
+        return {"query": batch_stats(self, "_query_batch") or {}, "embed": batch_stats(self, "_embed_batch") or {},
+                "search": batch_stats(self, "_search_batch") or {}}
 
     @serve.batch(max_batch_size=64, batch_wait_timeout_s=0.001, max_concurrent_batches=2)
     async def _search_batch(self, reqs: list) -> list:
@@ -385,16 +402,79 @@ class CellImageSearch:
         return v
 
     def _results(self, scores, ids) -> list:
+        cols = getattr(self, "_meta_cols", None)
+        if cols is None or getattr(self, "_meta_n", -1) != (len(self._metadata_df) if self._metadata_df is not None else 0):
+            self._prepare_results_tables()
+            cols = self._meta_cols
+        nmeta = self._meta_n
+        tb = getattr(self, "_thumbs_b64", None)
+        nth = len(self._thumbnails) if self._thumbnails is not None else 0
         out = []
-        for rank, (s, i) in enumerate(zip(scores, ids)):
+        for rank, (s, i) in enumerate(zip(scores.tolist(), ids.tolist())):
             if i < 0:
                 continue
-            meta = self._metadata_df.iloc[int(i)].to_dict() if self._metadata_df is not None and i < len(self._metadata_df) else {}
-            thumb = ""
-            if self._thumbnails is not None and i < len(self._thumbnails):
-                thumb = self._thumb_b64(int(i))
-            out.append({"rank": rank + 1, "score": float(s), "faiss_idx": int(i), **meta, "thumbnail_b64": thumb})
+            r = {"rank": rank + 1, "score": s, "faiss_idx": i}
+            if i < nmeta:
+                for c, col in cols:
+                    r[c] = col[i]
+            r["thumbnail_b64"] = (tb[i] if tb is not None else self._thumb_b64(i)) if i < nth else ""
+            out.append(r)
         return out
+
+    # One batched call per group of concurrent queries: decode-free GPU pre-processing (percentile
+    # stretch + bicubic resize + ImageNet norm, K18 kernels), ONE fp8 ViT-B/14 forward, ONE index
+    # scan, the query thumbnails from the same resized uint8 tensor, and every request's result list
+    # -- each request then does O(1) Python on the event loop (reference: per request decode, CPU
+    # stretch, PIL thumbnail, single-image embed and FAISS search, main.py:1373-1418).
+    @serve.batch(max_batch_size=64, batch_wait_timeout_s=0.002, max_concurrent_batches=2)
+    async def _query_batch(self, reqs: list) -> list:
+        """reqs: [(image HWC ndarray | None, embedding [D] | None, plow, phigh, top_k)] ->
+        [(results list, query thumbnail base64)]."""
+        import torch
+
+        from bioengine_worker_amd.search.ingestion import png_b64
+        from bioengine_worker_amd.search.preprocess import batch_to_dinov2
+
+        n = len(reqs)
+        groups: dict = {}
+        for i, (img, emb, pl, ph, _) in enumerate(reqs):
+            if emb is None:
+                groups.setdefault((img.shape, img.dtype.str, pl, ph), []).append(i)
+        kmax = max(int(r[4]) for r in reqs)
+
+        def run():
+            dev = self._worker.device
+            q = [None] * n
+            thumbs = {}
+            with self._gpu_lock:
+                for (_, _, pl, ph), idxs in groups.items():
+                    x = torch.from_numpy(np.ascontiguousarray(np.stack([reqs[i][0] for i in idxs]))).to(dev)
+                    t, u8 = batch_to_dinov2(x, None, pl, ph, return_u8=True)
+                    e = self._worker.engine.embed(t).float()
+                    u8h = u8.permute(0, 2, 3, 1).contiguous().cpu().numpy()
+                    for j, i in enumerate(idxs):
+                        q[i] = e[j]
+                        thumbs[i] = u8h[j]
+                for i, (_, emb, _, _, _) in enumerate(reqs):
+                    if emb is not None:
+                        v = torch.as_tensor(np.asarray(emb, np.float32), device=dev)
+                        q[i] = v / v.norm().clamp_min(1e-9)
+                S, I = self._index.search(torch.stack(q), kmax)
+            res = [self._results(S[i, : int(r[4])], I[i, : int(r[4])]) for i, r in enumerate(reqs)]
+            # PNG encoding releases the GIL: the batch's query thumbnails encode in parallel
+            order = sorted(thumbs)
+            enc = dict(zip(order, self._png_pool().map(lambda i: png_b64(thumbs[i], 1), order))) if order else {}
+            return [(res[i], enc.get(i, "")) for i in range(n)]
+
+        return await asyncio.to_thread(run)
+
+    def _png_pool(self):
+        pool = self.__dict__.get("_png_executor")
+        if pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            pool = self.__dict__["_png_executor"] = ThreadPoolExecutor(max_workers=8, thread_name_prefix="png")
+        return pool
 
     @schema_method
     async def search(self, image_b64: str | None = Field(None, description="Base64 image (PNG/JPG/TIFF or .npy bytes)."),
@@ -406,24 +486,18 @@ class CellImageSearch:
         if self._index is None:
             return {"error": "No index loaded. Add a dataset first.", "results": []}
         t0 = time.time()
-        qthumb = ""
-        if embedding is not None:
-            q = np.asarray(embedding, np.float32)
-            q = q / max(np.linalg.norm(q), 1e-9)
-        else:
-            raw = (await asyncio.to_thread(_decode_image_b64, image_b64)) if image_b64 is not None else np.asarray(image)
-            q, rgb = await self._embed_query(raw, plow, phigh)
+        from bioengine_worker_amd.search import reference as ref
 
-            def thumb():
-                from PIL import Image
-
-                from bioengine_worker_amd.search.ingestion import png_b64
-
-                return png_b64(np.asarray(Image.fromarray(rgb).resize((224, 224))))
-
-            qthumb = await asyncio.to_thread(thumb)
-        s_k, i_k = await self._search_batch((q, int(top_k)))
-        results = await asyncio.to_thread(self._results, s_k, i_k)  # metadata rows + thumbnails off the loop
+        img = None
+        if embedding is None:
+            if image_b64 is not None:
+                # .npy payloads decode in microseconds (no thread hop); compressed images in a thread
+                raw = _decode_image_b64(image_b64) if _is_npy_b64(image_b64) else \
+                    await asyncio.to_thread(_decode_image_b64, image_b64)
+            else:
+                raw = np.asarray(image)
+            img = ref.to_hwc(np.asarray(raw))
+        results, qthumb = await self._query_batch((img, embedding, float(plow), float(phigh), int(top_k)))
         return {"results": results, "query_thumbnail_b64": qthumb,
                 "elapsed_ms": round((time.time() - t0) * 1000, 1), "n_cells_searched": self._index.ntotal, "top_k": top_k}
 
@@ -481,6 +555,7 @@ class CellImageSearch:
             merged[c] = merged[c].fillna("unknown")
         merged.to_parquet(meta_path, index=False)
         self._metadata_df = merged
+        self._prepare_results_tables()
         for p in index_dir(self._workspace_dir).glob("umap_cache*.npz"):
             p.unlink()
         n_after = int((merged["compound"] != "unknown").sum()) if "compound" in merged.columns else 0

@@ -187,15 +187,18 @@ class MitoAnalysisDeployment:
                 "token": getattr(ds, "token", None)}
 
     def _model3d_root(self, model_id_3d: str) -> str:
-        from bioengine_worker_amd.bioimageio.package import write_unet3d_package
+        """Directory of an installed 3-D model.  Only ids already present in the local zoo resolve;
+        the id is caller input, so it is never turned into a path of its own, and a missing model is
+        an error (no placeholder weights are ever written under the caller's id)."""
         from bioengine_worker_amd.bioimageio.zoo import list_local_models
 
-        local = list_local_models().get(model_id_3d)
-        if local is not None:
-            return str(local["dir"])
-        root = Path(os.environ.get("HOME", ".")) / "model_zoo" / model_id_3d
+        local = list_local_models().get(str(model_id_3d))
+        if local is None:
+            raise FileNotFoundError(f"no installed 3-D model '{model_id_3d}' in the local model zoo; "
+                                    "install one (model-runner) or use inference='slice2d'")
+        root = Path(local["dir"]).resolve()
         if not (root / "rdf.yaml").exists():
-            write_unet3d_package(root, model_id_3d, in_channels=1, out_channels=1)
+            raise FileNotFoundError(f"model '{model_id_3d}' has no rdf.yaml")
         return str(root)
 
     @schema_method

@@ -34,6 +34,7 @@ import os
 import statistics
 import sys
 import time
+from pathlib import Path
 
 import torch
 import torch.distributed as dist
@@ -266,13 +267,112 @@ def bench_served_search(seconds: float = 4.0) -> dict:
 
     a = _ap.Namespace(concurrency=[1, 64], seconds=seconds, gpus=1, n_images=4, model="vitb14", max_ongoing=64,
                       replica_mode="process")
-    out = {}
+    out, b = {}, {}
     for r in asyncio.run(search_serve_bench.main_async(a)):
         c = r["concurrency"]
         out[f"search_served_qps_c{c}"] = r["qps"]
         out[f"search_served_p50_ms_c{c}"] = r["p50_ms"]
         out[f"search_served_p99_ms_c{c}"] = r["p99_ms"]
+        b = r.get("batching") or {}
+    if b:  # the app's query batcher over the whole run (all concurrency levels)
+        out["search_served_query_batching"] = {k: b[k] for k in ("batches", "requests", "mean_batch", "hist") if k in b}
     return out
+
+
+def bench_em_volume(args, world, rank, dev) -> dict:
+    """BASELINE config 4 (fibsem-mito-analysis): each rank owns a ``--em-z``-slice z-slab of a
+    2048 x 2048 synthetic EM volume (256 slices per GPU = the 2048^3 volume at N=8), written as its own
+    ``.npy`` and read back memory-mapped like the app's gang job reads a volume source
+    (``em.volume.VolumeSource``).  Timed, max over ranks: slab read + H2D, percentiles (all-reduced),
+    slice-wise 512/64 tiled 2-D U-Net inference (graph pass onto the HIP convs) with blending, the
+    sharded touching-object split (remove small, closing, EDT, peaks, marker watershed; halo exchange
+    over RCCL at N > 1), global instance statistics, and ``dist.gather`` of the int32 label volume
+    onto rank 0 (reference: ``apps/fibsem-mito-analysis/analysis_deployment.py:108-176``, which is 2-D
+    and CPU-side).  Stage timings are rank 0's."""
+    import shutil
+    import tempfile
+
+    import numpy as np
+
+    from bioengine_worker_amd.bioimageio.package import write_unet2d_package
+    from bioengine_worker_amd.bioimageio.runner import PredictionPipeline
+    from bioengine_worker_amd.em.volume import VolumeSource, analyze_volume, gather_to_rank0
+    from tools.em_volume_bench import synthetic_slab
+
+    Z, YX = args.em_z, args.em_yx
+    work = Path(tempfile.mkdtemp(prefix=f"be-em-bench-{rank}-", dir=os.environ.get("TMPDIR")))
+    try:
+        root = work / "mito-unet2d"
+        write_unet2d_package(root, "mito-unet2d", in_channels=1, out_channels=1, features=(32, 64, 128, 256),
+                             test_shape=(1, 1, 128, 128), torchscript=False)
+        pipe = PredictionPipeline(root, device=dev)
+        predict = lambda t: next(iter(pipe.predict_tensors(t).values()))  # noqa: E731
+        z0 = rank * Z
+        npy = work / "slab.npy"
+        np.save(npy, synthetic_slab(z0, z0 + Z, YX, YX, dev).cpu().numpy())
+        src = VolumeSource(str(npy))
+        warm = torch.from_numpy(src.read(0, 4)).to(dev)  # graph pass, kernels, allocator
+        analyze_volume(warm, predict, 512, 64, args.em_tile_batch, split_touching=True, norm_range=(90.0, 210.0))
+        del warm
+        _barrier(world)
+        t0 = time.perf_counter()
+        slab = torch.from_numpy(src.read(0, Z)).to(dev)
+        t_read = time.perf_counter()
+        res = analyze_volume(slab, predict, 512, 64, args.em_tile_batch, group=None, z_offset=z0, timings=True,
+                             split_touching=True)
+        tg = time.perf_counter()
+        full = gather_to_rank0(res["labels_slab_t"])
+        torch.cuda.synchronize(dev)
+        t_gather = time.perf_counter() - tg
+        _barrier(world)
+        dt = _max_over_ranks(time.perf_counter() - t0, world)
+        vox = Z * world * YX * YX
+        timings = dict(res["timings_s"])
+        timings["read_h2d"] = round(t_read - t0, 4)
+        timings["gather_rank0"] = round(t_gather, 4)
+        out = {"em_volume_voxels_per_sec": round(vox / dt, 1),
+               "em_volume_config": {"volume": [Z * world, YX, YX], "slab_per_gpu": [Z, YX, YX], "tile": 512,
+                                    "overlap": 64, "tiles_per_call": args.em_tile_batch,
+                                    "model": "BioImage.IO 2-D U-Net 32-64-128-256 (random init, graph pass)",
+                                    "source": "memory-mapped .npy slab per rank", "split_touching": True,
+                                    "gather": "rank0 (dist.gather of int32 labels)", "seconds": round(dt, 3),
+                                    "n_instances": res["n_instances"],
+                                    "rank0_volume": list(full.shape) if full is not None else None,
+                                    "stage_timings_s_rank0": timings}}
+        del slab, full, res
+        return out
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def bench_model_runner_cpu(reps: int = 10) -> dict:
+    """BASELINE config 1 (model-runner plumbing on CPU): one BioImage.IO 2-D U-Net package, a single
+    256x256 tile through the runtime's prediction pipeline on the CPU (pre-processing, padding,
+    forward, post-processing) -- the path ``apps/model-runner/runtime_deployment.py`` serves; reference
+    ``/root/reference/apps/model-runner/runtime_deployment.py:234-312``.  Median of ``reps`` calls."""
+    import tempfile
+
+    import numpy as np
+
+    from bioengine_worker_amd.bioimageio.package import write_unet2d_package
+    from bioengine_worker_amd.bioimageio.runner import PredictionPipeline
+
+    with tempfile.TemporaryDirectory(prefix="be-mr-bench-") as d:
+        root = write_unet2d_package(Path(d) / "unet2d", "unet2d-cpu", in_channels=1, out_channels=2,
+                                    test_shape=(1, 1, 256, 256), torchscript=False)
+        pipe = PredictionPipeline(root, device=torch.device("cpu"))
+        x = np.random.default_rng(0).random((1, 1, 256, 256), dtype=np.float32)
+        pipe.predict(x)
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            pipe.predict(x)
+            ts.append((time.perf_counter() - t) * 1e3)
+        ts.sort()
+        return {"model_runner_cpu_infer_ms": round(ts[len(ts) // 2], 2),
+                "model_runner_cpu_config": {"model": "BioImage.IO 2-D U-Net 32-64-128-256 (random init)",
+                                            "input": [1, 1, 256, 256], "device": "cpu",
+                                            "threads": torch.get_num_threads()}}
 
 
 def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int, force_dp: bool = False):
@@ -331,6 +431,10 @@ def main():
     ap.add_argument("--no-served", action="store_true", help="skip the served (full worker stack) measurement")
     ap.add_argument("--served-seconds", type=float, default=4.0, help="seconds per served concurrency level")
     ap.add_argument("--cpsam-batch", type=int, default=8, help="256x256 crops per step per GPU (Cellpose-SAM)")
+    ap.add_argument("--em-z", type=int, default=256, help="z-slices per GPU of the EM volume line (2048^3 at N=8)")
+    ap.add_argument("--em-yx", type=int, default=2048)
+    ap.add_argument("--em-tile-batch", type=int, default=32, help="512^2 tiles per U-Net call (EM volume line)")
+    ap.add_argument("--no-em", action="store_true", help="skip the EM volume line")
     ap.add_argument("--trace", default=None, metavar="PATH",
                     help="after the timed steps, run one more traced step and write a Chrome trace (rank 0)")
     args = ap.parse_args()
@@ -417,6 +521,16 @@ def main():
                 out["finetune_groupnorm_samples_per_sec"] = round(args.train_batch * args.train_steps / tdt, 2)
         except Exception as e:
             out["extras_error_train"] = f"{type(e).__name__}: {e}"
+        if not args.no_em:
+            try:
+                out.update(bench_em_volume(args, world, rank, dev))
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_em"] = f"{type(e).__name__}: {e}"
+        if rank == 0:
+            try:
+                out.update(bench_model_runner_cpu())
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_model_runner"] = f"{type(e).__name__}: {e}"
         try:
             sps, ms = bench_train_cpsam(args, world, rank, dev, args.cpsam_batch, args.train_steps)
             out["finetune_cpsam_samples_per_sec"] = round(sps, 2)

@@ -125,6 +125,31 @@ def resolve(requirements: list[str], extra_paths: list[str] | None = None) -> tu
     return ok, missing
 
 
+def shadowed(requirements: list[str]) -> list[tuple[str, str]]:
+    """Requirements whose distribution the WORKER environment already has at a version that does not
+    satisfy them.  An in-process replica would import the worker's copy whatever the app's target
+    directory holds (``import`` finds site-packages first), so such an app must run as a process
+    replica with its target at the front of PYTHONPATH."""
+    out = []
+    for raw in requirements or []:
+        raw = (raw or "").strip()
+        if not raw or raw.startswith("#"):
+            continue
+        try:
+            req = Requirement(raw)
+        except InvalidRequirement:
+            continue
+        if req.marker is not None and not req.marker.evaluate():
+            continue
+        name = canonicalize_name(req.name)
+        if name in PROVIDED or not req.specifier:
+            continue
+        ver = _installed_version(name, None)
+        if ver is not None and not req.specifier.contains(ver, prereleases=True):
+            out.append((raw, f"worker has {ver}"))
+    return out
+
+
 def invalid_requirements(requirements: list[str]) -> list[tuple[str, str]]:
     """Entries that must never reach the pip command line: unparsable strings (pip would read
     ``--target=/x``, ``-e path`` or ``--find-links=...`` as options) and direct-URL requirements
@@ -233,11 +258,16 @@ def ensure(requirements: list[str], target: str | Path, wheel_dirs: list[str] | 
         detail = ("no wheelhouse configured (set BIOENGINE_WHEELHOUSE to a directory of wheels)"
                   if not wheel_dirs else f"not satisfiable from the wheelhouse {wheel_dirs}")
         raise MissingRequirementsError(missing, detail)
-    if paths and add_to_sys_path:  # in-process replicas import from the target too
+    shadow = shadowed(pinned)
+    if shadow:
+        log.warning("requirements %s conflict with the worker's own packages: the app runs as a process "
+                    "replica (target first on PYTHONPATH), never in-process", shadow)
+    if paths and add_to_sys_path and not shadow:  # in-process replicas import from the target too
         # appended, not prepended: a package an app installs must never replace a module the worker
         # (or another in-process app) already imports; process replicas get the target at the FRONT
         # of their own PYTHONPATH instead (serve/replica.py), where it affects nobody else
         _APP_PATHS.add(paths[0])
         if paths[0] not in sys.path:
             sys.path.append(paths[0])
-    return {"pinned": pinned, "satisfied": True, "installed": installed, "target": paths[0] if paths else None}
+    return {"pinned": pinned, "satisfied": True, "installed": installed, "target": paths[0] if paths else None,
+            "shadowed": [r for r, _ in shadow]}

@@ -184,7 +184,17 @@ class PredictionPipeline:
         """Whether :meth:`predict_many` can run several requests as one forward: a single-input
         model with a leading batch axis, predicted whole (tiled requests batch their tiles already)."""
         blocksize = blocksize if blocksize is not None else self.blocksize
-        return blocksize is None and len(self.inputs) == 1 and self.inputs[0].axes[0].type == "batch"
+        if blocksize is not None or len(self.inputs) != 1:
+            return False
+        ax0 = self.inputs[0].axes[0]
+        if ax0.type != "batch":
+            return False
+        s = ax0.size  # a fixed batch size (int, or a {min, step: 0} range) cannot take concatenated requests
+        if isinstance(s, int):
+            return False
+        if isinstance(s, dict) and "min" in s and int(s.get("step", 0) or 0) == 0:
+            return False
+        return True
 
     def predict_many(self, samples: list, blocksize: int | None = None) -> list[dict[str, np.ndarray]]:
         """Predict several requests of this model.  Each request is pre- and post-processed on its
@@ -206,8 +216,21 @@ class PredictionPipeline:
             groups.setdefault(tuple(xp.shape), []).append(i)
         results: list = [None] * len(samples)
         for idx in groups.values():
+            if len(idx) == 1:
+                results[idx[0]] = self.predict(samples[idx[0]], blocksize)
+                continue
             xb = torch.cat([prepped[i][0] for i in idx], 0)
-            ys = self._forward([xb])
+            try:
+                ys = self._forward([xb])
+            except Exception:
+                # a graph with a static batch dim (ONNX / TorchScript) rejects the concatenated
+                # batch: run this group one request at a time so each request gets its own result
+                for i in idx:
+                    try:
+                        results[i] = self.predict(samples[i], blocksize)
+                    except Exception as e:  # noqa: BLE001 - per-request error, not the group's
+                        results[i] = e
+                continue
             sizes = [prepped[i][0].shape[0] for i in idx]
             parts = [torch.split(y, sizes, 0) for y in ys]
             for j, i in enumerate(idx):

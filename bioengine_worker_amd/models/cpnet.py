@@ -277,6 +277,7 @@ class CPnetEngine:
         self.style_s = torch.cat(ss, 0).contiguous()
         self.style_t = torch.cat(ts, 0).contiguous()
         self.pair = self._build_pairs(net) if os.environ.get("BE_CPNET_PAIR", "1") != "0" else {}
+        self.ig = self._build_igemm(net) if os.environ.get("BE_CPNET_IGEMM", "1") != "0" else {}
         # output layer fused into the last half-block's epilogue (ops/conv_pair.py HeadSpec)
         self.head = None
         if ("up", 0, 1) in self.pair and self.out.relu and self.nout <= 16 and os.environ.get("BE_CPNET_HEAD", "1") != "0":
@@ -327,6 +328,86 @@ class CPnetEngine:
             assert sp.supports(has_x2, res), key
         return pairs
 
+    def _build_igemm(self, net: CPnet) -> dict:
+        """Implicit-GEMM 3x3 convs (ops/conv_igemm.py) for the deep levels the fused pairs do not
+        cover: every 3x3 conv whose input is NOT resampled (pool2 / up2 inputs stay on the
+        per-layer kernel, which writes its consumer's activated input instead).  Keys:
+        ("down", n, k) / ("up", i, k)."""
+        from ..ops import conv_igemm as igops
+
+        ig = {}
+
+        def add(key, conv: nn.Conv2d):
+            cout, cin, kh, _ = conv.weight.shape
+            if kh == 3 and cin % 16 == 0 and cout % 64 == 0:
+                ig[key] = igops.IgemmConv.from_weight(conv.weight, conv.bias).to(self.device)
+
+        nup = len(net.upsample.up)
+        for n, blk in enumerate(net.downsample.down):
+            if ("down", n, 0) in self.pair or n == 0:
+                continue
+            for k in (1, 2, 3):
+                add(("down", n, k), blk.conv[k][-1])
+        for i, blk in enumerate(net.upsample.up):
+            if ("up", i, 0) in self.pair:
+                continue
+            if i == nup - 1:
+                add(("up", i, 0), blk.conv[0][-1])
+            for k in (1, 2, 3):
+                add(("up", i, k), blk.conv[k].conv[-1])
+        # a level runs on the igemm path only when all of its 3x3 convs do
+        levels = {}
+        for (kind, idx, k) in ig:
+            levels.setdefault((kind, idx), set()).add(k)
+        full = {lv for lv, ks in levels.items() if ks >= {1, 2, 3}}
+        return {key: v for key, v in ig.items() if (key[0], key[1]) in full}
+
+    def _ig_level(self, kind: str, idx: int, x: torch.Tensor, H: int, W: int) -> bool:
+        from ..ops import conv_igemm as igops
+
+        pk = self.ig.get((kind, idx, 1))
+        if pk is None or not x.is_cuda:
+            return False
+        return igops.supported(x.shape[0], H, W, pk.cout, pk.bn)
+
+    def _down_ig(self, n: int, e: dict, src: torch.Tensor, next_act=None) -> torch.Tensor:
+        """resdown on the igemm path: every conv's output is written already activated for its
+        consumer (producer-side pre-activation), so the 3x3 convs stage their inputs by DMA.
+        ``next_act`` = (scale, shift) of the following up block's first conv, which reads this
+        block's output through the igemm path too (written as a second, activated copy)."""
+        from ..ops import conv_igemm as igops
+
+        ig = self.ig
+        proj = e["proj"](src, inmode="pool2")
+        c1, c2, c3 = e["c1"], e["c2"], e["c3"]
+        ha = convops.fused_conv2d(src, e["c0"].pc, scale=e["c0"].scale, shift=e["c0"].shift, relu=True, inmode="pool2",
+                                  post_scale=c1.scale, post_shift=c1.shift, post_relu=True)
+        x1, x1a = igops.conv3_igemm(ha, ig[("down", n, 1)], residual=proj, ascale=c2.scale, ashift=c2.shift)
+        _, h2a = igops.conv3_igemm(x1a, ig[("down", n, 2)], want_out=False, ascale=c3.scale, ashift=c3.shift)
+        if next_act is None:
+            xd, _ = igops.conv3_igemm(h2a, ig[("down", n, 3)], residual=x1)
+            return xd, None
+        return igops.conv3_igemm(h2a, ig[("down", n, 3)], residual=x1, ascale=next_act[0], ashift=next_act[1])
+
+    def _up_ig(self, i: int, e: dict, xcur: torch.Tensor, y: torch.Tensor, shifts: dict, xcur_act=None):
+        from ..ops import conv_igemm as igops
+
+        ig = self.ig
+        c1, c2, c3 = e["c1"], e["c2"], e["c3"]
+        if ("up", i, 0) in ig:  # same resolution: c0 on the igemm path, its input activated upstream
+            proj = e["proj"](xcur)
+            _, h0a = igops.conv3_igemm(xcur_act, ig[("up", i, 0)], residual=y, want_out=False, ascale=c1.scale,
+                                       ashift=shifts[(i, 1)])
+        else:
+            proj = e["proj"](xcur, inmode="up2")
+            h0a = convops.fused_conv2d(xcur, e["c0"].pc, scale=e["c0"].scale, shift=e["c0"].shift, relu=True,
+                                       inmode="up2", residual=y, post_scale=c1.scale, post_shift=shifts[(i, 1)],
+                                       post_relu=True)
+        x1, x1a = igops.conv3_igemm(h0a, ig[("up", i, 1)], residual=proj, ascale=c2.scale, ashift=shifts[(i, 2)])
+        _, h2a = igops.conv3_igemm(x1a, ig[("up", i, 2)], want_out=False, ascale=c3.scale, ashift=shifts[(i, 3)])
+        out, _ = igops.conv3_igemm(h2a, ig[("up", i, 3)], residual=x1)
+        return out
+
     def _style_shifts(self, style: torch.Tensor) -> dict:
         st = style if self.style_on else torch.zeros_like(style)
         return self._split_shifts(styleops.style_shifts(st, self.style_w, self.style_b, self.style_s, self.style_t))
@@ -342,9 +423,18 @@ class CPnetEngine:
         xd = []
         h = x
         P = self.pair
+        nup = len(self.up)
+        top_act = None  # the deepest level's output, activated for up[nup-1].c0 (igemm path)
         for n, e in enumerate(self.down):
             im = "pool2" if n > 0 else "none"
             src = x if n == 0 else xd[-1]
+            if n > 0 and ("down", n, 1) in self.ig and self._ig_level("down", n, src, src.shape[1] // 2,
+                                                                       src.shape[2] // 2):
+                last = n == len(self.down) - 1 and ("up", nup - 1, 0) in self.ig
+                nxt = (self.up[nup - 1]["c0"].scale, self.up[nup - 1]["c0"].shift) if last else None
+                xdn, top_act = self._down_ig(n, e, src, nxt)
+                xd.append(xdn)
+                continue
             if ("down", n, 0) in P:
                 if n == 0:  # stem: projection computed inside the fused kernel (K concatenation)
                     x1 = pairops.conv_pair(src, P[("down", 0, 0)])
@@ -360,12 +450,16 @@ class CPnetEngine:
         style, shifts_all = styleops.style_and_shifts(xd[-1], self.style_w, self.style_b, self.style_s, self.style_t,
                                                       self.style_on)
         shifts = self._split_shifts(shifts_all)
-        nup = len(self.up)
         xcur = xd[-1]
         for i in range(nup - 1, -1, -1):
             e = self.up[i]
             im = "none" if i == nup - 1 else "up2"
             y = xd[i] if i < nup - 1 else xd[-1]
+            H2, W2 = (xcur.shape[1], xcur.shape[2]) if i == nup - 1 else (2 * xcur.shape[1], 2 * xcur.shape[2])
+            if ("up", i, 1) in self.ig and (("up", i, 0) not in self.ig or top_act is not None) and \
+                    self._ig_level("up", i, xcur, H2, W2):
+                xcur = self._up_ig(i, e, xcur, y, shifts, top_act if i == nup - 1 else None)
+                continue
             if ("up", i, 0) in P:
                 # 1x1 projection commutes with nearest upsampling: run it at half resolution and
                 # let the fused kernel read it through an up2 residual

@@ -208,12 +208,15 @@ def _affine_stride(t: torch.Tensor | None, N: int, C: int) -> int:
 def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=None, relu=False, residual=None,
                  inmode: str = "none", out_nchw_f32: bool = False, cout_valid: int | None = None,
                  nw: int | None = None, post_relu: bool = False, out: torch.Tensor | None = None,
-                 no_bias: bool = False) -> torch.Tensor:
+                 no_bias: bool = False, post_scale=None, post_shift=None) -> torch.Tensor:
     """Fused conv on NHWC activations.  ``x`` is [N, Hs, Ws, Cin_pad] bf16 (GPU) or any float (CPU).
     ``relu`` applies to the pre-activation input, ``post_relu`` to the output (after bias/residual).
     ``out`` (bf16 NHWC, contiguous) receives the result in place of a new tensor; it may be the
     ``residual`` itself (every output element reads its residual before it is stored).
-    ``no_bias`` skips ``pc.bias`` (partial sums of a depth-decomposed 3-D conv)."""
+    ``no_bias`` skips ``pc.bias`` (partial sums of a depth-decomposed 3-D conv).
+    ``post_scale`` [Cout] / ``post_shift`` ([Cout] or row-strided [N, Cout]) apply the NEXT conv's
+    pre-activation to the stored value (``y = bf16(y) * post_scale + post_shift``, then ``post_relu``):
+    the producer-side activation that feeds :func:`~.conv_igemm.conv3_igemm`."""
     N, Hs, Ws, Cin = x.shape
     if inmode == "up2":
         H, W = Hs * 2, Ws * 2
@@ -223,8 +226,18 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
         H, W = Hs, Ws
     if not x.is_cuda:
         y = fused_conv2d_ref(x, pc, x2, scale, shift, relu, residual, inmode, out_nchw_f32, cout_valid,
-                             act_dtype=torch.bfloat16 if x.dtype == torch.bfloat16 else None, post_relu=post_relu,
-                             no_bias=no_bias)
+                             act_dtype=torch.bfloat16 if x.dtype == torch.bfloat16 else None,
+                             post_relu=post_relu and post_scale is None and post_shift is None, no_bias=no_bias)
+        if post_scale is not None or post_shift is not None:
+            yf = y.to(torch.bfloat16).float()
+            if post_scale is not None:
+                yf = yf * post_scale.to(yf.device)
+            if post_shift is not None:
+                ps = post_shift.to(yf.device)
+                yf = yf + (ps[:, None, None, :] if ps.dim() == 2 else ps)
+            if post_relu:
+                yf = torch.relu(yf)
+            y = yf.to(y.dtype)
         if out is not None:
             out.copy_(y)
             return out
@@ -253,12 +266,16 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
     # slices of one stacked style GEMM output): rows are read as float4 runs at n * row_stride + c
     pscale_ns = _affine_stride(scale, N, Cin)
     pshift_ns = _affine_stride(shift, N, Cin)
+    qshift_ns = _affine_stride(post_shift, N, pc.cout)
+    if post_scale is not None:
+        assert post_scale.dtype == torch.float32 and post_scale.is_contiguous() and post_scale.numel() == pc.cout
     _native.call(
         "be_conv2d_nhwc",
         _native.ptr(x), _native.ptr(x2), _native.ptr(scale), _native.ptr(shift), pshift_ns, pscale_ns,
         int(bool(relu)) | (2 if post_relu else 0),
         _native.ptr(pc.wp), _native.ptr(None if no_bias else pc.bias), _native.ptr(residual), _native.ptr(out),
         N, H, W, Hs, Ws, Cin, cout_store, cout_valid, pc.ks, pc.ck, pc.tco, INMODES[inmode], int(out_nchw_f32),
-        int(nw or choose_nw(pc, H, W, inmode, x2 is not None)), _native.stream(x.device),
+        int(nw or choose_nw(pc, H, W, inmode, x2 is not None)), _native.ptr(post_scale), _native.ptr(post_shift),
+        qshift_ns, _native.stream(x.device),
     )
     return out

@@ -142,7 +142,8 @@ class VectorIndex:
         self.lists = None
         # list-sorted copy of the vectors: every IVF list is one contiguous HBM slab that the exact
         # scan kernel streams (be_ivf_scan_bf16); built chunk by chunk to bound the temporary
-        if self.device.type == "cuda" and self.dim % 128 == 0 and self.dim <= 1024:
+        # (be_ivf_scan_bf16 is instantiated for dim/128 in {1,2,3,4,6,8}; other dims use the bmm path)
+        if self.device.type == "cuda" and self.dim % 128 == 0 and self.dim // 128 in (1, 2, 3, 4, 6, 8):
             lv = torch.empty_like(self.vecs)
             for i in range(0, order.numel(), CHUNK):
                 lv[i:i + CHUNK] = self.vecs[order[i:i + CHUNK]]

@@ -196,12 +196,34 @@ def _thumbs(crops_u8: torch.Tensor, size: int = 96) -> np.ndarray:
     return t.round().clamp(0, 255).to(torch.uint8).permute(0, 2, 3, 1).cpu().numpy()
 
 
-def png_b64(rgb: np.ndarray) -> str:
+def png_b64(rgb: np.ndarray, compress_level: int = 6) -> str:
     from PIL import Image
 
     buf = io.BytesIO()
-    Image.fromarray(rgb, mode="RGB").save(buf, format="PNG")
+    Image.fromarray(rgb, mode="RGB").save(buf, format="PNG", compress_level=compress_level)
     return base64.b64encode(buf.getvalue()).decode()
+
+
+THUMBS_B64 = "thumbnails_b64.txt"
+
+
+def write_thumbnails_b64(out: Path, thumbs: np.ndarray, start: int = 0) -> None:
+    """Result thumbnails as base64 PNG, one per line, encoded once at ingestion (the reference stores
+    them as base64 strings too, ``apps/cell-image-search/main.py:1404-1408``): serving a result
+    is then a list lookup, never an encode.  ``start`` > 0 appends the thumbnails from that row."""
+    mode = "a" if start > 0 and (out / THUMBS_B64).exists() else "w"
+    rows = range(start if mode == "a" else 0, len(thumbs))
+    with open(out / THUMBS_B64, mode) as f:
+        for i in rows:
+            f.write(png_b64(thumbs[i]) + "\n")
+
+
+def read_thumbnails_b64(out: Path, n: int) -> list | None:
+    p = Path(out) / THUMBS_B64
+    if not p.exists():
+        return None
+    lines = p.read_text().splitlines()
+    return lines if len(lines) == n else None
 
 
 class EmbedWorker:
@@ -371,7 +393,11 @@ def build_or_append(ws: str, E: torch.Tensor, rows: list[dict], thumbs: np.ndarr
     df = df.astype({c: str for c in df.columns if df[c].dtype == object})
     info = idx.save(out)
     df.to_parquet(out / "metadata.parquet", index=False)
+    n_old = 0 if rebuild else len(thumbs) - len(rows)
     np.save(out / "thumbnails.npy", thumbs.astype(np.uint8))
+    if n_old and read_thumbnails_b64(out, n_old) is None:
+        n_old = 0  # no (or a stale) encoded file: encode everything
+    write_thumbnails_b64(out, thumbs.astype(np.uint8), n_old)
     for p in out.glob("umap_cache*.npz"):
         p.unlink()
     return info

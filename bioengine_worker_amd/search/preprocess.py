@@ -87,14 +87,22 @@ def _resample(u8: torch.Tensor, size: int) -> torch.Tensor:
 
 
 def batch_to_dinov2(crops: torch.Tensor, rgb_channels=None, plow: float = 1.0, phigh: float = 99.0,
-                    size: int = 224) -> torch.Tensor:
-    """crops [n, h, w, C] (any numeric dtype, GPU) -> bf16 [n, 3, size, size] ImageNet-normalised."""
+                    size: int = 224, return_u8: bool = False):
+    """crops [n, h, w, C] (any numeric dtype, GPU) -> bf16 [n, 3, size, size] ImageNet-normalised.
+    ``return_u8`` also returns the stretched, resized uint8 RGB [n, 3, size, size] -- the reference's
+    query thumbnail (``to_rgb_uint8`` + PIL bicubic resize to 224, reference main.py:1392-1397)."""
     n, h, w, C = crops.shape
     dev = crops.device
     if not crops.is_cuda:
         arr = crops.cpu().numpy()
-        out = [ref.to_dinov2_array(ref.to_rgb_uint8(a, rgb_channels, plow, phigh), size) for a in arr]
-        return torch.from_numpy(np.stack(out)).to(torch.bfloat16)
+        rgbs = [ref.to_rgb_uint8(a, rgb_channels, plow, phigh) for a in arr]
+        out = torch.from_numpy(np.stack([ref.to_dinov2_array(r, size) for r in rgbs])).to(torch.bfloat16)
+        if not return_u8:
+            return out
+        from PIL import Image
+
+        u8 = np.stack([np.asarray(Image.fromarray(r).resize((size, size), Image.BICUBIC)) for r in rgbs])
+        return out, torch.from_numpy(u8).permute(0, 3, 1, 2).contiguous()
     x = crops.float().contiguous()
     cm = ref.channel_map(C, rgb_channels)
     planes = torch.stack([x[..., c] if c >= 0 else (x[..., 0] + x[..., 1]) * 0.5 for c in cm], 1)  # n,3,h,w
@@ -109,4 +117,4 @@ def batch_to_dinov2(crops: torch.Tensor, rgb_channels=None, plow: float = 1.0, p
         u8 = _resample(u8.view(n * 3, h, w), size).view(n, 3, size, size)
     out = torch.empty(n, 3, size, size, dtype=torch.bfloat16, device=dev)
     _native.call("be_imagenet_norm", _native.ptr(u8), n, size, _native.ptr(out), st)
-    return out
+    return (out, u8) if return_u8 else out

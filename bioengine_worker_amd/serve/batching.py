@@ -125,7 +125,10 @@ class _BatchQueue:
                     raise RuntimeError(f"batched function returned {len(res)} results for {len(items)} inputs")
                 for (_, _, fut, _), r in zip(items, res):
                     if not fut.done():
-                        fut.set_result(r)
+                        if isinstance(r, BaseException):  # a per-request failure inside the batch
+                            fut.set_exception(r)
+                        else:
+                            fut.set_result(r)
             except BaseException as e:  # noqa: BLE001
                 for (_, _, fut, _) in items:
                     if not fut.done():

@@ -151,7 +151,17 @@ class DeploymentState:
             return True
         if mode == "local":
             return False
-        return self.cfg.num_gpus() > 0
+        if self.cfg.num_gpus() > 0:
+            return True
+        pip = (self.cfg.ray_actor_options.get("runtime_env") or {}).get("pip") or []
+        if isinstance(pip, dict):
+            pip = pip.get("packages") or []
+        if pip:
+            from ..apps.requirements import shadowed
+
+            if shadowed([str(r) for r in pip]):  # pinned versions differ from the worker's: isolate
+                return True
+        return False
 
     async def add_replica(self):
         cpus, gpus, mem = self.cfg.num_cpus(), self.cfg.num_gpus(), self.cfg.memory()

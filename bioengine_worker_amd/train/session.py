@@ -30,6 +30,15 @@ log = logging.getLogger("bioengine.train.session")
 STATUS_TYPES = ("waiting", "preparing", "running", "completed", "failed", "stopped", "unknown")
 
 
+def _save_atomic(obj, path: Path) -> None:
+    """torch.save to a temporary file in the same directory, then rename it over ``path``: a rank
+    that dies mid-write (what elastic restart recovers from) never leaves a truncated resume state."""
+    path = Path(path)
+    tmp = path.with_name(f"{path.name}.tmp{os.getpid()}")
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
+
+
 def now_iso() -> str:
     return datetime.now(timezone.utc).isoformat()
 
@@ -206,7 +215,7 @@ def train_session(session_dir: str | Path, params: dict, device=None, rank: int 
                          test_metrics=list(st.get("test_metrics") or []) + [metrics], current_epoch=ep,
                          elapsed_seconds=el, samples_per_sec=round(ep * len(imgs) / max(el, 1e-9), 3))
             save_checkpoint(sdir / "models" / "model", trainer.net)
-            torch.save(trainer.state_dict(), sdir / "models" / "trainer_state.pt")
+            _save_atomic(trainer.state_dict(), sdir / "models" / "trainer_state.pt")
 
         out = run_training(trainer, tx, tl, n_epochs, vx, vl, batch_callback=on_batch, epoch_callback=on_epoch,
                            stop_check=stop_file.exists, diams=diams, rescale=bool(params.get("rescale", False)),
@@ -216,7 +225,7 @@ def train_session(session_dir: str | Path, params: dict, device=None, rank: int 
             return {"rank": rank, "weights_sha256": digest}
         write_status(sdir, weights_sha256=digest)
         save_checkpoint(sdir / "models" / "model", trainer.net)
-        torch.save(trainer.state_dict(), sdir / "models" / "trainer_state.pt")
+        _save_atomic(trainer.state_dict(), sdir / "models" / "trainer_state.pt")
         if out.get("stopped"):
             return write_status(sdir, status_type="stopped", message="Training session stopped by user.")
         if timgs:

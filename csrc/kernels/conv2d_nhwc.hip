@@ -75,6 +75,11 @@ struct ConvArgs {
   int persist_blocks;  // 0 = auto
   int cot;             // output-channel blocks (block order 2)
   int order;           // conv2d_nhwc_kernel block order: 0 tile-major, 2 XCD-grouped co-major (1-D grid)
+  // optional post-activation of the stored value (the NEXT conv's pre-activation, applied by this
+  // producer): v = bf16(v) * qscale[co] + qshift[n * qshift_ns + co], then the prelu bit-1 ReLU
+  const float* qscale;
+  const float* qshift;
+  int qshift_ns;
 };
 
 // Block order of the one-block-per-tile kernel.  Tile-major (grid x = tile, y = cout block) sends
@@ -317,6 +322,21 @@ __device__ __forceinline__ void load_res_regs(const ConvArgs& a, int n, int ty0,
   }
 }
 
+// Post-activation (producer-side pre-activation of the consumer): the affine acts on the
+// bf16-rounded value, exactly as if the consumer re-read this tensor and applied it itself.
+__device__ __forceinline__ void post_affine(const ConvArgs& a, int n, int co, float& v0, float& v1, float& v2,
+                                            float& v3) {
+  if (!a.qscale && !a.qshift) return;
+  const float4 qs = a.qscale ? *reinterpret_cast<const float4*>(a.qscale + co) : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 qt = a.qshift ? *reinterpret_cast<const float4*>(a.qshift + (size_t)n * a.qshift_ns + co)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+  const uint32_t p0 = pack2bf(v0, v1), p1 = pack2bf(v2, v3);
+  v0 = fmaf(lo_bf(p0), qs.x, qt.x);
+  v1 = fmaf(hi_bf(p0), qs.y, qt.y);
+  v2 = fmaf(lo_bf(p1), qs.z, qt.z);
+  v3 = fmaf(hi_bf(p1), qs.w, qt.w);
+}
+
 // rvp: residual registers loaded earlier (load_res_regs), or null to load them here
 template <typename C>
 __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT][4], const float4 (&bias)[C::NCT],
@@ -367,9 +387,14 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
 #pragma unroll
       for (int ct = 0; ct < C::NCT; ++ct) {
         const int col = ct * 16 + kq * 4;
+        float v0 = acc[ct][pt][0] + bias[ct].x + lo_bf(rv[pt][ct][0]);
+        float v1 = acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]);
+        float v2 = acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]);
+        float v3 = acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]);
+        if (co0 + col < a.Cout) post_affine(a, n, co0 + col, v0, v1, v2, v3);
         u32x2 st;
-        st[0] = pack2bf(acc[ct][pt][0] + bias[ct].x + lo_bf(rv[pt][ct][0]), acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]));
-        st[1] = pack2bf(acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]), acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]));
+        st[0] = pack2bf(v0, v1);
+        st[1] = pack2bf(v2, v3);
         if (post) {
           st[0] = relu_bf16x2(st[0]);
           st[1] = relu_bf16x2(st[1]);
@@ -408,6 +433,7 @@ __device__ __forceinline__ void epilogue(const ConvArgs& a, f32x4 (&acc)[C::NCT]
       float v1 = acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]);
       float v2 = acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]);
       float v3 = acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]);
+      post_affine(a, n, co, v0, v1, v2, v3);
       u32x2 st;
       st[0] = pack2bf(v0, v1);
       st[1] = pack2bf(v2, v3);
@@ -645,8 +671,10 @@ int be_conv2d_packed_kp(int ks, int ck) { return ((ks * ks * ck + 31) / 32) * 32
 int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const float* pshift, int pshift_ns, int pscale_ns,
                    int prelu, const void* w, const float* bias, const void* res, void* out, int N, int H, int W,
                    int Hs, int Ws, int Cin, int Cout, int cout_valid, int ks, int ck, int tco, int inmode,
-                   int out_f32_nchw, int nw, hipStream_t stream) {
+                   int out_f32_nchw, int nw, const float* qscale, const float* qshift, int qshift_ns,
+                   hipStream_t stream) {
   if (Cin % ck != 0 || Cout % 4 != 0) return -10;
+  if ((qscale || qshift) && out_f32_nchw) return -14;
   if (!(ks == 1 || ks == 3)) return -11;
   ConvArgs a;
   a.x = (const bf16_t*)x; a.x2 = (const bf16_t*)x2; a.pscale = pscale; a.pshift = pshift;
@@ -656,6 +684,7 @@ int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const flo
   a.nchunk = Cin / ck; a.KP = be_conv2d_packed_kp(ks, ck);
   a.out_f32_nchw = out_f32_nchw;
   a.persist_blocks = g_persist_blocks;
+  a.qscale = qscale; a.qshift = qshift; a.qshift_ns = qshift_ns;
   const bool x2p = x2 != nullptr;
   if (ks == 3) {
     if (ck == 8) return dispatch_tco<3, 8>(tco, inmode, x2p, nw, a, stream);

@@ -126,8 +126,12 @@ def test_cell_image_search_app_e2e(tmp_path, monkeypatch):
             assert len(r["results"]) == 3 + i % 3
             assert r["results"][0]["faiss_idx"] == res["results"][0]["faiss_idx"]
         bs = await app.get_batch_stats()
-        assert bs["embed"]["requests"] >= 13 and bs["embed"]["mean_batch"] > 1.0, bs
-        assert bs["search"]["requests"] >= 13 and bs["search"]["batches"] < bs["search"]["requests"], bs
+        # one batched call per query group: pre-processing, embedding, scan and result lists
+        assert bs["query"]["requests"] >= 13 and bs["query"]["mean_batch"] > 1.0, bs
+        assert bs["query"]["batches"] < bs["query"]["requests"], bs
+        assert res["query_thumbnail_b64"] and many[0]["query_thumbnail_b64"]
+        emb = await app.search(embedding=[1.0] * int(stats.get("embed_dim", 768)), top_k=4)
+        assert len(emb["results"]) == 4 and emb["query_thumbnail_b64"] == ""
         up = await app.get_umap_preview(n_samples=100)
         assert len(up["x"]) == stats["n_cells"] and up["method"] in ("pca", "umap")
         pq = await app.project_query_onto_umap(image_b64=base64.b64encode(buf.getvalue()).decode())

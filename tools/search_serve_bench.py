@@ -93,7 +93,10 @@ async def main_async(a) -> list[dict]:
               "p99_ms": round(float(np.percentile(ms, 99)), 2), "n_cells": n_cells, "model": a.model}
         results.append(rr)
         print(json.dumps(rr), flush=True)
-    print(json.dumps({"batching": await app.get_batch_stats()}), flush=True)
+    bs = await app.get_batch_stats()
+    print(json.dumps({"batching": bs}), flush=True)
+    for rr in results:
+        rr["batching"] = bs.get("query", {})
     await svc.stop_app(application_id=aid)
     await w._cleanup()
     return results
