@@ -23,7 +23,7 @@ from . import _native
 
 @dataclass
 class IgemmConv:
-    """3x3 weights packed in the kernel's LDS image order: [Cout/bn][Cin/16][9][bn/32][2][32][8]."""
+    """3x3 weights packed in the kernel's LDS image order: [Cout/bnc][Cin/16][9][bnc/32][2][32][8]."""
 
     w: torch.Tensor            # fp32 [Cout, Cin, 3, 3]
     bias: torch.Tensor | None  # fp32 [Cout]
@@ -32,18 +32,26 @@ class IgemmConv:
     bn: int
     wp: torch.Tensor | None = None
 
+    @property
+    def bnc(self) -> int:
+        """Output channels per block (bn 65 is the 512 x 64, 8-wave A/B variant of bn 64)."""
+        return 128 if self.bn == 128 else 64
+
     @classmethod
     def from_weight(cls, weight: torch.Tensor, bias: torch.Tensor | None = None, bn: int | None = None) -> "IgemmConv":
+        """``bn``: 64 (default; 256 px x 64 ch on 4 waves, two blocks per CU), 128 (256 x 128, 8 waves)
+        or 65 (512 x 64, 8 waves)."""
         cout, cin, kh, kw = weight.shape
         assert kh == 3 and kw == 3 and cin % 16 == 0 and cout % 64 == 0, "3x3, Cin % 16 == 0, Cout % 64 == 0"
-        bn = bn or (128 if cout % 128 == 0 else 64)
+        bn = bn or 64
+        assert bn in (64, 65, 128) and cout % (128 if bn == 128 else 64) == 0
         pk = cls(w=weight.detach().float(), bias=None if bias is None else bias.detach().float().contiguous(),
                  cin=cin, cout=cout, bn=bn)
         pk.wp = pk.pack(pk.w)
         return pk
 
     def pack(self, w: torch.Tensor) -> torch.Tensor:
-        co, ci, bn = self.cout, self.cin, self.bn
+        co, ci, bn = self.cout, self.cin, self.bnc
         # [co_blk, f, co32, c16, h, j, t]
         t = w.reshape(co // bn, bn // 32, 32, ci // 16, 2, 8, 9)
         # -> [co_blk, c16, t, f, h, co32, j]

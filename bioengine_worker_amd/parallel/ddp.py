@@ -111,6 +111,7 @@ class BucketedAllReduce:
         self.pending = [len(m) for (_, _, m) in self.buckets]
         self.works = []
         self._bufs = []
+        self._order = []
 
     def mark_ready(self, params) -> None:
         """Explicit readiness for engines that write gradients without autograd
@@ -140,8 +141,31 @@ class BucketedAllReduce:
             w = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self._bufs.append((view, buf))
         else:
+            buf = None
             w = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.works.append(w)
+        self._order.append((bi, w, view, buf))
+
+    def finish_each(self, fn) -> None:
+        """Like :meth:`finish`, but hands each bucket to ``fn(start, end, grad_scale)`` as soon as ITS
+        all-reduce is done, in launch order (the order the backward completed them): the optimizer
+        update of the early buckets runs while the last buckets are still on the wire, instead of
+        one whole-model AdamW after the final all-reduce."""
+        if not self.active:
+            fn(0, self.fp.numel, 1.0)
+            return
+        for bi, n in enumerate(self.pending):
+            if n > 0:
+                self.pending[bi] = 0
+                self._launch(bi)
+        scale = 1.0 / self.world
+        for bi, w, view, buf in self._order:
+            w.wait()  # the current stream waits for this bucket's collective only
+            if buf is not None:
+                view.copy_(buf.float())
+            s, e, _ = self.buckets[bi]
+            fn(s, e, scale)
+        self.reset()
 
     def finish(self) -> float:
         """Wait for every bucket (launching any that never filled, e.g. unused params).

@@ -65,6 +65,8 @@ class TrainConfig:
     # batch 8 39.7 -> 41.4-41.8 ms, batch 1 15.3 -> 16.9-17.6 ms: the optimizer's HBM stream slows
     # the backward kernels more than it hides), so the flat update after the replay stays the default.
     cpsam_overlap_adamw: bool = False
+    # data-parallel CPSAM: AdamW per gradient bucket, each right after its own all-reduce
+    cpsam_bucket_adamw: bool = True
     # run the data-parallel step path (segmented graph + bucket all-reduces) even at world 1 over a
     # 1-rank process group: the on-one-GPU measurement of the DP code path's own overhead
     force_dp_path: bool = False
@@ -231,6 +233,14 @@ class CellposeTrainer:
             else:
                 loss = eng.loss_and_backward(x, lbl, keep,
                                              on_params_ready=self.ar.mark_ready if self.ar.active else None)
+        if self.ar.active and not fused_opt and self.cfg.cpsam_bucket_adamw:
+            # per-bucket AdamW, each on its own bucket's all-reduce completion: the update of the
+            # buckets the backward finished first overlaps the last buckets' collectives
+            self.step_count += 1
+            mirror = eng.mirror if eng.mirror is not self.fp.flat else None
+            with trace.span("train.grad_allreduce_adamw", cuda=True):
+                self.ar.finish_each(lambda s, e, sc: self._adamw_range(s, e, sc, mirror))
+            return loss
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
@@ -241,6 +251,13 @@ class CellposeTrainer:
             train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
                                   weight_decay=self.cfg.weight_decay, grad_scale=gscale, p_bf16=mirror)
         return loss
+
+    def _adamw_range(self, s: int, e: int, grad_scale: float, mirror) -> None:
+        """AdamW over flat elements [s, e) (bucket boundaries are 4-element aligned)."""
+        sl = slice(s, e)
+        train_ops.adamw_flat_(self.fp.flat[sl], self.fp.grad[sl], self.m[sl], self.v[sl], lr=self.lr,
+                              step=self.step_count, weight_decay=self.cfg.weight_decay, grad_scale=grad_scale,
+                              p_bf16=mirror[sl] if mirror is not None else None)
 
     def _adamw_group_cb(self, eng, side):
         """on_params_ready callback used during capture: AdamW over the group's flat range on ``side``."""
@@ -348,6 +365,11 @@ class CellposeTrainer:
                         pending[bi] -= 1
                         if pending[bi] == 0:
                             done.append(bi)
+                    if done and not any(pending):
+                        # the last bucket: its all-reduce follows the FINAL segment (which ends with
+                        # whatever the backward still does after this point) -- no empty segment
+                        state["last"] = done
+                        return
                     if done:
                         state["g"].capture_end()
                         segs.append((state["g"], done))
@@ -360,7 +382,7 @@ class CellposeTrainer:
                     state["g"].capture_begin()
                     out = eng.loss_and_backward(xs, ls, ks, on_params_ready=cut)
                     state["g"].capture_end()
-                segs.append((state["g"], [bi for bi, n in enumerate(pending) if n > 0]))
+                segs.append((state["g"], state.get("last", []) + [bi for bi, n in enumerate(pending) if n > 0]))
                 torch.cuda.current_stream(self.device).wait_stream(cap)
             except Exception as e:  # noqa: BLE001
                 import logging

@@ -18,17 +18,20 @@
 //    The tile's input halo is a contiguous range of "padded rows" R = n (H+2) + y + 1 (rows y = -1
 //    and y = H of every image are the zero rows), each W+2 pixels wide, so image boundaries inside a
 //    tile need no special case: a pixel's 3x3 taps never leave its own image's padded rows.
-//  * 8 waves = WM (pixels) x WN (channels); each wave owns 64 pixels x 64 channels = 2 x 2 tiles of
+//  * Waves = WM (pixels) x WN (channels); each wave owns 64 pixels x 64 channels = 2 x 2 tiles of
 //    v_mfma_f32_32x32x16_bf16 (64 fp32 accumulators/lane).  Weights are the A operand (rows = Cout),
-//    pixels the B operand, so a lane ends with 4 consecutive output channels of one pixel.
+//    pixels the B operand, so a lane ends with 4 consecutive output channels of one pixel.  The
+//    default block is 256 pixels x 64 channels on 4 waves with ~65-75 KB of LDS, so two blocks share
+//    a CU and one's barrier wait and epilogue stores overlap the other's MFMAs (one 8-wave block per
+//    CU measured no faster than the per-layer kernel: profiles/r04/conv/igemm_v1.jsonl).
 //  * K chunk = 16 input channels (one 32x32x16 K-step per tap, 9 per chunk).  Two LDS stage buffers:
 //    chunk c+1's DMA is issued right after the barrier that publishes chunk c, and lands under
 //    chunk c's 36 MFMAs per wave.  One barrier per chunk.
-//  * Halo image: 48 bytes per pixel = two 16-byte channel groups + one pad slot.  A fragment read
-//    (ds_read_b128, 16-lane groups {0-3,12-15,20-27}, ...) touches 16 distinct pixels p, whose slots
-//    3p mod 16 are all distinct (3 is odd), so every tap offset is conflict-free, and the tap offset
-//    is an additive constant (one v_add per read).  The DMA writes slots lane-linearly; pad-slot
-//    lanes read the zero page.  Out-of-image pixels read the zero page too (conv zero padding).
+//  * Halo image: 32 bytes per pixel (two 16-byte channel halves, swapped on every other group of 8
+//    pixels, hslot()): every fragment read is conflict-free at every tap shift.  The per-(tap,
+//    fragment) LDS addresses are computed once per tile (18 VGPRs).  The DMA writes slots
+//    lane-linearly, so the swizzle lives in the per-lane SOURCE address; out-of-image pixels read
+//    the zero page (conv zero padding).
 //  * Weights are pre-packed on the host in exactly the LDS image order ([tap][co frag][64 lanes x 16
 //    bytes]): each lane's A fragment is slot `lane` of a 1 KiB block, a linear, conflict-free read.
 //  * XCD-aware block order (T1): the co-blocks of one pixel tile are consecutive logical blocks on
@@ -42,8 +45,14 @@ namespace {
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int SLOT = 16;       // bytes per LDS slot (one dwordx4 DMA lane)
-constexpr int PIXB = 3 * SLOT;  // halo bytes per pixel per 16-channel chunk (2 data slots + 1 pad)
+constexpr int SLOT = 16;  // bytes per LDS slot (one dwordx4 DMA lane); a halo pixel = 2 slots (16 channels)
+
+// Halo slot of channel half h of halo pixel i: two slots per pixel, the halves swapped on every
+// other group of 8 pixels.  A B-fragment read (ds_read_b128, 16-lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31}, ... = 16 pixels at one half) then lands on bank slots
+// 2 (i mod 8) + ((i >> 3) & 1) ^ h, a bijection of i mod 16, and the 16 pixels of a group are
+// distinct mod 16 for ANY tap shift: conflict-free without the 50 % pad slot of a 48-byte stride.
+__device__ __forceinline__ int hslot(int i, int h) { return 2 * i + (h ^ ((i >> 3) & 1)); }
 
 struct IgArgs {
   const bf16_t* x;     // [N, H, W, Cin] activated input
@@ -72,7 +81,7 @@ struct IgCfg {
 };
 
 template <int WM, int WN, int HIMAX>
-__global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) {
+__global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 2) void conv3_igemm_kernel(IgArgs a) {
   using C = IgCfg<WM, WN, HIMAX>;
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -90,7 +99,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) 
   const int Rlo = n0 * H2 + y0;          // = R(n0, y0) - 1
   const int Rhi = n1 * H2 + y1 + 2;      // = R(n1, y1) + 1
   const int npix = (Rhi - Rlo + 1) * W2;
-  const int nhi = (3 * npix + 63) / 64;  // halo DMAs per stage (<= HIMAX * NW, host-checked)
+  const int nhi = (2 * npix + 63) / 64;  // halo DMAs per stage (<= HIMAX * NW, host-checked)
   const int bufb = C::WBYTES + a.hbytes;
 
   // ---- per-lane DMA sources for this tile (chunk 0; chunk c adds 16 channels per step)
@@ -99,9 +108,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) 
   for (int k = 0; k < HIMAX; ++k) {
     const int i = wave + k * C::NW;
     const int s = i * 64 + lane;
-    const int p = s / 3, q = s - 3 * (s / 3);
+    const int p = s >> 1, q = (s & 1) ^ ((p >> 3) & 1);  // inverse of hslot(): source of DMA slot s
     const bf16_t* src = a.zero;
-    if (i < nhi && q < 2 && p < npix) {
+    if (i < nhi && p < npix) {
       const int r = Rlo + p / W2;
       const int c = p - (p / W2) * W2 - 1;
       const int n = r / H2;
@@ -131,8 +140,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) 
     }
   };
 
-  // ---- per-lane B-fragment (pixel) addresses: halo byte offset of this lane's pixel, tap (1,1)
-  int paddr[2];
+  // ---- per-lane B-fragment (pixel) addresses, one per (tap, fragment): halo byte offsets
+  int paddr[9][2];
   int pn[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -142,8 +151,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) 
     const int rem = m - n * a.HW;
     const int y = rem / a.W, x = rem - (rem / a.W) * a.W;
     const int hidx = (n * H2 + y + 1 - Rlo) * W2 + x + 1;
-    paddr[j] = hidx * PIXB + (lane >> 5) * SLOT;
     pn[j] = n;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) paddr[t][j] = hslot(hidx + (t / 3 - 1) * W2 + (t % 3 - 1), lane >> 5) * SLOT;
   }
 
   f32x16 acc[2][2];
@@ -163,12 +173,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) 
     const unsigned char* hb = wb + C::WBYTES;
     bf16x8 wf[2][2], pf[2][2];
     auto ld = [&](int t, bf16x8 (&wfr)[2], bf16x8 (&pfr)[2]) {
-      const int toff = ((t / 3 - 1) * W2 + (t % 3 - 1)) * PIXB;
 #pragma unroll
       for (int f = 0; f < 2; ++f)
         wfr[f] = *reinterpret_cast<const bf16x8*>(wb + (t * C::NCF + wfrag0 + f) * 1024 + lane * SLOT);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) pfr[j] = *reinterpret_cast<const bf16x8*>(hb + paddr[j] + toff);
+      for (int j = 0; j < 2; ++j) pfr[j] = *reinterpret_cast<const bf16x8*>(hb + paddr[t][j]);
     };
     ld(0, wf[0], pf[0]);
 #pragma unroll
@@ -242,7 +251,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) 
 
 template <int WM, int WN>
 int launch_ig(IgArgs a, hipStream_t s) {
-  constexpr int HIMAX = 8;
+  constexpr int HIMAX = WM * WN == 4 ? 8 : 6;
   using C = IgCfg<WM, WN, HIMAX>;
   if (a.Cout % C::BN) return -20;
   a.cob = a.Cout / C::BN;
@@ -254,7 +263,7 @@ int launch_ig(IgArgs a, hipStream_t s) {
   const int rmax = a.N * (a.H + 2);
   if (rows > rmax) rows = rmax;
   const int npix = rows * (a.W + 2);
-  const int nhi = (3 * npix + 63) / 64;
+  const int nhi = (2 * npix + 63) / 64;
   if (nhi > HIMAX * C::NW) return -21;
   a.hbytes = nhi * 1024;
   const size_t lds = 2 * (size_t)(C::WBYTES + a.hbytes);
@@ -284,16 +293,27 @@ static const bf16_t* zero_page() {
 
 extern "C" {
 
+static int ig_geometry(int bn, int* BM, int* NW, int* HIMAX) {
+  // bn 64: 256 pixels x 64 channels, 4 waves (two workgroups per CU when the halo fits: one's
+  // barrier / epilogue overlaps the other's MFMAs); bn 128: 256 x 128, 8 waves; bn 65: 512 x 64,
+  // 8 waves (A/B configurations)
+  if (bn == 64) { *BM = 256; *NW = 4; *HIMAX = 8; return 64; }
+  if (bn == 128) { *BM = 256; *NW = 8; *HIMAX = 6; return 128; }
+  if (bn == 65) { *BM = 512; *NW = 8; *HIMAX = 6; return 64; }
+  return 0;
+}
+
 // LDS bytes a launch would use (0 = shape not supported by this kernel): lets the host pick a path.
 int be_conv3_igemm_lds(int N, int H, int W, int Cout, int bn) {
-  const int BM = bn == 128 ? 256 : 512;
-  const int NW = 8;
+  int BM, NW, HIMAX;
+  const int bnc = ig_geometry(bn, &BM, &NW, &HIMAX);
+  if (!bnc || Cout % bnc) return 0;
   const int HW = H * W;
   int rows = (BM - 1) / W + 2 + 2 * ((BM - 1) / HW + 1) + 2;
   if (rows > N * (H + 2)) rows = N * (H + 2);
-  const int nhi = (3 * rows * (W + 2) + 63) / 64;
-  if (nhi > 8 * NW || Cout % bn) return 0;
-  const long long lds = 2LL * (9 * (bn / 32) * 1024 + nhi * 1024);
+  const int nhi = (2 * rows * (W + 2) + 63) / 64;
+  if (nhi > HIMAX * NW) return 0;
+  const long long lds = 2LL * (9 * (bnc / 32) * 1024 + nhi * 1024);
   return lds > 160 * 1024 ? 0 : (int)lds;
 }
 
@@ -313,7 +333,8 @@ int be_conv3_igemm(const void* x, const void* w, const float* bias, const void* 
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.HW = H * W; a.NP = N * H * W;
   a.nchunk = Cin / 16;
   if (bn == 128) return launch_ig<4, 2>(a, stream);
-  if (bn == 64) return launch_ig<8, 1>(a, stream);
+  if (bn == 64) return launch_ig<4, 1>(a, stream);
+  if (bn == 65) return launch_ig<8, 1>(a, stream);
   return -14;
 }
 

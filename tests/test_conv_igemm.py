@@ -16,6 +16,8 @@ CASES = [
     (4, 56, 56, 128, 128, 128, False, "shared", False),
     (2, 13, 17, 32, 128, 128, True, "image", True),
     (2, 112, 112, 64, 64, 64, True, "image", False),
+    (2, 28, 28, 128, 128, 65, True, "image", False),
+    (3, 56, 56, 128, 128, 64, True, "shared", False),
     (5, 7, 9, 16, 64, 64, False, "shared", False),
 ]
 
@@ -91,7 +93,7 @@ def test_conv3_igemm_cpu_reference_path():
     x = torch.randn(1, 9, 11, 32, generator=g).to(torch.bfloat16)
     w = torch.randn(64, 32, 3, 3, generator=g) / 17
     pk = ig.IgemmConv.from_weight(w, torch.zeros(64))
-    assert pk.wp.numel() == 64 * 32 * 9 and pk.bn == 64
+    assert pk.wp.numel() == 64 * 32 * 9 and pk.bnc == 64
     # packing: block (c16=0, tap 4, f=0), slot h*32+co, element j == W[co][h*8+j][1][1]
     blk = pk.wp.view(1, 2, 9, 2, 2, 32, 8)[0, 0, 4, 0]
     assert torch.equal(blk[1, 5, 3], w[5, 11, 1, 1].to(torch.bfloat16))
