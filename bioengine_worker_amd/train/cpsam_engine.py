@@ -39,7 +39,14 @@ import torch
 import torch.nn.functional as F
 
 from ..models.cpsam import CPSAM, get_rel_pos
-from ..ops import gemm
+import os as _os
+
+# GEMM backend of the engine: the in-house bf16 MFMA GEMMs with fused epilogues (default), or the
+# hipBLASLt-backed helpers of ops/gemm.py (BE_CPSAM_GEMM=lib, the A/B baseline)
+if _os.environ.get("BE_CPSAM_GEMM", "hip") == "lib":
+    from ..ops import gemm
+else:
+    from ..ops import gemm_bf16 as gemm
 from ..ops import vit_train as vt
 from ..parallel.ddp import FlatParams
 

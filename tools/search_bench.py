@@ -43,6 +43,19 @@ def synth(n, d, dev, seed=0, chunk=1 << 22):
     return out
 
 
+def ood_queries(nq, d, dev, seed=7):
+    """Out-of-distribution queries: the database's class centres (same generator as ``synth``) with
+    sub-centre offsets that were NEVER used for indexed vectors, plus noise -- the nearest neighbours
+    are spread over the class instead of sitting next to the query, unlike indexed-vector + noise."""
+    g = torch.Generator(device=dev).manual_seed(0)
+    centres = torch.nn.functional.normalize(torch.randn(4096, d, device=dev, generator=g), dim=1)
+    gq = torch.Generator(device=dev).manual_seed(seed + 1000)
+    cls = torch.randint(0, 4096, (nq,), device=dev, generator=gq)
+    held_out = torch.nn.functional.normalize(torch.randn(nq, d, device=dev, generator=gq), dim=1) * 0.5
+    v = centres[cls] + held_out + 0.2 * torch.randn(nq, d, device=dev, generator=gq) / d ** 0.5
+    return torch.nn.functional.normalize(v, dim=1)
+
+
 def timeit(fn, reps):
     ts = []
     for _ in range(reps):
@@ -69,6 +82,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--nprobes", default="16,32,64,128,256")
     ap.add_argument("--no-pq", action="store_true")
+    ap.add_argument("--queries", default="near,ood", help="near: indexed vectors + small noise; "
+                    "ood: held-out sub-centres of the indexed classes (ood_queries)")
     a = ap.parse_args()
     from bioengine_worker_amd.search.index import VectorIndex
     from bioengine_worker_amd.search.ivfpq import IVFPQIndex, default_nlist
@@ -78,18 +93,24 @@ def main():
         x = synth(n, a.dim, dev)
         gq = torch.Generator(device=dev).manual_seed(7)
         qidx = torch.randint(0, n, (64,), device=dev, generator=gq)
-        q = torch.nn.functional.normalize(x[qidx].float() + 0.02 * torch.randn(64, a.dim, device=dev, generator=gq), dim=1)
+        qsets = {"near": torch.nn.functional.normalize(
+            x[qidx].float() + 0.02 * torch.randn(64, a.dim, device=dev, generator=gq), dim=1),
+            "ood": ood_queries(64, a.dim, dev)}
+        qsets = {k: v for k, v in qsets.items() if k in a.queries.split(",")}
         flat = VectorIndex(dim=a.dim, device=dev, index_type="flat")
         flat.vecs = x
         # ground truth in fp32 (fp32 query x bf16 vectors upcast per chunk): exact up to fp32 rounding
-        gs, gi = [], []
-        for i in range(0, n, 1 << 20):
-            sc = q @ x[i:i + (1 << 20)].float().T
-            ts, ti = torch.topk(sc, a.k, dim=1)
-            gs.append(ts)
-            gi.append(ti + i)
-        ts, j = torch.topk(torch.cat(gs, 1), a.k, dim=1)
-        gt = torch.gather(torch.cat(gi, 1), 1, j).cpu().numpy()
+        gts = {}
+        for qn, qv in qsets.items():
+            gs, gi = [], []
+            for i in range(0, n, 1 << 20):
+                sc = qv @ x[i:i + (1 << 20)].float().T
+                ts, ti = torch.topk(sc, a.k, dim=1)
+                gs.append(ts)
+                gi.append(ti + i)
+            ts, j = torch.topk(torch.cat(gs, 1), a.k, dim=1)
+            gts[qn] = torch.gather(torch.cat(gi, 1), 1, j).cpu().numpy()
+        q = next(iter(qsets.values()))
         for name, fn in (("flat_q1", lambda: flat.search(q[:1], a.k)), ("flat_q64", lambda: flat.search(q, a.k))):
             fn()
             p50, p95 = timeit(fn, a.reps)
@@ -104,13 +125,15 @@ def main():
         build = time.perf_counter() - t0
         nl = ivf.centroids.shape[0]
         for npb in [int(v) for v in a.nprobes.split(",")]:
-            got = ivf.search(q, a.k, nprobe=npb)[1]
-            r10, r1 = recalls(gt, got)
+            rec = {qn: recalls(gts[qn], ivf.search(qv, a.k, nprobe=npb)[1]) for qn, qv in qsets.items()}
+            r10, r1 = next(iter(rec.values()))
             for name, qq in (("q1", q[:1]), ("q64", q)):
                 ivf.search(qq, a.k, nprobe=npb)
                 p50, p95 = timeit(lambda: ivf.search(qq, a.k, nprobe=npb), a.reps)
                 print(json.dumps({"n": n, "tier": "IVF-exact-scan bf16 (HBM)", "nprobe": npb, "nlist": nl, "query": name,
                                   "p50_ms": round(p50, 3), "p95_ms": round(p95, 3), "recall@10": r10, "R@10": r1,
+                                  "recall@10_by_queries": {k: v[0] for k, v in rec.items()},
+                                  "R@10_by_queries": {k: v[1] for k, v in rec.items()},
                                   "build_s": round(build, 2), "hbm_gb": round(2 * x.numel() * 2 / 1e9, 2)}), flush=True)
         del ivf
         torch.cuda.empty_cache()
@@ -130,13 +153,15 @@ def main():
                              (200, "IVFPQ-GPU + exact rerank 4k")):
             vi = VectorIndex(dim=a.dim, device=dev, index_type="ivfpq", refine=refine)
             vi.vecs, vi.pq = x, pq
-            got = vi.search(q, a.k)[1]
-            r10, r1 = recalls(gt, got)
+            rec = {qn: recalls(gts[qn], vi.search(qv, a.k)[1]) for qn, qv in qsets.items()}
+            r10, r1 = next(iter(rec.values()))
             for name, qq in (("q1", q[:1]), ("q64", q)):
                 vi.search(qq, a.k)
                 p50, p95 = timeit(lambda: vi.search(qq, a.k), a.reps)
                 print(json.dumps({"n": n, "tier": tier, "query": name, "p50_ms": round(p50, 3), "p95_ms": round(p95, 3),
-                                  "recall@10": r10, "R@10": r1, "nlist": pq.nlist, "build_s": round(build, 2),
+                                  "recall@10": r10, "R@10": r1, "recall@10_by_queries": {k: v[0] for k, v in rec.items()},
+                                  "R@10_by_queries": {k: v[1] for k, v in rec.items()},
+                                  "nlist": pq.nlist, "build_s": round(build, 2),
                                   "codes_gb": round(pq.codes.numel() / 1e9, 3)}), flush=True)
         del x, flat, pq, vi
         torch.cuda.empty_cache()
