@@ -322,6 +322,10 @@ class CPnetEngine:
                     prev = e["c0"] if k == 1 else e["c2"]
                     if prev.pc.bias is not None:
                         self.style_t[off: off + c] += self.style_s[off: off + c] * prev.pc.bias[:c].to(self.device)
+        # BE_CPNET_PAIR_LEVELS (default "0,1"): the levels (0 = 32 ch at full res, 1 = 64 ch) that
+        # run on the fused pair kernels; the others fall to the igemm / per-layer paths (A/B)
+        keep = {int(v) for v in os.environ.get("BE_CPNET_PAIR_LEVELS", "0,1").split(",") if v.strip()}
+        pairs = {k: v for k, v in pairs.items() if k[1] in keep}
         for key, sp in pairs.items():
             has_x2 = key[0] == "up" and key[2] == 0
             res = "none" if key == ("down", 0, 0) else ("up2" if has_x2 else "full")
