@@ -35,16 +35,16 @@ class IgemmConv:
     @property
     def bnc(self) -> int:
         """Output channels per block (bn 65 is the 512 x 64, 8-wave A/B variant of bn 64)."""
-        return 128 if self.bn == 128 else 64
+        return 128 if self.bn % 1000 == 128 else 64
 
     @classmethod
     def from_weight(cls, weight: torch.Tensor, bias: torch.Tensor | None = None, bn: int | None = None) -> "IgemmConv":
         """``bn``: 64 (default; 256 px x 64 ch on 4 waves, two blocks per CU), 128 (256 x 128, 8 waves)
-        or 65 (512 x 64, 8 waves)."""
+        or 65 (512 x 64, 8 waves); + 1000 = three LDS stages (DMA two chunks ahead)."""
         cout, cin, kh, kw = weight.shape
         assert kh == 3 and kw == 3 and cin % 16 == 0 and cout % 64 == 0, "3x3, Cin % 16 == 0, Cout % 64 == 0"
         bn = bn or 64
-        assert bn in (64, 65, 128) and cout % (128 if bn == 128 else 64) == 0
+        assert bn in (64, 65, 128, 1065, 1128) and cout % (128 if bn % 1000 == 128 else 64) == 0
         pk = cls(w=weight.detach().float(), bias=None if bias is None else bias.detach().float().contiguous(),
                  cin=cin, cout=cout, bn=bn)
         pk.wp = pk.pack(pk.w)

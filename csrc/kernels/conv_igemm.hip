@@ -80,13 +80,30 @@ struct IgCfg {
   static constexpr int WPW = (WBLK + NW - 1) / NW;  // weight DMAs per wave per stage
 };
 
-template <int WM, int WN, int HIMAX>
-__global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 2) void conv3_igemm_kernel(IgArgs a) {
+// s_waitcnt immediate waiting for vmcnt <= n only (gfx9 encoding)
+constexpr int vm_imm(int n) { return (n & 0xf) | (0x7 << 4) | (0xf << 8) | ((n >> 4) << 14); }
+
+// vmcnt <= n for a wave-uniform runtime n (the immediate field needs a constant: one case each)
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+  switch (n) {
+#define BE_VM_CASE(k) \
+  case k: __builtin_amdgcn_s_waitcnt(vm_imm(k)); break;
+    BE_VM_CASE(1) BE_VM_CASE(2) BE_VM_CASE(3) BE_VM_CASE(4) BE_VM_CASE(5) BE_VM_CASE(6) BE_VM_CASE(7)
+    BE_VM_CASE(8) BE_VM_CASE(9) BE_VM_CASE(10) BE_VM_CASE(11) BE_VM_CASE(12) BE_VM_CASE(13) BE_VM_CASE(14)
+    BE_VM_CASE(15) BE_VM_CASE(16)
+#undef BE_VM_CASE
+    default: __builtin_amdgcn_s_waitcnt(vm_imm(0)); break;
+  }
+}
+
+template <int WM, int WN, int HIMAX, int NSTAGE>
+__global__ __launch_bounds__(WM * WN * 64, 2) void conv3_igemm_kernel(IgArgs a) {
   using C = IgCfg<WM, WN, HIMAX>;
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "two or three stage buffers");
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform: scalar branches
   const int wm = wave / WN, wn = wave % WN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = lid / a.cob, cb = lid % a.cob;
@@ -165,11 +182,32 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 2) void conv3_igem
       for (int r = 0; r < 16; ++r) acc[f][j][r] = 0.f;
 
   const int wfrag0 = wn * 2;
+  // this wave's DMAs per stage (wave-uniform, the same for every chunk of the tile)
+  int nw_loads = 0;
+#pragma unroll
+  for (int k = 0; k < C::WPW; ++k) nw_loads += (wave + k * C::NW < C::WBLK);
+#pragma unroll
+  for (int k = 0; k < HIMAX; ++k) nw_loads += (wave + k * C::NW < nhi);
   stage(0, smem);
+  if (NSTAGE == 3 && a.nchunk > 1) stage(1, smem + bufb);
   for (int c = 0; c < a.nchunk; ++c) {
-    __syncthreads();  // vmcnt(0): chunk c landed (every wave); WAR: chunk c-1's buffer is free
-    if (c + 1 < a.nchunk) stage(c + 1, smem + ((c + 1) & 1) * bufb);
-    const unsigned char* wb = smem + (c & 1) * bufb;
+    int cur_buf;
+    if constexpr (NSTAGE == 2) {
+      __syncthreads();  // vmcnt(0): chunk c landed (every wave); WAR: chunk c-1's buffer is free
+      if (c + 1 < a.nchunk) stage(c + 1, smem + ((c + 1) & 1) * bufb);
+      cur_buf = c & 1;
+    } else {
+      // three buffers, chunk c+1's DMA stays in flight across the barrier: wait until at most this
+      // wave's per-stage DMA count is outstanding (a counted wait; the count is wave-uniform)
+      if (c + 1 < a.nchunk) wait_vm_dyn(nw_loads);
+      else __builtin_amdgcn_s_waitcnt(vm_imm(0));
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // chunk c is in LDS for every wave; chunk c-1's buffer is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 2 < a.nchunk) stage(c + 2, smem + ((c + 2) % 3) * bufb);
+      cur_buf = c % 3;
+    }
+    const unsigned char* wb = smem + cur_buf * bufb;
     const unsigned char* hb = wb + C::WBYTES;
     bf16x8 wf[2][2], pf[2][2];
     auto ld = [&](int t, bf16x8 (&wfr)[2], bf16x8 (&pfr)[2]) {
@@ -249,7 +287,7 @@ __global__ __launch_bounds__(WM * WN * 64, WM * WN == 4 ? 2 : 2) void conv3_igem
   }
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int NSTAGE>
 int launch_ig(IgArgs a, hipStream_t s) {
   constexpr int HIMAX = WM * WN == 4 ? 8 : 6;
   using C = IgCfg<WM, WN, HIMAX>;
@@ -266,17 +304,17 @@ int launch_ig(IgArgs a, hipStream_t s) {
   const int nhi = (2 * npix + 63) / 64;
   if (nhi > HIMAX * C::NW) return -21;
   a.hbytes = nhi * 1024;
-  const size_t lds = 2 * (size_t)(C::WBYTES + a.hbytes);
+  const size_t lds = NSTAGE * (size_t)(C::WBYTES + a.hbytes);
   if (lds > 160 * 1024) return -22;
   const long long nblk = (long long)a.tiles * a.cob;
   if (nblk >= (1LL << 31)) return -23;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)conv3_igemm_kernel<WM, WN, HIMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv3_igemm_kernel<WM, WN, HIMAX, NSTAGE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv3_igemm_kernel<WM, WN, HIMAX>), dim3((unsigned)nblk), dim3(C::NT), lds, s, a);
+  hipLaunchKernelGGL((conv3_igemm_kernel<WM, WN, HIMAX, NSTAGE>), dim3((unsigned)nblk), dim3(C::NT), lds, s, a);
   return BE_CHECK_LAUNCH();
 }
 
@@ -304,7 +342,10 @@ static int ig_geometry(int bn, int* BM, int* NW, int* HIMAX) {
 }
 
 // LDS bytes a launch would use (0 = shape not supported by this kernel): lets the host pick a path.
+// bn + 1000: the three-stage variant.
 int be_conv3_igemm_lds(int N, int H, int W, int Cout, int bn) {
+  const int nst = bn >= 1000 ? 3 : 2;
+  bn %= 1000;
   int BM, NW, HIMAX;
   const int bnc = ig_geometry(bn, &BM, &NW, &HIMAX);
   if (!bnc || Cout % bnc) return 0;
@@ -313,7 +354,7 @@ int be_conv3_igemm_lds(int N, int H, int W, int Cout, int bn) {
   if (rows > N * (H + 2)) rows = N * (H + 2);
   const int nhi = (2 * rows * (W + 2) + 63) / 64;
   if (nhi > HIMAX * NW) return 0;
-  const long long lds = 2LL * (9 * (bnc / 32) * 1024 + nhi * 1024);
+  const long long lds = (long long)nst * (9 * (bnc / 32) * 1024 + nhi * 1024);
   return lds > 160 * 1024 ? 0 : (int)lds;
 }
 
@@ -332,9 +373,13 @@ int be_conv3_igemm(const void* x, const void* w, const float* bias, const void* 
   if (!a.zero) return -13;
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.HW = H * W; a.NP = N * H * W;
   a.nchunk = Cin / 16;
-  if (bn == 128) return launch_ig<4, 2>(a, stream);
-  if (bn == 64) return launch_ig<4, 1>(a, stream);
-  if (bn == 65) return launch_ig<8, 1>(a, stream);
+  switch (bn) {  // bn + 1000: three stage buffers (DMA two chunks ahead, counted waits)
+    case 128: return launch_ig<4, 2, 2>(a, stream);
+    case 64: return launch_ig<4, 1, 2>(a, stream);
+    case 65: return launch_ig<8, 1, 2>(a, stream);
+    case 1128: return launch_ig<4, 2, 3>(a, stream);
+    case 1065: return launch_ig<8, 1, 3>(a, stream);
+  }
   return -14;
 }
 

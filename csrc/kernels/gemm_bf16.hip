@@ -128,7 +128,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_bf16_kernel(GArgs a) {
   constexpr int ABYTES = BM * BK * 2, BBYTES = BN * BK * 2, SBYTES = ABYTES + BBYTES;
   constexpr int LOADS = BM / 8 / NW + BN / 8 / NW;  // DMAs per wave per stage (either layout)
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int sp = lid % a.split;
@@ -157,7 +157,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_bf16_kernel(GArgs a) {
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + 1 < nk) __builtin_amdgcn_s_waitcnt(vm_wait(LOADS));  // tile kt landed, kt+1 in flight
     else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();  // every wave's DMA of kt is in; every wave is done reading kt-1
+    __builtin_amdgcn_sched_barrier(0);  // no LDS read of tile kt is scheduled above the barrier
     if (kt + 2 < nk) stage(kt + 2, smem + ((kt + 2) % 3) * SBYTES);
     const unsigned char* ta = smem + (kt % 3) * SBYTES;
     const unsigned char* tb = ta + ABYTES;

@@ -17,6 +17,9 @@ CASES = [
     (2, 13, 17, 32, 128, 128, True, "image", True),
     (2, 112, 112, 64, 64, 64, True, "image", False),
     (2, 28, 28, 128, 128, 65, True, "image", False),
+    (3, 28, 28, 256, 256, 1128, True, "image", False),
+    (2, 56, 56, 128, 128, 1065, True, "shared", True),
+    (3, 13, 17, 64, 64, 1065, False, "image", False),
     (3, 56, 56, 128, 128, 64, True, "shared", False),
     (5, 7, 9, 16, 64, 64, False, "shared", False),
 ]

@@ -54,8 +54,8 @@ def main():
         t = torch.zeros(cout, device=dev)
         flops = 2.0 * N * H * W * cin * cout * 9
         rows = []
-        for bn in (64, 128, 65):
-            if cout % (128 if bn == 128 else 64) or not ig.supported(N, H, W, cout, bn):
+        for bn in (64, 128, 65, 1128, 1065):
+            if cout % (128 if bn % 1000 == 128 else 64) or not ig.supported(N, H, W, cout, bn):
                 continue
             pk = ig.IgemmConv.from_weight(w, b, bn=bn).to(dev)
             out = torch.empty(N, H, W, cout, device=dev, dtype=torch.bfloat16)
