@@ -30,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--batches", default="8,1")
+    ap.add_argument("--only", default="", help="substring of the GEMM name")
+    ap.add_argument("--impls", default="hip,torch")
     a = ap.parse_args()
     from bioengine_worker_amd.ops import gemm_bf16 as gb
     from bioengine_worker_amd.ops import vit_train as vt
@@ -43,6 +45,7 @@ def main():
         x, h = R(M, D), R(M, Hd)
         wq, wp, w1, w2 = R(3 * D, D) * 0.03, R(D, D) * 0.03, R(Hd, D) * 0.03, R(D, Hd) * 0.03
         bq, bp, b1, b2 = (torch.randn(n, device=dev) for n in (3 * D, D, Hd, D))
+        bqh, bph, b1h, b2h = (v.to(torch.bfloat16) for v in (bq, bp, b1, b2))
         dq, dD, dH = R(M, 3 * D), R(M, D), R(M, Hd)
         f = R(M, Hd)
         dbuf = torch.zeros(Hd, device=dev)
@@ -50,11 +53,11 @@ def main():
         outs = {n: torch.empty(n_, k_, device=dev) for n, (n_, k_) in
                 {"qkv": (3 * D, D), "proj": (D, D), "l1": (Hd, D), "l2": (D, Hd)}.items()}
         cases = [
-            ("fwd qkv", 2 * M * 3 * D * D, lambda: gb.linear(x, wq, bq), lambda: F.linear(x, wq, bq)),
-            ("fwd proj", 2 * M * D * D, lambda: gb.linear(x, wp, bp), lambda: F.linear(x, wp, bp)),
+            ("fwd qkv", 2 * M * 3 * D * D, lambda: gb.linear(x, wq, bq), lambda: F.linear(x, wq, bqh)),
+            ("fwd proj", 2 * M * D * D, lambda: gb.linear(x, wp, bp), lambda: F.linear(x, wp, bph)),
             ("fwd lin1+gelu", 2 * M * Hd * D, lambda: gb.linear_gelu(x, w1, b1),
-             lambda: vt.gelu_fwd(F.linear(x, w1, b1), zero)),
-            ("fwd lin2", 2 * M * D * Hd, lambda: gb.linear(h, w2, b2), lambda: F.linear(h, w2, b2)),
+             lambda: vt.gelu_fwd(F.linear(x, w1, b1h), zero)),
+            ("fwd lin2", 2 * M * D * Hd, lambda: gb.linear(h, w2, b2), lambda: F.linear(h, w2, b2h)),
             ("dgrad lin2+dgelu", 2 * M * Hd * D, lambda: gb.mm_dgelu(dD, w2, f, out_db=dbuf),
              lambda: vt.gelu_bwd(torch.mm(dD, w2), f, zero, out_db=dbuf)),
             ("dgrad lin1", 2 * M * D * Hd, lambda: gb.mm(dH, w1), lambda: torch.mm(dH, w1)),
@@ -71,7 +74,11 @@ def main():
         ]
         tot = {"hip": 0.0, "torch": 0.0}
         for name, fl, hip, ref in cases:
+            if a.only and a.only not in name:
+                continue
             for impl, fn in (("hip", hip), ("torch", ref)):
+                if impl not in a.impls.split(","):
+                    continue
                 try:
                     us = timeit(fn, a.reps)
                 except Exception as e:  # noqa: BLE001

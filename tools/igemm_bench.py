@@ -37,6 +37,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--only", default="")
+    ap.add_argument("--bns", default="64,128,65,1128,1065")
+    ap.add_argument("--variants", default="plain,res+act")
+    ap.add_argument("--no-ref", action="store_true", help="skip the per-layer reference kernel")
     a = ap.parse_args()
     from bioengine_worker_amd.ops import conv as convops
     from bioengine_worker_amd.ops import conv_igemm as ig
@@ -54,17 +57,19 @@ def main():
         t = torch.zeros(cout, device=dev)
         flops = 2.0 * N * H * W * cin * cout * 9
         rows = []
-        for bn in (64, 128, 65, 1128, 1065):
+        for bn in [int(v) for v in a.bns.split(",")]:
             if cout % (128 if bn % 1000 == 128 else 64) or not ig.supported(N, H, W, cout, bn):
                 continue
             pk = ig.IgemmConv.from_weight(w, b, bn=bn).to(dev)
             out = torch.empty(N, H, W, cout, device=dev, dtype=torch.bfloat16)
             aout = torch.empty_like(out)
             for variant, kw in (("plain", {}), ("res+act", dict(residual=res, ascale=s, ashift=t, aout=aout))):
+                if variant not in a.variants.split(","):
+                    continue
                 ms, mn = timeit(lambda: ig.conv3_igemm(x, pk, out=out, **kw), a.reps)
                 rows.append(dict(layer=name, kernel=f"igemm bn{bn}", variant=variant, ms=round(ms, 4),
                                  min_ms=round(mn, 4), TFs=round(flops / ms / 1e9, 1)))
-        if cin % 32 == 0:
+        if cin % 32 == 0 and not a.no_ref:
             pc = convops.PackedConv.from_weight(w, b).to(dev)
             sc = torch.ones(cin, device=dev)
             sh = torch.zeros(cin, device=dev)
