@@ -277,7 +277,11 @@ class CPnetEngine:
         self.style_s = torch.cat(ss, 0).contiguous()
         self.style_t = torch.cat(ts, 0).contiguous()
         self.pair = self._build_pairs(net) if os.environ.get("BE_CPNET_PAIR", "1") != "0" else {}
-        self.ig = self._build_igemm(net) if os.environ.get("BE_CPNET_IGEMM", "1") != "0" else {}
+        # deep levels on the implicit-GEMM kernels (BE_CPNET_IGEMM=1): opt-in -- whole-network A/B on
+        # MI355X measured 15.05 vs 14.69 ms per 288 tiles for the per-layer path
+        # (profiles/r04/conv/engine_ab_v2.jsonl): the producer-side activated copies cost more HBM
+        # traffic than the DMA-fed main loop saves
+        self.ig = self._build_igemm(net) if os.environ.get("BE_CPNET_IGEMM", "0") == "1" else {}
         # output layer fused into the last half-block's epilogue (ops/conv_pair.py HeadSpec)
         self.head = None
         if ("up", 0, 1) in self.pair and self.out.relu and self.nout <= 16 and os.environ.get("BE_CPNET_HEAD", "1") != "0":

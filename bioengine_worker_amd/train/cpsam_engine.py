@@ -41,12 +41,16 @@ import torch.nn.functional as F
 from ..models.cpsam import CPSAM, get_rel_pos
 import os as _os
 
-# GEMM backend of the engine: the in-house bf16 MFMA GEMMs with fused epilogues (default), or the
-# hipBLASLt-backed helpers of ops/gemm.py (BE_CPSAM_GEMM=lib, the A/B baseline)
-if _os.environ.get("BE_CPSAM_GEMM", "hip") == "lib":
+# GEMM backend of the engine: per shape, the faster of the in-house bf16 MFMA GEMMs with fused
+# epilogues and the library GEMM (ops/gemm_auto.py, decided on the eager warm-up steps);
+# BE_CPSAM_GEMM=hip / lib pins one side
+_GEMM = _os.environ.get("BE_CPSAM_GEMM", "auto")
+if _GEMM == "lib":
     from ..ops import gemm
-else:
+elif _GEMM == "hip":
     from ..ops import gemm_bf16 as gemm
+else:
+    from ..ops import gemm_auto as gemm
 from ..ops import vit_train as vt
 from ..parallel.ddp import FlatParams
 

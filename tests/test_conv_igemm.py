@@ -141,6 +141,7 @@ def test_cpnet_engine_igemm_path_matches_module(monkeypatch):
     with torch.no_grad():
         ref, style_ref = net(x)[:2]
     xin = to_nhwc_input(x, 8).to(dev)
+    monkeypatch.setenv("BE_CPNET_IGEMM", "1")
     eng = CPnetEngine(net, dev)
     assert ("down", 3, 1) in eng.ig and ("up", 3, 0) in eng.ig and ("up", 2, 1) in eng.ig
     y, st = eng(xin)

@@ -13,6 +13,7 @@ import torch  # noqa: E402
 
 CONFIGS = {
     "perlayer_deep": {"BE_CPNET_IGEMM": "0", "BE_CPNET_PAIR_LEVELS": "0,1"},
+    "perlayer_L1": {"BE_CPNET_IGEMM": "0", "BE_CPNET_PAIR_LEVELS": "0"},
     "igemm_deep": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0,1"},
     "igemm_deep_L1": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0"},
 }
