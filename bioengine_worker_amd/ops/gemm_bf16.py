@@ -13,6 +13,8 @@ The GELU is the erf form of the reference's ``nn.GELU`` in both directions.  On 
 is the plain fp32 PyTorch op (the reference math of the same call)."""
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -31,7 +33,8 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
 
 
 def _cfg(M: int, N: int) -> int:
-    """256x128 tiles when they fill the chip, else 128x128."""
+    """256x128 tiles when they fill the chip, else 128x128 (``BE_GEMM_CFG`` forces one: 0 = 256x128 on
+    8 waves, 1 = 128x128 on 4, 2 = 256x128 on 4 waves of 128x64, 3 = 128x256 on 4 waves of 64x128)."""
     return 0 if ((M + 255) // 256) * ((N + 127) // 128) >= 192 else 1
 
 
@@ -42,8 +45,12 @@ def _call(A, B, C, M, N, K, lda, ldb, ldc, ta, tb, epi, C2=None, bias=None, aux=
         wsb = ws.numel()
     if cfg is None:
         cfg = _cfg(M, N)
-        if ta == 1 and M % 256:
-            cfg = 1  # transposed A tiles are read whole: 128-row tiles
+        forced = os.environ.get("BE_GEMM_CFG")
+        if forced is not None:
+            cfg = int(forced)
+        bm, bn = {0: (256, 128), 1: (128, 128), 2: (256, 128), 3: (128, 256)}[cfg]
+        if (ta == 1 and M % bm) or (tb == 1 and N % bn):
+            cfg = 1  # transposed tiles are read whole: 128 x 128 tiles
     _native.call("be_gemm_bf16", _native.ptr(A), _native.ptr(B), _native.ptr(C), _native.ptr(C2), _native.ptr(bias),
                  _native.ptr(aux), _native.ptr(dbias), _native.ptr(ws), wsb, M, N, K, lda, ldb, ldc, ta, tb, epi,
                  cfg, split, _native.stream(A.device))

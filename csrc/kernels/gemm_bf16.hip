@@ -121,10 +121,11 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
 }
 
-template <int TA, int TB, int WM, int WN, int EPI>
+// wave tile = 16 FM (rows) x 16 FN (columns); block = WM x WN waves
+template <int TA, int TB, int WM, int WN, int FM, int FN, int EPI>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_bf16_kernel(GArgs a) {
   constexpr int NW = WM * WN;
-  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   constexpr int ABYTES = BM * BK * 2, BBYTES = BN * BK * 2, SBYTES = ABYTES + BBYTES;
   constexpr int LOADS = BM / 8 / NW + BN / 8 / NW;  // DMAs per wave per stage (either layout)
   extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -146,11 +147,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_bf16_kernel(GArgs a) {
     else dma_t<BN, NW>(a.B, a.ldb, n0, k0, buf + ABYTES, wave, lane);
   };
 
-  f32x4 acc[4][4];  // [n frag][m frag]
+  f32x4 acc[FN][FM];  // [n frag][m frag]
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FM; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   stage(0, smem);
   if (nk > 1) stage(1, smem + SBYTES);
@@ -163,40 +164,45 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_bf16_kernel(GArgs a) {
     if (kt + 2 < nk) stage(kt + 2, smem + ((kt + 2) % 3) * SBYTES);
     const unsigned char* ta = smem + (kt % 3) * SBYTES;
     const unsigned char* tb = ta + ABYTES;
+    // both K-steps' fragments are read up front (two register sets): the MFMAs of step 0 run
+    // while step 1's reads are in flight
+    bf16x8 af[2][FM], bf[2][FN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bf[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if constexpr (TA == 0) af[j] = frag_k(ta, wm * 64 + j * 16, ks, lane);
-        else af[j] = frag_t<BM>(ta, wm * 64 + j * 16, ks, lane);
+      for (int j = 0; j < FM; ++j) {
+        if constexpr (TA == 0) af[ks][j] = frag_k(ta, wm * 16 * FM + j * 16, ks, lane);
+        else af[ks][j] = frag_t<BM>(ta, wm * 16 * FM + j * 16, ks, lane);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (TB == 0) bf[i] = frag_k(tb, wn * 64 + i * 16, ks, lane);
-        else bf[i] = frag_t<BN>(tb, wn * 64 + i * 16, ks, lane);
+      for (int i = 0; i < FN; ++i) {
+        if constexpr (TB == 0) bf[ks][i] = frag_k(tb, wn * 16 * FN + i * 16, ks, lane);
+        else bf[ks][i] = frag_t<BN>(tb, wn * 16 * FN + i * 16, ks, lane);
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
     }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ks][i], af[ks][j], acc[i][j], 0, 0, 0);
   }
 
   // ---- epilogue: acc[i][j] lane -> row m = m0 + wm*64 + j*16 + (lane & 15),
   //                                  cols n = n0 + wn*64 + i*16 + 4*(lane >> 4) + 0..3
   const int ml = lane & 15, nq = 4 * (lane >> 4);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = n0 + wn * 64 + i * 16 + nq;
+  for (int i = 0; i < FN; ++i) {
+    const int n = n0 + wn * 16 * FN + i * 16 + nq;
     const bool nok = n < a.N;  // N % 4 == 0 (host-checked): a lane's 4 columns are all in or all out
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (EPI == E_BIAS || EPI == E_BIAS_GELU)
       if (nok && a.bias) bv = *reinterpret_cast<const float4*>(a.bias + n);
     float dsum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + wm * 64 + j * 16 + ml;
+    for (int j = 0; j < FM; ++j) {
+      const int m = m0 + wm * 16 * FM + j * 16 + ml;
       const bool ok = nok && m < a.M;
       const long long o = (long long)m * a.ldc + n;
       f32x4 v = acc[i][j];
@@ -260,13 +266,13 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
   }
 }
 
-template <int TA, int TB, int WM, int WN, int EPI>
+template <int TA, int TB, int WM, int WN, int FM, int FN, int EPI>
 int launch_gemm(GArgs a, hipStream_t s) {
-  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   constexpr size_t LDS = 3 * (size_t)(BM + BN) * BK * 2;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<TA, TB, WM, WN, EPI>,
+    if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<TA, TB, WM, WN, FM, FN, EPI>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS) != hipSuccess)
       return -30;
     attr = true;
@@ -275,7 +281,8 @@ int launch_gemm(GArgs a, hipStream_t s) {
   a.tiles_n = (a.N + BN - 1) / BN;
   a.tiles = ((a.M + BM - 1) / BM) * a.tiles_n;
   const long long nblk = (long long)a.tiles * a.split;
-  hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, WM, WN, EPI>), dim3((unsigned)nblk), dim3(WM * WN * 64), LDS, s, a);
+  hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, WM, WN, FM, FN, EPI>), dim3((unsigned)nblk), dim3(WM * WN * 64), LDS, s,
+                     a);
   return BE_CHECK_LAUNCH();
 }
 
@@ -285,7 +292,8 @@ extern "C" {
 
 // C = op(A) op(B)^T with a fused epilogue; see the header.  ta/tb: 0 = K-contiguous, 1 = M/N-contiguous.
 // epi: 0 none, 1 bias, 2 bias + GELU (C = f, C2 = gelu(f)), 3 GELU backward (aux = f, dbias += column
-// sums), 4 fp32 out.  cfg: 0 = 256 x 128 tile on 8 waves, 1 = 128 x 128 on 4 waves.  split > 1 (fp32
+// sums), 4 fp32 out.  cfg: 0 = 256 x 128 tile on 8 waves, 1 = 128 x 128 on 4 waves, 2 = 256 x 128 on 4
+// waves (128 x 64 each), 3 = 128 x 256 on 4 waves (64 x 128 each).  split > 1 (fp32
 // out only): K is split into `split` slices summed through `ws` (split * M * ldc floats).
 int be_gemm_bf16(const void* A, const void* B, void* C, void* C2, const float* bias, const void* aux, float* dbias,
                  void* ws, long long ws_bytes, int M, int N, int K, int lda, int ldb, int ldc, int ta, int tb, int epi,
@@ -299,8 +307,13 @@ int be_gemm_bf16(const void* A, const void* B, void* C, void* C2, const float* b
   a.aux = (const bf16_t*)aux; a.dbias = dbias;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.split = split; a.kchunk = K / split;
   int r = -43;
-#define BE_GEMM_CFG(TA, TB, EPI)                                                   \
-  r = cfg == 0 ? launch_gemm<TA, TB, 4, 2, EPI>(a, s) : launch_gemm<TA, TB, 2, 2, EPI>(a, s);
+#define BE_GEMM_CFG(TA, TB, EPI)                                                                         \
+  switch (cfg) {                                                                                         \
+    case 0: r = launch_gemm<TA, TB, 4, 2, 4, 4, EPI>(a, s); break;  /* 256 x 128, 8 waves of 64 x 64 */  \
+    case 1: r = launch_gemm<TA, TB, 2, 2, 4, 4, EPI>(a, s); break;  /* 128 x 128, 4 waves of 64 x 64 */  \
+    case 2: r = launch_gemm<TA, TB, 2, 2, 8, 4, EPI>(a, s); break;  /* 256 x 128, 4 waves of 128 x 64 */ \
+    case 3: r = launch_gemm<TA, TB, 2, 2, 4, 8, EPI>(a, s); break;  /* 128 x 256, 4 waves of 64 x 128 */ \
+  }
   if (ta == 0 && tb == 0 && epi == E_NONE) { BE_GEMM_CFG(0, 0, E_NONE) }
   else if (ta == 0 && tb == 0 && epi == E_BIAS) { BE_GEMM_CFG(0, 0, E_BIAS) }
   else if (ta == 0 && tb == 0 && epi == E_BIAS_GELU) { BE_GEMM_CFG(0, 0, E_BIAS_GELU) }

@@ -22,7 +22,7 @@ def _close(got, want, rtol=2e-2):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", SHAPES)
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 def test_linear_and_gelu(M, N, K, cfg):
     dev = torch.device("cuda", 0)
     x, w = _rand(M, K, dev=dev, seed=1), _rand(N, K, dev=dev, scale=K ** -0.5, seed=2)
@@ -43,7 +43,7 @@ def test_linear_and_gelu(M, N, K, cfg):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [s for s in SHAPES if s[1] % 128 == 0])
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
 def test_dgrad_and_dgelu(M, N, K, cfg):
     dev = torch.device("cuda", 0)
     dm, w2 = _rand(M, K, dev=dev, seed=3), _rand(K, N, dev=dev, scale=K ** -0.5, seed=4)

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--batches", default="8,1")
     ap.add_argument("--only", default="", help="substring of the GEMM name")
     ap.add_argument("--impls", default="hip,torch")
+    ap.add_argument("--cfgs", default="", help="comma list of BE_GEMM_CFG values to A/B for the hip impl")
     a = ap.parse_args()
     from bioengine_worker_amd.ops import gemm_bf16 as gb
     from bioengine_worker_amd.ops import vit_train as vt
@@ -76,16 +77,21 @@ def main():
         for name, fl, hip, ref in cases:
             if a.only and a.only not in name:
                 continue
-            for impl, fn in (("hip", hip), ("torch", ref)):
+            runs = [("torch", ref, None)] + ([("hip", hip, c) for c in a.cfgs.split(",")] if a.cfgs else [("hip", hip, None)])
+            for impl, fn, cfg in runs:
                 if impl not in a.impls.split(","):
                     continue
+                if cfg is not None:
+                    os.environ["BE_GEMM_CFG"] = cfg
+                else:
+                    os.environ.pop("BE_GEMM_CFG", None)
                 try:
                     us = timeit(fn, a.reps)
                 except Exception as e:  # noqa: BLE001
-                    print(json.dumps({"B": B, "gemm": name, "impl": impl, "error": str(e)[:200]}), flush=True)
+                    print(json.dumps({"B": B, "gemm": name, "impl": impl, "cfg": cfg, "error": str(e)[:200]}), flush=True)
                     continue
                 tot[impl] += us
-                print(json.dumps({"B": B, "gemm": name, "impl": impl, "us": round(us, 1),
+                print(json.dumps({"B": B, "gemm": name, "impl": impl, "cfg": cfg, "us": round(us, 1),
                                   "TFs": round(fl / us / 1e6, 1)}), flush=True)
         print(json.dumps({"B": B, "block_total_us": {k: round(v, 1) for k, v in tot.items()},
                           "step_ms_x24": {k: round(24 * v / 1e3, 2) for k, v in tot.items()}}), flush=True)
