@@ -74,8 +74,10 @@ def _decode_image_b64(s: str) -> np.ndarray:
 
 @serve.deployment(
     ray_actor_options={"num_cpus": 4, "num_gpus": 1, "memory": int(8 * 1024 ** 3)},
-    max_ongoing_requests=10,
-    max_queued_requests=100,
+    # queries are served in batches (one ViT forward + one scan per group): admit a full 64-query batch
+    # (the reference's per-request path caps this replica at 10, main.py:1033-1050)
+    max_ongoing_requests=64,
+    max_queued_requests=256,
     health_check_period_s=60.0,
     health_check_timeout_s=60.0,
     graceful_shutdown_timeout_s=600.0,
@@ -450,7 +452,8 @@ class CellImageSearch:
                 for (_, _, pl, ph), idxs in groups.items():
                     x = torch.from_numpy(np.ascontiguousarray(np.stack([reqs[i][0] for i in idxs]))).to(dev)
                     t, u8 = batch_to_dinov2(x, None, pl, ph, return_u8=True)
-                    e = self._worker.engine.embed(t).float()
+                    eng = self._worker.engine
+                    e = (eng.embed_graphed(t) if hasattr(eng, "embed_graphed") else eng.embed(t)).float()
                     u8h = u8.permute(0, 2, 3, 1).contiguous().cpu().numpy()
                     for j, i in enumerate(idxs):
                         q[i] = e[j]

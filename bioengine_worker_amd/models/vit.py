@@ -260,3 +260,44 @@ class ViTEngine:
         """CLS embeddings [B, D] fp32 (L2-normalised like embedder.py:89-92)."""
         cls = self.features(x)[:, 0].float()
         return F.normalize(cls, dim=1, eps=1e-9) if normalize else cls
+
+    #: batch buckets of :meth:`embed_graphed` (a request batch is padded up to the next one)
+    GRAPH_BUCKETS = (1, 2, 4, 8, 16, 32, 64)
+
+    @torch.no_grad()
+    def embed_graphed(self, x: torch.Tensor) -> torch.Tensor:
+        """:meth:`embed` replayed from a HIP graph per batch bucket: a serving batch of a few
+        queries is ~150 kernel launches of microseconds each, so launches, not the GPU, set its
+        latency.  The batch is zero-padded to the bucket; the graph (captured on first use of the
+        bucket, after one eager warm-up) reads a static input buffer."""
+        B = x.shape[0]
+        if not x.is_cuda or B > self.GRAPH_BUCKETS[-1]:
+            return self.embed(x)
+        bucket = next(b for b in self.GRAPH_BUCKETS if b >= B)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        key = (bucket, tuple(x.shape[1:]), x.dtype)
+        ent = graphs.get(key)
+        if ent is None:
+            xs = torch.zeros((bucket,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
+            xs[:B] = x
+            side = torch.cuda.Stream(x.device)
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            with torch.cuda.stream(side):
+                self.embed(xs)  # lazy state, kernels, allocator
+            torch.cuda.current_stream(x.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g):
+                    out = self.embed(xs)
+            except Exception:  # noqa: BLE001 -- a path that cannot be captured runs eagerly
+                graphs[key] = False
+                return self.embed(x)
+            ent = graphs[key] = (g, xs, out)
+        if ent is False:
+            return self.embed(x)
+        g, xs, out = ent
+        xs[:B].copy_(x)
+        if B < bucket:
+            xs[B:].zero_()
+        g.replay()
+        return out[:B].clone()
