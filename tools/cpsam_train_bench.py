@@ -51,12 +51,13 @@ def main():
         out = {"bench": "cpsam_finetune_step", "engine": "hip", "batch": B, "depth": args.depth,
                "ms_per_step": round(dt * 1e3, 3), "samples_per_sec": round(B / dt, 2), "loss": float(loss),
                "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
-               "gemm": "torch (hipBLASLt heuristics)" if os.environ.get("BE_LT", "0") != "1"
-               else "gemm_lt (tuned hipBLASLt, bias / dGELU(+bias-grad) epilogues)"}
-        if os.environ.get("BE_LT", "0") == "1":
-            from bioengine_worker_amd.ops import gemm
+               "gemm": os.environ.get("BE_CPSAM_GEMM", "auto")}
+        if out["gemm"] == "auto":
+            from bioengine_worker_amd.ops import gemm_auto
 
-            out["dgelu_variant"] = gemm.dgelu_modes()
+            ch = gemm_auto.choices()
+            out["gemm_choices"] = {"hip": sum(c["impl"] == "hip" for c in ch), "lib": sum(c["impl"] == "lib" for c in ch),
+                                   "table": ch}
         print(json.dumps(out), flush=True)
         del tr
         torch.cuda.empty_cache()
