@@ -225,6 +225,30 @@ class _FConv:
                                     cout_valid=cout_valid)
 
 
+class _PPConv:
+    """A 3x3 conv on the ping-pong implicit-GEMM kernel (ops/gemm_pp.py): weights [Cout][3][3][Cin]."""
+
+    def __init__(self, conv: nn.Conv2d, device):
+        from ..ops import gemm_pp as ppops
+
+        self.cout = conv.weight.shape[0]
+        self.wp = ppops.pack_conv3(conv.weight).to(device)
+        self.bias = None if conv.bias is None else conv.bias.detach().float().to(device).contiguous()
+        cfg = os.environ.get("BE_CPNET_PP_CFG")
+        self.cfg = None if cfg is None else int(cfg)
+
+
+def _igc(x, pk, **kw):
+    """(out, aout) of one deep 3x3 conv on the implicit-GEMM path the engine was built with."""
+    if isinstance(pk, _PPConv):
+        from ..ops import gemm_pp as ppops
+
+        return ppops.conv3(x, pk.wp, pk.bias, cfg=pk.cfg, **kw)
+    from ..ops import conv_igemm as igops
+
+    return igops.conv3_igemm(x, pk, **kw)
+
+
 class CPnetEngine:
     """Inference engine for an eval-mode (BatchNorm) :class:`CPnet`.
 
@@ -281,7 +305,8 @@ class CPnetEngine:
         # MI355X measured 15.05 vs 14.69 ms per 288 tiles for the per-layer path
         # (profiles/r04/conv/engine_ab_v2.jsonl): the producer-side activated copies cost more HBM
         # traffic than the DMA-fed main loop saves
-        self.ig = self._build_igemm(net) if os.environ.get("BE_CPNET_IGEMM", "0") == "1" else {}
+        self.ig_kind = os.environ.get("BE_CPNET_IGEMM", "0")
+        self.ig = self._build_igemm(net) if self.ig_kind in ("1", "pp") else {}
         # output layer fused into the last half-block's epilogue (ops/conv_pair.py HeadSpec)
         self.head = None
         if ("up", 0, 1) in self.pair and self.out.relu and self.nout <= 16 and os.environ.get("BE_CPNET_HEAD", "1") != "0":
@@ -342,12 +367,16 @@ class CPnetEngine:
         per-layer kernel, which writes its consumer's activated input instead).  Keys:
         ("down", n, k) / ("up", i, k)."""
         from ..ops import conv_igemm as igops
+        from ..ops import gemm_pp as ppops
 
         ig = {}
 
         def add(key, conv: nn.Conv2d):
             cout, cin, kh, _ = conv.weight.shape
-            if kh == 3 and cin % 16 == 0 and cout % 64 == 0:
+            if self.ig_kind == "pp":
+                if kh == 3 and ppops.conv3_supported(cin, cout):
+                    ig[key] = _PPConv(conv, self.device)
+            elif kh == 3 and cin % 16 == 0 and cout % 64 == 0:
                 ig[key] = igops.IgemmConv.from_weight(conv.weight, conv.bias).to(self.device)
 
         nup = len(net.upsample.up)
@@ -376,6 +405,8 @@ class CPnetEngine:
         pk = self.ig.get((kind, idx, 1))
         if pk is None or not x.is_cuda:
             return False
+        if isinstance(pk, _PPConv):
+            return True  # no halo budget: any image geometry
         return igops.supported(x.shape[0], H, W, pk.cout, pk.bn)
 
     def _down_ig(self, n: int, e: dict, src: torch.Tensor, next_act=None) -> torch.Tensor:
@@ -383,37 +414,33 @@ class CPnetEngine:
         consumer (producer-side pre-activation), so the 3x3 convs stage their inputs by DMA.
         ``next_act`` = (scale, shift) of the following up block's first conv, which reads this
         block's output through the igemm path too (written as a second, activated copy)."""
-        from ..ops import conv_igemm as igops
-
         ig = self.ig
         proj = e["proj"](src, inmode="pool2")
         c1, c2, c3 = e["c1"], e["c2"], e["c3"]
         ha = convops.fused_conv2d(src, e["c0"].pc, scale=e["c0"].scale, shift=e["c0"].shift, relu=True, inmode="pool2",
                                   post_scale=c1.scale, post_shift=c1.shift, post_relu=True)
-        x1, x1a = igops.conv3_igemm(ha, ig[("down", n, 1)], residual=proj, ascale=c2.scale, ashift=c2.shift)
-        _, h2a = igops.conv3_igemm(x1a, ig[("down", n, 2)], want_out=False, ascale=c3.scale, ashift=c3.shift)
+        x1, x1a = _igc(ha, ig[("down", n, 1)], residual=proj, ascale=c2.scale, ashift=c2.shift)
+        _, h2a = _igc(x1a, ig[("down", n, 2)], want_out=False, ascale=c3.scale, ashift=c3.shift)
         if next_act is None:
-            xd, _ = igops.conv3_igemm(h2a, ig[("down", n, 3)], residual=x1)
+            xd, _ = _igc(h2a, ig[("down", n, 3)], residual=x1)
             return xd, None
-        return igops.conv3_igemm(h2a, ig[("down", n, 3)], residual=x1, ascale=next_act[0], ashift=next_act[1])
+        return _igc(h2a, ig[("down", n, 3)], residual=x1, ascale=next_act[0], ashift=next_act[1])
 
     def _up_ig(self, i: int, e: dict, xcur: torch.Tensor, y: torch.Tensor, shifts: dict, xcur_act=None):
-        from ..ops import conv_igemm as igops
-
         ig = self.ig
         c1, c2, c3 = e["c1"], e["c2"], e["c3"]
         if ("up", i, 0) in ig:  # same resolution: c0 on the igemm path, its input activated upstream
             proj = e["proj"](xcur)
-            _, h0a = igops.conv3_igemm(xcur_act, ig[("up", i, 0)], residual=y, want_out=False, ascale=c1.scale,
+            _, h0a = _igc(xcur_act, ig[("up", i, 0)], residual=y, want_out=False, ascale=c1.scale,
                                        ashift=shifts[(i, 1)])
         else:
             proj = e["proj"](xcur, inmode="up2")
             h0a = convops.fused_conv2d(xcur, e["c0"].pc, scale=e["c0"].scale, shift=e["c0"].shift, relu=True,
                                        inmode="up2", residual=y, post_scale=c1.scale, post_shift=shifts[(i, 1)],
                                        post_relu=True)
-        x1, x1a = igops.conv3_igemm(h0a, ig[("up", i, 1)], residual=proj, ascale=c2.scale, ashift=shifts[(i, 2)])
-        _, h2a = igops.conv3_igemm(x1a, ig[("up", i, 2)], want_out=False, ascale=c3.scale, ashift=shifts[(i, 3)])
-        out, _ = igops.conv3_igemm(h2a, ig[("up", i, 3)], residual=x1)
+        x1, x1a = _igc(h0a, ig[("up", i, 1)], residual=proj, ascale=c2.scale, ashift=shifts[(i, 2)])
+        _, h2a = _igc(x1a, ig[("up", i, 2)], want_out=False, ascale=c3.scale, ashift=shifts[(i, 3)])
+        out, _ = _igc(h2a, ig[("up", i, 3)], residual=x1)
         return out
 
     def _style_shifts(self, style: torch.Tensor) -> dict:

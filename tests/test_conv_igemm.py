@@ -129,9 +129,11 @@ def test_fused_conv_post_activation(inmode, shift2d):
 
 
 @pytest.mark.gpu
-def test_cpnet_engine_igemm_path_matches_module(monkeypatch):
-    """The whole inference network with the deep levels on the igemm path (producer-side
-    activations) against the fp32 cellpose-style module; no worse than the per-layer path."""
+@pytest.mark.parametrize("kind", ["1", "pp"])
+def test_cpnet_engine_igemm_path_matches_module(monkeypatch, kind):
+    """The whole inference network with the deep levels on an implicit-GEMM path (producer-side
+    activations; kind 1 = conv_igemm.hip, pp = gemm_pp.hip) against the fp32 cellpose-style
+    module; no worse than the per-layer path."""
     from bioengine_worker_amd.models.cpnet import CPnet, CPnetEngine, to_nhwc_input
 
     dev = torch.device("cuda", 0)
@@ -141,7 +143,7 @@ def test_cpnet_engine_igemm_path_matches_module(monkeypatch):
     with torch.no_grad():
         ref, style_ref = net(x)[:2]
     xin = to_nhwc_input(x, 8).to(dev)
-    monkeypatch.setenv("BE_CPNET_IGEMM", "1")
+    monkeypatch.setenv("BE_CPNET_IGEMM", kind)
     eng = CPnetEngine(net, dev)
     assert ("down", 3, 1) in eng.ig and ("up", 3, 0) in eng.ig and ("up", 2, 1) in eng.ig
     y, st = eng(xin)

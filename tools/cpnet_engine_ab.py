@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """CPnet inference engine, whole network, one headline batch (288 tiles of 224x224 = 32 images of
 512x512), under engine configurations built in one process (A/B of the conv paths):
-baseline per-layer deep levels, igemm deep levels, igemm also at level 1 (pairs at level 0 only).
+baseline per-layer deep levels, igemm / ping-pong (gemm_pp) deep levels, either also at level 1
+(pairs at level 0 only).
 HIP-event median of --reps forwards; relative RMS of each config's output against the baseline."""
 import argparse
 import json
@@ -16,6 +17,8 @@ CONFIGS = {
     "perlayer_L1": {"BE_CPNET_IGEMM": "0", "BE_CPNET_PAIR_LEVELS": "0"},
     "igemm_deep": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0,1"},
     "igemm_deep_L1": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0"},
+    "pp_deep": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1"},
+    "pp_deep_L1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0"},
 }
 
 
@@ -23,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tiles", type=int, default=288)
+    ap.add_argument("--configs", default=",".join(CONFIGS))
     a = ap.parse_args()
     from bioengine_worker_amd.models.cpnet import CPnet, CPnetEngine
 
@@ -32,8 +36,8 @@ def main():
     x = torch.zeros(a.tiles, 224, 224, 8, device=dev, dtype=torch.bfloat16)
     x[..., :2] = torch.randn(a.tiles, 224, 224, 2, device=dev, generator=g).to(torch.bfloat16)
     base = None
-    for name, env in CONFIGS.items():
-        os.environ.update(env)
+    for name in a.configs.split(","):
+        os.environ.update(CONFIGS[name])
         eng = CPnetEngine(net, dev)
         y, _ = eng(x)
         torch.cuda.synchronize()
