@@ -373,8 +373,12 @@ class CellImageSearch:
         mean queueing wait) for the embedding forward and the index scan."""
         from bioengine_worker_amd.serve.batching import batch_stats
 
+        st = dict(self.__dict__.get("_stage_ms", {}))
+        nb = max(1, st.get("batches", 0))
+        stages = {k: round(v / nb, 3) for k, v in st.items() if k != "batches"}
         return {"query": batch_stats(self, "_query_batch") or {}, "embed": batch_stats(self, "_embed_batch") or {},
-                "search": batch_stats(self, "_search_batch") or {}}
+                "search": batch_stats(self, "_search_batch") or {},
+                "query_stage_ms_per_batch": stages}
 
     @serve.batch(max_batch_size=64, batch_wait_timeout_s=0.001, max_concurrent_batches=2)
     async def _search_batch(self, reqs: list) -> list:
@@ -434,7 +438,7 @@ class CellImageSearch:
         [(results list, query thumbnail base64)]."""
         import torch
 
-        from bioengine_worker_amd.search.ingestion import png_b64
+        from bioengine_worker_amd.search.ingestion import png_b64_batch
         from bioengine_worker_amd.search.preprocess import batch_to_dinov2
 
         n = len(reqs)
@@ -448,7 +452,9 @@ class CellImageSearch:
             dev = self._worker.device
             q = [None] * n
             thumbs = {}
+            tm = [time.perf_counter()]
             with self._gpu_lock:
+                tm.append(time.perf_counter())
                 for (_, _, pl, ph), idxs in groups.items():
                     x = torch.from_numpy(np.ascontiguousarray(np.stack([reqs[i][0] for i in idxs]))).to(dev)
                     t, u8 = batch_to_dinov2(x, None, pl, ph, return_u8=True)
@@ -462,22 +468,24 @@ class CellImageSearch:
                     if emb is not None:
                         v = torch.as_tensor(np.asarray(emb, np.float32), device=dev)
                         q[i] = v / v.norm().clamp_min(1e-9)
+                tm.append(time.perf_counter())
                 S, I = self._index.search(torch.stack(q), kmax)
+                tm.append(time.perf_counter())
             res = [self._results(S[i, : int(r[4])], I[i, : int(r[4])]) for i, r in enumerate(reqs)]
-            # PNG encoding releases the GIL: the batch's query thumbnails encode in parallel
+            tm.append(time.perf_counter())
+            # the batch's query thumbnails: one call into the host runtime's linear-time PNG encoder,
+            # spread over host threads outside the GIL (csrc/runtime/png.cpp)
             order = sorted(thumbs)
-            enc = dict(zip(order, self._png_pool().map(lambda i: png_b64(thumbs[i], 1), order))) if order else {}
+            enc = dict(zip(order, png_b64_batch(np.stack([thumbs[i] for i in order])))) if order else {}
+            tm.append(time.perf_counter())
+            st = self.__dict__.setdefault("_stage_ms", {"batches": 0, "lock": 0.0, "embed": 0.0, "scan": 0.0,
+                                                        "results": 0.0, "thumbs": 0.0})
+            st["batches"] += 1
+            for k, a, b in (("lock", 0, 1), ("embed", 1, 2), ("scan", 2, 3), ("results", 3, 4), ("thumbs", 4, 5)):
+                st[k] += (tm[b] - tm[a]) * 1e3
             return [(res[i], enc.get(i, "")) for i in range(n)]
 
         return await asyncio.to_thread(run)
-
-    def _png_pool(self):
-        pool = self.__dict__.get("_png_executor")
-        if pool is None:
-            from concurrent.futures import ThreadPoolExecutor
-
-            pool = self.__dict__["_png_executor"] = ThreadPoolExecutor(max_workers=8, thread_name_prefix="png")
-        return pool
 
     @schema_method
     async def search(self, image_b64: str | None = Field(None, description="Base64 image (PNG/JPG/TIFF or .npy bytes)."),

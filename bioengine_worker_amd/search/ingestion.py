@@ -204,6 +204,35 @@ def png_b64(rgb: np.ndarray, compress_level: int = 6) -> str:
     return base64.b64encode(buf.getvalue()).decode()
 
 
+def png_b64_batch(rgb: np.ndarray, threads: int = 8) -> list[str]:
+    """Base64 PNGs of uint8 RGB images [n, h, w, 3] from the host runtime's linear-time encoder
+    (``csrc/runtime/png.cpp``: filter-0 rows in stored deflate blocks -- no compression search, so a
+    224x224 thumbnail costs a fraction of a millisecond instead of PIL's 6-11 ms; the whole batch
+    runs on host threads outside the GIL).  Falls back to PIL when the runtime is not built."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    if rgb.ndim != 4 or rgb.shape[-1] != 3:
+        raise ValueError(f"expected [n, h, w, 3] uint8, got {rgb.shape}")
+    n, h, w, _ = rgb.shape
+    if n == 0:
+        return []
+    try:
+        from ..ops import _native
+
+        lib = _native.runtime()
+        cap = int(lib.be_rt_png_b64_cap(h, w))
+        if cap <= 0:
+            raise ValueError("image too large")
+        out = np.empty(cap * n, np.uint8)
+        lens = np.empty(n, np.int64)
+        _native.rt_call("be_rt_png_b64_batch", rgb.ctypes.data, n, h, w, out.ctypes.data, cap, lens.ctypes.data,
+                        int(threads))
+        return [out[i * cap: i * cap + int(lens[i])].tobytes().decode("ascii") for i in range(n)]
+    except (OSError, AttributeError, ImportError, ValueError) as e:
+        if isinstance(e, ValueError) and "too large" not in str(e):
+            raise
+        return [png_b64(rgb[i], 1) for i in range(n)]
+
+
 THUMBS_B64 = "thumbnails_b64.txt"
 
 

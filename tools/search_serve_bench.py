@@ -73,6 +73,8 @@ async def main_async(a) -> list[dict]:
     results = []
     for conc in a.concurrency:
         lat: list[float] = []
+        srv: list[float] = []
+        last: dict = {}
         stop = time.perf_counter() + a.seconds
 
         async def client(cid):
@@ -81,6 +83,8 @@ async def main_async(a) -> list[dict]:
                 t = time.perf_counter()
                 out = await app.search(image_b64=crops[k % 16], top_k=20)
                 lat.append(time.perf_counter() - t)
+                srv.append(out.get("elapsed_ms", 0.0))
+                last["o"] = out
                 assert len(out["results"]) == min(20, n_cells)
                 k += conc
 
@@ -90,7 +94,9 @@ async def main_async(a) -> list[dict]:
         ms = np.array(lat) * 1e3
         rr = {"concurrency": conc, "requests": len(lat), "qps": round(len(lat) / dt, 1),
               "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
-              "p99_ms": round(float(np.percentile(ms, 99)), 2), "n_cells": n_cells, "model": a.model}
+              "p99_ms": round(float(np.percentile(ms, 99)), 2), "n_cells": n_cells, "model": a.model,
+              "replica_p50_ms": round(float(np.percentile(srv, 50)), 2),
+              "response_kb": round(len(json.dumps(last.get("o", {}))) / 1024, 1)}
         results.append(rr)
         print(json.dumps(rr), flush=True)
     bs = await app.get_batch_stats()
