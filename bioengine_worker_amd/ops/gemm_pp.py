@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from . import _native
 
-P_NONE, P_BIAS, P_BIAS_GELU = 0, 1, 2
+P_NONE, P_BIAS, P_BIAS_GELU, P_DGELU = 0, 1, 2, 4
 TILES = {0: (256, 256), 1: (512, 128), 2: (256, 128)}
 
 
@@ -43,8 +43,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, cfg:
     if not x.is_cuda or not supported(M, N, K) or not (x.is_contiguous() and w.is_contiguous()):
         return F.linear(x, w, None if b is None else b.to(x.dtype))
     out = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
-    _native.call("be_gemm_pp", _native.ptr(x), _native.ptr(w), _native.ptr(out), None, _native.ptr(b), M, N, K, K, K, N,
-                 P_BIAS if b is not None else P_NONE, gemm_cfg(M, N) if cfg is None else cfg, _native.stream(x.device))
+    _native.call("be_gemm_pp", _native.ptr(x), _native.ptr(w), _native.ptr(out), None, _native.ptr(b), None, None,
+                 M, N, K, K, K, N, 0, P_BIAS if b is not None else P_NONE, gemm_cfg(M, N) if cfg is None else cfg,
+                 _native.stream(x.device))
     return out
 
 
@@ -57,9 +58,52 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, cfg: int | No
         return F.gelu(f.float()).to(x.dtype), f
     f = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
     g = torch.empty_like(f)
-    _native.call("be_gemm_pp", _native.ptr(x), _native.ptr(w), _native.ptr(f), _native.ptr(g), _native.ptr(b), M, N, K,
-                 K, K, N, P_BIAS_GELU, gemm_cfg(M, N) if cfg is None else cfg, _native.stream(x.device))
+    _native.call("be_gemm_pp", _native.ptr(x), _native.ptr(w), _native.ptr(f), _native.ptr(g), _native.ptr(b), None, None,
+                 M, N, K, K, K, N, 0, P_BIAS_GELU, gemm_cfg(M, N) if cfg is None else cfg, _native.stream(x.device))
     return g, f
+
+
+def _dgrad_cfg(M: int, N: int, cfg: int | None) -> int:
+    if cfg is not None:
+        return cfg
+    f = _forced()
+    if f is not None:
+        return f
+    return 0 if N % 256 == 0 and N >= 2048 else 2
+
+
+def mm(x: torch.Tensor, w: torch.Tensor, cfg: int | None = None) -> torch.Tensor:
+    """x [M, K] @ w [K, N] (the dgrad: W read as stored, transposed in LDS) -> bf16 [M, N]."""
+    M, K = x.shape
+    N = w.shape[1]
+    c = _dgrad_cfg(M, N, cfg)
+    if not x.is_cuda or not supported(M, N, K) or N % TILES[c][1] or not (x.is_contiguous() and w.is_contiguous()):
+        return torch.mm(x, w)
+    out = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    _native.call("be_gemm_pp", _native.ptr(x), _native.ptr(w), _native.ptr(out), None, None, None, None, M, N, K, K, N, N,
+                 1, P_NONE, c, _native.stream(x.device))
+    return out
+
+
+def mm_dgelu(dm: torch.Tensor, w2: torch.Tensor, f: torch.Tensor, out_db: torch.Tensor | None = None,
+             cfg: int | None = None) -> torch.Tensor:
+    """df = gelu'(f) * (dm @ w2), dm [M, K], w2 [K, N], f [M, N]; out_db [N] fp32 = column sums of df."""
+    M, K = dm.shape
+    N = w2.shape[1]
+    c = _dgrad_cfg(M, N, cfg)
+    if not dm.is_cuda or not supported(M, N, K) or N % TILES[c][1]:
+        x = f.float()
+        gp = 0.5 * (1.0 + torch.erf(x * 0.7071067811865476)) + x * torch.exp(-0.5 * x * x) * 0.3989422804014327
+        df = (gp * (dm.float() @ w2.float())).to(dm.dtype)
+        if out_db is not None:
+            torch.sum(df.float(), 0, out=out_db)
+        return df
+    df = torch.empty(M, N, device=dm.device, dtype=torch.bfloat16)
+    if out_db is not None:
+        out_db.zero_()
+    _native.call("be_gemm_pp", _native.ptr(dm), _native.ptr(w2), _native.ptr(df), None, None, _native.ptr(f),
+                 _native.ptr(out_db), M, N, K, K, N, N, 1, P_DGELU, c, _native.stream(dm.device))
+    return df
 
 
 # ---------------------------------------------------------------------------------------------

@@ -51,8 +51,35 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
 __device__ __forceinline__ int swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
 
-enum { P_NONE = 0, P_BIAS = 1, P_BIAS_GELU = 2, P_CONV = 3 };
+// N-contiguous B ([K][N] in memory, the dgrad's W as stored): the slot's B region is [32 k][BN] bf16,
+// read transposed with ds_read_b64_tr_b16; 16-byte chunk c of k-row k sits at c ^ tswz(k) (the 8
+// k-rows a 32-lane half reads land on 8 distinct slot pairs).
+__device__ __forceinline__ int tswz(int k) { return 2 * ((k & 3) | ((k >> 1) & 4)); }
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// 16x16x32 fragment (column c0 + (lane & 15), k 0..31) of a [32][C] k-row tile
+template <int C>
+__device__ __forceinline__ bf16x8 frag_t(const unsigned char* t, int c0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int k = g * 8 + q;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const unsigned char* a0 = t + k * (C * 2) + ((ch ^ tswz(k)) << 4) + 8 * (p & 1);
+  const unsigned char* a1 = t + (k + 4) * (C * 2) + ((ch ^ tswz(k + 4)) << 4) + 8 * (p & 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a0);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)a1);
+  bf16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+enum { P_NONE = 0, P_BIAS = 1, P_BIAS_GELU = 2, P_CONV = 3, P_DGELU = 4 };
 
 struct PArgs {
   const bf16_t* A;     // GEMM: [M][lda]; CONV: x NHWC [M][Cin]
@@ -60,6 +87,8 @@ struct PArgs {
   bf16_t* C;           // [M][ldc] (CONV: out, may be null)
   bf16_t* C2;          // P_BIAS_GELU: gelu(f)
   const float* bias;   // [N]
+  const bf16_t* aux;   // P_DGELU: f [M][ldc]
+  float* dbias;        // P_DGELU: += column sums of the output (fp32, pre-zeroed)
   const bf16_t* res;   // CONV: residual [M][ldc]
   bf16_t* aout;        // CONV: relu?(out * as + at)
   const float* as;     // [N]
@@ -71,7 +100,7 @@ struct PArgs {
   int tiles_n, nkh;
 };
 
-template <int WM, int WN, int FM, int FN, int EPI>
+template <int WM, int WN, int FM, int FN, int EPI, int TB>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
   static_assert(WM * WN == 8, "8 waves");
   constexpr bool CONV = EPI == P_CONV;
@@ -126,12 +155,24 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
     unsigned char* slot = smem + (J & (NSLOT - 1)) * SLOT;
     const int k0 = J * KH;
     if (part == 0) {
+      if constexpr (TB == 0) {
 #pragma unroll
-      for (int i = 0; i < GB; ++i) {
-        const int R = i * 128 + lr;
-        const int c = lch ^ swz(R);
-        __builtin_amdgcn_global_load_lds((const void*)(a.B + (long long)brow[i] * a.ldb + k0 + c * 8),
-                                         (lds_void*)(slot + ABYTES + (i * 128 + wave * 16) * 64), 16, 0, 0);
+        for (int i = 0; i < GB; ++i) {
+          const int R = i * 128 + lr;
+          const int c = lch ^ swz(R);
+          __builtin_amdgcn_global_load_lds((const void*)(a.B + (long long)brow[i] * a.ldb + k0 + c * 8),
+                                           (lds_void*)(slot + ABYTES + (i * 128 + wave * 16) * 64), 16, 0, 0);
+        }
+      } else {
+        constexpr int CPR = BN / 8, RPI = 64 / CPR;  // 16-byte chunks per k-row, k-rows per 1 KiB DMA
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+          const int blk = i * 8 + wave;              // 1 KiB DMA block of the [32][BN] region
+          const int kr = blk * RPI + lane / CPR;
+          const int c = (lane % CPR) ^ tswz(kr);
+          __builtin_amdgcn_global_load_lds((const void*)(a.B + (long long)(k0 + kr) * a.ldb + n0 + c * 8),
+                                           (lds_void*)(slot + ABYTES + blk * 1024), 16, 0, 0);
+        }
       }
     }
     int dy = 0, dx = 0, c0 = k0;
@@ -192,8 +233,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
       if (s == 0) {
 #pragma unroll
         for (int i = 0; i < FN; ++i) {
-          const int R = wn * 16 * FN + i * 16 + frow;
-          bfr[i] = *reinterpret_cast<const bf16x8*>(slot + ABYTES + R * 64 + ((fch ^ swz(R)) << 4));
+          if constexpr (TB == 0) {
+            const int R = wn * 16 * FN + i * 16 + frow;
+            bfr[i] = *reinterpret_cast<const bf16x8*>(slot + ABYTES + R * 64 + ((fch ^ swz(R)) << 4));
+          } else {
+            bfr[i] = frag_t<BN>(slot + ABYTES, wn * 16 * FN + i * 16, lane);
+          }
         }
       }
       // prefetch share: part s of K-half J + DPRE (its slot's part-s regions were last read a
@@ -228,12 +273,22 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f), sv = make_float4(1.f, 1.f, 1.f, 1.f);
     if (nok && a.bias) bv = *reinterpret_cast<const float4*>(a.bias + n);
     if (CONV && nok && a.as) sv = *reinterpret_cast<const float4*>(a.as + n);
+    float dsum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int m = m0 + wr * 2 * HR + (j / HF) * HR + (j % HF) * 16 + frow;
       if (!nok || m >= a.M) continue;
       const long long o = (long long)m * a.ldc + n;
       f32x4 v = acc[i][j];
+      if constexpr (EPI == P_DGELU) {
+        const u32x2 fr = *reinterpret_cast<const u32x2*>(a.aux + o);
+        u32x2 st;
+        st[0] = pack2bf(v[0] * gelu_erf_grad(lo_bf(fr[0])), v[1] * gelu_erf_grad(hi_bf(fr[0])));
+        st[1] = pack2bf(v[2] * gelu_erf_grad(lo_bf(fr[1])), v[3] * gelu_erf_grad(hi_bf(fr[1])));
+        *reinterpret_cast<u32x2*>(a.C + o) = st;
+        dsum[0] += lo_bf(st[0]); dsum[1] += hi_bf(st[0]); dsum[2] += lo_bf(st[1]); dsum[3] += hi_bf(st[1]);
+        continue;
+      }
       v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
       if (CONV && a.res) {
         const u32x2 r = *reinterpret_cast<const u32x2*>(a.res + o);
@@ -268,34 +323,47 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
         }
       }
     }
+    if constexpr (EPI == P_DGELU) {
+      // column sums over this wave's rows: the 16 lanes of a lane group share the columns
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) dsum[c] += __shfl_xor(dsum[c], off, 64);
+      }
+      if (frow == 0 && nok && a.dbias) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) atomicAdd(a.dbias + n + c, dsum[c]);
+      }
+    }
   }
 }
 
-template <int WM, int WN, int FM, int FN, int EPI>
+template <int WM, int WN, int FM, int FN, int EPI, int TB>
 int launch_pp(PArgs a, hipStream_t s) {
   constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   constexpr int LDS = NSLOT * (BM + BN) * 64;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_pp_kernel<WM, WN, FM, FN, EPI>,
+    if (hipFuncSetAttribute((const void*)gemm_pp_kernel<WM, WN, FM, FN, EPI, TB>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return -30;
     attr = true;
   }
+  if (TB == 1 && a.N % BN) return -33;  // k-row tiles are read whole
   a.tiles_n = (a.N + BN - 1) / BN;
   const long long nblk = (long long)((a.M + BM - 1) / BM) * a.tiles_n;
   if (nblk >= (1LL << 31)) return -31;
-  hipLaunchKernelGGL((gemm_pp_kernel<WM, WN, FM, FN, EPI>), dim3((unsigned)nblk), dim3(512), LDS, s, a);
+  hipLaunchKernelGGL((gemm_pp_kernel<WM, WN, FM, FN, EPI, TB>), dim3((unsigned)nblk), dim3(512), LDS, s, a);
   return BE_CHECK_LAUNCH();
 }
 
-template <int EPI>
+template <int EPI, int TB = 0>
 int launch_cfg(PArgs a, int cfg, hipStream_t s) {
   switch (cfg) {
-    case 0: return launch_pp<2, 4, 8, 4, EPI>(a, s);  // 256 x 256, waves 128 x 64
-    case 1: return launch_pp<4, 2, 8, 4, EPI>(a, s);  // 512 x 128, waves 128 x 64
-    case 2: return launch_pp<4, 2, 4, 4, EPI>(a, s);  // 256 x 128, waves 64 x 64
+    case 0: return launch_pp<2, 4, 8, 4, EPI, TB>(a, s);  // 256 x 256, waves 128 x 64
+    case 1: return launch_pp<4, 2, 8, 4, EPI, TB>(a, s);  // 512 x 128, waves 128 x 64
+    case 2: return launch_pp<4, 2, 4, 4, EPI, TB>(a, s);  // 256 x 128, waves 64 x 64
   }
   return -32;
 }
@@ -313,20 +381,31 @@ const bf16_t* zero_page() {
 
 extern "C" {
 
-// C = A B^T (A [M][K], B [N][K], both K-contiguous) with epi 0 none, 1 + bias, 2 + bias and
-// C2 = gelu(C).  cfg: 0 = 256 x 256 tiles, 1 = 512 x 128, 2 = 256 x 128.
-int be_gemm_pp(const void* A, const void* B, void* C, void* C2, const float* bias, int M, int N, int K, int lda,
-               int ldb, int ldc, int epi, int cfg, hipStream_t s) {
+// C = A op(B) with A [M][K] K-contiguous and B [N][K] (tb 0) or [K][N] (tb 1, the dgrad's W as
+// stored).  epi 0 none, 1 + bias, 2 + bias and C2 = gelu(C) (tb 0), 4 GELU backward
+// C = gelu'(aux) * (A B) with dbias += column sums (tb 1).  cfg: 0 = 256 x 256 tiles, 1 = 512 x 128,
+// 2 = 256 x 128.
+int be_gemm_pp(const void* A, const void* B, void* C, void* C2, const float* bias, const void* aux, float* dbias, int M,
+               int N, int K, int lda, int ldb, int ldc, int tb, int epi, int cfg, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (K % KH || N % 4 || lda % 8 || ldb % 8 || ldc % 4) return -40;
   if (epi == P_BIAS_GELU && !C2) return -41;
+  if (epi == P_DGELU && !aux) return -41;
   PArgs a = {};
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = (bf16_t*)C; a.C2 = (bf16_t*)C2; a.bias = bias;
+  a.aux = (const bf16_t*)aux; a.dbias = dbias;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.nkh = K / KH;
-  switch (epi) {
-    case P_NONE: return launch_cfg<P_NONE>(a, cfg, s);
-    case P_BIAS: return launch_cfg<P_BIAS>(a, cfg, s);
-    case P_BIAS_GELU: return launch_cfg<P_BIAS_GELU>(a, cfg, s);
+  if (tb == 0) {
+    switch (epi) {
+      case P_NONE: return launch_cfg<P_NONE>(a, cfg, s);
+      case P_BIAS: return launch_cfg<P_BIAS>(a, cfg, s);
+      case P_BIAS_GELU: return launch_cfg<P_BIAS_GELU>(a, cfg, s);
+    }
+  } else {
+    switch (epi) {
+      case P_NONE: return launch_cfg<P_NONE, 1>(a, cfg, s);
+      case P_DGELU: return launch_cfg<P_DGELU, 1>(a, cfg, s);
+    }
   }
   return -42;
 }

@@ -55,6 +55,26 @@ def test_linear_gelu_gpu(M, N, K, cfg):
     _close(g, F.gelu(f.float()))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(8192, 1024, 3072), (1000, 256, 4096), (300, 512, 96), (777, 1024, 32)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_dgrad_and_dgelu_gpu(M, N, K, cfg):
+    dev = torch.device("cuda", 0)
+    dm, w2 = _rand(M, K, dev=dev, seed=5), _rand(K, N, dev=dev, scale=K ** -0.5, seed=6)
+    if N % pp.TILES[cfg][1]:
+        pytest.skip("N not a whole number of tiles")
+    ref = dm.float() @ w2.float()
+    _close(pp.mm(dm, w2, cfg=cfg), ref)
+    f = _rand(M, N, dev=dev, seed=7)
+    db = torch.empty(N, device=dev)
+    df = pp.mm_dgelu(dm, w2, f, out_db=db, cfg=cfg)
+    x = f.float()
+    gp = 0.5 * (1.0 + torch.erf(x * 0.7071067811865476)) + x * torch.exp(-0.5 * x * x) * 0.3989422804014327
+    want = gp * ref
+    _close(df, want)
+    _close(db, df.float().sum(0), rtol=1e-2)
+
+
 CONV_SHAPES = [(2, 28, 28, 256, 256), (3, 56, 56, 128, 128), (2, 17, 23, 64, 128), (1, 5, 300, 32, 64),
                (4, 28, 28, 128, 256)]
 

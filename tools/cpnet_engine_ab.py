@@ -19,7 +19,11 @@ CONFIGS = {
     "igemm_deep_L1": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0"},
     "pp_deep": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1"},
     "pp_deep_L1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0"},
+    "pp_deep_cfg0": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "0"},
+    "pp_deep_cfg1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "1"},
+    "pp_deep_cfg2": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "2"},
 }
+KEYS = sorted({k for env in CONFIGS.values() for k in env})
 
 
 def main():
@@ -37,6 +41,8 @@ def main():
     x[..., :2] = torch.randn(a.tiles, 224, 224, 2, device=dev, generator=g).to(torch.bfloat16)
     base = None
     for name in a.configs.split(","):
+        for k in KEYS:
+            os.environ.pop(k, None)
         os.environ.update(CONFIGS[name])
         eng = CPnetEngine(net, dev)
         y, _ = eng(x)

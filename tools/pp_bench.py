@@ -67,6 +67,31 @@ def main():
                 ms = timeit(lambda: pp.linear(x, w, b, cfg=c), a.reps)
                 emit(case=name, impl=f"pp cfg{c}", ms=round(ms, 4), TFs=round(fl / ms / 1e9, 1))
             del x, w
+        dcases = [("dgrad qkv b8", 8192, 1024, 3072, False), ("dgrad lin1 b8", 8192, 1024, 4096, False),
+                  ("dgrad proj b8", 8192, 1024, 1024, False), ("dgrad lin2+dgelu b8", 8192, 4096, 1024, True)]
+        for name, M, N, K, dg in dcases:
+            if a.only and a.only not in name:
+                continue
+            dy = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+            w = (torch.randn(K, N, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+            f = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+            db = torch.empty(N, device=dev)
+            fl = 2.0 * M * N * K
+            if dg:
+                from bioengine_worker_amd.ops import vit_train as vt
+
+                zero = torch.zeros(N, device=dev)
+                ms = timeit(lambda: vt.gelu_bwd(torch.mm(dy, w), f, zero, out_db=db), a.reps)
+            else:
+                ms = timeit(lambda: torch.mm(dy, w), a.reps)
+            emit(case=name, impl="torch", ms=round(ms, 4), TFs=round(fl / ms / 1e9, 1))
+            for c in cfgs:
+                if N % pp.TILES[c][1]:
+                    continue
+                fn = (lambda: pp.mm_dgelu(dy, w, f, out_db=db, cfg=c)) if dg else (lambda: pp.mm(dy, w, cfg=c))
+                ms = timeit(fn, a.reps)
+                emit(case=name, impl=f"pp cfg{c}", ms=round(ms, 4), TFs=round(fl / ms / 1e9, 1))
+            del dy, w, f
     if "conv" in a.what:
         from bioengine_worker_amd.ops import conv as convops
         from bioengine_worker_amd.ops import conv_igemm as ig
