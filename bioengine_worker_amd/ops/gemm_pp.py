@@ -106,6 +106,41 @@ def mm_dgelu(dm: torch.Tensor, w2: torch.Tensor, f: torch.Tensor, out_db: torch.
     return df
 
 
+def wgrad_split(M: int, N: int, K: int, cfg: int) -> int:
+    """K slices for a [M, N] weight gradient over K tokens: enough blocks for 256 CUs while each slice
+    keeps >= 16 K-halves (512 tokens)."""
+    bm, bn = TILES[cfg]
+    tiles = (M // bm) * (N // bn)
+    split = 1
+    while tiles * split < 256 and K % (64 * split) == 0 and K // (split * 2) >= 512:
+        split *= 2
+    return split
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, cfg: int | None = None, split: int | None = None):
+    """out (fp32 [n, k], in place) = dy^T x, dy [m, n], x [m, k] bf16 (both read as stored)."""
+    out2 = out.view(out.shape[0], -1)
+    m, n = dy.shape
+    k = x.shape[1]
+    c = (0 if n >= 2048 else 2) if cfg is None else cfg
+    if _forced() is not None and cfg is None:
+        c = _forced()
+    bm, bn = TILES[c]
+    if not dy.is_cuda or n % bm or k % bn or m % 32 or not (dy.is_contiguous() and x.is_contiguous()
+                                                          and out2.is_contiguous()):
+        torch.mm(dy.t().float(), x.float(), out=out2)
+        return
+    sp = wgrad_split(n, k, m, c) if split is None else split
+    ws, wsb = None, 0
+    if sp > 1:
+        from .gemm_bf16 import _workspace
+
+        ws = _workspace(dy.device, sp * n * k * 4)
+        wsb = ws.numel()
+    _native.call("be_wgrad_pp", _native.ptr(dy), _native.ptr(x), _native.ptr(out2), _native.ptr(ws), wsb, n, k, m, n, k,
+                 k, c, sp, _native.stream(dy.device))
+
+
 # ---------------------------------------------------------------------------------------------
 # 3x3 conv
 

@@ -79,7 +79,7 @@ __device__ __forceinline__ bf16x8 frag_t(const unsigned char* t, int c0, int lan
   return v;
 }
 
-enum { P_NONE = 0, P_BIAS = 1, P_BIAS_GELU = 2, P_CONV = 3, P_DGELU = 4 };
+enum { P_NONE = 0, P_BIAS = 1, P_BIAS_GELU = 2, P_CONV = 3, P_DGELU = 4, P_F32 = 5 };
 
 struct PArgs {
   const bf16_t* A;     // GEMM: [M][lda]; CONV: x NHWC [M][Cin]
@@ -97,10 +97,11 @@ struct PArgs {
   int at_ns, arelu, post_relu;
   int M, N, K, lda, ldb, ldc;
   int H, W, HW, cpt;   // CONV geometry; cpt = Cin / 32 (K-halves per tap)
-  int tiles_n, nkh;
+  float* Cf;           // P_F32: fp32 [M][ldc] (split > 1: slabs [split][M][ldc])
+  int tiles_n, nkh, split, kchunk;
 };
 
-template <int WM, int WN, int FM, int FN, int EPI, int TB>
+template <int WM, int WN, int FM, int FN, int EPI, int TA, int TB>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
   static_assert(WM * WN == 8, "8 waves");
   constexpr bool CONV = EPI == P_CONV;
@@ -116,10 +117,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2;  // waves w and w + 4 share a SIMD
   const int wr = wave / WN, wn = wave % WN;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int lid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int sp = lid0 % a.split, lid = lid0 / a.split;  // a tile's K slices run back to back
   const int tm = lid / a.tiles_n, tn = lid % a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nkh = a.nkh;
+  const int kbase = sp * a.kchunk;
 
   // ---- this thread's DMA rows (fixed over K): A rows of both halves, B rows
   const int lr = wave * 16 + (lane >> 2);           // row within a 128-row DMA round
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
 
   auto stage = [&](int J, int part) {
     unsigned char* slot = smem + (J & (NSLOT - 1)) * SLOT;
-    const int k0 = J * KH;
+    const int k0 = kbase + J * KH;
     if (part == 0) {
       if constexpr (TB == 0) {
 #pragma unroll
@@ -181,6 +184,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
       c0 = (J - t * a.cpt) * KH;
       dy = t / 3 - 1;
       dx = t - (t / 3) * 3 - 1;
+    }
+    if constexpr (TA == 1) {
+      // M-contiguous A ([K][M], the wgrad's dy): half `part` is [32 k][BM/2 cols], cols [wr][HR]
+      constexpr int CPR = BM / 16, RPI = 64 / CPR;
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const int blk = i * 8 + wave;
+        const int kr = blk * RPI + lane / CPR;
+        const int cl = 8 * ((lane % CPR) ^ tswz(kr));  // logical column of this lane's chunk
+        const int m = (cl / HR) * 2 * HR + part * HR + (cl % HR);
+        __builtin_amdgcn_global_load_lds((const void*)(a.A + (long long)(k0 + kr) * a.lda + m0 + m),
+                                         (lds_void*)(slot + part * (32 * BM) + blk * 1024), 16, 0, 0);
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
@@ -227,8 +244,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
       // fragment reads of this phase
 #pragma unroll
       for (int jj = 0; jj < HF; ++jj) {
-        const int R = s * (BM / 2) + wr * HR + jj * 16 + frow;
-        af[jj] = *reinterpret_cast<const bf16x8*>(slot + R * 64 + ((fch ^ swz(R)) << 4));
+        if constexpr (TA == 0) {
+          const int R = s * (BM / 2) + wr * HR + jj * 16 + frow;
+          af[jj] = *reinterpret_cast<const bf16x8*>(slot + R * 64 + ((fch ^ swz(R)) << 4));
+        } else {
+          af[jj] = frag_t<BM / 2>(slot + s * (32 * BM), wr * HR + jj * 16, lane);
+        }
       }
       if (s == 0) {
 #pragma unroll
@@ -280,6 +301,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
       if (!nok || m >= a.M) continue;
       const long long o = (long long)m * a.ldc + n;
       f32x4 v = acc[i][j];
+      if constexpr (EPI == P_F32) {
+        *reinterpret_cast<float4*>(a.Cf + (long long)sp * a.M * a.ldc + o) = make_float4(v[0], v[1], v[2], v[3]);
+        continue;
+      }
       if constexpr (EPI == P_DGELU) {
         const u32x2 fr = *reinterpret_cast<const u32x2*>(a.aux + o);
         u32x2 st;
@@ -338,34 +363,47 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PArgs a) {
   }
 }
 
-template <int WM, int WN, int FM, int FN, int EPI, int TB>
+template <int WM, int WN, int FM, int FN, int EPI, int TA, int TB>
 int launch_pp(PArgs a, hipStream_t s) {
   constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   constexpr int LDS = NSLOT * (BM + BN) * 64;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm_pp_kernel<WM, WN, FM, FN, EPI, TB>,
+    if (hipFuncSetAttribute((const void*)gemm_pp_kernel<WM, WN, FM, FN, EPI, TA, TB>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return -30;
     attr = true;
   }
-  if (TB == 1 && a.N % BN) return -33;  // k-row tiles are read whole
+  if ((TB == 1 && a.N % BN) || (TA == 1 && a.M % BM)) return -33;  // k-row tiles are read whole
   a.tiles_n = (a.N + BN - 1) / BN;
-  const long long nblk = (long long)((a.M + BM - 1) / BM) * a.tiles_n;
+  const long long nblk = (long long)((a.M + BM - 1) / BM) * a.tiles_n * a.split;
   if (nblk >= (1LL << 31)) return -31;
-  hipLaunchKernelGGL((gemm_pp_kernel<WM, WN, FM, FN, EPI, TB>), dim3((unsigned)nblk), dim3(512), LDS, s, a);
+  hipLaunchKernelGGL((gemm_pp_kernel<WM, WN, FM, FN, EPI, TA, TB>), dim3((unsigned)nblk), dim3(512), LDS, s, a);
   return BE_CHECK_LAUNCH();
 }
 
-template <int EPI, int TB = 0>
+template <int EPI, int TB = 0, int TA = 0>
 int launch_cfg(PArgs a, int cfg, hipStream_t s) {
   switch (cfg) {
-    case 0: return launch_pp<2, 4, 8, 4, EPI, TB>(a, s);  // 256 x 256, waves 128 x 64
-    case 1: return launch_pp<4, 2, 8, 4, EPI, TB>(a, s);  // 512 x 128, waves 128 x 64
-    case 2: return launch_pp<4, 2, 4, 4, EPI, TB>(a, s);  // 256 x 128, waves 64 x 64
+    case 0: return launch_pp<2, 4, 8, 4, EPI, TA, TB>(a, s);  // 256 x 256, waves 128 x 64
+    case 1: return launch_pp<4, 2, 8, 4, EPI, TA, TB>(a, s);  // 512 x 128, waves 128 x 64
+    case 2: return launch_pp<4, 2, 4, 4, EPI, TA, TB>(a, s);  // 256 x 128, waves 64 x 64
   }
   return -32;
+}
+
+__global__ __launch_bounds__(256) void pp_slab_sum_kernel(const float* __restrict__ s, float* __restrict__ out, int split,
+                                                          long long n4) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 acc = reinterpret_cast<const float4*>(s)[i];
+    for (int k = 1; k < split; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(s + (long long)k * n4 * 4)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = acc;
+  }
 }
 
 const bf16_t* zero_page() {
@@ -395,6 +433,7 @@ int be_gemm_pp(const void* A, const void* B, void* C, void* C2, const float* bia
   a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.C = (bf16_t*)C; a.C2 = (bf16_t*)C2; a.bias = bias;
   a.aux = (const bf16_t*)aux; a.dbias = dbias;
   a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc; a.nkh = K / KH;
+  a.split = 1; a.kchunk = K;
   if (tb == 0) {
     switch (epi) {
       case P_NONE: return launch_cfg<P_NONE>(a, cfg, s);
@@ -425,7 +464,30 @@ int be_conv3_pp(const void* x, const void* w, const float* bias, const void* res
   if (!a.zero) return -13;
   a.M = N * H * W; a.N = Cout; a.K = 9 * Cin; a.lda = Cin; a.ldb = 9 * Cin; a.ldc = Cout;
   a.H = H; a.W = W; a.HW = H * W; a.cpt = Cin / KH; a.nkh = 9 * Cin / KH;
+  a.split = 1; a.kchunk = a.K;
   return launch_cfg<P_CONV>(a, cfg, s);
+}
+
+// Weight gradient out (fp32 [M][ldc]) = A^T B over K tokens with A [K][M] (dy) and B [K][N] (x), both
+// read as stored (transposed in LDS).  split > 1: K is cut into `split` slices written as fp32 slabs
+// into ws (split * M * ldc floats) and summed by a second pass.  M % BM == 0 and N % BN == 0.
+int be_wgrad_pp(const void* A, const void* B, float* out, void* ws, long long ws_bytes, int M, int N, int K, int lda,
+                int ldb, int ldc, int cfg, int split, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (N % 4 || lda % 8 || ldb % 8 || ldc % 4) return -40;
+  if (split < 1 || K % (split * KH)) return -41;
+  if (split > 1 && (!ws || ws_bytes < (long long)split * M * ldc * 4)) return -42;
+  PArgs a = {};
+  a.A = (const bf16_t*)A; a.B = (const bf16_t*)B; a.Cf = split > 1 ? (float*)ws : out;
+  a.M = M; a.N = N; a.K = K; a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.split = split; a.kchunk = K / split; a.nkh = a.kchunk / KH;
+  const int r = launch_cfg<P_F32, 1, 1>(a, cfg, s);
+  if (r != 0 || split == 1) return r;
+  const long long n4 = (long long)M * ldc / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(pp_slab_sum_kernel, dim3(blocks), dim3(256), 0, s, (const float*)ws, out, split, n4);
+  return BE_CHECK_LAUNCH();
 }
 
 }  // extern "C"

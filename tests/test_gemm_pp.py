@@ -75,6 +75,22 @@ def test_dgrad_and_dgelu_gpu(M, N, K, cfg):
     _close(db, df.float().sum(0), rtol=1e-2)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(8192, 3072, 1024), (1024, 1024, 4096), (2048, 256, 512), (96, 512, 256)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_wgrad_gpu(m, n, k, cfg):
+    dev = torch.device("cuda", 0)
+    bm, bn = pp.TILES[cfg]
+    if n % bm or k % bn:
+        pytest.skip("weight shape not a whole number of tiles")
+    dy, x = _rand(m, n, dev=dev, seed=8), _rand(m, k, dev=dev, seed=9)
+    ref = dy.float().t() @ x.float()
+    for split in (None, 1):
+        out = torch.full((n, k), float("nan"), device=dev)
+        pp.wgrad(dy, x, out, cfg=cfg, split=split)
+        _close(out, ref, rtol=5e-3)
+
+
 CONV_SHAPES = [(2, 28, 28, 256, 256), (3, 56, 56, 128, 128), (2, 17, 23, 64, 128), (1, 5, 300, 32, 64),
                (4, 28, 28, 128, 256)]
 

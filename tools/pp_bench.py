@@ -92,6 +92,28 @@ def main():
                 ms = timeit(fn, a.reps)
                 emit(case=name, impl=f"pp cfg{c}", ms=round(ms, 4), TFs=round(fl / ms / 1e9, 1))
             del dy, w, f
+        wcases = [("wgrad qkv b8", 8192, 3072, 1024), ("wgrad proj b8", 8192, 1024, 1024),
+                  ("wgrad lin1 b8", 8192, 4096, 1024), ("wgrad lin2 b8", 8192, 1024, 4096),
+                  ("wgrad qkv b1", 1024, 3072, 1024), ("wgrad lin1 b1", 1024, 4096, 1024)]
+        for name, m, n, k in wcases:
+            if a.only and a.only not in name:
+                continue
+            dy = torch.randn(m, n, device=dev, generator=g).to(torch.bfloat16)
+            x = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
+            out = torch.empty(n, k, device=dev)
+            fl = 2.0 * m * n * k
+            ms = timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=out), a.reps)
+            emit(case=name, impl="torch", ms=round(ms, 4), TFs=round(fl / ms / 1e9, 1))
+            ms = timeit(lambda: gb.wgrad(dy, x, out), a.reps)
+            emit(case=name, impl="gemm_bf16", ms=round(ms, 4), TFs=round(fl / ms / 1e9, 1))
+            for c in cfgs:
+                bm, bn = pp.TILES[c]
+                if n % bm or k % bn:
+                    continue
+                ms = timeit(lambda: pp.wgrad(dy, x, out, cfg=c), a.reps)
+                emit(case=name, impl=f"pp cfg{c}", split=pp.wgrad_split(n, k, m, c), ms=round(ms, 4),
+                     TFs=round(fl / ms / 1e9, 1))
+            del dy, x, out
     if "conv" in a.what:
         from bioengine_worker_amd.ops import conv as convops
         from bioengine_worker_amd.ops import conv_igemm as ig
