@@ -56,8 +56,7 @@ def main():
             from bioengine_worker_amd.ops import gemm_auto
 
             ch = gemm_auto.choices()
-            out["gemm_choices"] = {"hip": sum(c["impl"] == "hip" for c in ch), "lib": sum(c["impl"] == "lib" for c in ch),
-                                   "table": ch}
+            out["gemm_choices"] = {**{k: sum(c["impl"] == k for c in ch) for k in ("hip", "pp", "lib")}, "table": ch}
         print(json.dumps(out), flush=True)
         del tr
         torch.cuda.empty_cache()
