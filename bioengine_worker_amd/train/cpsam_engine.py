@@ -41,10 +41,14 @@ import torch.nn.functional as F
 from ..models.cpsam import CPSAM, get_rel_pos
 import os as _os
 
-# GEMM backend of the engine: per shape, the faster of the in-house bf16 MFMA GEMMs with fused
-# epilogues and the library GEMM (ops/gemm_auto.py, decided on the eager warm-up steps);
-# BE_CPSAM_GEMM=hip / lib pins one side
-_GEMM = _os.environ.get("BE_CPSAM_GEMM", "auto")
+# GEMM backend of the engine.  "auto" = per shape, the fastest in isolation of the in-house bf16 MFMA
+# GEMMs with fused epilogues (ops/gemm_bf16.py, ops/gemm_pp.py) and the library GEMM
+# (ops/gemm_auto.py, decided on the eager warm-up steps); "hip" / "lib" pin one side.  The default
+# is the library: on the whole graphed step it measured 11.35 / 31.70 ms at batch 1 / 8 against
+# 12.69 / 32.67 for "auto" (profiles/r04/cpsam/cpsam_gemm_*.jsonl) -- the in-house kernels win
+# several shapes alone, but hold a whole CU each (LDS) and so no longer overlap the weight
+# gradients the engine runs on its side stream
+_GEMM = _os.environ.get("BE_CPSAM_GEMM", "lib")
 if _GEMM == "lib":
     from ..ops import gemm
 elif _GEMM == "hip":

@@ -51,7 +51,7 @@ def main():
         out = {"bench": "cpsam_finetune_step", "engine": "hip", "batch": B, "depth": args.depth,
                "ms_per_step": round(dt * 1e3, 3), "samples_per_sec": round(B / dt, 2), "loss": float(loss),
                "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
-               "gemm": os.environ.get("BE_CPSAM_GEMM", "auto")}
+               "gemm": os.environ.get("BE_CPSAM_GEMM", "lib")}
         if out["gemm"] == "auto":
             from bioengine_worker_amd.ops import gemm_auto
 
