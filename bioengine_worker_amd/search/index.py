@@ -8,8 +8,11 @@ fixed-size chunks.  Past ``ivf_threshold`` vectors an IVF layer (spherical k-mea
 lists, whose list-sorted bf16 slabs are scored EXACTLY by the HIP scan kernel
 (``csrc/kernels/ivf_scan.hip``) -- the reference needs 8-bit PQ codes at this size because it is
 CPU/DRAM bound; on one 288 GB GPU the full vectors fit, so recall is limited only by probing.  The
-compressed IVF-PQ tier (``search/ivfpq.py``) is kept for collections that do not fit.
-Storage is plain ``.npy`` + JSON (no pickles).
+compressed IVF-PQ tier (``search/ivfpq.py``) is kept for collections that do not fit:
+:meth:`VectorIndex.compress` keeps only the PQ codes on the GPU (m=192: 192 B per vector, 11 GB at
+58 M) and moves the full vectors to HOST memory, where the PQ shortlist (``refine * k``
+candidates) is gathered and re-scored exactly on the GPU -- FAISS ``IndexRefineFlat`` with the
+refine store off the device.  Storage is plain ``.npy`` + JSON (no pickles).
 
 Layout at ``<workspace>/cell_search/``: ``vectors.npy`` (fp16 [N, D]), ``index_info.json``,
 ``ivf_centroids.npy`` / ``ivf_assign.npy`` (IVF only), ``metadata.parquet``, ``thumbnails.npy``.
@@ -66,6 +69,7 @@ class VectorIndex:
         self.centroids: torch.Tensor | None = None
         self.assign: torch.Tensor | None = None
         self.lists: list[torch.Tensor] | None = None
+        self.host_refine = False  # compressed tier: self.vecs lives in host memory (refine store only)
 
     # ------------------------------------------------------------------ build
     @property
@@ -81,7 +85,7 @@ class VectorIndex:
     def add(self, x) -> None:
         x = torch.as_tensor(np.asarray(x, np.float32) if not torch.is_tensor(x) else x).to(self.device, self.dtype)
         assert x.dim() == 2 and x.shape[1] == self.dim
-        self.vecs = torch.cat([self.vecs, x], 0)
+        self.vecs = torch.cat([self.vecs, x.to(self.vecs.device)], 0)
         if self.pq is not None:
             self.pq.add(x.float())
         elif self.kind == "ivfpq" or (self.kind == "auto" and self.ntotal >= self.ivfpq_threshold
@@ -106,10 +110,33 @@ class VectorIndex:
         n = self.ntotal
         nl = nlist or min(default_nlist(n), max(1, n // 39))
         pq = IVFPQIndex(self.dim, nl, self.pq_m, self.nprobe, self.device)
-        pq.train(self.vecs.float())
-        pq.add(self.vecs.float())
+        g = torch.Generator(device="cpu").manual_seed(0)
+        sample = self.vecs[torch.randperm(n, generator=g)[: min(n, max(262_144, 39 * nl))].to(self.vecs.device)]
+        pq.train(sample.float())
+        for i in range(0, n, 1 << 22):  # encode in chunks: no fp32 copy of the whole collection
+            pq.add(self.vecs[i:i + (1 << 22)].float())
         self.pq = pq
         self.centroids = None
+
+    def compress(self, pq_m: int = 192, refine: int = 50, nlist: int | None = None) -> dict:
+        """Switch to the compressed tier: IVF-PQ codes (``pq_m`` bytes per vector) on the GPU, the full
+        vectors in host memory as the exact re-rank store.  Search returns the top-k of the
+        ``refine * k`` PQ candidates re-scored exactly.  Returns the GPU / host footprint (bytes)."""
+        self.pq_m, self.refine = pq_m, refine
+        self.lvecs = None
+        self.train_ivfpq(nlist)
+        self.vecs = self.vecs.cpu()  # bf16 on the host: ~1.5 KB per vector, gathered per query
+        self.host_refine = True
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+        return {"gpu_bytes": self.pq.gpu_bytes(), "host_bytes": int(self.vecs.numel() * self.vecs.element_size())}
+
+    def _refine_rows(self, c: torch.Tensor) -> torch.Tensor:
+        """[Q, R] candidate ids (>= 0) -> their stored vectors [Q, R, D] on the index device."""
+        if not self.host_refine:
+            return self.vecs[c]
+        rows = self.vecs.index_select(0, c.reshape(-1).cpu())  # host gather (multi-threaded)
+        return rows.to(self.device, non_blocking=False).view(*c.shape, self.dim)
 
     def train_ivf(self, nlist: int | None = None, iters: int = 10, seed: int = 0) -> None:
         n = self.ntotal
@@ -170,7 +197,7 @@ class VectorIndex:
             _, cand = self.pq.search(q.float(), self.refine * k)
             c = torch.from_numpy(cand).to(self.device)
             ok = c >= 0
-            s = torch.einsum("qd,qkd->qk", q.float(), self.vecs[c.clamp(min=0)].float())
+            s = torch.einsum("qd,qkd->qk", q.float(), self._refine_rows(c.clamp(min=0)).float())
             s = torch.where(ok, s, torch.full_like(s, -float("inf")))
             ts, ti = torch.topk(s, min(k, s.shape[1]), dim=1)
             ids = torch.where(torch.isfinite(ts), torch.gather(c, 1, ti), torch.full_like(ti, -1))
@@ -244,7 +271,7 @@ class VectorIndex:
         return best_s, best_i
 
     def reconstruct_batch(self, ids) -> np.ndarray:
-        return self.vecs[torch.as_tensor(np.asarray(ids), device=self.device)].float().cpu().numpy()
+        return self.vecs[torch.as_tensor(np.asarray(ids), device=self.vecs.device)].float().cpu().numpy()
 
     # ------------------------------------------------------------------ persistence
     def save(self, out_dir) -> dict:
@@ -261,6 +288,7 @@ class VectorIndex:
         else:
             (out / "ivf_centroids.npy").unlink(missing_ok=True)
         info = {"n_cells": self.ntotal, "embed_dim": self.dim, "index_type": self.index_type,
+                "host_refine": self.host_refine, "refine": self.refine,
                 "index_size_mb": round((out / "vectors.npy").stat().st_size / 2 ** 20, 3),
                 "build_seconds": round(time.time() - t0, 3),
                 "build_time_iso": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
@@ -275,11 +303,17 @@ class VectorIndex:
             raise FileNotFoundError(f"No index at {p}")
         v = np.load(p)  # allow_pickle=False
         idx = cls(dim=v.shape[1], device=device)
-        idx.vecs = torch.from_numpy(v.astype(np.float32)).to(idx.device, idx.dtype)
+        ii = out / "index_info.json"
+        info = json.loads(ii.read_text()) if ii.exists() else {}
+        host = bool(info.get("host_refine")) and (out / "ivfpq_info.json").exists()
+        idx.vecs = torch.from_numpy(v.astype(np.float32)).to("cpu" if host else idx.device, idx.dtype)
         if (out / "ivfpq_info.json").exists():
             from .ivfpq import IVFPQIndex
 
             idx.pq = IVFPQIndex.load(out, device=idx.device)
+            idx.host_refine = host
+            idx.refine = int(info.get("refine", idx.refine))
+            idx.pq_m = idx.pq.m
             return idx
         c = out / "ivf_centroids.npy"
         if c.exists():

@@ -125,13 +125,29 @@ class IVFPQIndex:
             codes.append(_pq_encode(xc - self.centroids[a], self.codebooks))
             assigns.append(a.int())
         self._assign = torch.cat([self._assign] + assigns)
-        self._raw_codes = torch.cat([self._raw_codes] + codes)
+        raw = torch.cat([self._raw()] + codes)
         self.ntotal = int(self._assign.shape[0])
         order = torch.argsort(self._assign, stable=True)
-        self.codes = self._raw_codes[order].contiguous()
+        self.codes = raw[order].contiguous()
         self.ids = order
+        # id-order codes are not kept: the list-sorted copy + ids reconstruct them (_raw), so the GPU
+        # holds m + 12 bytes per vector (204 B at m = 192: 11.8 GB at 58 M)
+        self._raw_codes = None
+        del raw
         counts = torch.bincount(self._assign.long(), minlength=self.nlist)
         self.list_off = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0)])
+
+    def _raw(self) -> torch.Tensor:
+        """Codes in id order [N, m]."""
+        if self._raw_codes is not None:
+            return self._raw_codes
+        raw = torch.empty_like(self.codes)
+        raw[self.ids] = self.codes
+        return raw
+
+    def gpu_bytes(self) -> int:
+        t = [self.codes, self.ids, self._assign, self.centroids, self.codebooks, self.list_off]
+        return int(sum(x.numel() * x.element_size() for x in t if x is not None))
 
     # ------------------------------------------------------------------ search
     def _lut(self, q: torch.Tensor) -> torch.Tensor:
@@ -205,10 +221,10 @@ class IVFPQIndex:
         out.mkdir(parents=True, exist_ok=True)
         np.save(out / "ivfpq_centroids.npy", self.centroids.cpu().numpy())
         np.save(out / "ivfpq_codebooks.npy", self.codebooks.cpu().numpy())
-        np.save(out / "ivfpq_codes.npy", self._raw_codes.cpu().numpy())
+        np.save(out / "ivfpq_codes.npy", self._raw().cpu().numpy())
         np.save(out / "ivfpq_assign.npy", self._assign.cpu().numpy())
         info = {"n_cells": self.ntotal, "embed_dim": self.dim, "index_type": self.index_type, "nprobe": self.nprobe,
-                "index_size_mb": round(self._raw_codes.numel() / 2 ** 20, 3)}
+                "index_size_mb": round(self.codes.numel() / 2 ** 20, 3)}
         (out / "ivfpq_info.json").write_text(json.dumps(info, indent=2))
         return info
 
@@ -223,10 +239,11 @@ class IVFPQIndex:
         idx.codebooks = torch.from_numpy(cb).to(idx.device)
         codes = torch.from_numpy(np.load(out / "ivfpq_codes.npy")).to(idx.device)
         assign = torch.from_numpy(np.load(out / "ivfpq_assign.npy")).to(idx.device)
-        idx._raw_codes, idx._assign = codes, assign
+        idx._assign = assign
         idx.ntotal = int(assign.shape[0])
         order = torch.argsort(assign, stable=True)
         idx.codes, idx.ids = codes[order].contiguous(), order
+        idx._raw_codes = None
         counts = torch.bincount(assign.long(), minlength=idx.nlist)
         idx.list_off = torch.cat([counts.new_zeros(1), torch.cumsum(counts, 0)])
         return idx

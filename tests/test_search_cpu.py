@@ -143,3 +143,32 @@ def test_cell_image_search_app_e2e(tmp_path, monkeypatch):
 
     asyncio.run(asyncio.wait_for(main(), 600))
     reset_local_hubs()
+
+
+def test_compressed_tier_host_refine(tmp_path):
+    """compress(): PQ codes on the index device, full vectors in host memory as the exact re-rank
+    store; the refined top-k matches exact search, and save/load keeps the tier."""
+    import torch
+
+    from bioengine_worker_amd.search.index import VectorIndex
+
+    g = torch.Generator().manual_seed(0)
+    cent = torch.nn.functional.normalize(torch.randn(40, 64, generator=g), dim=1)
+    x = torch.nn.functional.normalize(cent[torch.randint(0, 40, (4000,), generator=g)]
+                                      + 0.3 * torch.randn(4000, 64, generator=g), dim=1)
+    q = torch.nn.functional.normalize(x[:16] + 0.05 * torch.randn(16, 64, generator=g), dim=1)
+    idx = VectorIndex(dim=64, device="cpu", index_type="flat")
+    idx.add(x)
+    _, exact = idx.search(q, 10)
+    fp = idx.compress(pq_m=16, refine=20, nlist=16)
+    assert idx.host_refine and idx.vecs.device.type == "cpu" and fp["host_bytes"] > 0 and fp["gpu_bytes"] > 0
+    idx.pq.nprobe = 16
+    _, got = idx.search(q, 10)
+    rec = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(exact, got)])
+    assert rec >= 0.9, rec
+    idx.save(tmp_path)
+    back = VectorIndex.load(tmp_path, device="cpu")
+    assert back.host_refine and back.pq is not None and back.refine == 20
+    back.pq.nprobe = 16
+    _, got2 = back.search(q, 10)
+    assert (got2 == got).all()

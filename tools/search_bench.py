@@ -82,6 +82,10 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--nprobes", default="16,32,64,128,256")
     ap.add_argument("--no-pq", action="store_true")
+    ap.add_argument("--tiers", default="ivf,pq96,compressed",
+                    help="ivf: exact-scan IVF; pq96: IVF-PQ m=96 (+ GPU re-rank); compressed: IVF-PQ m=192 on "
+                         "the GPU with the full vectors in host memory as the re-rank store (VectorIndex.compress)")
+    ap.add_argument("--refines", default="400,1000,2000", help="compressed tier: re-ranked candidates per query")
     ap.add_argument("--queries", default="near,ood", help="near: indexed vectors + small noise; "
                     "ood: held-out sub-centres of the indexed classes (ood_queries)")
     a = ap.parse_args()
@@ -116,15 +120,18 @@ def main():
             p50, p95 = timeit(fn, a.reps)
             print(json.dumps({"n": n, "tier": "FlatIP-GPU bf16", "query": name, "p50_ms": round(p50, 3),
                               "p95_ms": round(p95, 3), "recall@10": 1.0, "R@10": 1.0}), flush=True)
+        tiers = a.tiers.split(",")
         # ---- IVF exact scan over list-sorted HBM slabs
         t0 = time.perf_counter()
         ivf = VectorIndex(dim=a.dim, device=dev, index_type="ivf")
         ivf.vecs = x
-        ivf.train_ivf()
+        if "ivf" in tiers:
+            ivf.train_ivf()
+        nprobes = [int(v) for v in a.nprobes.split(",")] if "ivf" in tiers else []
         torch.cuda.synchronize()
         build = time.perf_counter() - t0
-        nl = ivf.centroids.shape[0]
-        for npb in [int(v) for v in a.nprobes.split(",")]:
+        nl = ivf.centroids.shape[0] if ivf.centroids is not None else 0
+        for npb in nprobes:
             rec = {qn: recalls(gts[qn], ivf.search(qv, a.k, nprobe=npb)[1]) for qn, qv in qsets.items()}
             r10, r1 = next(iter(rec.values()))
             for name, qq in (("q1", q[:1]), ("q64", q)):
@@ -138,6 +145,35 @@ def main():
         del ivf
         torch.cuda.empty_cache()
         if a.no_pq:
+            del x, flat
+            torch.cuda.empty_cache()
+            continue
+        if "compressed" in tiers:
+            # ---- compressed tier: m=192 PQ codes on the GPU, full vectors in host memory (re-rank store)
+            t0 = time.perf_counter()
+            cvi = VectorIndex(dim=a.dim, device=dev, index_type="ivfpq")
+            cvi.vecs = x
+            fp = cvi.compress(pq_m=192, refine=50)
+            torch.cuda.synchronize()
+            build = time.perf_counter() - t0
+            for R in [int(v) for v in a.refines.split(",")]:
+                cvi.refine = max(1, R // a.k)
+                rec = {qn: recalls(gts[qn], cvi.search(qv, a.k)[1]) for qn, qv in qsets.items()}
+                r10, r1 = next(iter(rec.values()))
+                for name, qq in (("q1", q[:1]), ("q64", q)):
+                    cvi.search(qq, a.k)
+                    p50, p95 = timeit(lambda: cvi.search(qq, a.k), max(3, a.reps // 2))
+                    print(json.dumps({"n": n, "tier": f"IVFPQ m=192 GPU + host re-rank {cvi.refine * a.k}",
+                                      "query": name, "p50_ms": round(p50, 3), "p95_ms": round(p95, 3),
+                                      "recall@10": r10, "R@10": r1,
+                                      "recall@10_by_queries": {k: v[0] for k, v in rec.items()},
+                                      "R@10_by_queries": {k: v[1] for k, v in rec.items()},
+                                      "nlist": cvi.pq.nlist, "nprobe": cvi.pq.nprobe, "build_s": round(build, 2),
+                                      "gpu_index_gb": round(fp["gpu_bytes"] / 1e9, 3),
+                                      "host_refine_gb": round(fp["host_bytes"] / 1e9, 3)}), flush=True)
+            del cvi
+            torch.cuda.empty_cache()
+        if "pq96" not in tiers:
             del x, flat
             torch.cuda.empty_cache()
             continue
