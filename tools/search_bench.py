@@ -150,6 +150,7 @@ def main():
             continue
         if "compressed" in tiers:
             # ---- compressed tier: m=192 PQ codes on the GPU, full vectors in host memory (re-rank store)
+            print(json.dumps({"n": n, "stage": "compressed tier build (IVF-PQ m=192 + host copy)"}), flush=True)
             t0 = time.perf_counter()
             cvi = VectorIndex(dim=a.dim, device=dev, index_type="ivfpq")
             cvi.vecs = x
