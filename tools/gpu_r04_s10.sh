@@ -13,3 +13,5 @@ rm -f $O/kt/t_kernel_trace.csv
 head -30 $O/kt_table.txt
 timeout -k 10 900 python -u tools/search_bench.py --n 58000000 --tiers compressed --refines 400,1000,2000 --reps 10 > $O/search58m.jsonl 2>&1 || { tail -20 $O/search58m.jsonl; exit 1; }
 grep '^{' $O/search58m.jsonl | cut -c1-600
+timeout -k 10 300 python -u tools/search_serve_bench.py --concurrency 64 --seconds 4 --profile gpurun_out/r04/s10/search_main_c64.prof.txt > $O/search_serve_prof.log 2>&1 || { tail -20 $O/search_serve_prof.log; exit 1; }
+grep '^{' $O/search_serve_prof.log | cut -c1-300

@@ -88,9 +88,24 @@ async def main_async(a) -> list[dict]:
                 assert len(out["results"]) == min(20, n_cells)
                 k += conc
 
+        prof = None
+        if getattr(a, "profile", None) and conc == max(a.concurrency):
+            import cProfile
+
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         await asyncio.gather(*[client(c) for c in range(conc)])
         dt = time.perf_counter() - t0
+        if prof is not None:
+            import io as _io
+            import pstats
+
+            prof.disable()
+            buf = _io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
+            pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(80)
+            Path(a.profile).write_text(buf.getvalue())
         ms = np.array(lat) * 1e3
         rr = {"concurrency": conc, "requests": len(lat), "qps": round(len(lat) / dt, 1),
               "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
@@ -117,6 +132,8 @@ def main():
     ap.add_argument("--model", default="vitb14")
     ap.add_argument("--max-ongoing", type=int, default=64)
     ap.add_argument("--replica-mode", default="process")
+    ap.add_argument("--profile", default=None, metavar="PATH",
+                    help="cProfile of this process (client + hub + bridge + router) at the highest concurrency")
     a = ap.parse_args()
     a.concurrency = [int(c) for c in a.concurrency.split(",")]
     asyncio.run(main_async(a))
