@@ -187,12 +187,66 @@ def _run_with_ctx(ctx, model_id, fn, args, kwargs):
 # ====================================================================== process replicas
 
 
+#: strings at least this long (base64 images and thumbnails in request / response dicts) travel as
+#: out-of-band UTF-8 buffers -- through the shared-memory ring with the arrays -- instead of inside
+#: the pickle header that crosses the socket (pickle's C fast path never offers str to a reducer)
+BIG_STR = 16 << 10
+
+
+def _big_str(buf) -> str:
+    return str(buf, "utf-8")
+
+
+class _BigStr:
+    __slots__ = ("b",)
+
+    def __init__(self, b: bytes):
+        self.b = b
+
+    def __reduce_ex__(self, protocol):
+        return _big_str, (pickle.PickleBuffer(self.b),)
+
+
+def _lift_strings(o, depth: int = 0):
+    """Copy of the plain dict / list / tuple skeleton of ``o`` with long strings wrapped as
+    :class:`_BigStr`; ``o`` itself when nothing qualifies (no copy)."""
+    t = type(o)
+    if t is str:
+        if len(o) >= BIG_STR:
+            try:
+                return _BigStr(o.encode("utf-8"))
+            except UnicodeEncodeError:
+                return o
+        return o
+    if depth >= 6:
+        return o
+    if t is dict:
+        out = None
+        for k, v in o.items():
+            w = _lift_strings(v, depth + 1)
+            if w is not v:
+                if out is None:
+                    out = dict(o)
+                out[k] = w
+        return o if out is None else out
+    if t is list or t is tuple:
+        items = None
+        for i, v in enumerate(o):
+            w = _lift_strings(v, depth + 1)
+            if w is not v:
+                if items is None:
+                    items = list(o)
+                items[i] = w
+        return o if items is None else (items if t is list else tuple(items))
+    return o
+
+
 def dumps(obj) -> list:
-    """Pickle-5 header + the out-of-band buffers as zero-copy memoryviews."""
+    """Pickle-5 header + the out-of-band buffers (arrays, long strings) as zero-copy memoryviews."""
     import cloudpickle
 
     bufs: list = []
-    head = cloudpickle.dumps(obj, protocol=5, buffer_callback=bufs.append)
+    head = cloudpickle.dumps(_lift_strings(obj), protocol=5, buffer_callback=bufs.append)
     return [head] + [b.raw() if hasattr(b, "raw") else memoryview(b) for b in bufs]
 
 
