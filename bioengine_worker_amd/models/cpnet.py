@@ -392,11 +392,17 @@ class CPnetEngine:
                 add(("up", i, 0), blk.conv[0][-1])
             for k in (1, 2, 3):
                 add(("up", i, k), blk.conv[k].conv[-1])
-        # a level runs on the igemm path only when all of its 3x3 convs do
+        # a level runs on the igemm path only when all of its 3x3 convs do; BE_CPNET_IGEMM_LEVELS
+        # (e.g. "3") restricts it to the listed down levels and the up blocks at their resolution
         levels = {}
         for (kind, idx, k) in ig:
             levels.setdefault((kind, idx), set()).add(k)
         full = {lv for lv, ks in levels.items() if ks >= {1, 2, 3}}
+        only = os.environ.get("BE_CPNET_IGEMM_LEVELS")
+        if only:
+            keep = {int(v) for v in only.split(",") if v.strip()}
+            # up block i writes level i's resolution (the last one stays at the deepest level's)
+            full = {lv for lv in full if lv[1] in keep}
         return {key: v for key, v in ig.items() if (key[0], key[1]) in full}
 
     def _ig_level(self, kind: str, idx: int, x: torch.Tensor, H: int, W: int) -> bool:

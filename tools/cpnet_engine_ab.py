@@ -17,6 +17,7 @@ CONFIGS = {
     "perlayer_L1": {"BE_CPNET_IGEMM": "0", "BE_CPNET_PAIR_LEVELS": "0"},
     "igemm_deep": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0,1"},
     "igemm_deep_L1": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0"},
+    "igemm_L3": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_IGEMM_LEVELS": "3"},
     "pp_deep": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1"},
     "pp_deep_L1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0"},
     "pp_deep_cfg0": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "0"},
