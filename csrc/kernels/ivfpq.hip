@@ -67,6 +67,9 @@ int be_ivfpq_scan(const void* lut, const float* base, const int* probes, const l
     case 48: hipLaunchKernelGGL(ivfpq_scan_kernel<48>, grid, dim3(256), 0, s, l, base, probes, list_off, cand_off, codes, nprobe, cand_stride, out); break;
     case 64: hipLaunchKernelGGL(ivfpq_scan_kernel<64>, grid, dim3(256), 0, s, l, base, probes, list_off, cand_off, codes, nprobe, cand_stride, out); break;
     case 96: hipLaunchKernelGGL(ivfpq_scan_kernel<96>, grid, dim3(256), 0, s, l, base, probes, list_off, cand_off, codes, nprobe, cand_stride, out); break;
+    // compressed tier (VectorIndex.compress): 4-dim sub-spaces; the 96 KB fp16 table still fits LDS
+    case 128: hipLaunchKernelGGL(ivfpq_scan_kernel<128>, grid, dim3(256), 0, s, l, base, probes, list_off, cand_off, codes, nprobe, cand_stride, out); break;
+    case 192: hipLaunchKernelGGL(ivfpq_scan_kernel<192>, grid, dim3(256), 0, s, l, base, probes, list_off, cand_off, codes, nprobe, cand_stride, out); break;
     default: return -1;
   }
   return BE_CHECK_LAUNCH();

@@ -58,16 +58,17 @@ def test_vector_index_ivfpq_tier_cpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_ivfpq_scan_kernel_matches_oracle(gpu):
+@pytest.mark.parametrize("m", [96, 192])
+def test_ivfpq_scan_kernel_matches_oracle(gpu, m):
     x, q = _data(n=20000, d=768 // 8 * 8, nq=16)
     x, q = torch.nn.functional.pad(x, (0, 768 - x.shape[1])), torch.nn.functional.pad(q, (0, 768 - q.shape[1]))
-    idx = IVFPQIndex(dim=768, nlist=64, m=96, nprobe=16, device=gpu)
+    idx = IVFPQIndex(dim=768, nlist=64, m=m, nprobe=16, device=gpu)
     idx.train(x.to(gpu))
     idx.add(x.to(gpu))
     S, I = idx.search(q.to(gpu), k=20)
-    cpu = IVFPQIndex(dim=768, nlist=64, m=96, nprobe=16, device="cpu")
+    cpu = IVFPQIndex(dim=768, nlist=64, m=m, nprobe=16, device="cpu")
     cpu.centroids, cpu.codebooks = idx.centroids.cpu(), idx.codebooks.cpu()
-    cpu._assign, cpu._raw_codes, cpu.ntotal = idx._assign.cpu(), idx._raw_codes.cpu(), idx.ntotal
+    cpu._assign, cpu._raw_codes, cpu.ntotal = idx._assign.cpu(), idx._raw().cpu(), idx.ntotal
     cpu.codes, cpu.ids, cpu.list_off = idx.codes.cpu(), idx.ids.cpu(), idx.list_off.cpu()
     S2, I2 = cpu.search(q, k=20)
     assert np.abs(S - S2).max() < 1e-3
