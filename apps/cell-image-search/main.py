@@ -26,6 +26,8 @@ from pathlib import Path
 from uuid import uuid4
 
 import numpy as np
+
+from bioengine_worker_amd.serve.replica import BIG_STR, Utf8Str
 from hypha_rpc.utils.schema import schema_method
 from pydantic import Field
 from ray import serve
@@ -423,7 +425,11 @@ class CellImageSearch:
             if i < nmeta:
                 for c, col in cols:
                     r[c] = col[i]
-            r["thumbnail_b64"] = (tb[i] if tb is not None else self._thumb_b64(i)) if i < nth else ""
+            t = (tb[i] if tb is not None else self._thumb_b64(i)) if i < nth else ""
+            if type(t) is str and len(t) >= BIG_STR and tb is not None:
+                # cached UTF-8 form: the thumbnail leaves the replica without a per-response encode
+                t = tb[i] = Utf8Str(t)
+            r["thumbnail_b64"] = t
             out.append(r)
         return out
 
@@ -476,7 +482,8 @@ class CellImageSearch:
             # the batch's query thumbnails: one call into the host runtime's linear-time PNG encoder,
             # spread over host threads outside the GIL (csrc/runtime/png.cpp)
             order = sorted(thumbs)
-            enc = dict(zip(order, png_b64_batch(np.stack([thumbs[i] for i in order])))) if order else {}
+            enc = dict(zip(order, (Utf8Str(v) for v in png_b64_batch(np.stack([thumbs[i] for i in order]))))) \
+                if order else {}
             tm.append(time.perf_counter())
             st = self.__dict__.setdefault("_stage_ms", {"batches": 0, "lock": 0.0, "embed": 0.0, "scan": 0.0,
                                                         "results": 0.0, "thumbs": 0.0})

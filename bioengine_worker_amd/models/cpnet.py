@@ -301,11 +301,12 @@ class CPnetEngine:
         self.style_s = torch.cat(ss, 0).contiguous()
         self.style_t = torch.cat(ts, 0).contiguous()
         self.pair = self._build_pairs(net) if os.environ.get("BE_CPNET_PAIR", "1") != "0" else {}
-        # deep levels on the implicit-GEMM kernels (BE_CPNET_IGEMM=1): opt-in -- whole-network A/B on
-        # MI355X measured 15.05 vs 14.69 ms per 288 tiles for the per-layer path
-        # (profiles/r04/conv/engine_ab_v2.jsonl): the producer-side activated copies cost more HBM
-        # traffic than the DMA-fed main loop saves
-        self.ig_kind = os.environ.get("BE_CPNET_IGEMM", "0")
+        # deepest level on the implicit-GEMM kernels (BE_CPNET_IGEMM=1, BE_CPNET_IGEMM_LEVELS=3 by
+        # default): whole-network A/B on MI355X 14.38 vs 14.62 ms per 288 tiles for the per-layer
+        # path (profiles/r04/conv/engine_ab_L3.jsonl).  On both deep levels the producer-side
+        # activated copies cost more HBM traffic than the DMA-fed main loop saves at 56^2 (14.68;
+        # engine_ab_v2.jsonl); BE_CPNET_IGEMM=0 / pp select the per-layer / ping-pong kernels
+        self.ig_kind = os.environ.get("BE_CPNET_IGEMM", "1")
         self.ig = self._build_igemm(net) if self.ig_kind in ("1", "pp") else {}
         # output layer fused into the last half-block's epilogue (ops/conv_pair.py HeadSpec)
         self.head = None
@@ -398,7 +399,7 @@ class CPnetEngine:
         for (kind, idx, k) in ig:
             levels.setdefault((kind, idx), set()).add(k)
         full = {lv for lv, ks in levels.items() if ks >= {1, 2, 3}}
-        only = os.environ.get("BE_CPNET_IGEMM_LEVELS")
+        only = os.environ.get("BE_CPNET_IGEMM_LEVELS", "3")
         if only:
             keep = {int(v) for v in only.split(",") if v.strip()}
             # up block i writes level i's resolution (the last one stays at the deepest level's)

@@ -207,10 +207,28 @@ class _BigStr:
         return _big_str, (pickle.PickleBuffer(self.b),)
 
 
+class Utf8Str(str):
+    """A ``str`` that carries its UTF-8 bytes (``.utf8``): long strings a server returns again and
+    again -- pre-encoded base64 thumbnails -- cross the process boundary without a per-message
+    ``encode``.  Behaves as a plain ``str`` everywhere else (JSON, msgpack, comparisons)."""
+
+    __slots__ = ("utf8",)
+
+    def __new__(cls, s: str, utf8: bytes | None = None):
+        o = super().__new__(cls, s)
+        o.utf8 = utf8 if utf8 is not None else s.encode("utf-8")
+        return o
+
+    def __reduce__(self):
+        return str, (str(self),)
+
+
 def _lift_strings(o, depth: int = 0):
     """Copy of the plain dict / list / tuple skeleton of ``o`` with long strings wrapped as
     :class:`_BigStr`; ``o`` itself when nothing qualifies (no copy)."""
     t = type(o)
+    if t is Utf8Str:
+        return _BigStr(o.utf8) if len(o.utf8) >= BIG_STR else o
     if t is str:
         if len(o) >= BIG_STR:
             try:

@@ -144,6 +144,7 @@ def test_cpnet_engine_igemm_path_matches_module(monkeypatch, kind):
         ref, style_ref = net(x)[:2]
     xin = to_nhwc_input(x, 8).to(dev)
     monkeypatch.setenv("BE_CPNET_IGEMM", kind)
+    monkeypatch.setenv("BE_CPNET_IGEMM_LEVELS", "2,3")
     eng = CPnetEngine(net, dev)
     assert ("down", 3, 1) in eng.ig and ("up", 3, 0) in eng.ig and ("up", 2, 1) in eng.ig
     y, st = eng(xin)

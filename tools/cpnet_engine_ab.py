@@ -13,16 +13,20 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 CONFIGS = {
+    "default": {},
     "perlayer_deep": {"BE_CPNET_IGEMM": "0", "BE_CPNET_PAIR_LEVELS": "0,1"},
     "perlayer_L1": {"BE_CPNET_IGEMM": "0", "BE_CPNET_PAIR_LEVELS": "0"},
-    "igemm_deep": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0,1"},
-    "igemm_deep_L1": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0"},
+    "igemm_deep": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_IGEMM_LEVELS": "2,3"},
+    "igemm_deep_L1": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0", "BE_CPNET_IGEMM_LEVELS": "1,2,3"},
     "igemm_L3": {"BE_CPNET_IGEMM": "1", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_IGEMM_LEVELS": "3"},
-    "pp_deep": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1"},
-    "pp_deep_L1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0"},
-    "pp_deep_cfg0": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "0"},
-    "pp_deep_cfg1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "1"},
-    "pp_deep_cfg2": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "2"},
+    "pp_deep": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_IGEMM_LEVELS": "2,3"},
+    "pp_deep_L1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0", "BE_CPNET_IGEMM_LEVELS": "1,2,3"},
+    "pp_deep_cfg0": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "0",
+                     "BE_CPNET_IGEMM_LEVELS": "2,3"},
+    "pp_deep_cfg1": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "1",
+                     "BE_CPNET_IGEMM_LEVELS": "2,3"},
+    "pp_deep_cfg2": {"BE_CPNET_IGEMM": "pp", "BE_CPNET_PAIR_LEVELS": "0,1", "BE_CPNET_PP_CFG": "2",
+                     "BE_CPNET_IGEMM_LEVELS": "2,3"},
 }
 KEYS = sorted({k for env in CONFIGS.values() for k in env})
 
