@@ -440,18 +440,17 @@ class CellImageSearch:
     # stretch, PIL thumbnail, single-image embed and FAISS search, main.py:1373-1418).
     @serve.batch(max_batch_size=64, batch_wait_timeout_s=0.002, max_concurrent_batches=2)
     async def _query_batch(self, reqs: list) -> list:
-        """reqs: [(image HWC ndarray | None, embedding [D] | None, plow, phigh, top_k)] ->
-        [(results list, query thumbnail base64)]."""
+        """reqs: [(image HWC ndarray | base64 .npy str | None, embedding [D] | None, plow, phigh, top_k)]
+        -> [(results list, query thumbnail base64)].  Base64 .npy payloads are decoded here, for the
+        whole batch at once on host threads outside the GIL (csrc/runtime/png.cpp), not per request
+        on the event loop."""
         import torch
 
-        from bioengine_worker_amd.search.ingestion import png_b64_batch
+        from bioengine_worker_amd.search import reference as ref
+        from bioengine_worker_amd.search.ingestion import b64decode_batch, png_b64_batch
         from bioengine_worker_amd.search.preprocess import batch_to_dinov2
 
         n = len(reqs)
-        groups: dict = {}
-        for i, (img, emb, pl, ph, _) in enumerate(reqs):
-            if emb is None:
-                groups.setdefault((img.shape, img.dtype.str, pl, ph), []).append(i)
         kmax = max(int(r[4]) for r in reqs)
 
         def run():
@@ -459,10 +458,19 @@ class CellImageSearch:
             q = [None] * n
             thumbs = {}
             tm = [time.perf_counter()]
+            imgs = [r[0] for r in reqs]
+            enc = [i for i, im in enumerate(imgs) if isinstance(im, str)]
+            if enc:
+                for i, raw in zip(enc, b64decode_batch([imgs[i] for i in enc])):
+                    imgs[i] = ref.to_hwc(np.load(io.BytesIO(memoryview(raw))))
+            groups: dict = {}
+            for i, (_, emb, pl, ph, _) in enumerate(reqs):
+                if emb is None:
+                    groups.setdefault((imgs[i].shape, imgs[i].dtype.str, pl, ph), []).append(i)
             with self._gpu_lock:
                 tm.append(time.perf_counter())
                 for (_, _, pl, ph), idxs in groups.items():
-                    x = torch.from_numpy(np.ascontiguousarray(np.stack([reqs[i][0] for i in idxs]))).to(dev)
+                    x = torch.from_numpy(np.ascontiguousarray(np.stack([imgs[i] for i in idxs]))).to(dev)
                     t, u8 = batch_to_dinov2(x, None, pl, ph, return_u8=True)
                     eng = self._worker.engine
                     e = (eng.embed_graphed(t) if hasattr(eng, "embed_graphed") else eng.embed(t)).float()
@@ -485,10 +493,10 @@ class CellImageSearch:
             enc = dict(zip(order, (Utf8Str(v) for v in png_b64_batch(np.stack([thumbs[i] for i in order]))))) \
                 if order else {}
             tm.append(time.perf_counter())
-            st = self.__dict__.setdefault("_stage_ms", {"batches": 0, "lock": 0.0, "embed": 0.0, "scan": 0.0,
+            st = self.__dict__.setdefault("_stage_ms", {"batches": 0, "decode": 0.0, "embed": 0.0, "scan": 0.0,
                                                         "results": 0.0, "thumbs": 0.0})
             st["batches"] += 1
-            for k, a, b in (("lock", 0, 1), ("embed", 1, 2), ("scan", 2, 3), ("results", 3, 4), ("thumbs", 4, 5)):
+            for k, a, b in (("decode", 0, 1), ("embed", 1, 2), ("scan", 2, 3), ("results", 3, 4), ("thumbs", 4, 5)):
                 st[k] += (tm[b] - tm[a]) * 1e3
             return [(res[i], enc.get(i, "")) for i in range(n)]
 
@@ -508,13 +516,12 @@ class CellImageSearch:
 
         img = None
         if embedding is None:
-            if image_b64 is not None:
-                # .npy payloads decode in microseconds (no thread hop); compressed images in a thread
-                raw = _decode_image_b64(image_b64) if _is_npy_b64(image_b64) else \
-                    await asyncio.to_thread(_decode_image_b64, image_b64)
+            if image_b64 is not None and _is_npy_b64(image_b64):
+                img = image_b64  # decoded with the rest of its batch (_query_batch)
             else:
-                raw = np.asarray(image)
-            img = ref.to_hwc(np.asarray(raw))
+                raw = await asyncio.to_thread(_decode_image_b64, image_b64) if image_b64 is not None \
+                    else np.asarray(image)
+                img = ref.to_hwc(np.asarray(raw))
         results, qthumb = await self._query_batch((img, embedding, float(plow), float(phigh), int(top_k)))
         return {"results": results, "query_thumbnail_b64": qthumb,
                 "elapsed_ms": round((time.time() - t0) * 1000, 1), "n_cells_searched": self._index.ntotal, "top_k": top_k}

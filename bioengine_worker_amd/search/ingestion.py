@@ -233,6 +233,38 @@ def png_b64_batch(rgb: np.ndarray, threads: int = 8) -> list[str]:
         return [png_b64(rgb[i], 1) for i in range(n)]
 
 
+def b64decode_batch(strings: list, threads: int = 8) -> list:
+    """Decoded bytes (uint8 ndarray views) of base64 strings, decoded by the host runtime on host
+    threads outside the GIL (``csrc/runtime/png.cpp``); falls back to :func:`base64.b64decode`."""
+    n = len(strings)
+    if n == 0:
+        return []
+    try:
+        import ctypes
+
+        from ..ops import _native
+
+        lib = _native.runtime()
+        # the ASCII bytes of each string: attached to strings received out of band (serve/replica.py
+        # Utf8Str), else one encode
+        raw = [np.frombuffer(s.utf8, np.uint8) if hasattr(s, "utf8") else
+               np.frombuffer(s.encode("ascii") if isinstance(s, str) else s, np.uint8) for s in strings]
+        ptrs = (ctypes.c_void_p * n)(*[r.ctypes.data for r in raw])
+        lens = np.array([r.size for r in raw], np.int64)
+        cap = int(lens.max()) * 3 // 4 + 3
+        out = np.empty(cap * n, np.uint8)
+        olen = np.empty(n, np.int64)
+        lib.be_rt_b64decode_batch.argtypes = None  # variadic-safe: pass ctypes objects as they are
+        rc = lib.be_rt_b64decode_batch(ptrs, lens.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(n),
+                                       out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(cap),
+                                       olen.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(int(threads)))
+        if rc != 0 or (olen < 0).any():
+            raise ValueError("b64 decode failed")
+        return [out[i * cap: i * cap + int(olen[i])] for i in range(n)]
+    except (OSError, AttributeError, ImportError, UnicodeEncodeError, ValueError):
+        return [np.frombuffer(base64.b64decode(s), np.uint8) for s in strings]
+
+
 THUMBS_B64 = "thumbnails_b64.txt"
 
 

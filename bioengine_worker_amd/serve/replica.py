@@ -194,7 +194,9 @@ BIG_STR = 16 << 10
 
 
 def _big_str(buf) -> str:
-    return str(buf, "utf-8")
+    # the received bytes stay attached: a consumer that wants them (base64 decoding, a re-send)
+    # reads .utf8 instead of encoding the string again
+    return Utf8Str(str(buf, "utf-8"), buf)
 
 
 class _BigStr:

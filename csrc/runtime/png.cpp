@@ -1,4 +1,5 @@
-// Base64 PNG encoding of RGB uint8 thumbnails for the served search path (SURVEY.md §2.8 cell-image-search;
+// Base64 codecs for the served search path: batch base64 DECODE of the query payloads and base64
+// PNG encoding of RGB uint8 thumbnails (SURVEY.md §2.8 cell-image-search;
 // the reference returns a 224x224 PNG query thumbnail per request, apps/cell-image-search/main.py:1394-1397).
 //
 // The served query thumbnail is encoded once per request on the host, on the critical path of every
@@ -182,6 +183,70 @@ int be_rt_png_b64_batch(const unsigned char* rgb, int n, int h, int w, char* out
     for (int i = t; i < n; i += threads) {
       encode_png(rgb + i * img, h, w, (long long)w * 3, png);
       lens[i] = b64(png, out + i * cap, cap);
+    }
+  };
+  if (threads == 1) {
+    work(0);
+    return 0;
+  }
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  return 0;
+}
+
+// Decode n base64 strings (src[i], src_len[i] chars; characters outside the alphabet are skipped,
+// as Python's base64.b64decode does by default) into out + i * cap_each; out_len[i] = decoded bytes
+// (-1: cap_each too small).  Spread over `threads` host threads (called without the GIL).
+int be_rt_b64decode_batch(const char* const* src, const long long* src_len, int n, unsigned char* out,
+                          long long cap_each, long long* out_len, int threads) {
+  if (n <= 0) return 0;
+  static const auto table = [] {
+    struct T { signed char v[256]; } t;
+    for (int i = 0; i < 256; ++i) t.v[i] = -1;
+    const char* A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    for (int i = 0; i < 64; ++i) t.v[(unsigned char)A[i]] = (signed char)i;
+    return t;
+  }();
+  if (threads < 1) threads = 1;
+  if (threads > n) threads = n;
+  auto work = [&](int t) {
+    for (int i = t; i < n; i += threads) {
+      const unsigned char* p = reinterpret_cast<const unsigned char*>(src[i]);
+      const long long len = src_len[i];
+      unsigned char* o = out + (long long)i * cap_each;
+      long long w = 0;
+      uint32_t acc = 0;
+      int bits = 0;
+      bool over = false;
+      long long k = 0;
+      // fast path: whole 4-character groups of alphabet characters -> 3 bytes
+      while (k + 4 <= len && w + 3 <= cap_each) {
+        const int a = table.v[p[k]], b = table.v[p[k + 1]], c = table.v[p[k + 2]], d = table.v[p[k + 3]];
+        if ((a | b | c | d) < 0) break;
+        const uint32_t v = ((uint32_t)a << 18) | ((uint32_t)b << 12) | ((uint32_t)c << 6) | (uint32_t)d;
+        o[w] = (unsigned char)(v >> 16);
+        o[w + 1] = (unsigned char)(v >> 8);
+        o[w + 2] = (unsigned char)v;
+        w += 3;
+        k += 4;
+      }
+      for (; k < len; ++k) {
+        const int v = table.v[p[k]];
+        if (v < 0) {
+          if (p[k] == '=') break;
+          continue;
+        }
+        acc = (acc << 6) | (uint32_t)v;
+        bits += 6;
+        if (bits >= 8) {
+          bits -= 8;
+          if (w >= cap_each) { over = true; break; }
+          o[w++] = (unsigned char)((acc >> bits) & 0xff);
+        }
+      }
+      out_len[i] = over ? -1 : w;
     }
   };
   if (threads == 1) {
