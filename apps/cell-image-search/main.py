@@ -61,6 +61,13 @@ def _upsert_registry(ws: str, entry: dict) -> None:
     _save_registry(ws, reg)
 
 
+#: query batching: up to _QUERY_BATCH concurrent searches share one ViT forward + scan, with up to
+#: _QUERY_CONC batches in flight, so one batch's result encoding / transport overlaps the next
+#: batch's forward (a single 64-wide batch at 64 concurrent clients serialises the whole closed loop)
+_QUERY_BATCH = int(os.environ.get("BIOENGINE_SEARCH_MAX_BATCH", "32"))
+_QUERY_CONC = int(os.environ.get("BIOENGINE_SEARCH_CONCURRENT_BATCHES", "2"))
+
+
 def _is_npy_b64(s: str) -> bool:
     return s[:8] == base64.b64encode(b"\x93NUMPY")[:8].decode()
 
@@ -438,7 +445,7 @@ class CellImageSearch:
     # scan, the query thumbnails from the same resized uint8 tensor, and every request's result list
     # -- each request then does O(1) Python on the event loop (reference: per request decode, CPU
     # stretch, PIL thumbnail, single-image embed and FAISS search, main.py:1373-1418).
-    @serve.batch(max_batch_size=64, batch_wait_timeout_s=0.002, max_concurrent_batches=2)
+    @serve.batch(max_batch_size=_QUERY_BATCH, batch_wait_timeout_s=0.002, max_concurrent_batches=_QUERY_CONC)
     async def _query_batch(self, reqs: list) -> list:
         """reqs: [(image HWC ndarray | base64 .npy str | None, embedding [D] | None, plow, phigh, top_k)]
         -> [(results list, query thumbnail base64)].  Base64 .npy payloads are decoded here, for the
