@@ -63,9 +63,11 @@ def _upsert_registry(ws: str, entry: dict) -> None:
 
 #: query batching: up to _QUERY_BATCH concurrent searches share one ViT forward + scan, with up to
 #: _QUERY_CONC batches in flight, so one batch's result encoding / transport overlaps the next
-#: batch's forward (a single 64-wide batch at 64 concurrent clients serialises the whole closed loop)
-_QUERY_BATCH = int(os.environ.get("BIOENGINE_SEARCH_MAX_BATCH", "32"))
-_QUERY_CONC = int(os.environ.get("BIOENGINE_SEARCH_CONCURRENT_BATCHES", "2"))
+#: batch's forward.  A single 64-wide batch at 64 concurrent clients serialises the whole closed
+#: loop: 1,396 q/s, p99 167 ms; 32 x 3: 2,305 q/s, p99 108 ms; 16 x 4: 2,401 q/s, p50 24.8 /
+#: p99 42.5 ms (MI355X, profiles/r04/search/search_batch_ab.jsonl)
+_QUERY_BATCH = int(os.environ.get("BIOENGINE_SEARCH_MAX_BATCH", "16"))
+_QUERY_CONC = int(os.environ.get("BIOENGINE_SEARCH_CONCURRENT_BATCHES", "4"))
 
 
 def _is_npy_b64(s: str) -> bool:
