@@ -22,6 +22,7 @@ Offline there are no pretrained weights: ``ViT(...).randomize_(seed)`` gives DIN
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -186,10 +187,16 @@ class ViTEngine:
                 fc2_b=bf(blk.mlp.fc2.bias), g2=ls(blk.ls2)))
         self.nw, self.nb = f32(net.norm.weight), f32(net.norm.bias)
         if precision == "fp8":
-            # e4m3 weights with per-output-channel scales; the bf16 copies are dropped
+            # e4m3 weights with per-output-channel scales; the bf16 copies are dropped.  qkv reads the
+            # LayerNorm's per-token e4m3 and has no fused epilogue, so it runs wherever its plain GEMM is
+            # fastest (BE_VIT_QKV_GEMM; hipBLASLt by default: 43.0 vs 60.9 us at batch 64,
+            # profiles/r03/fp8/fp8_bench_s23.jsonl); proj / fc1 / fc2 keep the HIP kernel for the
+            # MX-fp8 hand-offs its epilogues fuse
+            qkv_gemm = os.environ.get("BE_VIT_QKV_GEMM", "hipblaslt" if fp8_gemm == "hip" else fp8_gemm)
             for b in self.blocks:
                 for name in ("qkv", "proj", "fc1", "fc2"):
-                    b[name + "_q"] = Fp8Linear(b.pop(name + "_w"), b.pop(name + "_b"), gemm=fp8_gemm)
+                    b[name + "_q"] = Fp8Linear(b.pop(name + "_w"), b.pop(name + "_b"),
+                                               gemm=qkv_gemm if name == "qkv" else fp8_gemm)
 
     def patchify(self, x: torch.Tensor) -> torch.Tensor:
         """[B, C, H, W] -> [B, gh*gw, C*p*p] in conv-weight order (c, ky, kx) — a reshape + one copy."""

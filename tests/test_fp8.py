@@ -181,8 +181,11 @@ def test_gemm_fp8_mx_epilogue_and_block_scaled_input(gpu, M, N, K):
 
 
 @pytest.mark.gpu
-def test_vit_engine_fp8_hip_mx_embedding_close(gpu):
-    """The HIP fp8 path (MX-fp8 between fc1 and fc2) against the bf16 engine, end to end."""
+@pytest.mark.parametrize("qkv_gemm", ["hipblaslt", "hip"])
+def test_vit_engine_fp8_hip_mx_embedding_close(gpu, qkv_gemm, monkeypatch):
+    """The HIP fp8 path (MX-fp8 between fc1 and fc2; qkv on either GEMM) against the bf16 engine,
+    end to end."""
+    monkeypatch.setenv("BE_VIT_QKV_GEMM", qkv_gemm)
     net = ViT(ViTConfig.dinov2("vitb14")).randomize_(0).eval()
     x = torch.randn(4, 3, 224, 224)
     ref = ViTEngine(net, gpu).embed(x.to(gpu))
