@@ -141,9 +141,6 @@ def build_hip(jobs: int, variant: str | None = None, vsrc: str | None = None, vf
     if tl and Path(tl, "libamdhip64.so").exists():
         # Resolve libamdhip64 against the runtime PyTorch ships so the process has ONE HIP runtime.
         link += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
-    # gemm_lt.hip drives hipBLASLt (epilogue-fused, autotuned library GEMMs); with the torch lib dir
-    # first on the search path this resolves to the hipBLASLt PyTorch itself loads (one copy per process)
-    link += ["-lhipblaslt"]
     r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
