@@ -273,6 +273,7 @@ def bench_served_search(seconds: float = 4.0) -> dict:
         out[f"search_served_qps_c{c}"] = r["qps"]
         out[f"search_served_p50_ms_c{c}"] = r["p50_ms"]
         out[f"search_served_p99_ms_c{c}"] = r["p99_ms"]
+        out[f"search_served_mean_batch_c{c}"] = r.get("mean_query_batch")
         b = r.get("batching") or {}
     if b:  # the app's query batcher over the whole run (all concurrency levels)
         out["search_served_query_batching"] = {k: b[k] for k in ("batches", "requests", "mean_batch", "hist") if k in b}

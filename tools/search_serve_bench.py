@@ -29,6 +29,12 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 
+def _batch_delta(before: dict, after: dict) -> float | None:
+    """Mean query batch over one concurrency level (the app's counters are cumulative)."""
+    nb = after.get("batches", 0) - before.get("batches", 0)
+    return round((after.get("requests", 0) - before.get("requests", 0)) / nb, 2) if nb else None
+
+
 async def main_async(a) -> list[dict]:
     from bioengine_worker_amd.transport import connect_to_server
     from bioengine_worker_amd.transport.hub import get_local_hub
@@ -75,6 +81,7 @@ async def main_async(a) -> list[dict]:
         lat: list[float] = []
         srv: list[float] = []
         last: dict = {}
+        q0 = (await app.get_batch_stats()).get("query", {})
         stop = time.perf_counter() + a.seconds
 
         async def client(cid):
@@ -111,6 +118,7 @@ async def main_async(a) -> list[dict]:
               "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
               "p99_ms": round(float(np.percentile(ms, 99)), 2), "n_cells": n_cells, "model": a.model,
               "replica_p50_ms": round(float(np.percentile(srv, 50)), 2),
+              "mean_query_batch": _batch_delta(q0, (await app.get_batch_stats()).get("query", {})),
               "response_kb": round(len(json.dumps(last.get("o", {}))) / 1024, 1)}
         results.append(rr)
         print(json.dumps(rr), flush=True)
