@@ -66,6 +66,93 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
+// Same update, two float4 groups per thread per iteration with both groups' 4 loads issued before
+// any use (8 x 16 B in flight per lane), and streaming (non-temporal) accesses: every byte is
+// touched exactly once per step, so nothing is worth keeping in L2 / MALL.  A/B: be_adamw_set_variant.
+__global__ __launch_bounds__(256) void adamw2_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                     float* __restrict__ m, float* __restrict__ v,
+                                                     bf16_t* __restrict__ pbf, long long n, float lr, float b1,
+                                                     float b2, float eps, float wd, float bc1, float bc2, float gscale,
+                                                     const float* __restrict__ hp) {
+  if (hp) {
+    lr = hp[0]; wd = hp[1]; bc1 = hp[2]; bc2 = hp[3]; gscale = hp[4];
+  }
+  typedef __attribute__((ext_vector_type(4))) float f4;
+  const long long n4 = n / 4;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float step_size = lr / bc1;
+  const float rbc2 = rsqrtf(bc2);
+  const float decay = 1.f - lr * wd;
+  f4* P = reinterpret_cast<f4*>(p);
+  const f4* G = reinterpret_cast<const f4*>(g);
+  f4* M = reinterpret_cast<f4*>(m);
+  f4* V = reinterpret_cast<f4*>(v);
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const long long i2 = i + stride;
+    f4 pp[2], gg[2], mm[2], vv[2];
+    pp[0] = __builtin_nontemporal_load(P + i); pp[1] = __builtin_nontemporal_load(P + i2);
+    gg[0] = __builtin_nontemporal_load(G + i); gg[1] = __builtin_nontemporal_load(G + i2);
+    mm[0] = __builtin_nontemporal_load(M + i); mm[1] = __builtin_nontemporal_load(M + i2);
+    vv[0] = __builtin_nontemporal_load(V + i); vv[1] = __builtin_nontemporal_load(V + i2);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gj = gg[u][j] * gscale;
+        float pj = pp[u][j] * decay;
+        const float mj = b1 * mm[u][j] + (1.f - b1) * gj;
+        const float vj = b2 * vv[u][j] + (1.f - b2) * gj * gj;
+        pj -= step_size * mj / (sqrtf(vj) * rbc2 + eps);
+        pp[u][j] = pj; mm[u][j] = mj; vv[u][j] = vj;
+      }
+    }
+    __builtin_nontemporal_store(pp[0], P + i); __builtin_nontemporal_store(pp[1], P + i2);
+    __builtin_nontemporal_store(mm[0], M + i); __builtin_nontemporal_store(mm[1], M + i2);
+    __builtin_nontemporal_store(vv[0], V + i); __builtin_nontemporal_store(vv[1], V + i2);
+    if (pbf) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        u32x2 o;
+        o[0] = pack2bf(pp[u][0], pp[u][1]);
+        o[1] = pack2bf(pp[u][2], pp[u][3]);
+        __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(pbf) + (u ? i2 : i));
+      }
+    }
+  }
+  for (; i < n4; i += stride) {  // the last partial round
+    f4 pp = P[i], gg = G[i], mm = M[i], vv = V[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = gg[j] * gscale;
+      float pj = pp[j] * decay;
+      const float mj = b1 * mm[j] + (1.f - b1) * gj;
+      const float vj = b2 * vv[j] + (1.f - b2) * gj * gj;
+      pj -= step_size * mj / (sqrtf(vj) * rbc2 + eps);
+      pp[j] = pj; mm[j] = mj; vv[j] = vj;
+    }
+    P[i] = pp; M[i] = mm; V[i] = vv;
+    if (pbf) {
+      u32x2 o;
+      o[0] = pack2bf(pp[0], pp[1]);
+      o[1] = pack2bf(pp[2], pp[3]);
+      reinterpret_cast<u32x2*>(pbf)[i] = o;
+    }
+  }
+  const long long t0 = n4 * 4;  // scalar tail
+  for (long long k = t0 + (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const float gj = g[k] * gscale;
+    float pj = p[k] * decay;
+    const float mj = b1 * m[k] + (1.f - b1) * gj;
+    const float vj = b2 * v[k] + (1.f - b2) * gj * gj;
+    pj -= step_size * mj / (sqrtf(vj) * rbc2 + eps);
+    p[k] = pj; m[k] = mj; v[k] = vj;
+    if (pbf) pbf[k] = f2bf(pj);
+  }
+}
+
+int g_adamw_variant = 0;  // 1: adamw2_kernel, 0: adamw_kernel (default until the A/B)
+
 // sum of squares of a flat fp32 buffer (for gradient-norm clipping / logging); out must be zeroed.
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n, float* __restrict__ out) {
   float s = 0.f;
@@ -90,9 +177,19 @@ int be_adamw_flat(float* p, const float* g, float* m, float* v, void* pbf, long 
   const long long n4 = (n + 3) / 4;
   int blocks = (int)((n4 + 255) / 256);
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd, bc1, bc2,
-                     gscale, (const float*)nullptr);
+  if (g_adamw_variant == 1)
+    hipLaunchKernelGGL(adamw2_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd,
+                       bc1, bc2, gscale, (const float*)nullptr);
+  else
+    hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd, bc1,
+                       bc2, gscale, (const float*)nullptr);
   return BE_CHECK_LAUNCH();
+}
+
+// A/B switch of the flat update kernel: 1 = two float4 groups per lane + streaming accesses, 0 = one.
+int be_adamw_set_variant(int variant) {
+  g_adamw_variant = variant;
+  return 0;
 }
 
 // Same update with {lr, wd, bc1, bc2, gscale} read from device memory (graph-capturable).  p/g/m/v/
