@@ -27,4 +27,4 @@ def test_adamw_variants_match_reference(variant, n):
         _native.call("be_adamw_set_variant", 0)
     for got, want in ((p, ref[0]), (m, ref[2]), (v, ref[3])):
         assert torch.allclose(got.cpu(), want, rtol=1e-5, atol=1e-6), (got.cpu() - want).abs().max()
-    assert torch.equal(mirror.cpu(), ref[0].to(torch.bfloat16))
+    assert torch.equal(mirror.cpu(), p.cpu().to(torch.bfloat16))  # the mirror is the kernel's own p, rounded
