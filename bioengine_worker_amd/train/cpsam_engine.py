@@ -46,8 +46,9 @@ import os as _os
 # (ops/gemm_auto.py, decided on the eager warm-up steps); "hip" / "lib" pin one side.  The default
 # is the library: on the whole graphed step it measured 11.35 / 31.70 ms at batch 1 / 8 against
 # 12.69 / 32.67 for "auto" (profiles/r04/cpsam/cpsam_gemm_*.jsonl) -- the in-house kernels win
-# several shapes alone, but hold a whole CU each (LDS) and so no longer overlap the weight
-# gradients the engine runs on its side stream
+# several shapes when timed alone, but the eager per-shape timing did not predict the graphed step
+# (the cause is not pinned down: cold first-call timings and cache state between back-to-back
+# kernels are the candidates)
 _GEMM = _os.environ.get("BE_CPSAM_GEMM", "lib")
 if _GEMM == "lib":
     from ..ops import gemm
