@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void adamw2_kernel(float* __restrict__ p, cons
   }
 }
 
-int g_adamw_variant = 0;  // 1: adamw2_kernel, 0: adamw_kernel (default until the A/B)
+int g_adamw_variant = 1;  // 1: adamw2_kernel (1.916 vs 1.941 ms at ViT-L, profiles/r04/cpsam/adamw_ab.jsonl), 0: adamw_kernel
 
 // sum of squares of a flat fp32 buffer (for gradient-norm clipping / logging); out must be zeroed.
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, long long n, float* __restrict__ out) {
