@@ -12,6 +12,7 @@ CPU path: the numpy/torch oracle (:mod:`.reference`) — used by CPU tests and C
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -278,7 +279,7 @@ class CellposeRunner:
         before mask recovery of micro-batch i (which syncs the host on its own stream) starts."""
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_mask_stream", None) is None:
-            self._mask_stream = torch.cuda.Stream(self.device)
+            self._mask_stream = mask_stream(self.device)
         side = self._mask_stream
         parts = x.tensor_split(nch)
         ys, styles, masks = [], [], []
@@ -337,7 +338,7 @@ class CellposeRunner:
             ev.record(main)
         with mask_lock:
             if getattr(self, "_mask_stream", None) is None:
-                self._mask_stream = torch.cuda.Stream(self.device)
+                self._mask_stream = mask_stream(self.device)
             side = self._mask_stream
             with torch.cuda.stream(side):
                 side.wait_event(ev)
@@ -379,6 +380,14 @@ class CellposeRunner:
                                   max_size_fraction=p.max_size_fraction)
             out.append(torch.from_numpy(m.astype(np.int32)))
         return torch.stack(out)
+
+
+def mask_stream(device) -> "torch.cuda.Stream":
+    """The second stream mask recovery runs on, beside the next batch's network.
+    ``BE_MASK_STREAM_PRIO`` (A/B): HIP stream priority, -1 = high (its kernels dispatch ahead of the
+    queued conv workgroups), 0 = normal."""
+    prio = int(os.environ.get("BE_MASK_STREAM_PRIO", "0"))
+    return torch.cuda.Stream(device, priority=prio)
 
 
 class _GroupNormEngine:
@@ -450,7 +459,7 @@ class _EvalStream:
         self.cuda = runner.device.type == "cuda" and p.compute_masks
         if self.cuda:
             if getattr(runner, "_mask_stream", None) is None:
-                runner._mask_stream = torch.cuda.Stream(runner.device)
+                runner._mask_stream = mask_stream(runner.device)
             self.side = runner._mask_stream
 
     @torch.no_grad()

@@ -4,7 +4,8 @@ tiles, staggered wave groups, best at large M) -- and the library GEMM (:mod:`.g
 through PyTorch) for the CPSAM training engine.
 
 None wins everywhere (``profiles/r04/gemm/``).  The first EAGER call of each (op, shape) runs every
-eligible implementation (HIP-event median of 3, after one warm-up each), keeps the fastest and
+eligible implementation (median of 3 replays of a HIP graph of 10 calls, after one warm-up each:
+kernel time, not launch overhead), keeps the fastest and
 writes its result last; later calls -- and every call inside a HIP-graph capture, whose shapes the
 eager warm-up steps of the engine have already decided -- go straight to the winner.
 ``BE_GEMM_AUTO=hip`` / ``pp`` / ``lib`` pins one side (A/B), and :func:`choices` reports the table."""
@@ -28,16 +29,39 @@ def _capturing() -> bool:
         return False
 
 
-def _time(fn, reps: int = 3) -> float:
+def _time(fn, reps: int = 10) -> float:
+    """GPU time of one call, in ms.  The calls are captured into a HIP graph and replayed, so the
+    figure is kernel time: bracketing single eager launches with events (the first version) timed
+    the host launch path instead -- ~40 us per call against ~17-22 us on the GPU at batch 1 -- and
+    picked kernels that then lost inside the graphed step (profiles/r04/cpsam/)."""
     fn()
-    ts = []
-    for _ in range(reps):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        fn()
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e))
+    torch.cuda.synchronize()
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        ts = []
+        for _ in range(3):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            g.replay()
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e) / reps)
+        del g
+    except Exception:  # noqa: BLE001  (a path that cannot be captured: time it eagerly)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(3):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                fn()
+            e.record()
+            e.synchronize()
+            ts.append(s.elapsed_time(e) / reps)
     ts.sort()
     return ts[len(ts) // 2]
 

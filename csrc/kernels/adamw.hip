@@ -8,6 +8,8 @@
 // read).  The data-parallel gradient mean (1/world) and an optional gradient-norm clip factor are
 // folded in as `gscale`, so no separate scaling pass runs after the RCCL all-reduce.  An optional
 // bf16 mirror of the updated weights is written in the same pass for the bf16 compute kernels.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -199,10 +201,20 @@ int be_adamw_flat_dev(float* p, const float* g, float* m, float* v, void* pbf, l
   if (n <= 0) return 0;
   const long long n4 = (n + 3) / 4;
   int blocks = (int)((n4 + 255) / 256);
-  if (blocks > 2048) blocks = 2048;
-  if (blocks > 256) blocks = 256;  // a background stream: one block per CU, leave room for the backward
-  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, 0.f, b1, b2, eps, 0.f,
-                     1.f, 1.f, 1.f, hp);
+  // a background stream: at most one block per CU (BE_ADAMW_BG_BLOCKS caps it lower), leaving room
+  // for the backward kernels it runs beside
+  static const int cap = [] {
+    const char* e = getenv("BE_ADAMW_BG_BLOCKS");
+    const int c = e ? atoi(e) : 256;
+    return c > 0 ? c : 256;
+  }();
+  if (blocks > cap) blocks = cap;
+  if (g_adamw_variant == 1)
+    hipLaunchKernelGGL(adamw2_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, 0.f, b1, b2, eps, 0.f,
+                       1.f, 1.f, 1.f, hp);
+  else
+    hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n, 0.f, b1, b2, eps, 0.f,
+                       1.f, 1.f, 1.f, hp);
   return BE_CHECK_LAUNCH();
 }
 

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--depth", type=int, default=24)
     ap.add_argument("--baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=-1, help="override TrainConfig.graph (0/1)")
+    ap.add_argument("--overlap-adamw", type=int, default=-1,
+                    help="override TrainConfig.cpsam_overlap_adamw (0/1): per-group AdamW inside the graph")
     args = ap.parse_args()
     from bioengine_worker_amd.models.cpsam import CPSAM
     from bioengine_worker_amd.ops import train_ops
@@ -37,6 +39,8 @@ def main():
         cfg = TrainConfig(batch_size=B, bsize=256, lr=1e-5, weight_decay=1e-4)
         if args.graph >= 0:
             cfg.graph = bool(args.graph)
+        if args.overlap_adamw >= 0:
+            cfg.cpsam_overlap_adamw = bool(args.overlap_adamw)
         net = CPSAM(depth=args.depth).randomize_(0)
         tr = build_trainer(cfg, dev, net=net)
         batch = synthetic_train_batch(B, 256, device=dev)
@@ -51,7 +55,8 @@ def main():
         out = {"bench": "cpsam_finetune_step", "engine": "hip", "batch": B, "depth": args.depth,
                "ms_per_step": round(dt * 1e3, 3), "samples_per_sec": round(B / dt, 2), "loss": float(loss),
                "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
-               "gemm": os.environ.get("BE_CPSAM_GEMM", "lib")}
+               "gemm": os.environ.get("BE_CPSAM_GEMM", "lib"), "overlap_adamw": bool(cfg.cpsam_overlap_adamw),
+               "adamw_bg_blocks": int(os.environ.get("BE_ADAMW_BG_BLOCKS", "256"))}
         if out["gemm"] == "auto":
             from bioengine_worker_amd.ops import gemm_auto
 
