@@ -64,6 +64,8 @@ class TrainConfig:
     # buffer; same math as the flat update).  Measured slower on MI355X (profiles/r02/attn/README.md:
     # batch 8 39.7 -> 41.4-41.8 ms, batch 1 15.3 -> 16.9-17.6 ms: the optimizer's HBM stream slows
     # the backward kernels more than it hides), so the flat update after the replay stays the default.
+    # Re-measured in round 4 with the streaming kernel (profiles/r04/cpsam/overlap_adamw_ab.jsonl):
+    # batch 1 11.34 -> 12.02 ms, batch 8 33.11 -> 33.90 ms; capping its grid only makes it later.
     cpsam_overlap_adamw: bool = False
     # data-parallel CPSAM: AdamW per gradient bucket, each right after its own all-reduce
     cpsam_bucket_adamw: bool = True

@@ -16,6 +16,8 @@
 //    images, so each tile costs one barrier.
 //  * block = NW waves x 32 queries of one (batch, head); the linear block id is XCD-remapped so the
 //    blocks sharing a (batch, head)'s K/V stream run on one XCD's L2.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -340,9 +342,17 @@ int launch_nw(AttnArgs a, hipStream_t s) {
   return BE_CHECK_LAUNCH();
 }
 
-// nw = 0 picks the waves per block (2, 3 or 4 x 32 queries) that least overpads N.
+// nw = 0 picks the waves per block (2, 3 or 4 x 32 queries) that least overpads N, then drops to 2
+// when the grid would leave CUs idle (CPSAM at batch 1: 16 heads x 1024 queries = 128 four-wave
+// blocks for 256 CUs; 2-wave blocks make it 256).  BE_ATTN_NW pins it (A/B).
+static int g_attn_nw = [] {
+  const char* e = getenv("BE_ATTN_NW");
+  return e ? atoi(e) : 0;
+}();
+
 int attn_dispatch(AttnArgs a, int nw, hipStream_t stream) {
   const int N = a.N;
+  if (nw == 0) nw = g_attn_nw;
   if (nw == 0) {
     const int slices = (N + 31) / 32;
     int best = 4, waste = 1 << 30;
@@ -350,6 +360,8 @@ int attn_dispatch(AttnArgs a, int nw, hipStream_t stream) {
       const int w = ((slices + c - 1) / c) * c - slices;
       if (w < waste) { waste = w; best = c; }
     }
+    const long long bh = (long long)a.B * a.H;
+    if (best > 2 && bh * ((slices + best - 1) / best) < 256) best = 2;
     nw = best;
   }
   switch (nw) {
