@@ -39,6 +39,8 @@ def _cfg(M: int, N: int) -> int:
 
 
 def _call(A, B, C, M, N, K, lda, ldb, ldc, ta, tb, epi, C2=None, bias=None, aux=None, dbias=None, split=1, cfg=None):
+    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous()):
+        bias = bias.float().contiguous()  # the epilogue reads fp32 (the engine's biases are bf16 mirror views)
     ws, wsb = None, 0
     if split > 1:
         ws = _workspace(A.device, split * M * ldc * 4)

@@ -36,6 +36,13 @@ def supported(M: int, N: int, K: int) -> bool:
     return K % 32 == 0 and N % 4 == 0 and K % 8 == 0
 
 
+def _f32(b: torch.Tensor | None) -> torch.Tensor | None:
+    """The epilogue reads an fp32 bias; the CPSAM engine's biases are bf16 views of its weight mirror."""
+    if b is None or (b.dtype == torch.float32 and b.is_contiguous()):
+        return b
+    return b.float().contiguous()
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, cfg: int | None = None) -> torch.Tensor:
     """x [M, K] @ w [N, K]^T (+ b fp32 [N]) -> bf16 [M, N]."""
     M, K = x.shape
@@ -43,6 +50,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, cfg:
     if not x.is_cuda or not supported(M, N, K) or not (x.is_contiguous() and w.is_contiguous()):
         return F.linear(x, w, None if b is None else b.to(x.dtype))
     out = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    b = _f32(b)
     _native.call("be_gemm_pp", _native.ptr(x), _native.ptr(w), _native.ptr(out), None, _native.ptr(b), None, None,
                  M, N, K, K, K, N, 0, P_BIAS if b is not None else P_NONE, gemm_cfg(M, N) if cfg is None else cfg,
                  _native.stream(x.device))
@@ -58,6 +66,7 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, cfg: int | No
         return F.gelu(f.float()).to(x.dtype), f
     f = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
     g = torch.empty_like(f)
+    b = _f32(b)
     _native.call("be_gemm_pp", _native.ptr(x), _native.ptr(w), _native.ptr(f), _native.ptr(g), _native.ptr(b), None, None,
                  M, N, K, K, K, N, 0, P_BIAS_GELU, gemm_cfg(M, N) if cfg is None else cfg, _native.stream(x.device))
     return g, f

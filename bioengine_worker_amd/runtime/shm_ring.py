@@ -22,6 +22,29 @@ from ..ops import _native
 EAGAIN_TIMEOUT, TOO_LARGE, CLOSED = -2, -3, -4
 
 
+_MALLOC_TUNED = False
+
+
+def tune_malloc() -> bool:
+    """Keep freed payload-sized buffers in the process heap (``BE_REPLICA_MALLOC``, default off).
+
+    Every ring read allocates a fresh array for the payload; glibc serves multi-MiB requests from
+    fresh mmaps, or trims the heap top after a free, so each request may page-fault its buffer in
+    again (~1 ms per MiB on the VM hosts, see ``map_ring`` in shm_ring.cpp).  With the mmap
+    threshold at 64 MiB and the trim threshold at 512 MiB, the freed buffers are reused instead.
+    Applied once per process (router and replica)."""
+    global _MALLOC_TUNED
+    if _MALLOC_TUNED or os.environ.get("BE_REPLICA_MALLOC", "0") in ("0", "false", "no"):
+        return _MALLOC_TUNED
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        ok = libc.mallopt(-3, 64 << 20) == 1 and libc.mallopt(-1, 512 << 20) == 1  # M_MMAP_THRESHOLD, M_TRIM_THRESHOLD
+    except OSError:
+        ok = False
+    _MALLOC_TUNED = ok
+    return ok
+
+
 class RingClosed(RuntimeError):
     pass
 

@@ -380,8 +380,9 @@ class ProcessReplica(ReplicaBase):
         if cap <= 0:
             return
         try:
-            from ..runtime.shm_ring import ShmRing
+            from ..runtime.shm_ring import ShmRing, tune_malloc
 
+            tune_malloc()
             self.tx, self.rx = ShmRing.create(cap), ShmRing.create(cap)
         except Exception:  # runtime library unavailable or /dev/shm exhausted: socket-only
             self._drop_rings()

@@ -232,6 +232,9 @@ def _picklable_exc(e: BaseException) -> BaseException:
 
 def main():
     sys.path.insert(0, os.getcwd())
+    from ..runtime.shm_ring import tune_malloc
+
+    tune_malloc()
     from ..compat import install
 
     install()

@@ -41,14 +41,13 @@ import torch.nn.functional as F
 from ..models.cpsam import CPSAM, get_rel_pos
 import os as _os
 
-# GEMM backend of the engine.  "auto" = per shape, the fastest in isolation of the in-house bf16 MFMA
-# GEMMs with fused epilogues (ops/gemm_bf16.py, ops/gemm_pp.py) and the library GEMM
-# (ops/gemm_auto.py, decided on the eager warm-up steps); "hip" / "lib" pin one side.  The default
-# is the library: on the whole graphed step it measured 11.35 / 31.70 ms at batch 1 / 8 against
-# 12.69 / 32.67 for "auto" (profiles/r04/cpsam/cpsam_gemm_*.jsonl) -- the in-house kernels win
-# several shapes when timed alone, but the eager per-shape timing did not predict the graphed step
-# (the cause is not pinned down: cold first-call timings and cache state between back-to-back
-# kernels are the candidates)
+# GEMM backend of the engine.  "auto" = per shape, the fastest of the in-house bf16 MFMA GEMMs with
+# fused epilogues (ops/gemm_bf16.py, ops/gemm_pp.py) and the library GEMM (ops/gemm_auto.py,
+# decided on the eager warm-up steps); "hip" / "lib" pin one side.  The default is the library: on
+# the whole graphed step it measured 11.35 / 31.70 ms at batch 1 / 8 against 12.69 / 32.67 for
+# "auto" (profiles/r04/cpsam/cpsam_gemm_*.jsonl).  The first per-shape timing bracketed single
+# eager calls and so measured launch overhead; in the graph the library's kernels are the faster
+# ones (profiles/r04/cpsam/kt_step_b1_*.txt), and gemm_auto now times graph replays.
 _GEMM = _os.environ.get("BE_CPSAM_GEMM", "lib")
 if _GEMM == "lib":
     from ..ops import gemm

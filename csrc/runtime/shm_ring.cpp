@@ -20,9 +20,13 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <fcntl.h>
+#include <mutex>
+#include <thread>
 #include <linux/futex.h>
 #include <new>
 #include <sys/mman.h>
@@ -90,14 +94,100 @@ int wait_for(Ring* r, std::atomic<uint32_t>* seq, int64_t timeout_us, Pred pred)
   }
 }
 
+// Large payload copies are split over the calling thread plus a few persistent helpers: one core's
+// memcpy of a 2 MiB image is ~0.1-0.2 ms, on the critical path of every served request (once into
+// the ring in the sender, once out in the receiver).  BE_RING_COPY_THREADS (default 4, 1 = off) is
+// the total number of threads per copy; helpers sleep on a condition variable between copies.
+constexpr uint64_t kParMin = 512 << 10;
+
+struct CopyPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  unsigned char* dst = nullptr;
+  const unsigned char* src = nullptr;
+  uint64_t chunk = 0, n = 0;
+  uint64_t gen = 0;
+  std::atomic<int> pending{0};
+  int helpers = 0;
+  pid_t pid = 0;
+};
+
+int copy_threads() {
+  static const int t = [] {
+    const char* e = getenv("BE_RING_COPY_THREADS");
+    const int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+  }();
+  return t;
+}
+
+void helper_main(CopyPool* p, int idx) {
+  uint64_t seen = 0;
+  for (;;) {
+    unsigned char* d;
+    const unsigned char* s;
+    uint64_t lo, hi;
+    {
+      std::unique_lock<std::mutex> lk(p->mu);
+      p->cv.wait(lk, [&] { return p->gen != seen; });
+      seen = p->gen;
+      d = p->dst;
+      s = p->src;
+      lo = (uint64_t)(idx + 1) * p->chunk;
+      hi = lo + p->chunk < p->n ? lo + p->chunk : p->n;
+    }
+    if (lo < hi) std::memcpy(d + lo, s + lo, hi - lo);
+    p->pending.fetch_sub(1, std::memory_order_acq_rel);
+  }
+}
+
+// One pool per process (a forked child starts its own: the parent's helper threads do not exist
+// there).  Copies are serialised by `use`: the ring's two directions may copy from two threads.
+CopyPool* pool() {
+  static std::mutex init_mu;
+  static CopyPool* p = nullptr;
+  std::lock_guard<std::mutex> g(init_mu);
+  if (p == nullptr || p->pid != getpid()) {
+    p = new CopyPool;  // a pre-fork pool is leaked on purpose: its mutex may be held by a dead thread
+    p->pid = getpid();
+    p->helpers = copy_threads() - 1;
+    for (int i = 0; i < p->helpers; ++i) std::thread(helper_main, p, i).detach();
+  }
+  return p;
+}
+
+void par_memcpy(void* dst, const void* src, uint64_t n) {
+  if (n < kParMin || copy_threads() <= 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  static std::mutex use;
+  std::lock_guard<std::mutex> g(use);
+  CopyPool* p = pool();
+  const int parts = p->helpers + 1;
+  const uint64_t chunk = ((n + parts - 1) / parts + 63) & ~uint64_t(63);
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->dst = static_cast<unsigned char*>(dst);
+    p->src = static_cast<const unsigned char*>(src);
+    p->chunk = chunk;
+    p->n = n;
+    p->pending.store(p->helpers, std::memory_order_relaxed);
+    ++p->gen;
+  }
+  p->cv.notify_all();
+  std::memcpy(dst, src, chunk < n ? chunk : n);
+  while (p->pending.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+}
+
 void copy_in(Ring* r, uint64_t pos, const void* src, uint64_t n) {
   uint64_t off = pos & r->mask;
   uint64_t first = r->mask + 1 - off;
   if (first >= n) {
-    std::memcpy(r->data + off, src, n);
+    par_memcpy(r->data + off, src, n);
   } else {
-    std::memcpy(r->data + off, src, first);
-    std::memcpy(r->data, static_cast<const unsigned char*>(src) + first, n - first);
+    par_memcpy(r->data + off, src, first);
+    par_memcpy(r->data, static_cast<const unsigned char*>(src) + first, n - first);
   }
 }
 
@@ -105,10 +195,10 @@ void copy_out(Ring* r, uint64_t pos, void* dst, uint64_t n) {
   uint64_t off = pos & r->mask;
   uint64_t first = r->mask + 1 - off;
   if (first >= n) {
-    std::memcpy(dst, r->data + off, n);
+    par_memcpy(dst, r->data + off, n);
   } else {
-    std::memcpy(dst, r->data + off, first);
-    std::memcpy(static_cast<unsigned char*>(dst) + first, r->data, n - first);
+    par_memcpy(dst, r->data + off, first);
+    par_memcpy(static_cast<unsigned char*>(dst) + first, r->data, n - first);
   }
 }
 

@@ -87,16 +87,28 @@ def test_layernorm_gelu_cast_kernels(dev):
     assert torch.equal(yb.cpu(), yb_r) and _rel(col.cpu(), col_r) < 1e-5
 
 
-@pytest.mark.parametrize("side_wgrad", [False, True])
-def test_cpsam_engine_matches_fp32_autograd(dev, side_wgrad):
+@pytest.mark.parametrize("side_wgrad,backend", [(False, "lib"), (True, "lib"), (False, "hip"), (False, "auto")])
+def test_cpsam_engine_matches_fp32_autograd(dev, side_wgrad, backend, monkeypatch):
+    """GEMM backends: the library (default), the in-house kernels, and the per-shape choice.  The
+    biases are made non-zero (randomize_ zeroes them, which once hid a bf16-bias misread in the
+    in-house epilogues)."""
     from bioengine_worker_amd.models.cpsam import CPSAM
-    from bioengine_worker_amd.ops import train_ops
+    from bioengine_worker_amd.ops import gemm as gemm_lib
+    from bioengine_worker_amd.ops import gemm_auto, gemm_bf16, train_ops
     from bioengine_worker_amd.parallel.ddp import FlatParams
+    from bioengine_worker_amd.train import cpsam_engine
     from bioengine_worker_amd.train.cpsam_engine import CPSAMTrainEngine
 
+    monkeypatch.setattr(cpsam_engine, "gemm", {"lib": gemm_lib, "hip": gemm_bf16, "auto": gemm_auto}[backend])
+    monkeypatch.delenv("BE_GEMM_AUTO", raising=False)
     torch.manual_seed(0)
     B = 2
     net = CPSAM(dim=256, depth=2, heads=4, bsize=256).randomize_(0)
+    gb = torch.Generator().manual_seed(5)
+    with torch.no_grad():
+        for name, p in net.named_parameters():
+            if name.endswith("bias"):
+                p.copy_(torch.randn(p.shape, generator=gb) * 0.1)
     ref = copy.deepcopy(net).to(dev).train()
     x = torch.randn(B, 3, 256, 256, device=dev)
     lbl = torch.zeros(B, 3, 256, 256, device=dev)

@@ -26,9 +26,9 @@ def test_linear_and_wgrad_pick_and_match_fp32():
     g = torch.Generator(device="cpu").manual_seed(0)
     x = torch.randn(1024, 1024, generator=g).to("cuda", torch.bfloat16)
     w = (torch.randn(3072, 1024, generator=g) * 0.03).to("cuda", torch.bfloat16)
-    b = torch.randn(3072, generator=g).to("cuda")
+    b = torch.randn(3072, generator=g).to("cuda", torch.bfloat16)
     y = gemm_auto.linear(x, w, b)
-    ref = x.float() @ w.float().t() + b
+    ref = x.float() @ w.float().t() + b.float()
     assert _rel(y, ref) < 1e-2
     dy = torch.randn(1024, 3072, generator=g).to("cuda", torch.bfloat16)
     out = torch.full((3072, 1024), float("nan"), device="cuda")
