@@ -165,6 +165,53 @@ static void test_ring_threads() {
   CHECK(be_rt_ring_close(w) == 0);
 }
 
+// Frames past the parallel-copy threshold (512 KiB): the payload copies run on the helper pool, from
+// the producer and the consumer thread at once, across the wrap point of a 4 MiB ring; then a
+// forked child (whose pool must be its own: the parent's helper threads do not exist there)
+// streams more of them back.
+static void large_roundtrip(void* w, void* r, int msgs, uint64_t salt) {
+  std::thread c([&] {
+    std::vector<unsigned char> buf(3 << 20);
+    for (int m = 0; m < msgs; ++m) {
+      int64_t n = -1;
+      CHECK(be_rt_ring_next_len(r, &n, 5000000) == 0);
+      CHECK(n == (int64_t)((600 << 10) + (m * 104729) % (2 << 20)));
+      CHECK(be_rt_ring_read(r, buf.data(), (int64_t)buf.size()) == 0);
+      auto ref = payload(salt + m, (size_t)n);
+      CHECK(std::memcmp(buf.data(), ref.data(), (size_t)n) == 0);
+    }
+  });
+  for (int m = 0; m < msgs; ++m) {
+    auto f = payload(salt + m, (size_t)((600 << 10) + (m * 104729) % (2 << 20)));
+    const void* p = f.data();
+    int64_t l = (int64_t)f.size();
+    CHECK(be_rt_ring_write(w, &p, &l, 1, 5000000) == 0);
+  }
+  c.join();
+}
+
+static void test_ring_large(bool fork_ok) {
+  std::string name = "/be-ring-selftest-l-" + std::to_string(getpid());
+  void *w = nullptr, *r = nullptr;
+  CHECK(be_rt_ring_create(name.c_str(), 4 << 20, &w) == 0);
+  CHECK(be_rt_ring_open(name.c_str(), &r) == 0);
+  large_roundtrip(w, r, 40, 11);
+  if (fork_ok) {
+    pid_t pid = fork();
+    CHECK(pid >= 0);
+    if (pid == 0) {
+      large_roundtrip(w, r, 20, 77);
+      _exit(0);
+    }
+    int status = 0;
+    CHECK(waitpid(pid, &status, 0) == pid);
+    CHECK(WIFEXITED(status) && WEXITSTATUS(status) == 0);
+  }
+  CHECK(be_rt_ring_unlink(name.c_str()) == 0);
+  CHECK(be_rt_ring_close(r) == 0);
+  CHECK(be_rt_ring_close(w) == 0);
+}
+
 static void test_ring_fork() {
   std::string name = "/be-ring-selftest-p-" + std::to_string(getpid());
   void* w = nullptr;
@@ -193,6 +240,7 @@ int main(int argc, char** argv) {
   test_spacing();
   test_ring_threads();
   if (fork_ok) test_ring_fork();
+  test_ring_large(fork_ok);
   std::printf("runtime selftest ok\n");
   return 0;
 }
