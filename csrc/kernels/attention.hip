@@ -342,9 +342,9 @@ int launch_nw(AttnArgs a, hipStream_t s) {
   return BE_CHECK_LAUNCH();
 }
 
-// nw = 0 picks the waves per block (2, 3 or 4 x 32 queries) that least overpads N, then drops to 2
-// when the grid would leave CUs idle (CPSAM at batch 1: 16 heads x 1024 queries = 128 four-wave
-// blocks for 256 CUs; 2-wave blocks make it 256).  BE_ATTN_NW pins it (A/B).
+// nw = 0 picks the waves per block (2, 3 or 4 x 32 queries) that least overpads N.  BE_ATTN_NW pins
+// it (A/B).  Filling the CUs at CPSAM batch 1 (16 heads x 1024 queries = 128 four-wave blocks) with
+// 256 two-wave blocks measured slower: 26.5 vs 23.5 us per layer (profiles/r04/cpsam/attn_nw_ab.txt).
 static int g_attn_nw = [] {
   const char* e = getenv("BE_ATTN_NW");
   return e ? atoi(e) : 0;
@@ -360,8 +360,6 @@ int attn_dispatch(AttnArgs a, int nw, hipStream_t stream) {
       const int w = ((slices + c - 1) / c) * c - slices;
       if (w < waste) { waste = w; best = c; }
     }
-    const long long bh = (long long)a.B * a.H;
-    if (best > 2 && bh * ((slices + best - 1) / best) < 256) best = 2;
     nw = best;
   }
   switch (nw) {
