@@ -43,12 +43,21 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def _dist_setup(ngpus: int):
+    """One rank per GPU over RCCL.  Rehearsal knobs (never set by the driver): BE_BENCH_BACKEND=gloo
+    and BE_BENCH_SHARED_GPU=1 run the N-rank code paths as N processes on ONE GPU over gloo, so the
+    multi-rank lines can be exercised on a one-GPU box (timings are meaningless there)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BE_BENCH_SHARED_GPU") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BE_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 

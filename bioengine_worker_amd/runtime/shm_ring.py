@@ -26,15 +26,17 @@ _MALLOC_TUNED = False
 
 
 def tune_malloc() -> bool:
-    """Keep freed payload-sized buffers in the process heap (``BE_REPLICA_MALLOC``, default off).
+    """Keep freed payload-sized buffers in the process heap (``BE_REPLICA_MALLOC``, default on).
 
     Every ring read allocates a fresh array for the payload; glibc serves multi-MiB requests from
     fresh mmaps, or trims the heap top after a free, so each request may page-fault its buffer in
     again (~1 ms per MiB on the VM hosts, see ``map_ring`` in shm_ring.cpp).  With the mmap
     threshold at 64 MiB and the trim threshold at 512 MiB, the freed buffers are reused instead.
-    Applied once per process (router and replica)."""
+    Applied once per process (router and replica).  Measured on an MI355X box with the parallel ring
+    copies (tools/replica_hop_bench.py, profiles/r04/serve/replica_hop_ab.jsonl): a 2 MiB request
+    round trip 245 us -> 191 us (4 copy threads) -> 150 us (+ this)."""
     global _MALLOC_TUNED
-    if _MALLOC_TUNED or os.environ.get("BE_REPLICA_MALLOC", "0") in ("0", "false", "no"):
+    if _MALLOC_TUNED or os.environ.get("BE_REPLICA_MALLOC", "1") in ("0", "false", "no"):
         return _MALLOC_TUNED
     try:
         libc = ctypes.CDLL("libc.so.6")

@@ -58,7 +58,7 @@ async def main_async(a) -> list[dict]:
                 row = {"direction": direction, "bytes": n, "p50_ms": round(float(np.percentile(ms, 50)), 4),
                        "p10_ms": round(float(np.percentile(ms, 10)), 4), "p90_ms": round(float(np.percentile(ms, 90)), 4),
                        "copy_threads": os.environ.get("BE_RING_COPY_THREADS", "4"),
-                       "malloc_tuned": os.environ.get("BE_REPLICA_MALLOC", "0")}
+                       "malloc_tuned": os.environ.get("BE_REPLICA_MALLOC", "1")}
                 rows.append(row)
                 print(json.dumps(row), flush=True)
     finally:
