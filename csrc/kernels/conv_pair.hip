@@ -68,6 +68,9 @@ struct PairArgs {
   int nh;
   int N, H, W, Hs, Ws, Cin;
   int tiles_x, tiles_y;
+  // diagnostics (STAMP instantiations only): per-workgroup cycles of wave 0 in each tile phase,
+  // [grid][8] = {halo commit, stage-A MFMA, stage-A epilogue, stage-B MFMA, output epilogue, -, -, tiles}
+  unsigned long long* stamps;
 };
 
 template <int CK_, int CM_, int INMODE, bool X2, bool PROJ, int RES, int NCA>
@@ -646,7 +649,7 @@ __device__ __forceinline__ void epi_head(const PairArgs& a, TileXY t, const f32x
   }
 }
 
-template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false>
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
 __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -667,6 +670,15 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   u32x4 wraw[C::WUPT];
   issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t0), 0, tid0, hraw);
   if constexpr (!C::RESW) issue_w<C, NCA>(a, 0, tid0, wraw);
+  unsigned long long ph[5] = {0, 0, 0, 0, 0};
+  unsigned long long tprev = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](int k) {
+    if constexpr (STAMP) {
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      ph[k] += tn - tprev;
+      tprev = tn;
+    }
+  };
 
   for (int t = t0; t < t1; ++t) {
     // Opaque per-iteration copy of the thread id: without it LICM hoists every per-unit halo /
@@ -689,13 +701,16 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
       commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P);
       if constexpr (!C::RESW) commit_w<C>(tid, wraw, WL);
       __syncthreads();
+      stamp(0);
       if (c + 1 < NCA) issue_halo<C, INMODE, PROJ>(a, cur, c + 1, tid, hraw);
       else if (t + 1 < t1) issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t + 1), 0, tid, hraw);
       if constexpr (!C::RESW) issue_w<C, NCA>(a, c + 1, tid, wraw);
       mma_a<C>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
+      stamp(1);
     }
     __syncthreads();  // every wave is done with the input halo and the A weights
     epi_a<C, X2, RES, C::PF>(a, cur, acc_a, R, ep, wave, lrow, kq);
+    stamp(2);
     // ---- stage B: CM/32 chunks of h ----
     f32x4 acc_b[C::NCT][4];
 #pragma unroll
@@ -717,32 +732,62 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
       mma_b<C>(acc_b, R, C::RESW ? WL + NCA * C::WA_ELEMS + cb * C::WB_ELEMS : WL, cb, wave, lrow, kq);
     }
     if constexpr (PROJ) mma_p<C>(acc_b, P, WL + NCA * C::WA_ELEMS + C::NCB * C::WB_ELEMS, wave, lrow, kq);
+    stamp(3);
     if constexpr (HEAD) {
       epi_head<C, X2, RES, C::PF>(a, cur, acc_b, ep, hr, wave, lrow, kq);  // registers only: no LDS staging
     } else {
       __syncthreads();  // every wave is done reading h before the output staging overlays it
       epi_b<C, X2, RES, C::PF>(a, cur, acc_b, R, ep, wave, lrow, kq);
     }
+    stamp(4);
   }
+  if constexpr (STAMP) {
+    if (tid0 < 64) {  // wave 0: lane k stores slot k (a lane-indexed vector store)
+      unsigned long long v = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        if (tid0 == k) v = ph[k];
+      if (tid0 == 7) v = (unsigned long long)(t1 - t0);
+      if (tid0 < 8) a.stamps[(size_t)blockIdx.x * 8 + tid0] = v;
+    }
+  }
+}
+
+unsigned long long* g_pair_stamps = nullptr;  // diagnostics: be_conv_pair_set_stamps
+int g_pair_stamps_cap = 0;                    // workgroups the stamp buffer holds
+
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
+int launch_pair_k(PairArgs a, int g, hipStream_t s) {
+  using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP>), dim3(g), dim3(NT), C::LDS, s, a);
+  return BE_CHECK_LAUNCH();
 }
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false>
 int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
-  using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   a.tiles_x = (a.W + TW - 1) / TW;
   a.tiles_y = (a.H + TH - 1) / TH;
   const int tiles = a.N * a.tiles_x * a.tiles_y;
   int g = grid_cap > 0 ? grid_cap : 256;  // one 512-thread workgroup per CU
   if (g > tiles) g = tiles;
   if (g < 1) return 0;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
-    attr_set = true;
+  a.stamps = nullptr;
+  // phase-stamped build of the level-0/1 half-blocks (tools/pair_phase_profile.py); the buffer must
+  // hold [grid][8] words
+  if constexpr (!HEAD && !PROJ && CK == 32) {
+    if (g_pair_stamps != nullptr) {
+      if (g > g_pair_stamps_cap) return -30;
+      a.stamps = g_pair_stamps;
+      return launch_pair_k<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, true>(a, g, s);
+    }
   }
-  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD>), dim3(g), dim3(NT), C::LDS, s, a);
-  return BE_CHECK_LAUNCH();
+  return launch_pair_k<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, false>(a, g, s);
 }
 
 }  // namespace
@@ -757,6 +802,15 @@ extern "C" {
 
 int be_conv_pair_set_grid(int blocks) {
   g_pair_grid = blocks;
+  return 0;
+}
+
+// Diagnostics: route the level-0/1 half-blocks (not the stem / head) to the phase-stamped build,
+// which writes [workgroup][8] cycle counts into `buf` (device, >= cap_workgroups * 64 bytes);
+// nullptr switches back.  Not for production launches (the stamps cost ~1 % of the kernel).
+int be_conv_pair_set_stamps(void* buf, int cap_workgroups) {
+  g_pair_stamps = static_cast<unsigned long long*>(buf);
+  g_pair_stamps_cap = buf ? cap_workgroups : 0;
   return 0;
 }
 
