@@ -101,6 +101,7 @@ int wait_for(Ring* r, std::atomic<uint32_t>* seq, int64_t timeout_us, Pred pred)
 constexpr uint64_t kParMin = 512 << 10;
 
 struct CopyPool {
+  std::mutex use;  // one parallel copy at a time per process
   std::mutex mu;
   std::condition_variable cv;
   unsigned char* dst = nullptr;
@@ -142,7 +143,8 @@ void helper_main(CopyPool* p, int idx) {
 }
 
 // One pool per process (a forked child starts its own: the parent's helper threads do not exist
-// there).  Copies are serialised by `use`: the ring's two directions may copy from two threads.
+// there, and the parent's mutexes may have been held at the fork).  Copies are serialised by the
+// pool's `use`: the ring's two directions may copy from two threads.
 CopyPool* pool() {
   static std::mutex init_mu;
   static CopyPool* p = nullptr;
@@ -161,9 +163,8 @@ void par_memcpy(void* dst, const void* src, uint64_t n) {
     std::memcpy(dst, src, n);
     return;
   }
-  static std::mutex use;
-  std::lock_guard<std::mutex> g(use);
   CopyPool* p = pool();
+  std::lock_guard<std::mutex> g(p->use);
   const int parts = p->helpers + 1;
   const uint64_t chunk = ((n + parts - 1) / parts + 63) & ~uint64_t(63);
   {
