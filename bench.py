@@ -34,6 +34,7 @@ import os
 import statistics
 import sys
 import time
+import warnings
 from pathlib import Path
 
 import torch
@@ -321,6 +322,8 @@ def bench_em_volume(args, world, rank, dev) -> dict:
         npy = work / "slab.npy"
         np.save(npy, synthetic_slab(z0, z0 + Z, YX, YX, dev).cpu().numpy())
         src = VolumeSource(str(npy))
+        # the memory-mapped slab is read-only; torch only reads it (straight into the H2D copy)
+        warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
         warm = torch.from_numpy(src.read(0, 4)).to(dev)  # graph pass, kernels, allocator
         analyze_volume(warm, predict, 512, 64, args.em_tile_batch, split_touching=True, norm_range=(90.0, 210.0))
         del warm
