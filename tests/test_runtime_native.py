@@ -67,3 +67,37 @@ def test_shm_ring_cross_process():
     a2b.shutdown()
     with pytest.raises(RingClosed):
         a2b.write([b"x"])
+
+
+def _echo_big(rx_name, tx_name, n):
+    sys.path.insert(0, ROOT)
+    from bioengine_worker_amd.runtime.shm_ring import ShmRing, tune_malloc
+
+    tune_malloc()
+    rx, tx = ShmRing.open(rx_name), ShmRing.open(tx_name)
+    for _ in range(n):
+        tx.write([rx.read(timeout_s=30)])
+
+
+def test_shm_ring_large_frames_cross_process():
+    """Frames past the parallel-copy threshold (512 KiB, split over the copy pool's threads in both
+    processes), wrapping an 8 MiB ring many times, with the replicas' malloc tuning on."""
+    from bioengine_worker_amd.runtime.shm_ring import ShmRing, tune_malloc
+
+    assert tune_malloc()  # default on; idempotent
+    a2b, b2a = ShmRing.create(8 << 20), ShmRing.create(8 << 20)
+    n = 24
+    p = mp.get_context("spawn").Process(target=_echo_big, args=(a2b.name, b2a.name, n))
+    p.start()
+    rng = np.random.default_rng(1)
+    try:
+        for i in range(n):
+            x = rng.integers(0, 255, size=(512 << 10) + int(rng.integers(0, 3 << 20)), dtype=np.uint8)
+            a2b.write([x])
+            y = b2a.read(timeout_s=30)
+            assert y.nbytes == x.nbytes and np.array_equal(y, x)
+    finally:
+        p.join(30)
+        a2b.unlink()
+        b2a.unlink()
+    assert p.exitcode == 0
