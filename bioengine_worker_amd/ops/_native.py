@@ -141,8 +141,24 @@ def loaded_libraries() -> list[str]:
     return out
 
 
+class _TensorPtr(c_void_p):
+    """A tensor's device address that keeps the tensor alive.  Call sites often pass converted
+    temporaries (``ptr(q.float().contiguous())``, ``ptr(probes.int())``): with a bare address the
+    first temporary is freed while the argument list is still being built, the next conversion is
+    allocated into the same caching-allocator block and overwrites it before the kernel is even
+    launched (the IVF scan once read its query block as the probe-index integers).  Holding the
+    tensor until ``call`` returns keeps every operand distinct; after the launch, stream order
+    protects the memory."""
+
+    __slots__ = ("_t",)
+
+
 def ptr(t: torch.Tensor | None):
-    return None if t is None else c_void_p(t.data_ptr())
+    if t is None:
+        return None
+    p = _TensorPtr(t.data_ptr())
+    p._t = t
+    return p
 
 
 def stream(device: torch.device | int | None = None):

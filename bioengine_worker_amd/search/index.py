@@ -230,7 +230,11 @@ class VectorIndex:
         candidate exactly from the list-sorted bf16 slabs, then one top-k; CPU: one batched GEMM
         per query chunk.  No per-query Python loop either way."""
         nl = self.centroids.shape[0]
-        probes = torch.topk((q @ self.centroids.T).float(), min(nprobe or self.nprobe, nl), dim=1).indices
+        npb = min(nprobe or self.nprobe, nl)
+        if npb == nl:  # every list: no ranking needed (the candidate order does not matter)
+            probes = torch.arange(nl, device=q.device).expand(q.shape[0], nl).contiguous()
+        else:
+            probes = torch.topk((q @ self.centroids.T).float(), npb, dim=1).indices
         sizes = (self.list_off[1:] - self.list_off[:-1])[probes]  # [Q, nprobe]
         cand_off = torch.cumsum(sizes, 1) - sizes
         stride = int(sizes.sum(1).max())

@@ -44,3 +44,24 @@ d = (out - ref).abs()
 d[torch.isinf(ref) & torch.isinf(out)] = 0
 print("max |scan - ref|", float(d.max()), "bad slots", int((d > 1e-2).sum()), "of", out.numel(), flush=True)
 print("dtype list_off", idx.list_off.dtype, "cand_off", cand_off.dtype, "probes", probes.dtype, "stride", stride)
+# post-processing of the scan output on the GPU vs the same tensors on the CPU
+def post(out, probes, cand_off, list_off, sorted_ids, ntotal):
+    ts, ti = torch.topk(out, 10, dim=1)
+    p = (torch.searchsorted(cand_off.contiguous(), ti.contiguous(), right=True) - 1).clamp(min=0)
+    rows = list_off[torch.gather(probes, 1, p)] + (ti - torch.gather(cand_off, 1, p))
+    ids = sorted_ids[rows.clamp(0, ntotal - 1)]
+    return ts, ti, p, rows, ids
+
+
+g = post(out, probes, cand_off, idx.list_off, idx.sorted_ids, idx.ntotal)
+c = post(out.cpu(), probes.cpu(), cand_off.cpu(), idx.list_off.cpu(), idx.sorted_ids.cpu(), idx.ntotal)
+for name, a, b in zip(("ts", "ti", "p", "rows", "ids"), g, c):
+    a = a.cpu()
+    print(name, "mismatches", int((a != b).sum()), "of", a.numel(), flush=True)
+print("empty lists", int(((idx.list_off[1:] - idx.list_off[:-1]) == 0).sum()), "of", nl)
+ssg = torch.searchsorted(cand_off.contiguous(), g[1].contiguous(), right=True)
+ssc = torch.searchsorted(cand_off.cpu().contiguous(), g[1].cpu().contiguous(), right=True)
+print("searchsorted gpu vs cpu mismatches", int((ssg.cpu() != ssc).sum()))
+i = int(torch.nonzero((ssg.cpu() != ssc).any(1))[0]) if (ssg.cpu() != ssc).any() else None
+if i is not None:
+    print("row", i, "ti", g[1][i].tolist(), "gpu", ssg[i].tolist(), "cpu", ssc[i].tolist())
