@@ -153,9 +153,14 @@ class _TensorPtr(c_void_p):
     __slots__ = ("_t",)
 
 
+_KEEP = os.environ.get("BE_NATIVE_PTR_KEEP", "1") != "0"  # 0: bare addresses (A/B only)
+
+
 def ptr(t: torch.Tensor | None):
     if t is None:
         return None
+    if not _KEEP:
+        return c_void_p(t.data_ptr())
     p = _TensorPtr(t.data_ptr())
     p._t = t
     return p
