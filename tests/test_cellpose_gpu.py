@@ -283,6 +283,12 @@ def test_cross_batch_stream_and_locked_eval_match_eval(gpu):
     def work(i):
         m, f, _, ev = r.eval_locked(batches[i], net_lock, mask_lock)
         ev.synchronize()
+        # m lives in the mask stream's pool; the clones run on this thread's stream, queued behind
+        # other threads' network kernels: without record_stream, m's block could be handed to the
+        # next batch's mask stage before the clone has read it (a rare failure of this test)
+        cur = torch.cuda.current_stream()
+        m.record_stream(cur)
+        f.record_stream(cur)
         res[i] = (m.clone(), f.clone())
 
     th = [threading.Thread(target=work, args=(i,)) for i in range(len(batches))]
