@@ -14,6 +14,8 @@
 //    key list (count << 32 | raster index) that torch.sort orders exactly like cellpose's argsort.
 //  * expansion: one wave per seed, its 11x11 window in LDS, 5 dilations, labels committed with
 //    atomicMax (seeds are rank-ordered by count, so "last writer wins" == max rank).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -129,6 +131,78 @@ __global__ __launch_bounds__(256) void follow_flows_xcd_kernel(const float2* __r
   const int lin = iy * Wp + ix;
   pos[g] = lin;
   atomicAdd(hist + (size_t)b * (H + 2 * RPAD) * Wp + lin, 1);
+}
+
+// Same, with PPT x 256 pixels per block compacted together: at the ~12 % foreground of a Cellpose
+// batch a 256-pixel block leaves ~31 live lanes in one wave, so every Euler step issued its four
+// float2 gathers for a half-empty wave (the loop is bound by gather issue, not by latency).  Pooling
+// 1,024 pixels gives ~2 full waves per block.  Each pixel's result is independent of the order the
+// list is walked in (integer histogram atomics), so the output equals the 256-pixel kernel's.
+template <int PPT>
+__global__ __launch_bounds__(256) void follow_flows_xcd_pool_kernel(const float2* __restrict__ flow2,
+                                                                    const uint8_t* __restrict__ fg, int* __restrict__ hist,
+                                                                    int* __restrict__ pos, int B, int H, int W, int niter) {
+  __shared__ int list[256 * PPT];
+  __shared__ int wcount[4 * PPT];
+  const int HW = H * W;
+  const long long n = (long long)B * HW;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const long long gid0 = (long long)blk * (256 * PPT);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long m[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {  // coalesced: pass k covers pixels gid0 + k*256 + [0, 256)
+    const long long g = gid0 + k * 256 + threadIdx.x;
+    const bool in = g < n;
+    const bool f = in && fg[g];
+    if (in && !f) pos[g] = -1;
+    m[k] = __ballot(f);
+    if (lane == 0) wcount[k * 4 + wv] = __popcll(m[k]);
+  }
+  __syncthreads();
+  int total = 0;
+#pragma unroll
+  for (int i = 0; i < 4 * PPT; ++i) total += wcount[i];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    int base = 0;
+    for (int i = 0; i < k * 4 + wv; ++i) base += wcount[i];
+    if ((m[k] >> lane) & 1ull) list[base + __popcll(m[k] & ((1ull << lane) - 1ull))] = k * 256 + threadIdx.x;
+  }
+  __syncthreads();
+  const float sy_scale = (H > 1) ? (float)H / (float)(H - 1) : 0.f;
+  const float sx_scale = (W > 1) ? (float)W / (float)(W - 1) : 0.f;
+  const float ymax = (float)(H - 1), xmax = (float)(W - 1);
+  const int Wp = W + 2 * RPAD;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const long long g = gid0 + list[e];
+    const int b = (int)(g / HW);
+    const int pix = (int)(g % HW);
+    const float2* fl = flow2 + (size_t)b * HW;
+    float py = (float)(pix / W), px = (float)(pix % W);
+    for (int t = 0; t < niter; ++t) {
+      const float sy = py * sy_scale - 0.5f;
+      const float sx = px * sx_scale - 0.5f;
+      const float fy = floorf(sy), fx = floorf(sx);
+      const int y0 = (int)fy, x0 = (int)fx;
+      const float wy = sy - fy, wx = sx - fx;
+      const float2 a = ldflow(fl, H, W, y0, x0);
+      const float2 bq = ldflow(fl, H, W, y0, x0 + 1);
+      const float2 c = ldflow(fl, H, W, y0 + 1, x0);
+      const float2 d = ldflow(fl, H, W, y0 + 1, x0 + 1);
+      const float w00 = (1.f - wy) * (1.f - wx), w01 = (1.f - wy) * wx, w10 = wy * (1.f - wx), w11 = wy * wx;
+      const float dy = a.x * w00 + bq.x * w01 + c.x * w10 + d.x * w11;
+      const float dx = a.y * w00 + bq.y * w01 + c.y * w10 + d.y * w11;
+      py = fminf(fmaxf(py + dy, 0.f), ymax);
+      px = fminf(fmaxf(px + dx, 0.f), xmax);
+    }
+    int iy = (int)py + RPAD, ix = (int)px + RPAD;
+    iy = min(max(iy, 0), H + RPAD - 1);
+    ix = min(max(ix, 0), W + RPAD - 1);
+    const int lin = iy * Wp + ix;
+    pos[g] = lin;
+    atomicAdd(hist + (size_t)b * (H + 2 * RPAD) * Wp + lin, 1);
+  }
 }
 
 // Seeds: h > 10 and h == max over the 5x5 neighbourhood (zero outside).
@@ -264,11 +338,22 @@ int be_cp_follow_flows(const void* flow2, const void* fg, int* hist, int* pos, i
   return BE_CHECK_LAUNCH();
 }
 
-// Same result as be_cp_follow_flows (XCD-ordered, block-compacted launch).
+// Same result as be_cp_follow_flows (XCD-ordered, block-compacted launch).  BE_FOLLOW_POOL (A/B):
+// pixels pooled per block for the compaction, 1 (256) or 4 (1,024, the default).
+static int g_follow_pool = [] {
+  const char* e = getenv("BE_FOLLOW_POOL");
+  return e ? atoi(e) : 4;
+}();
+
 int be_cp_follow_flows_xcd(const void* flow2, const void* fg, int* hist, int* pos, int B, int H, int W, int niter,
                            hipStream_t s) {
   const long long n = (long long)B * H * W;
   if (n == 0) return 0;
+  if (g_follow_pool == 4) {
+    hipLaunchKernelGGL(follow_flows_xcd_pool_kernel<4>, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, s,
+                       (const float2*)flow2, (const uint8_t*)fg, hist, pos, B, H, W, niter);
+    return BE_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(follow_flows_xcd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float2*)flow2,
                      (const uint8_t*)fg, hist, pos, B, H, W, niter);
   return BE_CHECK_LAUNCH();
