@@ -339,10 +339,12 @@ int be_cp_follow_flows(const void* flow2, const void* fg, int* hist, int* pos, i
 }
 
 // Same result as be_cp_follow_flows (XCD-ordered, block-compacted launch).  BE_FOLLOW_POOL (A/B):
-// pixels pooled per block for the compaction, 1 (256) or 4 (1,024, the default).
+// pixels pooled per block for the compaction, 1 (256, the default) or 4 (1,024).  Pooling fills
+// the waves but measured 1.52 vs 1.47 ms per batch of 32 (profiles/r04/headline/follow_pool_ab.txt):
+// the Euler loop is bound by its dependent gather latency, and fewer waves hide less of it.
 static int g_follow_pool = [] {
   const char* e = getenv("BE_FOLLOW_POOL");
-  return e ? atoi(e) : 4;
+  return e ? atoi(e) : 1;
 }();
 
 int be_cp_follow_flows_xcd(const void* flow2, const void* fg, int* hist, int* pos, int B, int H, int W, int niter,
