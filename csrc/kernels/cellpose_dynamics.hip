@@ -361,6 +361,16 @@ int be_cp_follow_flows_xcd(const void* flow2, const void* fg, int* hist, int* po
   return BE_CHECK_LAUNCH();
 }
 
+// The pooled-compaction launch on its own entry (tests / A/B without the BE_FOLLOW_POOL switch).
+int be_cp_follow_flows_xcd_pool(const void* flow2, const void* fg, int* hist, int* pos, int B, int H, int W, int niter,
+                                hipStream_t s) {
+  const long long n = (long long)B * H * W;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(follow_flows_xcd_pool_kernel<4>, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, s,
+                     (const float2*)flow2, (const uint8_t*)fg, hist, pos, B, H, W, niter);
+  return BE_CHECK_LAUNCH();
+}
+
 int be_cp_seeds(const int* hist, int B, int Hp, int Wp, long long* keys, int* nseeds, int cap, hipStream_t s) {
   const long long n = (long long)B * Hp * Wp;
   hipLaunchKernelGGL(seeds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hist, B, Hp, Wp, keys, nseeds, cap);

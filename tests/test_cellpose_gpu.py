@@ -170,7 +170,7 @@ def test_runner_end_to_end(gpu):
 
 @pytest.mark.gpu
 def test_follow_flows_launch_variants_identical(gpu, monkeypatch):
-    """The XCD-ordered, block-compacted flow-following launch gives bit-identical masks to the plain
+    """The XCD-ordered, block-compacted flow-following launches (256-pixel blocks, and 1,024 pooled) give bit-identical masks to the plain
     pixel-per-lane launch (same per-pixel float sequence, order-independent histogram atomics)."""
     from bioengine_worker_amd.cellpose import gpu as cg
 
@@ -181,10 +181,10 @@ def test_follow_flows_launch_variants_identical(gpu, monkeypatch):
         ys.append(np.concatenate([dP, cp[None]], 0))
     y = torch.from_numpy(np.stack(ys)).to(gpu)
     outs = []
-    for entry in ("be_cp_follow_flows", "be_cp_follow_flows_xcd"):
+    for entry in ("be_cp_follow_flows", "be_cp_follow_flows_xcd", "be_cp_follow_flows_xcd_pool"):
         monkeypatch.setattr(cg, "FOLLOW_FLOWS_ENTRY", entry)
         outs.append(cg.compute_masks_gpu(y).cpu())
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 @pytest.mark.gpu
