@@ -549,21 +549,40 @@ __device__ __forceinline__ int stage_off(int p, int co) {
 }
 
 // bias + residual, staged through LDS, 16-byte coalesced NHWC stores
-template <typename C, bool X2, int RES, bool PF>
+template <typename C, int RES>
+struct LateEpi {  // CM = 64 (no tile-start prefetch): residual + bias issued right after stage B's MFMAs
+  u32x2 rv[4][C::NCT];
+  float4 bias[C::NCT];
+};
+
+template <typename C, int RES>
+__device__ __forceinline__ void issue_late(const PairArgs& a, TileXY t, int wave, int lrow, int kq, LateEpi<C, RES>& l) {
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct) l.rv[pt][ct] = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct) l.bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
+}
+
+template <typename C, bool X2, int RES, bool PF, bool LATE = false>
 __device__ __forceinline__ void epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][4], bf16_t* stage,
-                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq) {
+                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq,
+                                      const LateEpi<C, RES>* late = nullptr) {
   u32x2 rv[4][C::NCT];
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
     for (int ct = 0; ct < C::NCT; ++ct) {
       if constexpr (PF && RES != 0) rv[pt][ct] = e.rv[pt][ct];
+      else if constexpr (LATE) rv[pt][ct] = late->rv[pt][ct];
       else rv[pt][ct] = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
     }
   float4 bias[C::NCT];
 #pragma unroll
   for (int ct = 0; ct < C::NCT; ++ct) {
     if constexpr (PF) bias[ct] = e.bias[ct];
+    else if constexpr (LATE) bias[ct] = late->bias[ct];
     else bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
   }
   bf16_t* ws = stage + wave * C::OUT_WAVE;
@@ -649,7 +668,10 @@ __device__ __forceinline__ void epi_head(const PairArgs& a, TileXY t, const f32x
   }
 }
 
-template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
+// LATE (CM = 64 A/B, BE_PAIR_LATE_EPI): the output epilogue's residual and bias loads are issued
+// right after stage B's MFMAs, so they are in flight across the barrier before the epilogue.
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false,
+          bool LATE = false>
 __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -735,6 +757,11 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
     stamp(3);
     if constexpr (HEAD) {
       epi_head<C, X2, RES, C::PF>(a, cur, acc_b, ep, hr, wave, lrow, kq);  // registers only: no LDS staging
+    } else if constexpr (LATE && !C::PF && RES != 0) {
+      LateEpi<C, RES> late;
+      issue_late<C, RES>(a, cur, wave, lrow, kq, late);
+      __syncthreads();  // every wave is done reading h before the output staging overlays it
+      epi_b<C, X2, RES, C::PF, true>(a, cur, acc_b, R, ep, wave, lrow, kq, &late);
     } else {
       __syncthreads();  // every wave is done reading h before the output staging overlays it
       epi_b<C, X2, RES, C::PF>(a, cur, acc_b, R, ep, wave, lrow, kq);
@@ -756,17 +783,32 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
 unsigned long long* g_pair_stamps = nullptr;  // diagnostics: be_conv_pair_set_stamps
 int g_pair_stamps_cap = 0;                    // workgroups the stamp buffer holds
 
-template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
-int launch_pair_k(PairArgs a, int g, hipStream_t s) {
+static int g_pair_late = [] {  // A/B: BE_PAIR_LATE_EPI=1 selects the LATE build of the CM = 64 pairs
+  const char* e = getenv("BE_PAIR_LATE_EPI");
+  return e ? atoi(e) : 0;
+}();
+
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, bool LATE>
+int launch_pair_l(PairArgs a, int g, hipStream_t s) {
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+    hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, LATE>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP>), dim3(g), dim3(NT), C::LDS, s, a);
+  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, LATE>), dim3(g), dim3(NT), C::LDS,
+                     s, a);
   return BE_CHECK_LAUNCH();
+}
+
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
+int launch_pair_k(PairArgs a, int g, hipStream_t s) {
+  if constexpr (CM == 64 && RES != 0) {
+    if (g_pair_late) return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, true>(a, g, s);
+  }
+  return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, false>(a, g, s);
 }
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false>
