@@ -341,7 +341,7 @@ __device__ __forceinline__ void load_resident(const PairArgs& a, int tid, bf16_t
 }
 
 // ---- stage A: h region (612 px, linear order) from the input halo ---------------------------------
-template <typename C>
+template <typename C, bool ROLL = false>
 __device__ __forceinline__ void mma_a(f32x4 (&acc)[C::NCT][APT], const bf16_t* rin, const bf16_t* wl, int wave,
                                       int lrow, int kq) {
   int base[APT];
@@ -378,6 +378,30 @@ __device__ __forceinline__ void mma_a(f32x4 (&acc)[C::NCT][APT], const bf16_t* r
 #pragma unroll
         for (int j = 0; j < APT; ++j)
           acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bf[cur][j], acc[ct][j], 0, 0, 0);
+    }
+  } else if constexpr (ROLL) {
+    // CM = 64, rolling reload: one fragment set, and each fragment of K-step ks+1 is read into its
+    // register right after its last MFMA of step ks (pixel fragments after their 4-MFMA group,
+    // weight fragments during the last group), so the reads run under the remaining MFMAs of ks
+    // instead of being exposed at the top of every step, with no extra registers
+    bf16x8 af[C::NCT], bf[APT];
+    frags(0, af, bf);
+#pragma unroll
+    for (int ks = 0; ks < C::KSA; ++ks) {
+      const bool more = ks + 1 < C::KSA;
+      const int kn = more ? ks + 1 : ks;
+      const int offn = ((kn / 3) * IW + kn % 3) * C::PSTRI;
+#pragma unroll
+      for (int j = 0; j < APT; ++j) {
+#pragma unroll
+        for (int ct = 0; ct < C::NCT; ++ct) {
+          acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[j], acc[ct][j], 0, 0, 0);
+          if (j == APT - 1 && more)
+            af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTRA + kn * 32 + kq * 8);
+        }
+        if (more) bf[j] = *reinterpret_cast<const bf16x8*>(rin + base[j] + offn);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   } else {  // CM = 64: 80 accumulator VGPRs; single fragment set, the scheduler overlaps the reads
 #pragma unroll
@@ -668,11 +692,14 @@ __device__ __forceinline__ void epi_head(const PairArgs& a, TileXY t, const f32x
   }
 }
 
-// LATE (CM = 64 A/B, BE_PAIR_LATE_EPI): the output epilogue's residual and bias loads are issued
-// right after stage B's MFMAs, so they are in flight across the barrier before the epilogue.
+// VAR (CM = 64 A/B): bit 0 = LATE (BE_PAIR_LATE_EPI): the output epilogue's residual and bias loads
+// are issued right after stage B's MFMAs, in flight across the barrier before the epilogue; bit 1 =
+// ROLL (BE_PAIR_ROLL): stage A's rolling fragment reload (see mma_a).
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false,
-          bool LATE = false>
+          int VAR = 0>
 __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
+  constexpr bool LATE = (VAR & 1) != 0;
+  constexpr bool ROLL = (VAR & 2) != 0;
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* R = reinterpret_cast<bf16_t*>(smem);
@@ -727,7 +754,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
       if (c + 1 < NCA) issue_halo<C, INMODE, PROJ>(a, cur, c + 1, tid, hraw);
       else if (t + 1 < t1) issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t + 1), 0, tid, hraw);
       if constexpr (!C::RESW) issue_w<C, NCA>(a, c + 1, tid, wraw);
-      mma_a<C>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
+      mma_a<C, ROLL>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
       stamp(1);
     }
     __syncthreads();  // every wave is done with the input halo and the A weights
@@ -783,22 +810,24 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
 unsigned long long* g_pair_stamps = nullptr;  // diagnostics: be_conv_pair_set_stamps
 int g_pair_stamps_cap = 0;                    // workgroups the stamp buffer holds
 
-static int g_pair_late = [] {  // A/B: BE_PAIR_LATE_EPI=1 selects the LATE build of the CM = 64 pairs
-  const char* e = getenv("BE_PAIR_LATE_EPI");
-  return e ? atoi(e) : 0;
+// A/B of the CM = 64 builds (see conv_pair_kernel's VAR): BE_PAIR_LATE_EPI=1 -> bit 0, BE_PAIR_ROLL=1 -> bit 1
+static int g_pair_var = [] {
+  const char* l = getenv("BE_PAIR_LATE_EPI");
+  const char* r = getenv("BE_PAIR_ROLL");
+  return ((l && atoi(l)) ? 1 : 0) | ((r && atoi(r)) ? 2 : 0);
 }();
 
-template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, bool LATE>
+template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, int VAR>
 int launch_pair_l(PairArgs a, int g, hipStream_t s) {
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, LATE>),
+        reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, VAR>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, LATE>), dim3(g), dim3(NT), C::LDS,
+  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, VAR>), dim3(g), dim3(NT), C::LDS,
                      s, a);
   return BE_CHECK_LAUNCH();
 }
@@ -806,9 +835,14 @@ int launch_pair_l(PairArgs a, int g, hipStream_t s) {
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
 int launch_pair_k(PairArgs a, int g, hipStream_t s) {
   if constexpr (CM == 64 && RES != 0) {
-    if (g_pair_late) return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, true>(a, g, s);
+    switch (g_pair_var) {
+      case 1: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 1>(a, g, s);
+      case 2: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 2>(a, g, s);
+      case 3: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 3>(a, g, s);
+      default: break;
+    }
   }
-  return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, false>(a, g, s);
+  return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 0>(a, g, s);
 }
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false>
