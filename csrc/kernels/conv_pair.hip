@@ -810,11 +810,13 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
 unsigned long long* g_pair_stamps = nullptr;  // diagnostics: be_conv_pair_set_stamps
 int g_pair_stamps_cap = 0;                    // workgroups the stamp buffer holds
 
-// A/B of the CM = 64 builds (see conv_pair_kernel's VAR): BE_PAIR_LATE_EPI=1 -> bit 0, BE_PAIR_ROLL=1 -> bit 1
+// A/B of the CM = 64 builds (see conv_pair_kernel's VAR): BE_PAIR_LATE_EPI (default 1) -> bit 0,
+// BE_PAIR_ROLL=1 -> bit 1.  LATE measured -0.5..-2.2 % cycles per tile on the three CM = 64 pairs and
+// +0.4 % on the headline, two alternating runs each (profiles/r04/conv/pair_late_epi_ab.txt).
 static int g_pair_var = [] {
   const char* l = getenv("BE_PAIR_LATE_EPI");
   const char* r = getenv("BE_PAIR_ROLL");
-  return ((l && atoi(l)) ? 1 : 0) | ((r && atoi(r)) ? 2 : 0);
+  return ((l ? atoi(l) : 1) ? 1 : 0) | ((r && atoi(r)) ? 2 : 0);
 }();
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, int VAR>
