@@ -230,12 +230,27 @@ __device__ __forceinline__ void unpack_aff(const float4 (&f)[4], float (&sc)[8],
   sh[0] = f[2].x; sh[1] = f[2].y; sh[2] = f[2].z; sh[3] = f[2].w; sh[4] = f[3].x; sh[5] = f[3].y; sh[6] = f[3].z; sh[7] = f[3].w;
 }
 
+// CM = 64, EARLY build: this chunk's actA affine loaded before the barrier that precedes the commit
+template <typename C>
+__device__ __forceinline__ void load_aff(const PairArgs& a, TileXY t, int ch, int tid, float4 (&f)[4]) {
+  int pix0, cg0;
+  unit_pc<C::CGI>(tid, pix0, cg0);
+  const int c = ch * C::CGI * 8 + cg0 * 8;
+  f[0] = *reinterpret_cast<const float4*>(a.sa + c);
+  f[1] = *reinterpret_cast<const float4*>(a.sa + c + 4);
+  const float* tr = a.ta + (size_t)t.n * a.ta_ns + c;
+  f[2] = *reinterpret_cast<const float4*>(tr);
+  f[3] = *reinterpret_cast<const float4*>(tr + 4);
+}
+
 template <typename C, bool PROJ>
 __device__ __forceinline__ void commit_halo(const PairArgs& a, TileXY t, int ch, int tid, const HaloRegs<C>& hr,
-                                            bf16_t* rin, bf16_t* preg) {
+                                            bf16_t* rin, bf16_t* preg, const float4 (*aff_pre)[4] = nullptr) {
   float sc[8], sh[8];
   if constexpr (C::PF) {
     unpack_aff(hr.aff, sc, sh);
+  } else if (aff_pre) {
+    unpack_aff(*aff_pre, sc, sh);
   } else {  // CM = 64: no registers to spare across the MFMA stage; read the (L2-hot) affine here
     int pix0, cg0;
     unit_pc<C::CGI>(tid, pix0, cg0);
@@ -694,12 +709,14 @@ __device__ __forceinline__ void epi_head(const PairArgs& a, TileXY t, const f32x
 
 // VAR (CM = 64 A/B): bit 0 = LATE (BE_PAIR_LATE_EPI): the output epilogue's residual and bias loads
 // are issued right after stage B's MFMAs, in flight across the barrier before the epilogue; bit 1 =
-// ROLL (BE_PAIR_ROLL): stage A's rolling fragment reload (see mma_a).
+// ROLL (BE_PAIR_ROLL): stage A's rolling fragment reload (see mma_a); bit 2 = EARLY
+// (BE_PAIR_EARLY_AFF): each chunk's actA affine loaded before the barrier ahead of its halo commit.
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false,
           int VAR = 0>
 __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   constexpr bool LATE = (VAR & 1) != 0;
   constexpr bool ROLL = (VAR & 2) != 0;
+  constexpr bool EARLY = (VAR & 4) != 0;
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* R = reinterpret_cast<bf16_t*>(smem);
@@ -746,8 +763,15 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
     // ---- stage A: NCA input chunks ----
 #pragma unroll 1
     for (int c = 0; c < NCA; ++c) {
-      __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
-      commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P);
+      if constexpr (EARLY && !C::PF) {
+        float4 aff[4];
+        load_aff<C>(a, cur, c, tid, aff);  // in flight across the barrier
+        __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
+        commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P, &aff);
+      } else {
+        __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
+        commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P);
+      }
       if constexpr (!C::RESW) commit_w<C>(tid, wraw, WL);
       __syncthreads();
       stamp(0);
@@ -816,7 +840,8 @@ int g_pair_stamps_cap = 0;                    // workgroups the stamp buffer hol
 static int g_pair_var = [] {
   const char* l = getenv("BE_PAIR_LATE_EPI");
   const char* r = getenv("BE_PAIR_ROLL");
-  return ((l ? atoi(l) : 1) ? 1 : 0) | ((r && atoi(r)) ? 2 : 0);
+  const char* e = getenv("BE_PAIR_EARLY_AFF");
+  return ((l ? atoi(l) : 1) ? 1 : 0) | ((r && atoi(r)) ? 2 : 0) | ((e && atoi(e)) ? 4 : 0);
 }();
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, int VAR>
@@ -841,6 +866,7 @@ int launch_pair_k(PairArgs a, int g, hipStream_t s) {
       case 1: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 1>(a, g, s);
       case 2: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 2>(a, g, s);
       case 3: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 3>(a, g, s);
+      case 5: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 5>(a, g, s);
       default: break;
     }
   }
