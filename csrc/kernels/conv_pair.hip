@@ -835,14 +835,15 @@ unsigned long long* g_pair_stamps = nullptr;  // diagnostics: be_conv_pair_set_s
 int g_pair_stamps_cap = 0;                    // workgroups the stamp buffer holds
 
 // A/B of the CM = 64 builds (see conv_pair_kernel's VAR): BE_PAIR_LATE_EPI (default 1) -> bit 0,
-// BE_PAIR_ROLL (default 1) -> bit 1, BE_PAIR_EARLY_AFF -> bit 2.  LATE: -0.5..-2.2 % cycles per tile on
-// the three CM = 64 pairs, +0.4 % headline; ROLL on top: stage A -8..-23 %, tiles -2.6..-6.2 %, +0.3 %
-// headline; two alternating runs each (profiles/r04/conv/pair_{late_epi,roll}_ab.txt).
+// BE_PAIR_ROLL (default 1) -> bit 1, BE_PAIR_EARLY_AFF (default 1) -> bit 2.  LATE: -0.5..-2.2 % cycles
+// per tile on the three CM = 64 pairs, +0.4 % headline; ROLL on top: stage A -8..-23 %, tiles
+// -2.6..-6.2 %, +0.3 % headline; EARLY on top: halo commit -2..-9 %, tiles -1.1..-2.4 %, +0.4 %
+// headline; two alternating runs each (profiles/r04/conv/pair_{late_epi,roll,early_aff}_ab.txt).
 static int g_pair_var = [] {
   const char* l = getenv("BE_PAIR_LATE_EPI");
   const char* r = getenv("BE_PAIR_ROLL");
   const char* e = getenv("BE_PAIR_EARLY_AFF");
-  return ((l ? atoi(l) : 1) ? 1 : 0) | ((r ? atoi(r) : 1) ? 2 : 0) | ((e && atoi(e)) ? 4 : 0);
+  return ((l ? atoi(l) : 1) ? 1 : 0) | ((r ? atoi(r) : 1) ? 2 : 0) | ((e ? atoi(e) : 1) ? 4 : 0);
 }();
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, int VAR>
