@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 4 step 36: final tree with the level-1 pair builds on by default -- full GPU suite, smoke,
+# default 1-GPU bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=$PWD/gpurun_out/r04/s36
+mkdir -p $O
+timeout -k 10 500 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $O/gpu_tests_full.log 2>&1; echo "suite rc=$?"; tail -2 $O/gpu_tests_full.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 $O/smoke.log
+timeout -k 10 400 python3 bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+tail -c 600 $O/bench_default.json
