@@ -490,10 +490,33 @@ __device__ __forceinline__ void issue_epi(const PairArgs& a, TileXY t, int wave,
   }
 }
 
+// CM = 64, EPIA build: actB's scale / shift (and the skip operand) of the stage-A epilogue loaded
+// before the barrier that precedes it, in flight while the slower waves finish their MFMAs
+template <typename C, bool X2>
+struct EpiA {
+  float4 s[C::NCT], sh[C::NCT];
+  u32x2 xv[X2 ? APT : 1][C::NCT];
+};
+
+template <typename C, bool X2>
+__device__ __forceinline__ void issue_epia(const PairArgs& a, TileXY t, int wave, int lrow, int kq, EpiA<C, X2>& p) {
+#pragma unroll
+  for (int ct = 0; ct < C::NCT; ++ct) {
+    const int c = ct * 16 + kq * 4;
+    p.s[ct] = *reinterpret_cast<const float4*>(a.sb + c);
+    p.sh[ct] = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
+    if constexpr (X2) {
+#pragma unroll
+      for (int j = 0; j < APT; ++j) p.xv[j][ct] = load_x2<C, X2>(a, t, j, ct, wave, lrow, kq);
+    }
+  }
+}
+
 // actB(+skip) of stage A's accumulators -> h (bf16) in LDS; zero outside the image
 template <typename C, bool X2, int RES, bool PF>
 __device__ __forceinline__ void epi_a(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][APT], bf16_t* rh,
-                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq) {
+                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq,
+                                      const EpiA<C, X2>* pre = nullptr) {
 #pragma unroll
   for (int ct = 0; ct < C::NCT; ++ct) {
     const int c = ct * 16 + kq * 4;
@@ -501,6 +524,9 @@ __device__ __forceinline__ void epi_a(const PairArgs& a, TileXY t, const f32x4 (
     if constexpr (PF) {
       s = e.sb[ct];
       sh = e.tb[ct];
+    } else if (pre) {
+      s = pre->s[ct];
+      sh = pre->sh[ct];
     } else {
       s = *reinterpret_cast<const float4*>(a.sb + c);
       sh = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
@@ -509,6 +535,7 @@ __device__ __forceinline__ void epi_a(const PairArgs& a, TileXY t, const f32x4 (
 #pragma unroll
     for (int j = 0; j < APT; ++j) {
       if constexpr (PF && X2) xv[j] = e.xv[j][ct];
+      else if (X2 && pre) xv[j] = pre->xv[j][ct];
       else xv[j] = load_x2<C, X2>(a, t, j, ct, wave, lrow, kq);
     }
 #pragma unroll
@@ -717,6 +744,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   constexpr bool LATE = (VAR & 1) != 0;
   constexpr bool ROLL = (VAR & 2) != 0;
   constexpr bool EARLY = (VAR & 4) != 0;
+  constexpr bool EPIA = (VAR & 8) != 0;
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* R = reinterpret_cast<bf16_t*>(smem);
@@ -781,8 +809,15 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
       mma_a<C, ROLL>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
       stamp(1);
     }
-    __syncthreads();  // every wave is done with the input halo and the A weights
-    epi_a<C, X2, RES, C::PF>(a, cur, acc_a, R, ep, wave, lrow, kq);
+    if constexpr (EPIA && !C::PF && !X2) {  // with the skip operand too it spills (320 B)
+      EpiA<C, X2> pa;
+      issue_epia<C, X2>(a, cur, wave, lrow, kq, pa);
+      __syncthreads();  // every wave is done with the input halo and the A weights
+      epi_a<C, X2, RES, C::PF>(a, cur, acc_a, R, ep, wave, lrow, kq, &pa);
+    } else {
+      __syncthreads();  // every wave is done with the input halo and the A weights
+      epi_a<C, X2, RES, C::PF>(a, cur, acc_a, R, ep, wave, lrow, kq);
+    }
     stamp(2);
     // ---- stage B: CM/32 chunks of h ----
     f32x4 acc_b[C::NCT][4];
@@ -843,7 +878,9 @@ static int g_pair_var = [] {
   const char* l = getenv("BE_PAIR_LATE_EPI");
   const char* r = getenv("BE_PAIR_ROLL");
   const char* e = getenv("BE_PAIR_EARLY_AFF");
-  return ((l ? atoi(l) : 1) ? 1 : 0) | ((r ? atoi(r) : 1) ? 2 : 0) | ((e ? atoi(e) : 1) ? 4 : 0);
+  const char* p = getenv("BE_PAIR_EPIA");
+  return ((l ? atoi(l) : 1) ? 1 : 0) | ((r ? atoi(r) : 1) ? 2 : 0) | ((e ? atoi(e) : 1) ? 4 : 0) |
+         ((p && atoi(p)) ? 8 : 0);
 }();
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, int VAR>
@@ -870,6 +907,7 @@ int launch_pair_k(PairArgs a, int g, hipStream_t s) {
       case 3: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 3>(a, g, s);
       case 5: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 5>(a, g, s);
       case 7: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 7>(a, g, s);
+      case 15: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 15>(a, g, s);
       default: break;
     }
   }
