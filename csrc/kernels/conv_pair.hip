@@ -745,11 +745,16 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   constexpr bool ROLL = (VAR & 2) != 0;
   constexpr bool EARLY = (VAR & 4) != 0;
   constexpr bool EPIA = (VAR & 8) != 0;
+  // SEPS (CM = 32, BE_PAIR_SEPS): output staging in its own LDS region (wave-private slots) after the
+  // weights, so the next tile's halo commit never overlays it and needs no barrier of its own: the
+  // barrier ahead of the output epilogue already fences stage B's reads of h
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
+  constexpr bool SEPS = (VAR & 16) != 0 && C::RESW && !HEAD;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* R = reinterpret_cast<bf16_t*>(smem);
   bf16_t* P = R + C::RREG;
   bf16_t* WL = P + C::PREG;
+  bf16_t* S = WL + C::WREG;  // SEPS only (the launch adds R_OUT elements of LDS)
   const int tid0 = threadIdx.x;
   const int total = a.N * a.tiles_x * a.tiles_y;
   // contiguous tile range per workgroup (tiles sharing halo rows run back to back on one CU)
@@ -797,7 +802,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
         __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
         commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P, &aff);
       } else {
-        __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
+        if (!(SEPS && c == 0)) __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
         commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P);
       }
       if constexpr (!C::RESW) commit_w<C>(tid, wraw, WL);
@@ -850,7 +855,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
       epi_b<C, X2, RES, C::PF, true>(a, cur, acc_b, R, ep, wave, lrow, kq, &late);
     } else {
       __syncthreads();  // every wave is done reading h before the output staging overlays it
-      epi_b<C, X2, RES, C::PF>(a, cur, acc_b, R, ep, wave, lrow, kq);
+      epi_b<C, X2, RES, C::PF>(a, cur, acc_b, SEPS ? S : R, ep, wave, lrow, kq);
     }
     stamp(4);
   }
@@ -879,29 +884,36 @@ static int g_pair_var = [] {
   const char* r = getenv("BE_PAIR_ROLL");
   const char* e = getenv("BE_PAIR_EARLY_AFF");
   const char* p = getenv("BE_PAIR_EPIA");
+  const char* q = getenv("BE_PAIR_SEPS");
   return ((l ? atoi(l) : 1) ? 1 : 0) | ((r ? atoi(r) : 1) ? 2 : 0) | ((e ? atoi(e) : 1) ? 4 : 0) |
-         ((p && atoi(p)) ? 8 : 0);
+         ((p && atoi(p)) ? 8 : 0) | ((q && atoi(q)) ? 16 : 0);
 }();
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, int VAR>
 int launch_pair_l(PairArgs a, int g, hipStream_t s) {
   using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
+  constexpr bool seps = (VAR & 16) != 0 && C::RESW && !HEAD;
+  constexpr size_t lds = C::LDS + (seps ? (size_t)C::R_OUT * sizeof(bf16_t) : 0);
+  static_assert(lds <= 160 * 1024, "LDS budget (separate output staging)");
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(
         reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, VAR>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS);
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, VAR>), dim3(g), dim3(NT), C::LDS,
-                     s, a);
+  hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, VAR>), dim3(g), dim3(NT), lds, s,
+                     a);
   return BE_CHECK_LAUNCH();
 }
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
 int launch_pair_k(PairArgs a, int g, hipStream_t s) {
+  if constexpr (CM == 32 && CK == 32 && !HEAD) {  // level-0 half-blocks: only the SEPS bit applies
+    if (g_pair_var & 16) return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 16>(a, g, s);
+  }
   if constexpr (CM == 64 && RES != 0) {
-    switch (g_pair_var) {
+    switch (g_pair_var & 15) {
       case 1: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 1>(a, g, s);
       case 2: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 2>(a, g, s);
       case 3: return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 3>(a, g, s);
