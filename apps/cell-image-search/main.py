@@ -126,7 +126,10 @@ class CellImageSearch:
             self._workspace_dir = os.path.join(os.environ.get("HOME", os.getcwd()), "cell_search_data")
         Path(self._workspace_dir).mkdir(parents=True, exist_ok=True)
         dev = "cuda:0" if torch.cuda.is_available() else "cpu"
-        self._worker = await asyncio.to_thread(EmbedWorker, dev, lambda d: default_engine_factory(d, self._model))
+        # ingestion embeds under the same lock as the query path, so it never runs inside the query
+        # path's HIP-graph capture of the same engine (models/vit.py embed_graphed)
+        self._worker = await asyncio.to_thread(EmbedWorker, dev, lambda d: default_engine_factory(d, self._model),
+                                               64, self._gpu_lock)
         loaded = await self._try_load_index()
         if self._auto_ingest and not loaded:
             await self._start_dataset_ingestion({"name": "Synthetic Cell Painting", "type": "synthetic",
@@ -460,22 +463,45 @@ class CellImageSearch:
         from bioengine_worker_amd.search.preprocess import batch_to_dinov2
 
         n = len(reqs)
-        kmax = max(int(r[4]) for r in reqs)
 
         def run():
             dev = self._worker.device
             q = [None] * n
             thumbs = {}
+            # one bad payload fails only its own request: its slot carries the exception, which the
+            # batcher turns into that caller's error (serve/batching.py), and it leaves the batch
+            err: dict = {}
             tm = [time.perf_counter()]
             imgs = [r[0] for r in reqs]
             enc = [i for i, im in enumerate(imgs) if isinstance(im, str)]
             if enc:
                 for i, raw in zip(enc, b64decode_batch([imgs[i] for i in enc])):
-                    imgs[i] = ref.to_hwc(np.load(io.BytesIO(memoryview(raw))))
+                    try:
+                        if raw is None:
+                            raise ValueError("image_b64 is not valid base64")
+                        imgs[i] = ref.to_hwc(np.load(io.BytesIO(memoryview(raw)), allow_pickle=False))
+                    except Exception as e:  # noqa: BLE001
+                        err[i] = ValueError(f"could not decode the query image: {e}")
             groups: dict = {}
+            embs: dict = {}
             for i, (_, emb, pl, ph, _) in enumerate(reqs):
-                if emb is None:
-                    groups.setdefault((imgs[i].shape, imgs[i].dtype.str, pl, ph), []).append(i)
+                if i in err:
+                    continue
+                try:
+                    if emb is None:
+                        im = imgs[i]
+                        if not isinstance(im, np.ndarray) or im.ndim != 3 or im.shape[0] < 1 or im.shape[1] < 1:
+                            raise ValueError(f"query image must be HxWxC, got {getattr(im, 'shape', type(im))}")
+                        groups.setdefault((im.shape, im.dtype.str, pl, ph), []).append(i)
+                    else:
+                        v = np.asarray(emb, np.float32)
+                        if v.shape != (self._index.dim,) or not np.isfinite(v).all():
+                            raise ValueError(f"embedding must be {self._index.dim} finite floats, got shape {v.shape}")
+                        embs[i] = v
+                except Exception as e:  # noqa: BLE001
+                    err[i] = e
+            ok = [i for i in range(n) if i not in err]
+            S = I = None
             with self._gpu_lock:
                 tm.append(time.perf_counter())
                 for (_, _, pl, ph), idxs in groups.items():
@@ -487,14 +513,18 @@ class CellImageSearch:
                     for j, i in enumerate(idxs):
                         q[i] = e[j]
                         thumbs[i] = u8h[j]
-                for i, (_, emb, _, _, _) in enumerate(reqs):
-                    if emb is not None:
-                        v = torch.as_tensor(np.asarray(emb, np.float32), device=dev)
-                        q[i] = v / v.norm().clamp_min(1e-9)
+                for i, v in embs.items():
+                    v = torch.as_tensor(v, device=dev)
+                    q[i] = v / v.norm().clamp_min(1e-9)
                 tm.append(time.perf_counter())
-                S, I = self._index.search(torch.stack(q), kmax)
+                if ok:
+                    kmax = max(int(reqs[i][4]) for i in ok)
+                    S, I = self._index.search(torch.stack([q[i] for i in ok]), kmax)
                 tm.append(time.perf_counter())
-            res = [self._results(S[i, : int(r[4])], I[i, : int(r[4])]) for i, r in enumerate(reqs)]
+            res = [None] * n
+            for row, i in enumerate(ok):
+                k = int(reqs[i][4])
+                res[i] = self._results(S[row, :k], I[row, :k])
             tm.append(time.perf_counter())
             # the batch's query thumbnails: one call into the host runtime's linear-time PNG encoder,
             # spread over host threads outside the GIL (csrc/runtime/png.cpp)
@@ -507,7 +537,7 @@ class CellImageSearch:
             st["batches"] += 1
             for k, a, b in (("decode", 0, 1), ("embed", 1, 2), ("scan", 2, 3), ("results", 3, 4), ("thumbs", 4, 5)):
                 st[k] += (tm[b] - tm[a]) * 1e3
-            return [(res[i], enc.get(i, "")) for i in range(n)]
+            return [err[i] if i in err else (res[i], enc.get(i, "")) for i in range(n)]
 
         return await asyncio.to_thread(run)
 

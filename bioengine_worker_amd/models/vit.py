@@ -270,6 +270,8 @@ class ViTEngine:
 
     #: batch buckets of :meth:`embed_graphed` (a request batch is padded up to the next one)
     GRAPH_BUCKETS = (1, 2, 4, 8, 16, 32, 64)
+    #: capture attempts per bucket before it stays eager for the process
+    GRAPH_MAX_TRIES = 3
 
     @torch.no_grad()
     def embed_graphed(self, x: torch.Tensor) -> torch.Tensor:
@@ -284,6 +286,10 @@ class ViTEngine:
         graphs = self.__dict__.setdefault("_graphs", {})
         key = (bucket, tuple(x.shape[1:]), x.dtype)
         ent = graphs.get(key)
+        if isinstance(ent, int):  # earlier capture attempts failed
+            if ent >= self.GRAPH_MAX_TRIES:
+                return self.embed(x)
+            ent = None
         if ent is None:
             xs = torch.zeros((bucket,) + tuple(x.shape[1:]), device=x.device, dtype=x.dtype)
             xs[:B] = x
@@ -294,14 +300,14 @@ class ViTEngine:
             torch.cuda.current_stream(x.device).wait_stream(side)
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g):
+                # thread_local: another thread's eager work on this device (e.g. the search app's
+                # ingestion embedding) neither breaks this capture nor is broken by it
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     out = self.embed(xs)
-            except Exception:  # noqa: BLE001 -- a path that cannot be captured runs eagerly
-                graphs[key] = False
+            except Exception:  # noqa: BLE001 -- counted: a transient failure is retried on later calls
+                graphs[key] = int(graphs.get(key) or 0) + 1
                 return self.embed(x)
             ent = graphs[key] = (g, xs, out)
-        if ent is False:
-            return self.embed(x)
         g, xs, out = ent
         xs[:B].copy_(x)
         if B < bucket:

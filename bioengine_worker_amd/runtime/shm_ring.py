@@ -25,19 +25,25 @@ EAGAIN_TIMEOUT, TOO_LARGE, CLOSED = -2, -3, -4
 _MALLOC_TUNED = False
 
 
-def tune_malloc() -> bool:
+def tune_malloc(role: str = "replica") -> bool:
     """Keep freed payload-sized buffers in the process heap (``BE_REPLICA_MALLOC``, default on).
+
+    ``role="router"``: the router is the main worker process that hosts every in-process app, so a
+    process-wide 512 MiB trim threshold there could hold large amounts of freed memory across its
+    many threads' arenas; it is applied there only when ``BE_ROUTER_MALLOC=1``.
 
     Every ring read allocates a fresh array for the payload; glibc serves multi-MiB requests from
     fresh mmaps, or trims the heap top after a free, so each request may page-fault its buffer in
     again (~1 ms per MiB on the VM hosts, see ``map_ring`` in shm_ring.cpp).  With the mmap
     threshold at 64 MiB and the trim threshold at 512 MiB, the freed buffers are reused instead.
-    Applied once per process (router and replica).  Measured on an MI355X box with the parallel ring
+    Applied once per replica process.  Measured on an MI355X box with the parallel ring
     copies (tools/replica_hop_bench.py, profiles/r04/serve/replica_hop_ab.jsonl): a 2 MiB request
     round trip 245 us -> 191 us (4 copy threads) -> 150 us (+ this)."""
     global _MALLOC_TUNED
     if _MALLOC_TUNED or os.environ.get("BE_REPLICA_MALLOC", "1") in ("0", "false", "no"):
         return _MALLOC_TUNED
+    if role == "router" and os.environ.get("BE_ROUTER_MALLOC", "0") not in ("1", "true", "yes"):
+        return False
     try:
         libc = ctypes.CDLL("libc.so.6")
         ok = libc.mallopt(-3, 64 << 20) == 1 and libc.mallopt(-1, 512 << 20) == 1  # M_MMAP_THRESHOLD, M_TRIM_THRESHOLD

@@ -262,7 +262,14 @@ def b64decode_batch(strings: list, threads: int = 8) -> list:
             raise ValueError("b64 decode failed")
         return [out[i * cap: i * cap + int(olen[i])] for i in range(n)]
     except (OSError, AttributeError, ImportError, UnicodeEncodeError, ValueError):
-        return [np.frombuffer(base64.b64decode(s), np.uint8) for s in strings]
+        # per item, so one malformed payload yields None in its own slot, not a failed batch
+        res = []
+        for s in strings:
+            try:
+                res.append(np.frombuffer(base64.b64decode(s, validate=False), np.uint8))
+            except (ValueError, TypeError):
+                res.append(None)
+        return res
 
 
 THUMBS_B64 = "thumbnails_b64.txt"
@@ -290,10 +297,15 @@ def read_thumbnails_b64(out: Path, n: int) -> list | None:
 class EmbedWorker:
     """Owns one GPU's ViT engine; embeds crop batches."""
 
-    def __init__(self, device, engine_factory: Callable[[Any], Any], batch_size: int = 64):
+    def __init__(self, device, engine_factory: Callable[[Any], Any], batch_size: int = 64, gpu_lock=None):
+        import contextlib
+
         self.device = torch.device(device)
         self.engine = engine_factory(self.device)
         self.batch_size = batch_size
+        # held around every engine call: an app that also serves queries from this engine (and
+        # captures HIP graphs of it) passes its own lock so ingestion never runs inside a capture
+        self.gpu_lock = gpu_lock if gpu_lock is not None else contextlib.nullcontext()
 
     def process(self, image: np.ndarray, n_crops: int, rgb_channels=None):
         from . import reference as ref
@@ -311,7 +323,8 @@ class EmbedWorker:
         for i in range(0, crops.shape[0], self.batch_size):
             c = crops[i:i + self.batch_size]
             x = batch_to_dinov2(c.to(self.device), rgb_channels)
-            embs.append(self.engine.embed(x))
+            with self.gpu_lock:
+                embs.append(self.engine.embed(x))
             # thumbnails of the displayed RGB composite (ImageNet de-normalised)
             mean = torch.tensor([0.485, 0.456, 0.406], device=x.device)[None, :, None, None]
             std = torch.tensor([0.229, 0.224, 0.225], device=x.device)[None, :, None, None]

@@ -382,7 +382,7 @@ class ProcessReplica(ReplicaBase):
         try:
             from ..runtime.shm_ring import ShmRing, tune_malloc
 
-            tune_malloc()
+            tune_malloc("router")
             self.tx, self.rx = ShmRing.create(cap), ShmRing.create(cap)
         except Exception:  # runtime library unavailable or /dev/shm exhausted: socket-only
             self._drop_rings()

@@ -256,6 +256,10 @@ class CellposeTrainer:
 
     def _adamw_range(self, s: int, e: int, grad_scale: float, mirror) -> None:
         """AdamW over flat elements [s, e) (bucket boundaries are 4-element aligned)."""
+        # the streaming kernel reads flat/grad/m/v[s:] as float4 and the bf16 mirror as 4 x bf16:
+        # a sub-range must start on a 4-element boundary (16 B fp32 / 8 B bf16)
+        if s % 4:
+            raise ValueError(f"AdamW sub-range start {s} is not 4-element aligned")
         sl = slice(s, e)
         train_ops.adamw_flat_(self.fp.flat[sl], self.fp.grad[sl], self.m[sl], self.v[sl], lr=self.lr,
                               step=self.step_count, weight_decay=self.cfg.weight_decay, grad_scale=grad_scale,

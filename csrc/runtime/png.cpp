@@ -50,7 +50,7 @@ void put32(std::vector<unsigned char>& v, uint32_t x) {
 void encode_png(const unsigned char* rgb, int h, int w, long long stride, std::vector<unsigned char>& png) {
   const size_t row = (size_t)w * 3 + 1;
   const size_t raw = row * (size_t)h;
-  const size_t nblk = raw / 65535 + 1;
+  const size_t nblk = raw ? (raw + 65534) / 65535 : 1;  // stored blocks the loop below writes
   const size_t idat = 2 + nblk * 5 + raw + 4;
   png.clear();
   png.reserve(8 + 25 + 12 + idat + 12);
@@ -163,7 +163,7 @@ extern "C" {
 // Upper bound of the base64 length for an h x w RGB image.
 int be_rt_png_b64_cap(int h, int w) {
   const long long raw = ((long long)w * 3 + 1) * h;
-  const long long png = 8 + 25 + 12 + 2 + (raw / 65535 + 1) * 5 + raw + 4 + 12;
+  const long long png = 8 + 25 + 12 + 2 + (raw ? (raw + 65534) / 65535 : 1) * 5 + raw + 4 + 12;
   const long long cap = (png + 2) / 3 * 4;
   return cap > 0x7fffffffLL ? -1 : (int)cap;
 }

@@ -101,3 +101,41 @@ def test_shm_ring_large_frames_cross_process():
         a2b.unlink()
         b2a.unlink()
     assert p.exitcode == 0
+
+
+@pytest.mark.parametrize("hw", [(771, 28), (96, 96), (224, 224), (1, 1), (3, 5)])
+def test_native_png_roundtrips_through_pil(hw):
+    """The host runtime's stored-deflate PNG encoder (csrc/runtime/png.cpp) decodes bit-exactly in
+    PIL, including raw sizes that are exact multiples of the 65535-byte block (28 x 771: (3*28+1)*771
+    = 65535), where the IDAT length once counted one block too many."""
+    import base64
+    import io
+
+    from PIL import Image
+
+    from bioengine_worker_amd.search.ingestion import png_b64_batch
+
+    h, w = hw
+    rng = np.random.default_rng(h * 1000 + w)
+    rgb = rng.integers(0, 256, (3, h, w, 3), dtype=np.uint8)
+    for i, s in enumerate(png_b64_batch(rgb)):
+        im = Image.open(io.BytesIO(base64.b64decode(s)))
+        im.load()
+        assert im.size == (w, h) and im.mode == "RGB"
+        assert np.array_equal(np.asarray(im), rgb[i])
+
+
+def test_native_b64decode_matches_stdlib():
+    import base64
+
+    from bioengine_worker_amd.search.ingestion import b64decode_batch
+
+    rng = np.random.default_rng(7)
+    payloads = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (0, 1, 2, 3, 4, 5, 63, 64, 65, 1000, 65537)]
+    enc = [base64.b64encode(p).decode() for p in payloads]
+    for p, got in zip(payloads, b64decode_batch(enc)):
+        assert bytes(got) == p
+    # one malformed string yields None in its own slot only
+    got = b64decode_batch([enc[9], "abc", enc[10]])
+    assert bytes(got[0]) == payloads[9] and bytes(got[2]) == payloads[10]
+    assert got[1] is None or bytes(got[1]) != b""

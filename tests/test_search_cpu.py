@@ -130,6 +130,22 @@ def test_cell_image_search_app_e2e(tmp_path, monkeypatch):
         assert bs["query"]["requests"] >= 13 and bs["query"]["mean_batch"] > 1.0, bs
         assert bs["query"]["batches"] < bs["query"]["requests"], bs
         assert res["query_thumbnail_b64"] and many[0]["query_thumbnail_b64"]
+        # a malformed payload in the same batch fails only its own request: a truncated
+        # .npy, a non-base64 .npy-looking string and a wrong-length embedding beside good queries
+        raw = buf.getvalue()
+        bad_npy = base64.b64encode(raw[:64]).decode()
+        bad_b64 = b64[:8] + "!!!!" + b64[8:40] + "="
+        mixed = await asyncio.gather(
+            app.search(image_b64=b64, top_k=3), app.search(image_b64=bad_npy, top_k=3),
+            app.search(image_b64=b64, top_k=4), app.search(embedding=[1.0] * 5, top_k=3),
+            app.search(image_b64=bad_b64, top_k=3), app.search(image_b64=b64, top_k=5),
+            return_exceptions=True)
+        for j, k in ((0, 3), (2, 4), (5, 5)):
+            assert not isinstance(mixed[j], BaseException), mixed[j]
+            assert len(mixed[j]["results"]) == k
+            assert mixed[j]["results"][0]["faiss_idx"] == res["results"][0]["faiss_idx"]
+        for j in (1, 3, 4):
+            assert isinstance(mixed[j], BaseException), mixed[j]
         emb = await app.search(embedding=[1.0] * int(stats.get("embed_dim", 768)), top_k=4)
         assert len(emb["results"]) == 4 and emb["query_thumbnail_b64"] == ""
         up = await app.get_umap_preview(n_samples=100)
