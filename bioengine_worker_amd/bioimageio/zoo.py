@@ -8,6 +8,12 @@ The cache keeps one directory per model id under ``cache_dir`` with the referenc
 cross-replica coordination: atomic ``os.rename`` publication of a finished download, a
 ``.downloading`` marker other replicas wait on, ``.last_access`` files for LRU eviction, and
 in-use leases that make a package non-evictable while a request holds it.
+
+Crash recovery (reference ``entry_deployment.py:384-411, 833-837``): leases and download markers
+record their owner (host, pid) and start time.  A lease older than :data:`LEASE_MAX_AGE_S` or whose
+owner process on this host has exited no longer blocks eviction; a download marker whose owner has
+exited, or that is older than :data:`DOWNLOAD_TIMEOUT_S`, is removed and the download claimed again --
+a replica that dies mid-download no longer leaves every later request waiting out the timeout.
 """
 from __future__ import annotations
 
@@ -18,7 +24,55 @@ import shutil
 import time
 from pathlib import Path
 
+import socket
+import uuid
+
 import yaml
+
+#: an in-use lease older than this no longer blocks eviction (the reference's 10 minutes)
+LEASE_MAX_AGE_S = 600.0
+#: a download marker older than this is stale whatever its owner
+DOWNLOAD_TIMEOUT_S = float(os.environ.get("BIOENGINE_MODEL_DOWNLOAD_TIMEOUT_S", "1800"))
+_HOST = socket.gethostname()
+
+
+def _owner() -> dict:
+    return {"host": _HOST, "pid": os.getpid(), "t": time.time()}
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return True
+
+
+def _owner_stale(info: dict | None, max_age: float, mtime: float) -> bool:
+    """An owner record is stale when its process (on this host) is gone or it is older than max_age."""
+    t = float(info.get("t", mtime)) if info else mtime
+    if time.time() - t > max_age:
+        return True
+    if info and info.get("host") == _HOST and isinstance(info.get("pid"), int):
+        return not _pid_alive(int(info["pid"]))
+    return False
+
+
+def _read_owner(p: Path) -> dict | None:
+    try:
+        return json.loads(p.read_text())
+    except (OSError, ValueError):
+        return None
+
+
+def lease_live(p: Path) -> bool:
+    try:
+        mt = p.stat().st_mtime
+    except OSError:
+        return False
+    return not _owner_stale(_read_owner(p), LEASE_MAX_AGE_S, mt)
 
 
 def local_zoo_root() -> Path | None:
@@ -68,8 +122,8 @@ class PackageLease:
         return self.source / "rdf.yaml"
 
     async def __aenter__(self):
-        self._lease = self.source / f".in_use.{os.getpid()}.{id(self)}"
-        self._lease.touch()
+        self._lease = self.source / f".in_use.{os.getpid()}.{uuid.uuid4().hex[:12]}"
+        self._lease.write_text(json.dumps(_owner()))
         (self.source / ".last_access").write_text(str(time.time()))
         return self
 
@@ -102,7 +156,7 @@ class ModelCache:
                 la = d / ".last_access"
                 out.append({"model_id": d.name, "path": str(d), "size_bytes": self._size(d),
                             "last_access": float(la.read_text()) if la.exists() else 0.0,
-                            "in_use": any(d.glob(".in_use.*"))})
+                            "in_use": any(lease_live(p) for p in d.glob(".in_use.*"))})
         return out
 
     async def ensure_space(self, needed: int) -> None:
@@ -122,6 +176,22 @@ class ModelCache:
         if sum(m["size_bytes"] for m in self.cached_models()) + needed > self.cache_size_bytes:
             raise RuntimeError("model cache full (all cached packages in use)")
 
+    @staticmethod
+    def _reclaim_stale_marker(marker: Path) -> bool:
+        """Remove a download marker left by a dead downloader (or older than the download timeout);
+        True when it was removed and the caller may claim the download."""
+        try:
+            mt = marker.stat().st_mtime
+        except OSError:
+            return True  # gone meanwhile
+        info = _read_owner(marker / "owner.json")
+        if info is None and time.time() - mt < 5.0:
+            return False  # just created; its owner record follows the mkdir
+        if not _owner_stale(info, DOWNLOAD_TIMEOUT_S, mt):
+            return False
+        shutil.rmtree(marker, ignore_errors=True)
+        return True
+
     async def get_model_package(self, model_id: str, stage: bool = False, skip_cache: bool = False,
                                 allow_unpublished: bool = True) -> PackageLease:
         if "://" in model_id:
@@ -138,8 +208,11 @@ class ModelCache:
             try:
                 marker.mkdir()  # atomic: only one replica downloads
             except FileExistsError:
+                if self._reclaim_stale_marker(marker):
+                    continue
                 await asyncio.sleep(0.1)
                 continue
+            (marker / "owner.json").write_text(json.dumps(_owner()))
             try:
                 tmp = self.cache_dir / f".{d.name}.{self.replica_id}.tmp"
                 shutil.rmtree(tmp, ignore_errors=True)
@@ -159,5 +232,5 @@ class ModelCache:
                     shutil.rmtree(d, ignore_errors=True)
                 os.rename(tmp, d)
             finally:
-                marker.rmdir()
+                shutil.rmtree(marker, ignore_errors=True)
         raise TimeoutError(f"timed out waiting for model '{model_id}' download")

@@ -115,3 +115,74 @@ def test_test_model_report(pkg):
     rep = run_model_test(pkg, device="cpu")
     assert rep["status"] == "passed", rep
     assert rep["details"][1]["name"].startswith("Reproduce")
+
+
+def _hang_downloader(cache_dir, ready_path):
+    """Child process: claims the download of 'remote-model', then hangs inside the fetch."""
+    import asyncio as aio
+    from pathlib import Path as P
+
+    from bioengine_worker_amd.bioimageio.zoo import ModelCache as MC
+
+    async def fetch(model_id, dest, stage):
+        P(ready_path).write_text("claimed")
+        await aio.sleep(3600)
+
+    aio.run(MC(cache_dir, replica_id="dead", fetch_remote=fetch).get_model_package("remote-model"))
+
+
+def test_model_cache_recovers_from_dead_downloader_and_stale_leases(tmp_path, monkeypatch):
+    """A replica killed mid-download leaves its marker behind: the next request reclaims it at once
+    instead of waiting out the timeout; a dead process's in-use lease no longer blocks eviction
+    (reference entry_deployment.py:384-411, 833-837)."""
+    import asyncio
+    import json
+    import multiprocessing as mp
+    import os
+    import signal
+    import time
+
+    from bioengine_worker_amd.bioimageio import zoo
+
+    monkeypatch.delenv("BIOENGINE_MODEL_ZOO", raising=False)
+    cache_dir = tmp_path / "cache"
+    ready = tmp_path / "ready"
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_hang_downloader, args=(str(cache_dir), str(ready)))
+    p.start()
+    try:
+        for _ in range(600):
+            if ready.exists():
+                break
+            time.sleep(0.1)
+        assert ready.exists(), "child never claimed the download"
+        assert (cache_dir / ".remote-model.downloading").is_dir()
+    finally:
+        os.kill(p.pid, signal.SIGKILL)
+        p.join(10)
+
+    async def fetch(model_id, dest, stage):
+        (dest / "rdf.yaml").write_text("id: remote-model\n")
+        (dest / "weights.bin").write_bytes(b"\0" * 1024)
+        return 123.0
+
+    cache = zoo.ModelCache(cache_dir, cache_size_in_gb=1.0, replica_id="live", fetch_remote=fetch)
+    t0 = time.time()
+    lease = asyncio.run(cache.get_model_package("remote-model"))
+    assert time.time() - t0 < 5.0
+    assert lease.rdf_path.exists() and not (cache_dir / ".remote-model.downloading").exists()
+
+    # a lease from a dead pid on this host, and one older than the max age: neither pins the package
+    d = lease.source
+    (d / ".in_use.999999999.x").write_text(json.dumps({"host": zoo._HOST, "pid": 999999999, "t": time.time()}))
+    old = d / ".in_use.1.y"
+    old.write_text(json.dumps({"host": "elsewhere", "pid": 1, "t": time.time() - 2 * zoo.LEASE_MAX_AGE_S}))
+    assert not any(m["in_use"] for m in cache.cached_models())
+
+    async def held():
+        async with lease:
+            return [m["in_use"] for m in cache.cached_models()]
+    assert any(asyncio.run(held()))
+    cache.cache_size_bytes = 10  # force eviction of everything not in use
+    asyncio.run(cache.ensure_space(0))
+    assert not d.exists()
