@@ -162,6 +162,9 @@ def clahe_image(img: np.ndarray, device=None) -> np.ndarray:
 
 @serve.deployment(
     ray_actor_options={"num_gpus": 1, "num_cpus": 4, "memory": 12 * 1024 ** 3},
+    # one GPU-pinned replica by default (the reference app's single replica); a node-level deployment
+    # sets BIOENGINE_CELLPOSE_REPLICAS to its GPU count and the router spreads requests over them
+    num_replicas=int(os.environ.get("BIOENGINE_CELLPOSE_REPLICAS", "1")),
     max_ongoing_requests=64,  # >= 2 full continuous batches in flight at the replica
     max_queued_requests=256,
     health_check_period_s=30.0,

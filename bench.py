@@ -247,6 +247,46 @@ def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
     return out
 
 
+def bench_served_node(args, world: int, rank: int) -> dict:
+    """Node-level serving at world > 1: after the per-rank lines every rank frees
+    its cached HBM and waits on a host-side (gloo) barrier; rank 0 then deploys the Cellpose app
+    through the worker stack with one process replica per GPU (HIP_VISIBLE_DEVICES-pinned children,
+    nothing re-execs a GPU process) and drives c = 64 x N closed-loop clients, so the router fans the
+    requests out over the node -- the reference's replica scaling
+    (bioengine/apps/proxy_deployment.py:35-44, apps/model-runner/runtime_deployment.py:40-50)."""
+    import argparse as _ap
+    import asyncio
+    import gc
+
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    gl = dist.new_group(backend="gloo")
+    dist.barrier(group=gl)
+    out = {}
+    if rank == 0:
+        try:
+            sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+            import serve_bench
+
+            nrep = max(1, min(world, torch.cuda.device_count()))
+            os.environ["BIOENGINE_CELLPOSE_REPLICAS"] = str(nrep)
+            os.environ["BIOENGINE_GPU_IDS"] = ",".join(str(i) for i in range(nrep))
+            conc = 64 * world
+            a = _ap.Namespace(size=512, concurrency=[conc], seconds=max(4.0, 2 * args.served_seconds), gpus=nrep,
+                              replica_mode="process", max_ongoing=conc, model="cyto3", profile=None)
+            r = asyncio.run(serve_bench.main_async(a))[-1]
+            out[f"served_imgs_per_sec_node_c{conc}"] = r["imgs_per_s"]
+            out[f"served_p50_ms_node_c{conc}"] = r["p50_ms"]
+            out[f"served_p99_ms_node_c{conc}"] = r["p99_ms"]
+            out["served_node_config"] = {"replicas": nrep, "gpus_per_replica": 1, "replica_mode": "process",
+                                         "clients": conc, "image": [512, 512, 2], "layer": "hub -> router -> replicas"}
+        except Exception as e:  # noqa: BLE001
+            out["extras_error_served_node"] = f"{type(e).__name__}: {e}"
+    dist.barrier(group=gl)
+    return out
+
+
 def bench_vit_embed(dev, batch: int = 64, steps: int = 20) -> float:
     """DINOv2 ViT-B/14 embedding throughput, fp8 e4m3 GEMMs, batch 64 of 224x224 (the reference's
     embedder batch and resolution, apps/cell-image-search/embedder.py:59-95; ~500 img/s/A100 fp16)."""
@@ -413,6 +453,93 @@ def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int, force_dp: 
     return batch * steps * world / dt, dt / steps * 1e3
 
 
+def bench_cpsam_infer(dev, batch: int = 8, steps: int = 4, lat_n: int = 10) -> dict:
+    """Cellpose-SAM inference -- the reference app's default ``infer`` model
+    (apps/cellpose-finetuning/main.py:4966-5144, bf16 Transformer :126-127): 512x512x3 images through
+    cellpose 4's 256-tile / 0.1-overlap path (9 tiles per image), the ViT-L/8 engine on the in-house
+    GEMMs replayed from its HIP graph, taper blend, dynamics (niter 200), flow QC and fill holes.
+    Random-init weights, synthetic images."""
+    from bioengine_worker_amd.cellpose.pipeline import CellposeRunner, EvalParams, synthetic_cells
+    from bioengine_worker_amd.models.cpsam import CPSAM
+
+    runner = CellposeRunner(net=CPSAM().randomize_(0), device=dev)
+    imgs = torch.from_numpy(synthetic_cells(batch, 512, 512, nchan=3, seed=0)).to(dev)
+    p = EvalParams(niter=200, flow_threshold=0.4, cellprob_threshold=0.0, min_size=15)
+    for _ in range(2):
+        runner.eval(imgs, p)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.eval(imgs, p)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    one = imgs[:1]
+    for _ in range(2):
+        runner.eval(one, p)
+    lat = []
+    for _ in range(lat_n):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        m, _, _ = runner.eval(one, p)
+        m.cpu()
+        lat.append((time.perf_counter() - t) * 1e3)
+    lat.sort()
+    gemm = runner.engine.GEMM
+    del runner
+    torch.cuda.empty_cache()
+    return {"cpsam_infer_imgs_per_s": round(batch * steps / dt, 2),
+            "cpsam_infer_p50_ms_batch1": round(lat[len(lat) // 2], 2),
+            "cpsam_infer_config": {"model": "Cellpose-SAM ViT-L/8 (dim 1024, 24 blocks), random init",
+                                   "image": [512, 512, 3], "batch": batch, "tiles": "256 / 0.1 overlap (9 per image)",
+                                   "gemm": "in-house macro-tile MFMA (gemm_mt)" if gemm == "mt" else "hipBLASLt",
+                                   "graph": "one HIP graph per tile count", "masks": "dynamics niter 200, QC 0.4"}}
+
+
+def bench_train_autograd(dev, arch: str, batch: int, steps: int = 6, warmup: int = 2, bf16: bool = False) -> float:
+    """Reference-algorithm fine-tune step: the network as a plain torch module, PyTorch
+    autograd, torch.optim.AdamW (lr 1e-5, wd 1e-4) and cellpose's ``_loss_fn_seg`` (flows MSE against
+    5x targets / 2 + BCE-with-logits on cellprob) on the same 256x256 crops as the native lines, fp32
+    like the reference's training (apps/cellpose-finetuning/main.py:1350-1358, 1483-1546) or under
+    bf16 autocast.  Returns samples/s."""
+    import torch.nn.functional as F
+
+    from bioengine_worker_amd.models.cpnet import CPnet
+    from bioengine_worker_amd.models.cpsam import CPSAM
+
+    torch.manual_seed(0)
+    if arch == "cpsam":
+        net, nch = CPSAM().randomize_(0), 3
+    else:
+        net, nch = CPnet().randomize_(0), 2
+    net = net.to(dev).float().train()
+    opt = torch.optim.AdamW(net.parameters(), lr=1e-5, weight_decay=1e-4)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randn(batch, nch, 256, 256, generator=g).to(dev)
+    lbl = torch.randn(batch, 3, 256, 256, generator=g).to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=bf16):
+            y = net(x)[0]
+        y = y.float()
+        loss = F.mse_loss(y[:, :2], 5.0 * lbl[:, 1:]) / 2.0 + \
+            F.binary_cross_entropy_with_logits(y[:, -1], (lbl[:, 0] > 0.5).float())
+        loss.backward()
+        opt.step()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del net, opt
+    torch.cuda.empty_cache()
+    return batch * steps / dt
+
+
 def bench_train(args, world, rank, dev, norm="auto"):
     from bioengine_worker_amd.train.cellpose_train import TrainConfig, synthetic_train_batch, build_trainer
 
@@ -571,6 +698,28 @@ def main():
                     dist.destroy_process_group()
         except Exception as e:  # noqa: BLE001
             out["extras_error_train_cpsam"] = f"{type(e).__name__}: {e}"
+        if rank == 0:
+            try:
+                out.update(bench_cpsam_infer(dev))
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_cpsam_infer"] = f"{type(e).__name__}: {e}"
+        if rank == 0:
+            # reference-algorithm anchors of the two fine-tune lines (plain autograd + torch AdamW)
+            try:
+                out["finetune_autograd_samples_per_sec"] = round(
+                    bench_train_autograd(dev, "cpnet", args.train_batch), 2)
+                out["finetune_cpsam_autograd_samples_per_sec"] = round(
+                    bench_train_autograd(dev, "cpsam", args.cpsam_batch, steps=4), 2)
+                out["finetune_cpsam_autograd_bf16_samples_per_sec"] = round(
+                    bench_train_autograd(dev, "cpsam", args.cpsam_batch, steps=4, bf16=True), 2)
+                out["finetune_autograd_config"] = {
+                    "what": "plain PyTorch autograd + torch.optim.AdamW + cellpose _loss_fn_seg, same crops "
+                            "and batch as the native lines, no augmentation", "dtype": "fp32 (reference); "
+                            "*_bf16: torch.autocast bf16"}
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_train_autograd"] = f"{type(e).__name__}: {e}"
+    if world > 1 and not args.no_extras and not args.no_served:
+        out.update(bench_served_node(args, world, rank))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

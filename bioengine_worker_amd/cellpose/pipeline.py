@@ -147,7 +147,7 @@ class CellposeRunner:
         x[:, :, :by, :bx] = tiles[..., :3].permute(0, 3, 1, 2)
         out = []
         for i in range(0, T, 64):  # bounded activation memory for very large batches
-            out.append(self.engine(x[i: i + 64]))
+            out.append(self.engine.graphed(x[i: i + 64]))
         y = torch.cat(out) if len(out) > 1 else out[0]
         return y[:, :, :by, :bx].contiguous()
 

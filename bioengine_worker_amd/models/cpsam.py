@@ -12,10 +12,12 @@ a pixel-shuffle back to 3 x 256 x 256 (dY, dX, cellprob).
   attn.rel_pos_w,norm2,mlp.lin1,mlp.lin2}``, ``encoder.neck.{0..3}``, ``out``, ``W2``,
   ``diam_labels``, ``diam_mean``) so a ``cpsam`` checkpoint loads with ``weights_only=True``.
   Reference path + training (``rdrop`` per-sample stochastic depth as cellpose 4 does).
-* :class:`CPSAMEngine` — bf16 inference on the framework's kernels: hipBLASLt GEMMs, the
+* :class:`CPSAMEngine` — bf16 inference on the framework's kernels: the macro-tile MFMA GEMM
+  (``ops/gemm_mt.py``) for every linear layer with bias / bias + GELU in its epilogue, the
   flash-attention kernel with the decomposed rel-pos bias fused into the score tile (the 1024x1024
-  bias never exists), residual fused into LayerNorm, bias+GELU fused, the neck's 3x3 conv on the
-  NHWC MFMA conv kernel, and the readout + pixel shuffle as one GEMM + reshape.
+  bias never exists), residual fused into LayerNorm, the neck's 3x3 conv on the NHWC MFMA conv
+  kernel, and the readout + pixel shuffle as one GEMM + reshape.  :meth:`CPSAMEngine.graphed`
+  replays the whole forward (~170 launches) from one HIP graph per tile count.
 """
 from __future__ import annotations
 
@@ -24,6 +26,8 @@ import math
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+import os
 
 from ..ops.conv import PackedConv, fused_conv2d
 from ..ops.transformer import add_layernorm, attention_ref, bias_gelu_, flash_attention
@@ -208,35 +212,79 @@ class CPSAMEngine:
         self.out_w = bf(net.out.weight.reshape(net.out.weight.shape[0], -1))
         self.out_b = bf(net.out.bias)
 
+    #: GEMM backend of the inference engine: "mt" (the framework's macro-tile MFMA GEMM, default) or
+    #: "lib" (PyTorch -> hipBLASLt, the A/B reference)
+    GEMM = os.environ.get("BE_CPSAM_INFER_GEMM", "mt")
+
+    def _gemms(self):
+        if self.GEMM == "lib":
+            def lin(x, w, b=None):
+                return F.linear(x, w, b)
+
+            def lin_gelu(x, w, b):
+                return bias_gelu_(F.linear(x, w), b)
+            return lin, lin_gelu
+        from ..ops import gemm_mt
+
+        return gemm_mt.linear, gemm_mt.linear_gelu_only
+
     @torch.no_grad()
     def __call__(self, x: torch.Tensor) -> torch.Tensor:
         """x [B, 3, bsize, bsize] float -> flows [B, nout, bsize, bsize] fp32."""
         B = x.shape[0]
         ps, g, D, Hh = self.ps, self.grid, self.dim, self.heads
         N = g * g
+        lin, lin_gelu = self._gemms()
         x = x.to(self.device, torch.bfloat16)
-        patches = x.reshape(B, 3, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B, N, 3 * ps * ps)
-        t = (F.linear(patches, self.pe_w, self.pe_b) + self.pos).contiguous()
+        patches = x.reshape(B, 3, g, ps, g, ps).permute(0, 2, 4, 1, 3, 5).reshape(B * N, 3 * ps * ps)
+        t = (lin(patches, self.pe_w, self.pe_b).view(B, N, D) + self.pos).contiguous()
         blocks = self.blocks
         h = add_layernorm(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"])
         for i, b in enumerate(blocks):
-            qkv = F.linear(h, b["qkv_w"], b["qkv_b"]).view(B, N, 3, Hh, D // Hh)
+            qkv = lin(h.view(B * N, D), b["qkv_w"], b["qkv_b"]).view(B, N, 3, Hh, D // Hh)
             q = qkv[:, :, 0]
             rel_h, rel_w = rel_pos_terms(q, b["Rh"], b["Rw"], g, g)
-            a = flash_attention(q, qkv[:, :, 1], qkv[:, :, 2], (D // Hh) ** -0.5, rel_h, rel_w).view(B, N, D)
-            y = F.linear(a, b["proj_w"], b["proj_b"])
+            a = flash_attention(q, qkv[:, :, 1], qkv[:, :, 2], (D // Hh) ** -0.5, rel_h, rel_w).view(B * N, D)
+            y = lin(a, b["proj_w"], b["proj_b"]).view(B, N, D)
             h2 = add_layernorm(t, y, None, b["n2w"], b["n2b"])
-            m = F.linear(bias_gelu_(F.linear(h2, b["l1_w"]), b["l1_b"]), b["l2_w"], b["l2_b"])
+            m = lin(lin_gelu(h2.view(B * N, D), b["l1_w"], b["l1_b"]), b["l2_w"], b["l2_b"]).view(B, N, D)
             if i + 1 < len(blocks):
                 h = add_layernorm(t, m, None, blocks[i + 1]["n1w"], blocks[i + 1]["n1b"])
             else:
                 t.add_(m)
         # neck: 1x1 conv (GEMM) -> LN2d -> 3x3 conv (NHWC MFMA kernel) -> LN2d
-        n0 = F.linear(t, self.neck0)                                   # [B, N, 256]
+        n0 = lin(t.view(B * N, D), self.neck0).view(B, N, -1)          # [B, N, 256]
         n0 = add_layernorm(n0, None, None, self.ln1w, self.ln1b)
         n2 = fused_conv2d(n0.view(B, g, g, -1), self.neck2)            # NHWC [B, g, g, 256]
         n2 = add_layernorm(n2.view(B, N, -1), None, None, self.ln2w, self.ln2b)
-        o = F.linear(n2, self.out_w, self.out_b).float()               # [B, N, nout*ps*ps]
+        o = lin(n2.view(B * N, -1), self.out_w, self.out_b).float()    # [B * N, nout*ps*ps]
         # conv_transpose2d with the identity W2 == pixel shuffle
         o = o.view(B, g, g, self.nout, ps, ps).permute(0, 3, 1, 4, 2, 5).reshape(B, self.nout, g * ps, g * ps)
         return o
+
+    @torch.no_grad()
+    def graphed(self, x: torch.Tensor) -> torch.Tensor:
+        """:meth:`__call__` replayed from a HIP graph captured once per tile count (static input
+        buffer; the output is a fresh copy).  Falls back to the eager forward off-GPU."""
+        if not (x.is_cuda and self.device.type == "cuda"):
+            return self(x)
+        B = x.shape[0]
+        graphs = self.__dict__.setdefault("_graphs", {})
+        ent = graphs.get(B)
+        if ent is None:
+            xs = torch.empty((B,) + tuple(x.shape[1:]), device=self.device, dtype=torch.bfloat16)
+            xs.copy_(x)
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                self(xs)  # lazy state (kernel attributes, workspaces) outside the capture
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+                out = self(xs)
+            ent = graphs[B] = (gr, xs, out)
+        gr, xs, out = ent
+        xs.copy_(x)
+        gr.replay()
+        return out.clone()
+

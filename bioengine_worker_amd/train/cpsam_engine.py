@@ -51,6 +51,8 @@ import os as _os
 _GEMM = _os.environ.get("BE_CPSAM_GEMM", "lib")
 if _GEMM == "lib":
     from ..ops import gemm
+elif _GEMM == "mt":
+    from ..ops import gemm_mt as gemm
 elif _GEMM == "hip":
     from ..ops import gemm_bf16 as gemm
 else:

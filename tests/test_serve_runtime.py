@@ -266,3 +266,38 @@ def test_process_replica_bulk_data_through_shm_rings(monkeypatch):
         await serve.delete("vol")
 
     asyncio.run(main())
+
+
+@serve.deployment(ray_actor_options={"num_cpus": 0, "num_gpus": 1}, num_replicas=4, max_ongoing_requests=64)
+class GpuEcho:
+    def __init__(self):
+        self.dev = os.environ.get("HIP_VISIBLE_DEVICES", "?")
+        self.pid = os.getpid()
+
+    async def work(self, i):
+        await asyncio.sleep(0.01)
+        return self.dev, self.pid
+
+
+@pytest.mark.unit
+def test_router_fans_requests_over_gpu_pinned_process_replicas(monkeypatch):
+    """Node-level serving: one process replica per GPU, each pinned with
+    HIP_VISIBLE_DEVICES, and the router spreading concurrent requests over all of them (the
+    reference's replica scaling, bioengine/apps/proxy_deployment.py:35-44)."""
+    monkeypatch.setenv("BIOENGINE_REPLICA_MODE", "process")
+    monkeypatch.setenv("BIOENGINE_GPU_IDS", "0,1,2,3")
+
+    async def main():
+        h = await serve.run(GpuEcho.bind(), name="fan")
+        res = await asyncio.gather(*[h.work.remote(i) for i in range(256)])
+        await serve.delete("fan")
+        return res
+
+    res = asyncio.run(main())
+    devs = {}
+    for d, pid in res:
+        devs.setdefault(d, set()).add(pid)
+    assert sorted(devs) == ["0", "1", "2", "3"], devs
+    assert all(len(p) == 1 for p in devs.values())  # one process per GPU
+    counts = {d: sum(1 for r in res if r[0] == d) for d in devs}
+    assert min(counts.values()) >= 256 // 4 // 3, counts  # every replica carries load

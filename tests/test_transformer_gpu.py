@@ -100,3 +100,27 @@ def test_cpsam_engine_matches_fp32(gpu):
     out = CPSAMEngine(net, gpu)(x)
     rel = ((out - ref).norm() / ref.norm()).item()
     assert rel < 0.05, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gemm", ["mt", "lib"])
+def test_cpsam_engine_vit_l_matches_fp32(gpu, gemm, monkeypatch):
+    """The inference engine at the reference's ViT-L/8 shapes (dim 1024, 24 blocks, 16 heads, 1024
+    tokens) against the fp32 CPSAM.forward, eager and replayed from its HIP graph; every linear layer
+    on the in-house GEMM (default) or the library (A/B)."""
+    from bioengine_worker_amd.models.cpsam import CPSAM, CPSAMEngine
+
+    monkeypatch.setattr(CPSAMEngine, "GEMM", gemm)
+    net = CPSAM().randomize_(0).eval().to(gpu)
+    x = torch.randn(2, 3, 256, 256, device=gpu)
+    with torch.no_grad():
+        ref, _ = net(x)
+    eng = CPSAMEngine(net, gpu)
+    out = eng(x)
+    rel = ((out - ref).norm() / ref.norm()).item()
+    assert rel < 0.05, rel
+    g1 = eng.graphed(x)
+    g2 = eng.graphed(x * 0.5)  # replay with new input in the static buffer
+    assert torch.equal(g1, out)
+    rel2 = ((g2 - eng(x * 0.5)).norm() / g2.norm()).item()
+    assert rel2 == 0.0, rel2

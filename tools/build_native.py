@@ -56,7 +56,9 @@ HIP_FLAGS = [
 # default contraction fuses them into FMAs even under `#pragma clang fp contract(off)`.
 # attention: MFMA accumulators in arch VGPRs (the default AGPR form moved every S / O tile through
 # v_accvgpr_read/write around the softmax: 192 moves per KV tile); forward 0.085 -> 0.076 ms at B=8.
-PER_SOURCE_FLAGS = {"clahe": ["-ffp-contract=off"], "attention": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# gemm_mt: same, and without it hipcc shuffles the accumulators through a scratch AGPR quad every MFMA.
+PER_SOURCE_FLAGS = {"clahe": ["-ffp-contract=off"], "attention": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+                    "gemm_mt": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread", "-I", str(CSRC / "runtime")]
 
 

@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 5 step 2: gemm_mt numerics (GPU tests) then the per-shape sweep against the library GEMM
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r05/s2
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gemm_mt.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/tests.log; tail -15 $O/tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u tools/gemm_mt_bench.py --table > $O/sweep.jsonl 2>&1
+rc=$?; echo "sweep rc=$rc" >> $O/sweep.jsonl; grep -v '"mt"' $O/sweep.jsonl | tail -30
+exit $rc
