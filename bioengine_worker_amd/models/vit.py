@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.fp8 import Fp8Linear, add_layernorm_fp8, quantize_rows
+from ..ops.fp8 import Fp8Linear, add_layernorm_fp8, add_layernorm_mx, quantize_rows
 from ..ops.transformer import add_layernorm, attention_ref, bias_gelu_, flash_attention, flash_attention_mx
 
 
@@ -192,7 +192,7 @@ class ViTEngine:
             # fastest (BE_VIT_QKV_GEMM; hipBLASLt by default: 43.0 vs 60.9 us at batch 64,
             # profiles/r03/fp8/fp8_bench_s23.jsonl); proj / fc1 / fc2 keep the HIP kernel for the
             # MX-fp8 hand-offs its epilogues fuse
-            qkv_gemm = os.environ.get("BE_VIT_QKV_GEMM", "hipblaslt" if fp8_gemm == "hip" else fp8_gemm)
+            qkv_gemm = os.environ.get("BE_VIT_QKV_GEMM", fp8_gemm)
             for b in self.blocks:
                 for name in ("qkv", "proj", "fc1", "fc2"):
                     b[name + "_q"] = Fp8Linear(b.pop(name + "_w"), b.pop(name + "_b"),
@@ -244,7 +244,10 @@ class ViTEngine:
         run as one pass between the two library GEMMs."""
         cfg, blocks = self.cfg, self.blocks
         D, Hh = cfg.embed_dim, cfg.num_heads
-        hq = add_layernorm_fp8(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"], cfg.eps)
+        # qkv on the block-scaled HIP GEMM reads MX-fp8 (E8M0 per 32 channels) straight from the LayerNorm;
+        # on hipBLASLt it reads per-token-scaled e4m3
+        ln_q = add_layernorm_mx if blocks[0]["qkv_q"].gemm == "hip" else add_layernorm_fp8
+        hq = ln_q(t, None, None, blocks[0]["n1w"], blocks[0]["n1b"], cfg.eps)
         for i, b in enumerate(blocks):
             qkv = b["qkv_q"](hq).view(B, N, 3, Hh, D // Hh)
             if b["proj_q"].gemm == "hip":  # attention epilogue -> MX-fp8 -> proj's MFMA scale operand
@@ -259,7 +262,7 @@ class ViTEngine:
             else:
                 m = b["fc2_q"](quantize_rows(b["fc1_q"](h2q), gelu=True))
             if i + 1 < len(blocks):
-                hq = add_layernorm_fp8(t, m, b["g2"], blocks[i + 1]["n1w"], blocks[i + 1]["n1b"], cfg.eps)
+                hq = ln_q(t, m, b["g2"], blocks[i + 1]["n1w"], blocks[i + 1]["n1b"], cfg.eps)
         return add_layernorm(t, m, blocks[-1]["g2"], self.nw, self.nb, cfg.eps)
 
     @torch.no_grad()

@@ -187,6 +187,29 @@ def add_layernorm_fp8(x: torch.Tensor, y: torch.Tensor | None, gamma: torch.Tens
     return q, s
 
 
+def add_layernorm_mx(x: torch.Tensor, y: torch.Tensor | None, gamma: torch.Tensor | None, w: torch.Tensor,
+                     b: torch.Tensor, eps: float = 1e-6) -> tuple[torch.Tensor, torch.Tensor]:
+    """``x <- x + gamma * y`` (in place) and returns ``mx_quantize(LN(x) * w + b)``: e4m3fn values and
+    one E8M0 scale per 32 channels -- the block-scaled GEMM's A operand (``linear_fp8_mx``)."""
+    if not x.is_cuda:
+        from .transformer import add_layernorm
+
+        return mx_quantize_ref(add_layernorm(x, y, gamma, w, b, eps).float())
+    C = x.shape[-1]
+    rows = x.numel() // C
+    assert x.dtype == torch.bfloat16 and x.is_contiguous() and C % MX_BLOCK == 0
+    if y is not None:
+        assert y.shape == x.shape and y.dtype == torch.bfloat16
+        y = y.contiguous()
+    q = torch.empty(x.shape, dtype=FP8_DTYPE, device=x.device)
+    s = torch.empty(*x.shape[:-1], C // MX_BLOCK, dtype=torch.uint8, device=x.device)
+    g = gamma.float().contiguous() if gamma is not None else None
+    _native.call("be_add_layernorm_mx", _native.ptr(x), _native.ptr(y), _native.ptr(g),
+                 _native.ptr(w.float().contiguous()), _native.ptr(b.float().contiguous()), _native.ptr(q),
+                 _native.ptr(s), rows, C, float(eps), 1, _native.stream(x.device))
+    return q, s
+
+
 def linear_fp8_hipblaslt(xq: torch.Tensor, sx: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor,
                          bias: torch.Tensor | None = None) -> torch.Tensor:
     """The same row-wise-scaled fp8 GEMM as :func:`linear_fp8` (no GELU) through hipBLASLt

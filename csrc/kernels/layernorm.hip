@@ -35,7 +35,20 @@ __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d
   return (uint32_t)w;
 }
 
-template <int NV, bool Q8 = false>
+// MX: the normalised row as MX-fp8 -- e4m3fn q8 with one E8M0 power-of-two scale per 32 consecutive
+// channels (uint8 [rows][C / 32], byte = e + 127, the smallest e with amax / 2^e <= 448): the A-operand
+// format of the block-scaled GEMM (gemm_fp8.hip be_gemm_fp8_mx), so qkv / fc1 get MX activations
+// straight from the LayerNorm.  A 32-channel block is 4 consecutive lanes' 8-channel vectors.
+__device__ __forceinline__ int e8m0_exp(float amax) {
+  if (!(amax > 0.f)) return -127;
+  const float r = amax * (1.f / 448.f);
+  const int bits = __float_as_int(r);
+  int e = ((bits >> 23) & 0xff) - 127 + ((bits & 0x7fffff) ? 1 : 0);  // ceil(log2 r), normal r
+  if (amax * __builtin_ldexpf(1.f, -e) > 448.f) ++e;
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
+template <int NV, bool Q8 = false, bool MX = false>
 __global__ __launch_bounds__(256) void add_ln_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
                                                      const float* __restrict__ gamma, const float* __restrict__ w,
                                                      const float* __restrict__ bias, bf16_t* __restrict__ out,
@@ -116,6 +129,27 @@ __global__ __launch_bounds__(256) void add_ln_kernel(bf16_t* __restrict__ x, con
       }
     }
   }
+  if (Q8 && MX) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      float bm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bm = fmaxf(bm, fabsf(v[k][j]));
+      bm = fmaxf(bm, __shfl_xor(bm, 1, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 2, 64));
+      if (c < C) {
+        const int e = e8m0_exp(bm);
+        const float inv = __builtin_ldexpf(1.f, -e);
+        u32x2 o;
+        o[0] = pack4_fp8(v[k][0] * inv, v[k][1] * inv, v[k][2] * inv, v[k][3] * inv);
+        o[1] = pack4_fp8(v[k][4] * inv, v[k][5] * inv, v[k][6] * inv, v[k][7] * inv);
+        *reinterpret_cast<u32x2*>(q8 + row * C + c) = o;
+        if ((lane & 3) == 0) reinterpret_cast<uint8_t*>(qscale)[row * (C / 32) + c / 32] = (uint8_t)(e + 127);
+      }
+    }
+    return;
+  }
   if (Q8) {
     amax = fmaxf(wave_max(amax), 1e-12f);
     const float inv = 448.f / amax;
@@ -195,6 +229,27 @@ int be_add_layernorm_fp8(void* x, const void* y, const float* gamma, const float
     default: return -1;
   }
 #undef LNQ
+  return BE_CHECK_LAUNCH();
+}
+
+// As be_add_layernorm_fp8, with MX-fp8 output: q8 e4m3fn [rows, C] + E8M0 block scales (uint8
+// [rows, C / 32]) in qscale.  C % 32 == 0.
+int be_add_layernorm_mx(void* x, const void* y, const float* gamma, const float* w, const float* b, void* q8,
+                        void* qscale, long long rows, int C, float eps, int write_x, hipStream_t s) {
+  if (C % 32 != 0 || C > 64 * 8 * MAXV || !w || !b || !q8 || !qscale) return -1;
+  const int nv = (C / 8 + 63) / 64;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+#define LNM(NV)                                                                                                \
+  case NV:                                                                                                     \
+    hipLaunchKernelGGL((add_ln_kernel<NV, true, true>), grid, dim3(256), 0, s, (bf16_t*)x, (const bf16_t*)y,  \
+                       gamma, w, b, (bf16_t*)nullptr, (float*)nullptr, rows, C, eps, write_x, (uint8_t*)q8,    \
+                       (float*)qscale);                                                                        \
+    break;
+  switch (nv) {
+    LNM(1) LNM(2) LNM(3) LNM(4)
+    default: return -1;
+  }
+#undef LNM
   return BE_CHECK_LAUNCH();
 }
 

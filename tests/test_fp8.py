@@ -216,3 +216,27 @@ def test_attention_mx_fp8_output_matches_reference(gpu, B, N, H):
     deq = mx_dequant_ref(oq.reshape(B * N, H * 64), os_).cpu()
     step = torch.exp2(os_.cpu().float() - 127.0).repeat_interleave(32, dim=1) * 32  # e4m3 step at the block max
     assert ((deq - ref.cpu()).abs() <= step).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [768, 1024])
+def test_add_layernorm_mx_matches_reference(gpu, C):
+    """LayerNorm -> MX-fp8 (E8M0 per 32 channels): the scale bytes equal mx_quantize_ref's on the fp32
+    LN output, and the dequantised values are within e4m3 rounding of it."""
+    from bioengine_worker_amd.ops.fp8 import add_layernorm_mx, mx_dequant_ref, mx_quantize_ref
+
+    g = torch.Generator().manual_seed(C + 1)
+    x = torch.randn(300, C, generator=g).bfloat16()
+    y = torch.randn(300, C, generator=g).bfloat16()
+    gamma, w, b = (torch.randn(C, generator=g) for _ in range(3))
+    xn_ref, out_ref = add_layernorm_ref(x, y, gamma, w, b, 1e-6)
+    xg = x.to(gpu)
+    q, s = add_layernorm_mx(xg, y.to(gpu), gamma.to(gpu), w.to(gpu), b.to(gpu), 1e-6)
+    torch.testing.assert_close(xg.cpu(), xn_ref)
+    _, s_ref = mx_quantize_ref(out_ref.float())
+    # the reference normalises in bf16 before quantising; allow a one-step exponent difference at ties
+    assert (s.cpu().int() - s_ref.int()).abs().max() <= 1
+    deq = mx_dequant_ref(q.cpu(), s.cpu())
+    blk = out_ref.float().reshape(300, C // 32, 32).abs().amax(-1, keepdim=True).clamp_min(1e-6)
+    err = ((deq - out_ref.float()).reshape(300, C // 32, 32).abs() / blk).max()
+    assert err < 2 ** -3, err

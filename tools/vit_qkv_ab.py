@@ -1,43 +1,44 @@
 #!/usr/bin/env python3
-"""DINOv2 ViT-B/14 fp8 embedding throughput (batch 64, 224^2) with qkv on hipBLASLt vs the HIP fp8
-GEMM (BE_VIT_QKV_GEMM), same process, alternating to cancel clock drift.  One JSON line per arm."""
+"""A/B of the ViT-B/14 fp8 embedder's qkv GEMM (DINOv2, batch 64, 224^2): the HIP block-scaled MX-fp8
+GEMM fed by the LayerNorm's MX output vs hipBLASLt row-scaled fp8.  Interleaved rounds, one process."""
 import json
 import os
+import statistics
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch  # noqa: E402
+
+import torch
+
+from bioengine_worker_amd.models.vit import ViT, ViTConfig, ViTEngine
 
 
-def main():
-    from bioengine_worker_amd.search.ingestion import default_engine_factory
-
+def main(rounds=5, steps=20, batch=64):
     dev = torch.device("cuda", 0)
-    x = torch.randn(64, 3, 224, 224, device=dev)
+    net = ViT(ViTConfig.dinov2("vitb14")).randomize_(0).eval()
     engs = {}
-    for arm in ("hipblaslt", "hip"):
-        os.environ["BE_VIT_QKV_GEMM"] = arm
-        engs[arm] = default_engine_factory(dev, "vitb14")
-        for _ in range(5):
-            engs[arm].embed(x)
-    torch.cuda.synchronize()
-    res = {a: [] for a in engs}
-    for _ in range(5):
-        for arm, eng in engs.items():
+    for q in ("hip", "hipblaslt"):
+        os.environ["BE_VIT_QKV_GEMM"] = q
+        engs[q] = ViTEngine(net, dev, precision="fp8", fp8_gemm="hip")
+    ref = ViTEngine(net, dev)
+    x = torch.randn(batch, 3, 224, 224, device=dev)
+    r = ref.embed(x)
+    cos = {q: float(torch.nn.functional.cosine_similarity(e.embed(x), r, dim=1).min()) for q, e in engs.items()}
+    t = {q: [] for q in engs}
+    for _ in range(rounds):
+        for q, e in engs.items():
+            for _ in range(3):
+                e.embed(x)
             torch.cuda.synchronize()
-            t = time.perf_counter()
-            for _ in range(20):
-                eng.embed(x)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                e.embed(x)
             torch.cuda.synchronize()
-            res[arm].append((time.perf_counter() - t) / 20)
-    ref = engs["hip"].embed(x[:8])
-    for arm, ts in res.items():
-        ts.sort()
-        cos = torch.nn.functional.cosine_similarity(engs[arm].embed(x[:8]), ref, dim=1).min().item()
-        print(json.dumps({"qkv_gemm": arm, "ms_per_batch64": round(ts[len(ts) // 2] * 1e3, 3),
-                          "imgs_per_s": round(64 / ts[len(ts) // 2], 1), "cos_min_vs_hip_qkv": round(cos, 5)}),
-              flush=True)
+            t[q].append(batch * steps / (time.perf_counter() - t0))
+    for q in engs:
+        print(json.dumps({"qkv_gemm": q, "imgs_per_s_median": round(statistics.median(t[q]), 1),
+                          "imgs_per_s": [round(v, 1) for v in t[q]], "cos_min_vs_bf16": round(cos[q], 5)}), flush=True)
 
 
 if __name__ == "__main__":
