@@ -398,6 +398,67 @@ def bench_em_volume(args, world, rank, dev) -> dict:
         shutil.rmtree(work, ignore_errors=True)
 
 
+def bench_em_volume3d(args, world, rank, dev) -> dict:
+    """BASELINE config 4 as real 3-D tiled inference: each rank's z-slab through a
+    BioImage.IO 3-D U-Net (16-32-64-128, Conv3d 3x3x3 + BN + ReLU on the one-launch implicit-GEMM
+    kernel after the graph pass), 128 x 128 x 32 tiles with 16 / 8 voxels of overlap blended by the
+    separable Gaussian window (be_blend_gather), then the same sharded post-processing and rank-0
+    gather as the 2-D line.  Slab size per rank from --em3d-z / --em3d-yx (the 2048^3 volume at N = 8
+    is --em3d-z 256 --em3d-yx 2048: same code, longer run)."""
+    import shutil
+    import tempfile
+
+    import numpy as np
+
+    from bioengine_worker_amd.bioimageio.package import write_unet3d_package
+    from bioengine_worker_amd.bioimageio.runner import PredictionPipeline
+    from bioengine_worker_amd.em.volume import VolumeSource, analyze_volume, gather_to_rank0
+    from tools.em_volume_bench import synthetic_slab
+
+    Z, YX = args.em3d_z, args.em3d_yx
+    work = Path(tempfile.mkdtemp(prefix=f"be-em3d-bench-{rank}-", dir=os.environ.get("TMPDIR")))
+    try:
+        root = work / "mito-unet3d"
+        write_unet3d_package(root, "mito-unet3d", in_channels=1, out_channels=1, features=(16, 32, 64, 128),
+                             test_shape=(1, 1, 16, 32, 32))
+        pipe = PredictionPipeline(root, device=dev)
+        predict3d = lambda t: next(iter(pipe.predict_tensors(t).values()))  # noqa: E731
+        z0 = rank * Z
+        npy = work / "slab.npy"
+        np.save(npy, synthetic_slab(z0, z0 + Z, YX, YX, dev).cpu().numpy())
+        src = VolumeSource(str(npy))
+        warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
+        kw = dict(tile=128, overlap=16, batch=4, tile_z=32, overlap_z=8, split_touching=True)
+        warm = torch.from_numpy(src.read(0, min(Z, 40))).to(dev)[:, :256, :256].contiguous()
+        analyze_volume(warm, None, predict3d=predict3d, norm_range=(90.0, 210.0), **kw)
+        del warm
+        _barrier(world)
+        t0 = time.perf_counter()
+        slab = torch.from_numpy(src.read(0, Z)).to(dev)
+        t_read = time.perf_counter()
+        res = analyze_volume(slab, None, predict3d=predict3d, group=None, z_offset=z0, timings=True, **kw)
+        tg = time.perf_counter()
+        full = gather_to_rank0(res["labels_slab_t"])
+        torch.cuda.synchronize(dev)
+        t_gather = time.perf_counter() - tg
+        _barrier(world)
+        dt = _max_over_ranks(time.perf_counter() - t0, world)
+        timings = dict(res["timings_s"])
+        timings["read_h2d"] = round(t_read - t0, 4)
+        timings["gather_rank0"] = round(t_gather, 4)
+        out = {"em_volume3d_voxels_per_sec": round(Z * world * YX * YX / dt, 1),
+               "em_volume3d_config": {"volume": [Z * world, YX, YX], "slab_per_gpu": [Z, YX, YX],
+                                      "tile": [32, 128, 128], "overlap": [8, 16, 16], "tiles_per_call": 4,
+                                      "model": "BioImage.IO 3-D U-Net 16-32-64-128 (random init, graph pass, "
+                                               "implicit-GEMM 3x3x3 conv)",
+                                      "split_touching": True, "gather": "rank0", "seconds": round(dt, 3),
+                                      "n_instances": res["n_instances"], "stage_timings_s_rank0": timings}}
+        del slab, full, res
+        return out
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def bench_model_runner_cpu(reps: int = 10) -> dict:
     """BASELINE config 1 (model-runner plumbing on CPU): one BioImage.IO 2-D U-Net package, a single
     256x256 tile through the runtime's prediction pipeline on the CPU (pre-processing, padding,
@@ -575,6 +636,8 @@ def main():
     ap.add_argument("--em-yx", type=int, default=2048)
     ap.add_argument("--em-tile-batch", type=int, default=32, help="512^2 tiles per U-Net call (EM volume line)")
     ap.add_argument("--no-em", action="store_true", help="skip the EM volume line")
+    ap.add_argument("--em3d-z", type=int, default=32, help="z-slices per GPU of the 3-D U-Net EM line")
+    ap.add_argument("--em3d-yx", type=int, default=512)
     ap.add_argument("--trace", default=None, metavar="PATH",
                     help="after the timed steps, run one more traced step and write a Chrome trace (rank 0)")
     args = ap.parse_args()
@@ -666,6 +729,10 @@ def main():
                 out.update(bench_em_volume(args, world, rank, dev))
             except Exception as e:  # noqa: BLE001
                 out["extras_error_em"] = f"{type(e).__name__}: {e}"
+            try:
+                out.update(bench_em_volume3d(args, world, rank, dev))
+            except Exception as e:  # noqa: BLE001
+                out["extras_error_em3d"] = f"{type(e).__name__}: {e}"
         if rank == 0:
             try:
                 out.update(bench_model_runner_cpu())

@@ -1,4 +1,12 @@
-"""3-D convolution (1x1x1 / 3x3x3, stride 1, "same" zero padding) on the fused NHWC MFMA conv kernel.
+"""3-D convolution (1x1x1 / 3x3x3, stride 1, "same" zero padding) on the framework's MFMA kernels.
+
+3x3x3 convs run as ONE implicit-GEMM launch over the whole batch (``be_conv3d_mt`` in
+``csrc/kernels/gemm_mt.hip``): M = N*D*H*W output voxels, N = Cout, K = 27 taps x Cin (tap-major),
+each DMA lane fetching its voxel's tap-shifted 8-channel chunk (the zero page at the volume faces),
+fp32 accumulation across all 27 taps and one bf16 rounding of the output, bias + ReLU in the
+epilogue.  The older depth-tap decomposition below (``BE_CONV3D=taps``) is kept as the A/B path.
+
+Depth-tap decomposition (A/B path):
 
 BioImage.IO 3-D U-Nets (PlantSeg / 3D-UNet family; the model runner's 3-D path, SURVEY.md §2.5 K16,
 and the fibsem volume workloads) are stacks of Conv3d(k=3) + BN + ReLU.  On MI355X they run on
@@ -22,6 +30,9 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+import os
+
+from . import _native
 from .conv import PackedConv, fused_conv2d
 
 
@@ -38,10 +49,19 @@ class PackedConv3d:
         self.taps = [PackedConv.from_weight(self.w[:, :, dz], self.bias if dz == kd // 2 else None,
                                             cout_pad_to=cout_pad_to) for dz in range(kd)]
         self.cin_pad = self.taps[0].cin_pad
+        if kd == 3:
+            # implicit-GEMM weights [Cout][kpad], k = (9 dz + 3 dy + dx) * cin_pad + c, zero-padded to 64
+            w = self.w.permute(0, 2, 3, 4, 1)  # [Cout, 3, 3, 3, Cin]
+            w = F.pad(w, (0, self.cin_pad - cin)).reshape(cout, 27 * self.cin_pad)
+            self.kpad = (27 * self.cin_pad + 63) // 64 * 64
+            self.w_mt = F.pad(w, (0, self.kpad - 27 * self.cin_pad)).to(torch.bfloat16).contiguous()
+            self.b_mt = (self.bias if self.bias is not None else torch.zeros(cout)).float().contiguous()
 
     def to(self, device) -> "PackedConv3d":
         for t in self.taps:
             t.to(device)
+        if self.ks == 3:
+            self.w_mt, self.b_mt = self.w_mt.to(device), self.b_mt.to(device)
         self.w = self.w.to(device)
         if self.bias is not None:
             self.bias = self.bias.to(device)
@@ -71,6 +91,12 @@ def fused_conv3d(x: torch.Tensor, pc: PackedConv3d, post_relu: bool = False) -> 
     if pc.ks == 1:
         y = fused_conv2d(x.view(N * D, H, W, C), pc.taps[0], post_relu=post_relu)
         return y.view(N, D, H, W, pc.cout)
+    if os.environ.get("BE_CONV3D", "igemm") != "taps" and pc.cout % 4 == 0:
+        out = torch.empty(N, D, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
+        cfg = 5 if pc.cout <= 32 else (6 if pc.cout <= 64 else 4)
+        _native.call("be_conv3d_mt", _native.ptr(x), _native.ptr(pc.w_mt), _native.ptr(pc.b_mt), _native.ptr(out),
+                     N, D, H, W, C, pc.cout, pc.kpad, int(post_relu), cfg, _native.stream(x.device))
+        return out
     out = torch.empty(N, D, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
     below, centre, above = pc.taps
     for n in range(N):

@@ -84,7 +84,7 @@ __device__ __forceinline__ bf16x8 frag_t(const unsigned char* t, int c0, int lan
   return v;
 }
 
-enum { E_NONE = 0, E_BIAS = 1, E_BIAS_GELU = 2, E_DGELU = 4, E_F32 = 5, E_BIAS_RES = 6 };
+enum { E_NONE = 0, E_BIAS = 1, E_BIAS_GELU = 2, E_DGELU = 4, E_F32 = 5, E_BIAS_RES = 6, E_CONV = 7 };
 
 struct MArgs {
   const bf16_t* A;      // TA 0: [M][lda] (K-contiguous); TA 1: [K][lda] (M-contiguous)
@@ -101,6 +101,10 @@ struct MArgs {
   int bias_bf16;
   int M, N, K, lda, ldb, ldc;
   int tiles_n, nkt, split;
+  // TA 2 (implicit 3x3x3 conv): A = x NDHWC [M voxels][cin], K = 27 taps x cin (tap-major, padded to
+  // 64 with the zero page), zero padding at the volume faces
+  const bf16_t* zero;
+  int D, H, W, cin, relu;
 };
 
 template <int WM, int WN, int FM, int FN, int NST, int EPI, int TA, int TB>
@@ -127,6 +131,21 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
   // K-contiguous operand: wave-instruction i covers rows (4 i + wave) * 8 + lane / 8, 128 B each
   const int lr = lane >> 3;
   const int swzc = (lane & 7) ^ ((wave * 4 + (lr >> 1)) & 7);  // logical chunk this lane fetches
+  // TA 2: this thread's DMA rows as output voxels (index, z, y, x), decoded once; z = -1: past M
+  int vox[TA == 2 ? GA : 1], vz[TA == 2 ? GA : 1], vy[TA == 2 ? GA : 1], vx[TA == 2 ? GA : 1];
+  if constexpr (TA == 2) {
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int r = m0 + (i * NW + wave) * 8 + lr;
+      const int rr = r < a.M ? r : a.M - 1;
+      int q = rr / a.W;
+      vx[i] = rr - q * a.W;
+      const int q2 = q / a.H;
+      vy[i] = q - q2 * a.H;
+      vz[i] = r < a.M ? q2 - (q2 / a.D) * a.D : -1;
+      vox[i] = rr;
+    }
+  }
   auto stage = [&](int t) {
     unsigned char* st = smem + (t % NST) * STB;
     // past the slice's end the DMA re-reads its last tile into a stage nothing reads any more: every
@@ -139,6 +158,19 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
         r = r < a.M ? r : a.M - 1;
         __builtin_amdgcn_global_load_lds((const void*)(a.A + (long long)r * a.lda + k0 + swzc * 8),
                                          (lds_void*)(st + (i * NW + wave) * 1024), 16, 0, 0);
+      }
+    } else if constexpr (TA == 2) {
+      // this lane's 8-channel chunk of K: one tap (cin % 8 == 0), a whole-voxel shift of the row
+      const int kg = k0 + swzc * 8;
+      const int tap = kg / a.cin, ch = kg - tap * a.cin;
+      const int dz = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dx = tap % 3 - 1;
+      const int off = (dz * a.H + dy) * a.W + dx;
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const bool ok = tap < 27 && vz[i] >= 0 && (unsigned)(vz[i] + dz) < (unsigned)a.D &&
+                        (unsigned)(vy[i] + dy) < (unsigned)a.H && (unsigned)(vx[i] + dx) < (unsigned)a.W;
+        const bf16_t* src = ok ? a.A + (long long)(vox[i] + off) * a.cin + ch : a.zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(st + (i * NW + wave) * 1024), 16, 0, 0);
       }
     } else {
       constexpr int CPR = BM / 8, RPI = 64 / CPR;
@@ -184,7 +216,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
     const unsigned char* st = smem + (t % NST) * STB;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      if constexpr (TA == 0) {
+      if constexpr (TA != 1) {
         const int r = wr * 16 * FM + i * 16 + frow;
         fa[i] = *reinterpret_cast<const bf16x8*>(st + r * 128 + (((ks * 4 + fch) ^ fsw) << 4));
       } else {
@@ -338,7 +370,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
     const int n = n0 + wc * 16 * FN + j * 16 + nq;
     const bool nok = n < a.N;  // N % 4 == 0 (host-checked)
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == E_BIAS || EPI == E_BIAS_GELU || EPI == E_BIAS_RES) {
+    if constexpr (EPI == E_BIAS || EPI == E_BIAS_GELU || EPI == E_BIAS_RES || EPI == E_CONV) {
       if (nok && a.bias) {
         if (a.bias_bf16) {
           const u32x2 w = *reinterpret_cast<const u32x2*>((const bf16_t*)a.bias + n);
@@ -372,6 +404,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
       u32x2 st;
       st[0] = pack2bf(v[0], v[1]);
       st[1] = pack2bf(v[2], v[3]);
+      if constexpr (EPI == E_CONV) {
+        if (a.relu) {
+          st[0] = relu_bf16x2(st[0]);
+          st[1] = relu_bf16x2(st[1]);
+        }
+      }
       if (EPI != E_BIAS_GELU || a.C) *reinterpret_cast<u32x2*>(a.C + o) = st;  // inference: gelu only
       if constexpr (EPI == E_BIAS_GELU) {
         u32x2 gt;
@@ -439,6 +477,27 @@ int launch_cfg(MArgs a, int cfg, hipStream_t s) {
   return -32;
 }
 
+// implicit 3x3x3 conv tiles (narrow Cout): 5 = 256 x 32, 6 = 256 x 64 (4 waves of 64 x 32 / 64 x 64),
+// 4 = 128 x 128, 2 = 256 x 128
+int launch_conv(MArgs a, int cfg, hipStream_t s) {
+  switch (cfg) {
+    case 5: return launch_mt<4, 1, 4, 2, 4, E_CONV, 2, 0>(a, s);
+    case 6: return launch_mt<4, 1, 4, 4, 3, E_CONV, 2, 0>(a, s);
+    case 4: return launch_mt<2, 2, 4, 4, 4, E_CONV, 2, 0>(a, s);
+    case 2: return launch_mt<2, 2, 8, 4, 3, E_CONV, 2, 0>(a, s);
+  }
+  return -32;
+}
+
+const bf16_t* conv_zero_page() {
+  static bf16_t* z = nullptr;
+  if (!z) {
+    if (hipMalloc((void**)&z, 4096) != hipSuccess) return nullptr;
+    if (hipMemset(z, 0, 4096) != hipSuccess) return nullptr;
+  }
+  return z;
+}
+
 }  // namespace
 
 extern "C" {
@@ -483,6 +542,24 @@ int be_gemm_mt(const void* A, const void* B, void* C, void* C2, const void* bias
   }
   return -42;
 #endif
+}
+
+// 3x3x3 / stride 1 / zero-pad 1 conv of x NDHWC bf16 [N][D][H][W][cin] (cin % 8 == 0) with w bf16
+// [cout][kpad] (k = tap * cin + c, tap = 9 dz + 3 dy + dx, zero past 27 cin; kpad % 64 == 0):
+// out NDHWC [N][D][H][W][cout] = relu?(conv + bias[cout] (fp32)).  One launch over the whole batch,
+// fp32 accumulation across all 27 taps.  cfg: 5 / 6 / 4 / 2 (launch_conv).
+int be_conv3d_mt(const void* x, const void* w, const float* bias, void* out, int N, int D, int H, int W, int cin,
+                 int cout, int kpad, int relu, int cfg, hipStream_t s) {
+  if (cin % 8 || cout % 4 || kpad % BK || kpad < 27 * cin || kpad - 27 * cin >= BK) return -10;
+  const long long M = (long long)N * D * H * W;
+  if (M >= (1LL << 31) || M * cin >= (1LL << 40)) return -11;
+  MArgs a = {};
+  a.A = (const bf16_t*)x; a.B = (const bf16_t*)w; a.C = (bf16_t*)out; a.bias = bias; a.bias_bf16 = 0;
+  a.M = (int)M; a.N = cout; a.K = kpad; a.lda = cin; a.ldb = kpad; a.ldc = cout; a.nkt = kpad / BK; a.split = 1;
+  a.zero = conv_zero_page();
+  if (!a.zero) return -13;
+  a.D = D; a.H = H; a.W = W; a.cin = cin; a.relu = relu;
+  return launch_conv(a, cfg, s);
 }
 
 }  // extern "C"

@@ -106,3 +106,24 @@ def test_unet3d_package_and_tiled_volume_gpu(gpu, pkg3d):
     assert whole.shape == tiled.shape == (1, 1, 40, 96, 80)
     # tiles see reflect-padded context instead of the neighbouring voxels: compare the interiors
     assert np.abs(whole - tiled)[:, :, 4:-4, 4:-4, 4:-4].mean() < 0.02
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,D,H,W,Cin,Cout", [(1, 8, 40, 72, 32, 64), (2, 5, 33, 20, 16, 32), (1, 7, 20, 36, 1, 16),
+                                             (1, 12, 24, 24, 64, 128), (2, 9, 17, 23, 48, 96)])
+def test_conv3d_igemm_single_rounding(gpu, N, D, H, W, Cin, Cout, monkeypatch):
+    """The implicit-GEMM 3x3x3 kernel (one launch, K = 27 x Cin, fp32 accumulation over all taps)
+    against fp32 F.conv3d of the same bf16 operands with ONE bf16 rounding of the output."""
+    monkeypatch.setenv("BE_CONV3D", "igemm")
+    g = torch.Generator().manual_seed(D * H + Cout)
+    x = torch.randn(N, D, H, W, Cin, generator=g).bfloat16()
+    w = torch.randn(Cout, Cin, 3, 3, 3, generator=g) / (Cin * 27) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    pc = PackedConv3d(w, b)
+    wb = w.bfloat16().float()
+    ref = torch.relu(F.conv3d(x.float().permute(0, 4, 1, 2, 3), wb, b, padding=1)).permute(0, 2, 3, 4, 1)
+    xp = F.pad(x, (0, pc.cin_pad - Cin)).contiguous().to(gpu)
+    y = fused_conv3d(xp, pc.to(gpu), post_relu=True).float().cpu()
+    err = (y - ref).abs()
+    # one bf16 rounding of the output (2^-8 relative) plus fp32 summation-order noise
+    assert (err <= ref.abs() * 2 ** -8 + 1e-4 * ref.abs().max()).all(), err.max()
