@@ -17,9 +17,9 @@
 //    back to back with the next k-step's fragment reads interleaved.
 //  * K is consumed in 64-deep tiles staged by global_load_lds (16 B per lane) into full 128-byte
 //    LDS rows: every DMA wave-instruction moves 8 whole 128-byte lines (the fragment-shaped 64-byte
-//    row loads of the older kernels cost TA time, §5 "Projection GEMM" item 3).  NST stages, the
-//    DMA of tile t + NST - 1 issued at the top of tile t, one counted vmcnt + raw s_barrier per
-//    tile, placed in the middle of the last k-step's MFMAs so the next tile's first fragment reads
+//    row loads of the older kernels cost TA time, §5 "Projection GEMM" item 3).  NST stages, one
+//    counted vmcnt + raw s_barrier per tile, placed in the middle of the last k-step's MFMAs: after
+//    it the tile's stage is refilled with tile t + NST and the next tile's first fragment reads
 //    issue under the remaining MFMAs.
 //  * K-contiguous operands: row r, 16-byte chunk c stored at chunk c ^ ((r >> 1) & 7): the 16
 //    lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, ...) hit 16 distinct bank slots.  The
@@ -245,10 +245,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
 
   bf16x8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
 
-  // ---- prologue: tiles 0 .. NST-2 in flight, tile 0 landed everywhere
+  // ---- prologue: tiles 0 .. NST-1 in flight, tile 0 landed everywhere
 #pragma unroll
-  for (int t = 0; t < NST - 1; ++t) stage(t);
-  wait_vm_c<G * (NST - 2)>();
+  for (int t = 0; t < NST; ++t) stage(t);
+  wait_vm_c<G * (NST - 1)>();
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -263,7 +263,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
     read_b(t, 1, fb1);
     read_a(t, 1, fa1);
     __builtin_amdgcn_sched_barrier(0);  // the k-step-1 reads issue ahead of the k-step-0 MFMAs
-    stage(t + NST - 1);
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -279,6 +278,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mt_kernel(MArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    // every wave's reads of tile t retired before the barrier: its stage takes tile t + NST now, a
+    // whole tile of MFMAs before that tile's wait (issued at the top of the tile it would leave only
+    // half of one)
+    stage(t + NST);
     read_b(t + 1, 0, fb0);
     read_a(t + 1, 0, fa0);
 #pragma unroll
