@@ -93,6 +93,7 @@ class CellposeRunner:
         self.cin_pad = (self.nchan + 7) // 8 * 8
         self._pinned: torch.Tensor | None = None  # host staging for numpy batches (pinned -> async DMA)
         self._plans: dict = {}
+        self._net_graphs: dict = {}
 
     # ---------------------------------------------------------------- network
     def _plan(self, H, W, p: EvalParams):
@@ -236,8 +237,57 @@ class CellposeRunner:
         np.copyto(t.numpy(), a)
         return t
 
+    #: batches up to this many images run normalize99 + tiling + network + blend from a HIP graph
+    #: (captured once per shape / params): a small batch is a few hundred microsecond-scale launches,
+    #: so the host launch path, not the GPU, would set its latency
+    GRAPH_NET_MAX_B = int(os.environ.get("BE_CELLPOSE_GRAPH_MAX_B", "8"))
+
+    def _net_graphed(self, x, p: EvalParams):
+        """(y, style) of the network stage (rescale 1) replayed from its HIP graph, or None when this
+        call should run eagerly (large batch, CPU, capture failed for this shape)."""
+        B = x.shape[0]
+        if self.device.type != "cuda" or B > self.GRAPH_NET_MAX_B or not x.is_cuda:
+            return None
+        key = (tuple(x.shape), x.dtype, bool(p.normalize), bool(p.tile), p.bsize, p.tile_overlap, p.max_tiles)
+        ent = self._net_graphs.get(key)
+        if ent is False:
+            return None
+        if ent is None:
+            xs = x.clone()
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+
+            def body():
+                xx = self._normalize(xs) if p.normalize else xs
+                return self.run_net(xx, p)
+
+            try:
+                with torch.cuda.stream(side):
+                    body()  # lazy state (plans, kernel attributes, workspaces) outside the capture
+                torch.cuda.current_stream(self.device).wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    y, style = body()
+            except Exception:  # noqa: BLE001 -- this shape runs eagerly
+                self._net_graphs[key] = False
+                return None
+            ent = self._net_graphs[key] = (g, xs, y, style)
+        g, xs, y, style = ent
+        xs.copy_(x)
+        g.replay()
+        return y.clone(), style.clone()
+
     def _eval_one(self, x, p: EvalParams):
         B, C, H, W = x.shape
+        if not (p.diameter is not None and p.diameter > 0 and abs(self.diam_mean / float(p.diameter) - 1.0) > 1e-3):
+            r = self._net_graphed(x, p)
+            if r is not None:
+                y, style = r
+                if not p.compute_masks:
+                    return None, y, style
+                with trace.span("cellpose.masks", cuda=True, images=B):
+                    masks = self.compute_masks(y, p, 1.0)
+                return masks, y, style
         if p.normalize:
             with trace.span("cellpose.normalize99", cuda=True, images=B):
                 x = self._normalize(x)

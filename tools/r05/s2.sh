@@ -11,7 +11,7 @@ rc=$?; echo "pytest rc=$rc" >> $O/tests.log; tail -15 $O/tests.log
 timeout -k 10 420 python -u tools/gemm_mt_bench.py --table --rounds 5 > $O/sweep.jsonl 2>&1
 rc=$?; echo "sweep rc=$rc" >> $O/sweep.jsonl; grep -v '"mt"' $O/sweep.jsonl | tail -30
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u -m pytest tests/test_fp8.py tests/test_transformer_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/tests2.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_fp8.py tests/test_transformer_gpu.py tests/test_conv3d.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/tests2.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/tests2.log; tail -5 $O/tests2.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python -u tools/vit_qkv_ab.py > $O/vit_qkv_ab.jsonl 2>&1
