@@ -309,6 +309,10 @@ class CellposeRunner:
 
     def _net_stage(self, x, p: EvalParams):
         B, C, H, W = x.shape
+        if not (p.diameter is not None and p.diameter > 0 and abs(self.diam_mean / float(p.diameter) - 1.0) > 1e-3):
+            r = self._net_graphed(x, p)
+            if r is not None:
+                return r[0], r[1], 1.0
         if p.normalize:
             with trace.span("cellpose.normalize99", cuda=True, images=B):
                 x = self._normalize(x)
