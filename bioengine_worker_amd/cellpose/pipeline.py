@@ -240,7 +240,7 @@ class CellposeRunner:
     #: batches up to this many images run normalize99 + tiling + network + blend from a HIP graph
     #: (captured once per shape / params): a small batch is a few hundred microsecond-scale launches,
     #: so the host launch path, not the GPU, would set its latency
-    GRAPH_NET_MAX_B = int(os.environ.get("BE_CELLPOSE_GRAPH_MAX_B", "8"))
+    GRAPH_NET_MAX_B = int(os.environ.get("BE_CELLPOSE_GRAPH_MAX_B", "64"))
 
     def _net_graphed(self, x, p: EvalParams):
         """(y, style) of the network stage (rescale 1) replayed from its HIP graph, or None when this
