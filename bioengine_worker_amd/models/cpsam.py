@@ -12,8 +12,8 @@ a pixel-shuffle back to 3 x 256 x 256 (dY, dX, cellprob).
   attn.rel_pos_w,norm2,mlp.lin1,mlp.lin2}``, ``encoder.neck.{0..3}``, ``out``, ``W2``,
   ``diam_labels``, ``diam_mean``) so a ``cpsam`` checkpoint loads with ``weights_only=True``.
   Reference path + training (``rdrop`` per-sample stochastic depth as cellpose 4 does).
-* :class:`CPSAMEngine` — bf16 inference on the framework's kernels: the macro-tile MFMA GEMM
-  (``ops/gemm_mt.py``) for every linear layer with bias / bias + GELU in its epilogue, the
+* :class:`CPSAMEngine` — bf16 inference on the framework's kernels: every linear layer on hipBLASLt
+  (default) or the macro-tile MFMA GEMM (``ops/gemm_mt.py``, bias / bias + GELU in its epilogue), the
   flash-attention kernel with the decomposed rel-pos bias fused into the score tile (the 1024x1024
   bias never exists), residual fused into LayerNorm, the neck's 3x3 conv on the NHWC MFMA conv
   kernel, and the readout + pixel shuffle as one GEMM + reshape.  :meth:`CPSAMEngine.graphed`
@@ -212,9 +212,11 @@ class CPSAMEngine:
         self.out_w = bf(net.out.weight.reshape(net.out.weight.shape[0], -1))
         self.out_b = bf(net.out.bias)
 
-    #: GEMM backend of the inference engine: "mt" (the framework's macro-tile MFMA GEMM, default) or
-    #: "lib" (PyTorch -> hipBLASLt, the A/B reference)
-    GEMM = os.environ.get("BE_CPSAM_INFER_GEMM", "mt")
+    #: GEMM backend of the inference engine: "lib" (PyTorch -> hipBLASLt, default) or "mt" (the
+    #: framework's macro-tile MFMA GEMM with the bias / GELU epilogues).  Measured on MI355X at 512^2 x
+    #: batch 8: lib 99.7 img/s, mt 84.4 / 84.8 (profiles/r05/cpsam/infer_mt_vs_lib_s23.jsonl): the
+    #: in-house GEMM trails hipBLASLt by 10-15 % per forward shape, so the library stays the default.
+    GEMM = os.environ.get("BE_CPSAM_INFER_GEMM", "lib")
 
     def _gemms(self):
         if self.GEMM == "lib":

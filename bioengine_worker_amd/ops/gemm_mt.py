@@ -30,8 +30,19 @@ TILES = {0: (256, 256), 1: (256, 192), 2: (256, 128), 3: (128, 256), 4: (128, 12
 NCU = 256
 
 #: (kind, M, N, K) -> (cfg, split).  kind: "nt" forward, "nn" data gradient, "tn" weight gradient.
-#: Filled from the per-shape sweep of tools/gemm_mt_bench.py (profiles/r05/gemm_mt/).
-TABLE: dict = {}
+#: The fastest configuration per Cellpose-SAM shape in the per-shape sweep of tools/gemm_mt_bench.py
+#: on an MI355X (profiles/r05/gemm/gemm_mt_sweep_s23.jsonl, graph-replayed, median of 5 rounds).
+TABLE: dict = {
+    ("nn", 1024, 1024, 1024): (4, 1), ("nn", 1024, 1024, 3072): (4, 1), ("nn", 1024, 1024, 4096): (4, 1),
+    ("nn", 1024, 4096, 1024): (4, 1), ("nn", 8192, 1024, 1024): (2, 1), ("nn", 8192, 1024, 3072): (2, 1),
+    ("nn", 8192, 1024, 4096): (2, 1), ("nn", 8192, 4096, 1024): (0, 1),
+    ("nt", 1024, 1024, 1024): (4, 1), ("nt", 1024, 1024, 4096): (4, 1), ("nt", 1024, 3072, 1024): (4, 1),
+    ("nt", 1024, 4096, 1024): (4, 1), ("nt", 8192, 1024, 1024): (2, 1), ("nt", 8192, 1024, 4096): (3, 1),
+    ("nt", 8192, 3072, 1024): (1, 1), ("nt", 8192, 4096, 1024): (0, 1),
+    ("tn", 1024, 1024, 1024): (4, 1), ("tn", 1024, 1024, 8192): (4, 4), ("tn", 1024, 4096, 1024): (4, 1),
+    ("tn", 1024, 4096, 8192): (0, 4), ("tn", 3072, 1024, 1024): (4, 1), ("tn", 3072, 1024, 8192): (0, 5),
+    ("tn", 4096, 1024, 1024): (4, 1), ("tn", 4096, 1024, 8192): (0, 4),
+}
 
 
 def _forced():
