@@ -238,9 +238,11 @@ class CellposeRunner:
         return t
 
     #: batches up to this many images run normalize99 + tiling + network + blend from a HIP graph
-    #: (captured once per shape / params): a small batch is a few hundred microsecond-scale launches,
-    #: so the host launch path, not the GPU, would set its latency
-    GRAPH_NET_MAX_B = int(os.environ.get("BE_CELLPOSE_GRAPH_MAX_B", "64"))
+    #: (captured once per shape / params).  Off by default: measured on MI355X it did not help --
+    #: headline 1,813 / 1,813 img/s graphed vs 1,819 / 1,815 eager, batch-1 p50 2.05 / 2.08 vs
+    #: 1.99 / 2.03 ms (profiles/r05/headline/graph_ab_s5.jsonl): the eager launches already hide
+    #: behind the kernels and the replay adds the static-buffer copies.
+    GRAPH_NET_MAX_B = int(os.environ.get("BE_CELLPOSE_GRAPH_MAX_B", "0"))
 
     def _net_graphed(self, x, p: EvalParams):
         """(y, style) of the network stage (rescale 1) replayed from its HIP graph, or None when this
