@@ -81,7 +81,10 @@ class NodeAgent:
                 "n_replicas": len(self.replicas), "uptime": time.time() - self.started}
 
     async def start_replica(self, tag: str, app: str, dep: str, payload: bytes, gpu_ids: list, env: dict | None = None):
-        cls, args, kwargs = cloudpickle.loads(payload)
+        # unpickling the deployment class imports its app module (torch, numpy, ...): off the event
+        # loop, or a slow import on a loaded host starves the hub connection's heartbeat and the hub
+        # drops this node mid-start ("client disconnected")
+        cls, args, kwargs = await asyncio.to_thread(cloudpickle.loads, payload)
         r = ProcessReplica(app, dep, cls, args, kwargs, list(gpu_ids or []), env or {}, log_dir=self.log_dir)
         r.tag = tag
         r.node_id = self.node_id

@@ -190,15 +190,25 @@ __device__ __forceinline__ void issue_halo(const PairArgs& a, TileXY t, int ch, 
     }
   }
   u32x4 (&hraw)[C::HUPT] = hr.h;
+  // CM = 32 (PF): unconditional loads (unit and coordinates clamped to valid memory): commit_halo
+  // zeroes what lies outside the image and skips units past HU, so only the addresses need to stay in
+  // bounds.  With no branch around them the compiler counts these loads exactly, and its later vmcnt
+  // waits (the epilogues) no longer drain the next tile's halo along with the operands they need.
+  // (CM = 64 keeps the branches: the clamps cost it registers it does not have.)
+  constexpr bool CL = C::PF;
 #pragma unroll
   for (int i = 0; i < C::HUPT; ++i) {
-    const int u = tid + i * NT;
+    const int u = CL ? min(tid + i * NT, C::HU - 1) : tid + i * NT;
     u32x4 r = (u32x4){0u, 0u, 0u, 0u};
-    if (u < C::HU) {
+    if (CL || u < C::HU) {
       int pix, cg;
       unit_pc<C::CGI>(u, pix, cg);
-      const int gy = t.ty0 - 2 + pix / IW, gx = t.tx0 - 2 + pix % IW;
-      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+      int gy = t.ty0 - 2 + pix / IW, gx = t.tx0 - 2 + pix % IW;
+      if (CL) {
+        gy = min(max(gy, 0), a.H - 1);
+        gx = min(max(gx, 0), a.W - 1);
+      }
+      if (CL || (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)) {
         const int c = c0 + cg * 8;
         if (INMODE == 0) {
           r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + gy) * a.Ws + gx) * a.Cin + c);
@@ -243,7 +253,7 @@ __device__ __forceinline__ void load_aff(const PairArgs& a, TileXY t, int ch, in
   f[3] = *reinterpret_cast<const float4*>(tr + 4);
 }
 
-template <typename C, bool PROJ>
+template <typename C, bool PROJ, bool DRAIN = false>
 __device__ __forceinline__ void commit_halo(const PairArgs& a, TileXY t, int ch, int tid, const HaloRegs<C>& hr,
                                             bf16_t* rin, bf16_t* preg, const float4 (*aff_pre)[4] = nullptr) {
   float sc[8], sh[8];
@@ -265,6 +275,12 @@ __device__ __forceinline__ void commit_halo(const PairArgs& a, TileXY t, int ch,
   }
   float ps[8], pt[8];
   if constexpr (PROJ) unpack_aff(hr.paff, ps, pt);
+  // DRAIN (LATEEPI builds, nothing but the halo in flight): every halo register is consumed here, so
+  // one unconditional wait instead of the compiler's waits
+  // inside the per-unit bounds branches, whose skipped paths left the halo loads "pending" in its
+  // tracking and made it wait again, for loads issued later, further down the tile.
+  // (the builtin, not inline asm: the compiler's wait tracking sees it)
+  if constexpr (DRAIN) __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xf << 8));  // vmcnt(0)
   const u32x4 (&hraw)[C::HUPT] = hr.h;
 #pragma unroll
   for (int i = 0; i < C::HUPT; ++i) {
@@ -445,19 +461,33 @@ struct EpiRegs {
 
 template <typename C, bool X2>
 __device__ __forceinline__ u32x2 load_x2(const PairArgs& a, TileXY t, int j, int ct, int wave, int lrow, int kq) {
+  // CM = 32: clamped, unconditional load (see issue_halo): epi_a stores zero outside the image and
+  // nothing for padding lanes, so only the address must stay valid
   int ry, rx;
   const bool ok = apix(wave + j * NW, lrow, ry, rx);
-  const int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
+  int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
   u32x2 v = (u32x2){0u, 0u};
-  if (X2 && ok && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)
+  if constexpr (C::PF) {
+    gy = min(max(gy, 0), a.H - 1);
+    gx = min(max(gx, 0), a.W - 1);
+    if (X2) v = *reinterpret_cast<const u32x2*>(a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * C::CM + ct * 16 + kq * 4);
+  } else if (X2 && ok && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
     v = *reinterpret_cast<const u32x2*>(a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * C::CM + ct * 16 + kq * 4);
+  }
   return v;
 }
 
 template <typename C, int RES>
 __device__ __forceinline__ u32x2 load_res(const PairArgs& a, TileXY t, int pt, int ct, int wave, int lrow, int kq) {
-  const int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
-  if (RES == 0 || py >= a.H || px >= a.W) return (u32x2){0u, 0u};
+  // CM = 32: clamped, unconditional load (see issue_halo): pixels outside the image are never stored
+  int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+  if constexpr (C::PF) {
+    py = min(py, a.H - 1);
+    px = min(px, a.W - 1);
+  } else if (py >= a.H || px >= a.W) {
+    return (u32x2){0u, 0u};
+  }
+  if (RES == 0) return (u32x2){0u, 0u};
   size_t pix;
   if (RES == 1) pix = ((size_t)t.n * a.H + py) * a.W + px;
   else pix = ((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1);
@@ -745,6 +775,10 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
   constexpr bool ROLL = (VAR & 2) != 0;
   constexpr bool EARLY = (VAR & 4) != 0;
   constexpr bool EPIA = (VAR & 8) != 0;
+  using C0 = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
+  // BE_PAIR_TOPEPI=1 -> the round-4 order (A/B); NCA = 2 keeps it (its skip operand prefetch on top
+  // of the next chunk's halo spills), with exact vmcnt counts now that the loads are unconditional
+  constexpr bool LATEEPI = (VAR & 32) == 0 && NCA == 1 && C0::PF;
   // SEPS (CM = 32, BE_PAIR_SEPS): output staging in its own LDS region (wave-private slots) after the
   // weights, so the next tile's halo commit never overlays it and needs no barrier of its own: the
   // barrier ahead of the output epilogue already fences stage B's reads of h
@@ -787,15 +821,18 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
     const int lane = tid & 63, wave = tid >> 6, lrow = lane & 15, kq = lane >> 4;
     const TileXY cur = tile_xy(a, t);
     EpiRegs<C, X2, RES, C::PF> ep;
-    issue_epi<C, X2, RES, C::PF>(a, cur, wave, lrow, kq, ep);
+    // LATEEPI (default): the epilogue operands are issued after the last halo commit, not at the
+    // top of the tile: loads issued ahead of the commit sit behind the halo registers in the
+    // in-order vmcnt queue, and the commit's wait for its halo then also waited for them (~1 L2 / HBM
+    // round trip per tile).  They are first needed by epi_a, after stage A's MFMAs.
+    if constexpr (!LATEEPI) issue_epi<C, X2, RES, C::PF>(a, cur, wave, lrow, kq, ep);
     f32x4 acc_a[C::NCT][APT];
 #pragma unroll
     for (int i = 0; i < C::NCT; ++i)
 #pragma unroll
       for (int j = 0; j < APT; ++j) acc_a[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     // ---- stage A: NCA input chunks ----
-#pragma unroll 1
-    for (int c = 0; c < NCA; ++c) {
+    auto chunk = [&](const int c) {
       if constexpr (EARLY && !C::PF) {
         float4 aff[4];
         load_aff<C>(a, cur, c, tid, aff);  // in flight across the barrier
@@ -803,16 +840,26 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
         commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P, &aff);
       } else {
         if (!(SEPS && c == 0)) __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
-        commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P);
+        commit_halo<C, PROJ, LATEEPI>(a, cur, c, tid, hraw, R, P);
       }
       if constexpr (!C::RESW) commit_w<C>(tid, wraw, WL);
       __syncthreads();
       stamp(0);
+      if (LATEEPI && c == NCA - 1) issue_epi<C, X2, RES, C::PF>(a, cur, wave, lrow, kq, ep);
       if (c + 1 < NCA) issue_halo<C, INMODE, PROJ>(a, cur, c + 1, tid, hraw);
       else if (t + 1 < t1) issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t + 1), 0, tid, hraw);
       if constexpr (!C::RESW) issue_w<C, NCA>(a, c + 1, tid, wraw);
       mma_a<C, ROLL>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
       stamp(1);
+    };
+    // CM = 32: unrolled, so each chunk's vmcnt waits are counted on its own path (the rolled loop
+    // merges chunk 0's, with the epilogue operands in flight, into every chunk's)
+    if constexpr (C::PF) {
+#pragma unroll
+      for (int c = 0; c < NCA; ++c) chunk(c);
+    } else {
+#pragma unroll 1
+      for (int c = 0; c < NCA; ++c) chunk(c);
     }
     if constexpr (EPIA && !C::PF && !X2) {  // with the skip operand too it spills (320 B)
       EpiA<C, X2> pa;
@@ -885,8 +932,9 @@ static int g_pair_var = [] {
   const char* e = getenv("BE_PAIR_EARLY_AFF");
   const char* p = getenv("BE_PAIR_EPIA");
   const char* q = getenv("BE_PAIR_SEPS");
+  const char* te = getenv("BE_PAIR_TOPEPI");
   return ((l ? atoi(l) : 1) ? 1 : 0) | ((r ? atoi(r) : 1) ? 2 : 0) | ((e ? atoi(e) : 1) ? 4 : 0) |
-         ((p && atoi(p)) ? 8 : 0) | ((q && atoi(q)) ? 16 : 0);
+         ((p && atoi(p)) ? 8 : 0) | ((q && atoi(q)) ? 16 : 0) | ((te && atoi(te)) ? 32 : 0);
 }();
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD, bool STAMP, int VAR>
@@ -909,8 +957,15 @@ int launch_pair_l(PairArgs a, int g, hipStream_t s) {
 
 template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false>
 int launch_pair_k(PairArgs a, int g, hipStream_t s) {
-  if constexpr (CM == 32 && CK == 32 && !HEAD) {  // level-0 half-blocks: only the SEPS bit applies
-    if (g_pair_var & 16) return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 16>(a, g, s);
+  if constexpr (CM == 32 && CK == 32 && !HEAD) {  // level-0 half-blocks: the SEPS bit applies
+    if (g_pair_var & 16) {
+      if constexpr (NCA == 1)
+        if (g_pair_var & 32) return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 48>(a, g, s);
+      return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 16>(a, g, s);
+    }
+  }
+  if constexpr (CM == 32 && NCA == 1) {  // the TOPEPI bit (see conv_pair_kernel's LATEEPI)
+    if (g_pair_var & 32) return launch_pair_l<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, 32>(a, g, s);
   }
   if constexpr (CM == 64 && RES != 0) {
     switch (g_pair_var & 15) {
@@ -947,6 +1002,544 @@ int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
   return launch_pair_k<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, false>(a, g, s);
 }
 
+// =====================================================================================================
+// Ping-pong level-0 half-block (CK = CM = 32, NCA = 1, full-resolution input, + x residual): the
+// resdown / resup c2 + c3 pairs at 224^2, and the final one with the output head fused (HEAD).
+//
+// The one-group kernel above runs every phase of a tile on all 8 waves between workgroup barriers,
+// so the MFMA pipe idles through the VALU / LDS-store phases (halo activation, the two epilogues):
+// ~65 % of a tile (tools/pair_phase_profile.py, profiles/r04/conv/pair_phases.jsonl).  Here the 8
+// waves are TWO GROUPS of 4 (waves w and w + 4 share a SIMD) that own alternate tiles of the
+// workgroup's range, each in its own LDS region, and run ONE PHASE APART on the same barriers: while
+// one group's wave issues MFMAs on a SIMD, the other group's wave on that SIMD runs a VALU phase.
+//
+//   phases per tile (each ends at a workgroup barrier):
+//     P1 commit   input halo registers -> actA -> LDS image               VALU + ds_write
+//     P2 stage A  h-region implicit GEMM (10 pixel tiles x 2 ct per wave)  MFMA   (s_setprio 1)
+//     P3 epi A    actB -> h (bf16) over the input image                    VALU + ds_write
+//     P4 stage B  output implicit GEMM (8 pixel tiles x 2 ct per wave)     MFMA   (s_setprio 1);
+//                 issues this tile's residual first
+//     P5 epi B    issues the group's next halo; bias + residual -> staged
+//                 16-byte stores (or the head)                               VALU + stores
+//   group 1 starts one barrier late, so the slots pair (P2,P1) (P3,P2) (P4,P3) (P5,P4) (P1,P5).
+//
+// LDS: 2 group regions of 45 KiB (the 20 x 36 input image; h and the output staging overlay it) +
+// both weight panels (38 KiB) = 128 KiB.  The fp32-accumulated regions hold 64-byte pixels with NO
+// padding (the one-group kernel pads to 96 B; two 69 KiB images would not fit) and an XOR swizzle
+// of the 16-byte chunk c, chosen by search over the ds_read_b128 lane groups so that every
+// 16-pixel fragment read is conflict-free at every tap offset:
+//     input image  c ^ 2 * (((x >> 2) ^ y) & 1)   (x, y in the 36-wide halo; edge tiles 2-way)
+//     h, staging   c ^ ((x >> 1) & 3)             (ds_write_b64 of the epilogues 2-way)
+// Both depend on the lane and on the parity of the tap row only, so every fragment address is a
+// per-lane base + a compile-time ds_read offset (no per-read VALU).
+namespace ppk {
+constexpr int GW = 4, GT = GW * 64;     // waves / threads per group
+constexpr int IN_B = IPIX * 64;         // 46080
+constexpr int H_B = RPIX * 64;          // 39168
+constexpr int OUTW_B = 4 * TW * 64;     // 8192: one wave's 4 x 32 output pixels
+constexpr int RB = IN_B;                // one group's region
+constexpr int WSTR = 9 * 32 + 16;       // 304: weight row stride (elements; 8 (mod 16) dwords)
+constexpr int W_B = 32 * WSTR * 2;      // one conv's panel, bytes
+constexpr int APT = 10, BPT = 8;        // pixel tiles per wave: stage A (39 in 40 slots), stage B
+constexpr int HU = IPIX * 4;            // 16-byte halo units per tile
+constexpr int HUPT = (HU + GT - 1) / GT;
+static_assert(H_B <= RB && GW * OUTW_B <= RB, "ping-pong region overlays");
+static_assert(APT * GW >= RPT && (APT - 1) * GW <= 2 * RH && BPT * GW * 16 == TH * TW, "tile maps");
+}  // namespace ppk
+
+struct PPHalo {
+  u32x4 h[ppk::HUPT];
+  float4 aff[4];  // actA scale / shift of this thread's 8 channels ((gt & 3) * 8 ..)
+};
+
+__device__ __forceinline__ int pp_in_off(int pi, int c) {  // byte offset of chunk c of input-image pixel pi
+  const int y = pi / IW, x = pi - y * IW;
+  return pi * 64 + ((c ^ ((((x >> 2) ^ y) & 1) << 1)) << 4);
+}
+
+template <int INMODE, int CIN>
+__device__ __forceinline__ void pp_issue_halo(const PairArgs& a, TileXY t, int ch, int gt, PPHalo& hr) {
+  const int c = ch * 32 + (gt & 3) * 8;  // a thread's chunk is the same for every unit (GT % 4 == 0)
+  hr.aff[0] = *reinterpret_cast<const float4*>(a.sa + c);
+  hr.aff[1] = *reinterpret_cast<const float4*>(a.sa + c + 4);
+  const float* tr = a.ta + (size_t)t.n * a.ta_ns + c;
+  hr.aff[2] = *reinterpret_cast<const float4*>(tr);
+  hr.aff[3] = *reinterpret_cast<const float4*>(tr + 4);
+#pragma unroll
+  for (int i = 0; i < ppk::HUPT; ++i) {  // clamped, unconditional (exact vmcnt counts; see issue_halo)
+    const int pi = min(gt + i * ppk::GT, ppk::HU - 1) >> 2;
+    const int y = pi / IW, x = pi - y * IW;
+    const int gy = min(max(t.ty0 - 2 + y, 0), a.H - 1), gx = min(max(t.tx0 - 2 + x, 0), a.W - 1);
+    if constexpr (INMODE == 0)
+      hr.h[i] = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + gy) * a.Ws + gx) * CIN + c);
+    else  // nearest 2x upsampling of the half-resolution input
+      hr.h[i] = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * CIN + c);
+  }
+}
+
+__device__ __forceinline__ void pp_commit(const PairArgs& a, TileXY t, int gt, const PPHalo& hr, unsigned char* rin) {
+  float sc[8], sh[8];
+  unpack_aff(hr.aff, sc, sh);
+  const int c = gt & 3;
+#pragma unroll
+  for (int i = 0; i < ppk::HUPT; ++i) {
+    const int u = gt + i * ppk::GT;
+    if (u >= ppk::HU) continue;
+    const int pi = u >> 2;
+    const int y = pi / IW, x = pi - y * IW;
+    const int gy = t.ty0 - 2 + y, gx = t.tx0 - 2 + x;
+    u32x4 pk = (u32x4){0u, 0u, 0u, 0u};
+    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        pk[j] = relu_bf16x2(pack2bf(fmaf(lo_bf(hr.h[i][j]), sc[2 * j], sh[2 * j]),
+                                    fmaf(hi_bf(hr.h[i][j]), sc[2 * j + 1], sh[2 * j + 1])));
+    }
+    *reinterpret_cast<u32x4*>(rin + pi * 64 + ((c ^ ((((x >> 2) ^ y) & 1) << 1)) << 4)) = pk;
+  }
+}
+
+// stage A: wave gw's row tiles j = 0..8 are region row (gw >> 1) + 2j, columns (gw & 1) * 16 + lrow;
+// j = 9 is edge / padding tile gw + 36 (columns 32, 33 of rows 8 gw ..)
+__device__ __forceinline__ void pp_mma_a(f32x4 (&acc)[2][ppk::APT], const unsigned char* rin, const bf16_t* wa, int gw,
+                                         int lrow, int kq) {
+  const int par = (gw >> 1) & 1;
+  const int b0 = ((gw >> 1) * IW + (gw & 1) * 16 + lrow) * 64;
+  int A0[3][2];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+      A0[dx][pr] = b0 + dx * 64 + ((kq ^ (((((lrow + dx) >> 2) ^ par ^ pr) & 1) << 1)) << 4);
+  int ry9 = 8 * gw + (lrow >> 1), rx9 = 32 + (lrow & 1);
+  if (ry9 >= RH) { ry9 = 0; rx9 = 0; }  // padding lanes: valid data, never stored
+  int E[2];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) E[pr] = (ry9 * IW + rx9) * 64 + ((kq ^ ((((ry9 & 1) ^ pr) & 1) << 1)) << 4);
+  auto frags = [&](int ks, bf16x8 (&af)[2], bf16x8 (&bf)[ppk::APT]) {
+    const int dy = ks / 3, dx = ks % 3;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+      af[ct] = *reinterpret_cast<const bf16x8*>(wa + (ct * 16 + lrow) * ppk::WSTR + ks * 32 + kq * 8);
+#pragma unroll
+    for (int j = 0; j < ppk::APT - 1; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(rin + A0[dx][dy & 1] + j * 2 * IW * 64 + dy * IW * 64);
+    bf[ppk::APT - 1] = *reinterpret_cast<const bf16x8*>(rin + E[dy & 1] + dx * 64 + dy * IW * 64);
+  };
+  // one pixel-fragment set, rolling reload: each pixel fragment of K-step ks + 1 is read right after
+  // its last MFMA of step ks (80 accumulator VGPRs leave no room for a second set); the two weight
+  // fragments of ks + 1 are read at the top of step ks into a second pair (read after the last
+  // pixel tile they would be waited on two MFMAs later)
+  bf16x8 af[2], afn[2], bf[ppk::APT];
+  frags(0, af, bf);
+#pragma unroll
+  for (int ks = 0; ks < 9; ++ks) {
+    const bool more = ks + 1 < 9;
+    const int kn = more ? ks + 1 : ks, dy = kn / 3, dx = kn % 3;
+#pragma unroll
+    for (int j = 0; j < ppk::APT; ++j) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[j], acc[ct][j], 0, 0, 0);
+        if (j == 0 && more)
+          afn[ct] = *reinterpret_cast<const bf16x8*>(wa + (ct * 16 + lrow) * ppk::WSTR + kn * 32 + kq * 8);
+      }
+      if (more) {
+        if (j < ppk::APT - 1)
+          bf[j] = *reinterpret_cast<const bf16x8*>(rin + A0[dx][dy & 1] + j * 2 * IW * 64 + dy * IW * 64);
+        else
+          bf[j] = *reinterpret_cast<const bf16x8*>(rin + E[dy & 1] + dx * 64 + dy * IW * 64);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) {
+      af[0] = afn[0];
+      af[1] = afn[1];
+    }
+  }
+}
+
+// X2: the skip operand of stage A's output (resup: convA(x) + skip) at this lane's h pixels
+struct PPSkip {
+  u32x2 xv[ppk::APT][2];
+};
+
+__device__ __forceinline__ void pp_issue_skip(const PairArgs& a, TileXY t, int gw, int lrow, int kq, PPSkip& sk) {
+#pragma unroll
+  for (int j = 0; j < ppk::APT; ++j) {
+    int ry, rx;
+    if (j < ppk::APT - 1) {
+      ry = (gw >> 1) + 2 * j;
+      rx = (gw & 1) * 16 + lrow;
+    } else {
+      ry = 8 * gw + (lrow >> 1);
+      rx = 32 + (lrow & 1);
+    }
+    // clamped, unconditional: pp_epi_a stores zero outside the image and nothing for padding lanes
+    const int gy = min(max(t.ty0 - 1 + ry, 0), a.H - 1), gx = min(max(t.tx0 - 1 + rx, 0), a.W - 1);
+    const bf16_t* xp = a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * 32 + kq * 4;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) sk.xv[j][ct] = *reinterpret_cast<const u32x2*>(xp + ct * 16);
+  }
+}
+
+// actB(+ skip) -> h (bf16) in the region, zero outside the image; h pixel (ry, rx) of the 18 x 34 region
+template <bool X2>
+__device__ __forceinline__ void pp_epi_a(const PairArgs& a, TileXY t, const f32x4 (&acc)[2][ppk::APT],
+                                         unsigned char* rh, const float4 (&s)[2], const float4 (&sh)[2],
+                                         const PPSkip& sk, int gw, int lrow, int kq) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int hc = ((2 * ct) | (kq >> 1));
+    const int hw = (((gw >> 1) * RW + (gw & 1) * 16 + lrow) * 64) + ((hc ^ ((lrow >> 1) & 3)) << 4) + (kq & 1) * 8;
+#pragma unroll
+    for (int j = 0; j < ppk::APT; ++j) {
+      int ry, rx, off;
+      if (j < ppk::APT - 1) {
+        ry = (gw >> 1) + 2 * j;
+        rx = (gw & 1) * 16 + lrow;
+        off = hw + j * 2 * RW * 64;
+      } else {
+        ry = 8 * gw + (lrow >> 1);
+        rx = 32 + (lrow & 1);
+        if (ry >= RH) continue;
+        off = (ry * RW + rx) * 64 + ((hc ^ ((rx >> 1) & 3)) << 4) + (kq & 1) * 8;
+      }
+      const int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
+      float v0 = acc[ct][j][0], v1 = acc[ct][j][1], v2 = acc[ct][j][2], v3 = acc[ct][j][3];
+      if constexpr (X2) {
+        u32x2 xv = sk.xv[j][ct];
+        asm volatile("" : "+v"(xv));  // unpacked here, not next to its load (see pp_epi_b)
+        v0 += lo_bf(xv[0]); v1 += hi_bf(xv[0]); v2 += lo_bf(xv[1]); v3 += hi_bf(xv[1]);
+      }
+      u32x2 st = (u32x2){0u, 0u};
+      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+        st[0] = relu_bf16x2(pack2bf(fmaf(v0, s[ct].x, sh[ct].x), fmaf(v1, s[ct].y, sh[ct].y)));
+        st[1] = relu_bf16x2(pack2bf(fmaf(v2, s[ct].z, sh[ct].z), fmaf(v3, s[ct].w, sh[ct].w)));
+      }
+      *reinterpret_cast<u32x2*>(rh + off) = st;
+    }
+  }
+}
+
+// stage B: wave gw owns output rows 4 gw .. 4 gw + 3; pixel tile pt = row (pt >> 1), half (pt & 1)
+__device__ __forceinline__ void pp_mma_b(f32x4 (&acc)[2][ppk::BPT], const unsigned char* rh, const bf16_t* wb, int gw,
+                                         int lrow, int kq) {
+  int B0[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) B0[dx] = ((4 * gw) * RW + lrow + dx) * 64 + ((kq ^ (((lrow + dx) >> 1) & 3)) << 4);
+  auto frags = [&](int ks, bf16x8 (&af)[2], bf16x8 (&bf)[ppk::BPT]) {
+    const int dy = ks / 3, dx = ks % 3;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+      af[ct] = *reinterpret_cast<const bf16x8*>(wb + (ct * 16 + lrow) * ppk::WSTR + ks * 32 + kq * 8);
+#pragma unroll
+    for (int pt = 0; pt < ppk::BPT; ++pt)
+      bf[pt] = *reinterpret_cast<const bf16x8*>(rh + B0[dx] + ((pt >> 1) + dy) * RW * 64 + (pt & 1) * 16 * 64);
+  };
+  bf16x8 af[2], afn[2], bf[ppk::BPT];  // rolling reload, weight pair read a step ahead (as pp_mma_a)
+  frags(0, af, bf);
+#pragma unroll
+  for (int ks = 0; ks < 9; ++ks) {
+    const bool more = ks + 1 < 9;
+    const int kn = more ? ks + 1 : ks, dy = kn / 3, dx = kn % 3;
+#pragma unroll
+    for (int pt = 0; pt < ppk::BPT; ++pt) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[pt], acc[ct][pt], 0, 0, 0);
+        if (pt == 0 && more)
+          afn[ct] = *reinterpret_cast<const bf16x8*>(wb + (ct * 16 + lrow) * ppk::WSTR + kn * 32 + kq * 8);
+      }
+      if (more) bf[pt] = *reinterpret_cast<const bf16x8*>(rh + B0[dx] + ((pt >> 1) + dy) * RW * 64 + (pt & 1) * 16 * 64);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) {
+      af[0] = afn[0];
+      af[1] = afn[1];
+    }
+  }
+}
+
+struct PPRes {
+  u32x2 rv[ppk::BPT][2];
+  float4 bias[2];
+};
+
+template <int RES>
+__device__ __forceinline__ void pp_issue_res(const PairArgs& a, TileXY t, int gw, int lrow, int kq, PPRes& r) {
+#pragma unroll
+  for (int pt = 0; pt < ppk::BPT; ++pt) {
+    const int py = min(t.ty0 + 4 * gw + (pt >> 1), a.H - 1), px = min(t.tx0 + (pt & 1) * 16 + lrow, a.W - 1);
+    const bf16_t* rp = RES == 1 ? a.res + (((size_t)t.n * a.H + py) * a.W + px) * 32 + kq * 4
+                                : a.res + (((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1)) * 32 + kq * 4;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) r.rv[pt][ct] = *reinterpret_cast<const u32x2*>(rp + ct * 16);
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) r.bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
+}
+
+// bias + residual -> wave-private staging (swizzled like h) -> 16-byte coalesced NHWC stores
+__device__ __forceinline__ void pp_epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[2][ppk::BPT], const PPRes& r,
+                                         unsigned char* ws, int gw, int lrow, int kq, bool act) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int ow = lrow * 64 + ((((2 * ct) | (kq >> 1)) ^ ((lrow >> 1) & 3)) << 4) + (kq & 1) * 8;
+#pragma unroll
+    for (int pt = 0; pt < ppk::BPT; ++pt) {
+      u32x2 rv = r.rv[pt][ct];
+      asm volatile("" : "+v"(rv));  // keeps the bf16 unpacking here, not hoisted next to the loads in P4
+      u32x2 st;
+      st[0] = pack2bf(acc[ct][pt][0] + r.bias[ct].x + lo_bf(rv[0]), acc[ct][pt][1] + r.bias[ct].y + hi_bf(rv[0]));
+      st[1] = pack2bf(acc[ct][pt][2] + r.bias[ct].z + lo_bf(rv[1]), acc[ct][pt][3] + r.bias[ct].w + hi_bf(rv[1]));
+      *reinterpret_cast<u32x2*>(ws + ow + ((pt >> 1) * 32 + (pt & 1) * 16) * 64) = st;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int lane = lrow + 16 * kq;
+  const int rd = (lane >> 2) * 64 + (((lane & 3) ^ ((lane >> 3) & 3)) << 4);
+  // Buffer stores through a per-image descriptor: a pixel outside the image (or a tile that is not
+  // this group's) gets an out-of-range offset and the range check drops it, so exactly PP_EPI_STORES
+  // stores are issued on every path and the next P1's halo wait can be a counted vmcnt.  One unit in
+  // flight at a time (the next halo's registers are live through this phase).
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      a.out + (size_t)t.n * a.H * a.W * 32, (short)0, a.H * a.W * 64, 0x00020000);
+  const int py0 = t.ty0 + 4 * gw, px0 = t.tx0 + (lane >> 2);
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int py = py0 + (it >> 1), px = px0 + (it & 1) * 16;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ws + rd + it * 1024);
+    const int off = (act && py < a.H && px < a.W) ? ((py * a.W + px) * 32 + (lane & 3) * 8) * 2 : 0x7ffffff0;
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// HEAD: out = bf16(acc + bias + res), then the output layer (see epi_head) straight from registers
+__device__ __forceinline__ void pp_epi_head(const PairArgs& a, TileXY t, const f32x4 (&acc)[2][ppk::BPT], const PPRes& r,
+                                            const HeadRegs& hr, int gw, int lrow, int kq, bool act) {
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      a.hout + (size_t)t.n * a.nh * a.H * a.W, (short)0, a.nh * a.H * a.W * 4, 0x00020000);
+#pragma unroll
+  for (int pt = 0; pt < ppk::BPT; ++pt) {
+    u32x4 bw;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      u32x2 rv = r.rv[pt][ct];
+      asm volatile("" : "+v"(rv));  // see pp_epi_b
+      const float4 bias = r.bias[ct];
+      const uint32_t o0 = pack2bf(acc[ct][pt][0] + bias.x + lo_bf(rv[0]), acc[ct][pt][1] + bias.y + hi_bf(rv[0]));
+      const uint32_t o1 = pack2bf(acc[ct][pt][2] + bias.z + lo_bf(rv[1]), acc[ct][pt][3] + bias.w + hi_bf(rv[1]));
+      bw[2 * ct] = relu_bf16x2(pack2bf(fmaf(lo_bf(o0), hr.s[ct].x, hr.t[ct].x), fmaf(hi_bf(o0), hr.s[ct].y, hr.t[ct].y)));
+      bw[2 * ct + 1] = relu_bf16x2(pack2bf(fmaf(lo_bf(o1), hr.s[ct].z, hr.t[ct].z), fmaf(hi_bf(o1), hr.s[ct].w, hr.t[ct].w)));
+    }
+    const f32x4 y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hr.w, *reinterpret_cast<const bf16x8*>(&bw), zero, 0, 0, 0);
+    const int py = t.ty0 + 4 * gw + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+    const bool ok = act && py < a.H && px < a.W;
+    const float bb[4] = {hr.b.x, hr.b.y, hr.b.z, hr.b.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // unconditional buffer stores, out-of-range offsets dropped (see pp_epi_b)
+      const int co = kq * 4 + i;
+      const int off = (ok && co < a.nh) ? ((co * a.H + py) * a.W + px) * 4 : 0x7ffffff0;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y[i] + bb[i]), rs, off, 0, 0);
+    }
+  }
+}
+
+// NCA input chunks of 32 channels (Cin = 32 NCA), INMODE 0 (full resolution) or 1 (nearest 2x up),
+// X2: + skip operand on stage A's output, RES 1 (full) or 2 (up2 of a half-resolution map).
+template <int NCA, int INMODE, bool X2, int RES, bool HEAD, bool STAMP = false>
+__global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
+  constexpr int CIN = 32 * NCA;
+  // STAMP (diagnostics, tools/pp_phase_profile.py): wave 0 of each group accumulates s_memtime
+  // cycles of every phase's own work and of its wait at the closing barrier, [grid][2 groups][16]
+  unsigned long long ph_work[7] = {0, 0, 0, 0, 0, 0, 0}, ph_wait[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tstamp = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  auto pre = [&](int i) {
+    if constexpr (STAMP) {
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      ph_work[i] += tn - tstamp;
+      tstamp = tn;
+    }
+  };
+  auto post = [&](int i) {
+    if constexpr (STAMP) {
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      ph_wait[i] += tn - tstamp;
+      tstamp = tn;
+    }
+  };
+  constexpr int NST = HEAD ? 32 : 8;  // buffer stores per P5 (counted wait in P1)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid0 = threadIdx.x;
+  const int total = a.N * a.tiles_x * a.tiles_y;
+  const int t0 = (int)(((long long)blockIdx.x * total) / gridDim.x);
+  const int t1 = (int)(((long long)(blockIdx.x + 1) * total) / gridDim.x);
+  if (t0 >= t1) return;  // workgroup-uniform
+  bf16_t* wl = reinterpret_cast<bf16_t*>(smem + 2 * ppk::RB);
+  // NCA stage-A panels then the stage-B panel, [32 rows][304] each (from the packed [Cout][NCA][288]
+  // and [Cout][1][288] layouts)
+  for (int u = tid0; u < (NCA + 1) * 32 * 36; u += NT) {
+    const int pnl = u / (32 * 36), q = u % (32 * 36), r = q / 36, k8 = q % 36;
+    const bf16_t* src = pnl < NCA ? a.wa + ((size_t)r * NCA + pnl) * 288 + k8 * 8 : a.wb + (size_t)r * 288 + k8 * 8;
+    *reinterpret_cast<u32x4*>(wl + pnl * 32 * ppk::WSTR + r * ppk::WSTR + k8 * 8) = *reinterpret_cast<const u32x4*>(src);
+  }
+  const bf16_t* wb = wl + NCA * 32 * ppk::WSTR;
+  // wave-uniform values in SGPRs (readfirstlane): the group / wave-in-group branches stay scalar
+  const int grp = __builtin_amdgcn_readfirstlane(tid0 >> 8);  // waves 0-3 | 4-7 (w and w + 4 share a SIMD)
+  const int gt0 = tid0 & (ppk::GT - 1);
+  unsigned char* reg = smem + grp * ppk::RB;
+  HeadRegs hr;
+  if constexpr (HEAD) load_head(a, tid0 & 15, (tid0 & 63) >> 4, hr);
+  PPHalo halo;
+  pp_issue_halo<INMODE, CIN>(a, tile_xy(a, min(t0 + grp, t1 - 1)), 0, gt0, halo);
+  __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xf << 8));  // vmcnt(0): see the counted wait in P1
+  __syncthreads();  // weights resident
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 runs one phase behind
+  const int iters = (t1 - t0 + 1) >> 1;
+  for (int k = 0; k < iters; ++k) {
+    int gt = gt0;
+    asm volatile("" : "+v"(gt));  // per-iteration opaque copy (see conv_pair_kernel)
+    const int gw = __builtin_amdgcn_readfirstlane(gt >> 6), lane = gt & 63, lrow = lane & 15, kq = lane >> 4;
+    const int t = t0 + 2 * k + grp;
+    // A group without a tile in the last iteration (odd range) recomputes the range's last tile and
+    // stores nothing: every phase runs unconditionally (no divergent-looking branches around the
+    // big register sets, which the allocator handled badly), only the global stores are predicated.
+    const bool act = t < t1;
+    const TileXY cur = tile_xy(a, act ? t : t1 - 1);
+    f32x4 acc_a[2][ppk::APT];
+    float4 sb[2], tb[2];
+    PPSkip sk;
+#pragma unroll
+    for (int c = 0; c < NCA; ++c) {
+      // P1: input chunk c -> activated image.  For c = 0 in flight: the halo (issued in P4), then
+      // exactly the previous P5's NST buffer stores; the counted wait retires the halo only (the
+      // builtin, so the compiler's own wait tracking sees it and adds no vmcnt(0) behind the stores).
+      if (c == 0) __builtin_amdgcn_s_waitcnt((NST & 0xf) | (0x7 << 4) | (0xf << 8) | ((NST >> 4) << 14));
+      int gc = gt0;
+      asm volatile("" : "+v"(gc));  // per chunk: the unit addresses are recomputed, not kept across P2
+      pp_commit(a, cur, gc, halo, reg);
+      pre(2 * c);
+      __syncthreads();
+      post(2 * c);
+      // P2: stage A over chunk c (the next chunk's halo, or the epilogue operands, in flight)
+      if (c + 1 < NCA) pp_issue_halo<INMODE, CIN>(a, cur, c + 1, gt, halo);
+      if (c == NCA - 1) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          sb[ct] = *reinterpret_cast<const float4*>(a.sb + ct * 16 + kq * 4);
+          tb[ct] = *reinterpret_cast<const float4*>(a.tb + (size_t)cur.n * a.tb_ns + ct * 16 + kq * 4);
+        }
+        if constexpr (X2) pp_issue_skip(a, cur, gw, lrow, kq, sk);
+      }
+      if (c == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < ppk::APT; ++j) acc_a[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      __builtin_amdgcn_s_setprio(1);
+      pp_mma_a(acc_a, reg, wl + c * 32 * ppk::WSTR, gw, lrow, kq);
+      __builtin_amdgcn_s_setprio(0);
+      pre(2 * c + 1);
+      __syncthreads();
+      post(2 * c + 1);
+    }
+    // P3: epilogue A -> h
+    int g3 = gt0;
+    asm volatile("" : "+v"(g3));
+    pp_epi_a<X2>(a, cur, acc_a, reg, sb, tb, sk, gw, g3 & 15, (g3 & 63) >> 4);
+    pre(2 * NCA);
+    __syncthreads();
+    post(2 * NCA);
+    // P4: stage B; this tile's residual first, the group's next halo behind the MFMAs (its registers
+    // are free once the fragments are; it is needed two phases later).  Fresh opaque lane index:
+    // the P4 / P5 addresses are computed here, not hoisted into P1 and kept (spilled) across.
+    int g4 = gt0;
+    asm volatile("" : "+v"(g4));
+    const int lrow4 = g4 & 15, kq4 = (g4 & 63) >> 4;
+    f32x4 acc_b[2][ppk::BPT];
+    PPRes res;
+    pp_issue_res<RES>(a, cur, gw, lrow4, kq4, res);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < ppk::BPT; ++j) acc_b[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    __builtin_amdgcn_s_setprio(1);
+    pp_mma_b(acc_b, reg, wb, gw, lrow4, kq4);
+    __builtin_amdgcn_s_setprio(0);
+    pre(2 * NCA + 1);
+    __syncthreads();
+    post(2 * NCA + 1);
+    // P5: the group's next halo (issued here, not behind the stage-B MFMAs: the issue of 16 wide
+    // loads stalled the MFMA phase, the longest slot; it is needed at the next phase), then the
+    // output epilogue (its staging overlays h: every wave of the group is past stage B)
+    int g5 = gt0;
+    asm volatile("" : "+v"(g5));
+    const int lrow5 = g5 & 15, kq5 = (g5 & 63) >> 4;
+    pp_issue_halo<INMODE, CIN>(a, tile_xy(a, min(t + 2, t1 - 1)), 0, g5, halo);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (HEAD) pp_epi_head(a, cur, acc_b, res, hr, gw, lrow5, kq5, act);
+    else pp_epi_b(a, cur, acc_b, res, reg + gw * ppk::OUTW_B, gw, lrow5, kq5, act);
+    pre(2 * NCA + 2);
+    __syncthreads();
+    post(2 * NCA + 2);
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  if constexpr (STAMP) {
+    if ((tid0 & 255) < 16) {  // wave 0 of each group: lane k stores slot k (lane-indexed vector store)
+      const int k = tid0 & 15;
+      unsigned long long v = 0;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        if (k == i) v = ph_work[i];
+        if (k == 8 + i) v = ph_wait[i];
+      }
+      if (k == 15) v = (unsigned long long)iters;
+      a.stamps[((size_t)blockIdx.x * 2 + grp) * 16 + k] = v;
+    }
+  }
+}
+
+unsigned long long* g_pp_stamps = nullptr;  // diagnostics: be_conv_pair_pp_set_stamps
+int g_pp_stamps_cap = 0;
+
+template <int NCA, int INMODE, bool X2, int RES, bool HEAD>
+int launch_pair_pp(PairArgs a, int grid_cap, hipStream_t s) {
+  constexpr int lds = 2 * ppk::RB + (NCA + 1) * ppk::W_B;
+  static_assert(lds <= 160 * 1024, "ping-pong LDS budget");
+  a.tiles_x = (a.W + TW - 1) / TW;
+  a.tiles_y = (a.H + TH - 1) / TH;
+  const int tiles = a.N * a.tiles_x * a.tiles_y;
+  int g = grid_cap > 0 ? grid_cap : 256;
+  if (g > tiles) g = tiles;
+  if (g < 1) return 0;
+  a.stamps = nullptr;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr_set = true;
+  }
+  if (g_pp_stamps != nullptr) {
+    if (g > g_pp_stamps_cap) return -30;
+    a.stamps = g_pp_stamps;
+    static bool attr_st = false;
+    if (!attr_st) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_st = true;
+    }
+    hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, true>), dim3(g), dim3(NT), lds, s, a);
+    return BE_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD>), dim3(g), dim3(NT), lds, s, a);
+  return BE_CHECK_LAUNCH();
+}
 }  // namespace
 
 // tuning override (0 = one workgroup per CU); BE_PAIR_GRID sets it for A/B runs
@@ -954,6 +1547,22 @@ static int g_pair_grid = [] {
   const char* e = getenv("BE_PAIR_GRID");
   return e ? atoi(e) : 0;
 }();
+
+// BE_PAIR_PP (default 1): the level-0 32 -> 32 half-blocks (+ the head) on the ping-pong kernel
+static int g_pair_pp = [] {
+  const char* e = getenv("BE_PAIR_PP");
+  return e ? atoi(e) : 1;
+}();
+
+// The ping-pong kernel pays off when each workgroup has tiles for both groups: with fewer than two
+// tiles per workgroup (batch-1 latency calls) the second group would only recompute a dummy tile,
+// so those calls keep the one-group kernel.
+static bool pp_ok(const PairArgs& a, int grid_cap) {
+  if (!g_pair_pp || g_pair_stamps != nullptr) return false;
+  const long long tiles = (long long)a.N * ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
+  const int g = grid_cap > 0 ? grid_cap : 256;
+  return tiles >= 2LL * g;
+}
 
 extern "C" {
 
@@ -968,6 +1577,15 @@ int be_conv_pair_set_grid(int blocks) {
 int be_conv_pair_set_stamps(void* buf, int cap_workgroups) {
   g_pair_stamps = static_cast<unsigned long long*>(buf);
   g_pair_stamps_cap = buf ? cap_workgroups : 0;
+  return 0;
+}
+
+// Diagnostics: the ping-pong half-blocks write [workgroup][group][16] u64 phase stamps into `buf`
+// (work cycles of phase i at slot i, barrier-wait cycles at 8 + i, iterations at 15); nullptr
+// switches back.  Not for production launches.
+int be_conv_pair_pp_set_stamps(void* buf, int cap_workgroups) {
+  g_pp_stamps = static_cast<unsigned long long*>(buf);
+  g_pp_stamps_cap = buf ? cap_workgroups : 0;
   return 0;
 }
 
@@ -1004,10 +1622,15 @@ int be_conv_pair(const void* x, const void* x2, const float* sa, const float* ta
   const int g = g_pair_grid;
   if (CM == 32 && Cin == 8 && inmode == 0 && !hx2 && proj && resmode == 0)
     return launch_pair<8, 32, 0, false, true, 0, 1>(a, g, stream);
-  if (CM == 32 && Cin == 32 && inmode == 0 && !hx2 && !proj && resmode == 1)
+  if (CM == 32 && Cin == 32 && inmode == 0 && !hx2 && !proj && resmode == 1) {
+    if (pp_ok(a, g) && Hs == H && Ws == W) return launch_pair_pp<1, 0, false, 1, false>(a, g, stream);
     return launch_pair<32, 32, 0, false, false, 1, 1>(a, g, stream);
-  if (CM == 32 && Cin == 64 && inmode == 1 && hx2 && !proj && resmode == 2)
+  }
+  if (CM == 32 && Cin == 64 && inmode == 1 && hx2 && !proj && resmode == 2) {
+    if (pp_ok(a, g) && 2 * Hs == H && 2 * Ws == W)
+      return launch_pair_pp<2, 1, true, 2, false>(a, g, stream);
     return launch_pair<32, 32, 1, true, false, 2, 2>(a, g, stream);
+  }
   if (CM == 64 && Cin == 32 && inmode == 2 && !hx2 && !proj && resmode == 1)
     return launch_pair<32, 64, 2, false, false, 1, 1>(a, g, stream);
   if (CM == 64 && Cin == 64 && inmode == 0 && !hx2 && !proj && resmode == 1)
@@ -1032,6 +1655,7 @@ int be_conv_pair_head(const void* x, const float* sa, const float* ta, int ta_ns
   a.res = (const bf16_t*)res; a.out = nullptr;
   a.sh = sh; a.th = th; a.wh = (const bf16_t*)wh; a.bh = bh; a.hout = hout; a.nh = nh;
   a.N = N; a.H = H; a.W = W; a.Hs = H; a.Ws = W; a.Cin = 32;
+  if (pp_ok(a, g_pair_grid)) return launch_pair_pp<1, 0, false, 1, true>(a, g_pair_grid, stream);
   return launch_pair<32, 32, 0, false, false, 1, 1, true>(a, g_pair_grid, stream);
 }
 

@@ -57,8 +57,11 @@ HIP_FLAGS = [
 # attention: MFMA accumulators in arch VGPRs (the default AGPR form moved every S / O tile through
 # v_accvgpr_read/write around the softmax: 192 moves per KV tile); forward 0.085 -> 0.076 ms at B=8.
 # gemm_mt: same, and without it hipcc shuffles the accumulators through a scratch AGPR quad every MFMA.
+# conv_pair: no SLP vectorisation -- packed-f32 VALU (v_pk_fma_f32) issued beside another wave's
+# MFMAs is slow on CDNA4; the ping-pong half-blocks run their VALU phases exactly there
+# (profiles/r05/conv/pp_noslp_ab: stem -18 %, 32->32 -7.5 %, 64->32 up -9 %, headline +1.5 %)
 PER_SOURCE_FLAGS = {"clahe": ["-ffp-contract=off"], "attention": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-                    "gemm_mt": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+                    "gemm_mt": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"], "conv_pair": ["-fno-slp-vectorize"]}
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread", "-I", str(CSRC / "runtime")]
 
 
