@@ -1032,6 +1032,9 @@ int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
 //     h, staging   c ^ ((x >> 1) & 3)             (ds_write_b64 of the epilogues 2-way)
 // Both depend on the lane and on the parity of the tap row only, so every fragment address is a
 // per-lane base + a compile-time ds_read offset (no per-read VALU).
+#ifndef PP_VAR
+#define PP_VAR 1  // tuning variants (tools/build_native.py --variant ... --vflags=-DPP_VAR=n)
+#endif
 namespace ppk {
 constexpr int GW = 4, GT = GW * 64;     // waves / threads per group
 constexpr int IN_B = IPIX * 64;         // 46080
@@ -1057,7 +1060,7 @@ __device__ __forceinline__ int pp_in_off(int pi, int c) {  // byte offset of chu
   return pi * 64 + ((c ^ ((((x >> 2) ^ y) & 1) << 1)) << 4);
 }
 
-template <int INMODE, int CIN>
+template <int INMODE, int CIN, bool INT = false>
 __device__ __forceinline__ void pp_issue_halo(const PairArgs& a, TileXY t, int ch, int gt, PPHalo& hr) {
   const int c = ch * 32 + (gt & 3) * 8;  // a thread's chunk is the same for every unit (GT % 4 == 0)
   hr.aff[0] = *reinterpret_cast<const float4*>(a.sa + c);
@@ -1069,7 +1072,8 @@ __device__ __forceinline__ void pp_issue_halo(const PairArgs& a, TileXY t, int c
   for (int i = 0; i < ppk::HUPT; ++i) {  // clamped, unconditional (exact vmcnt counts; see issue_halo)
     const int pi = min(gt + i * ppk::GT, ppk::HU - 1) >> 2;
     const int y = pi / IW, x = pi - y * IW;
-    const int gy = min(max(t.ty0 - 2 + y, 0), a.H - 1), gx = min(max(t.tx0 - 2 + x, 0), a.W - 1);
+    const int gy = INT ? t.ty0 - 2 + y : min(max(t.ty0 - 2 + y, 0), a.H - 1);
+    const int gx = INT ? t.tx0 - 2 + x : min(max(t.tx0 - 2 + x, 0), a.W - 1);
     if constexpr (INMODE == 0)
       hr.h[i] = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + gy) * a.Ws + gx) * CIN + c);
     else  // nearest 2x upsampling of the half-resolution input
@@ -1077,6 +1081,12 @@ __device__ __forceinline__ void pp_issue_halo(const PairArgs& a, TileXY t, int c
   }
 }
 
+// INT: the tile's whole 20 x 36 halo lies inside the image (most tiles): no bounds tests
+__device__ __forceinline__ bool pp_interior(const PairArgs& a, TileXY t) {
+  return t.ty0 >= 2 && t.ty0 + TH + 2 <= a.H && t.tx0 >= 2 && t.tx0 + TW + 2 <= a.W;
+}
+
+template <bool INT>
 __device__ __forceinline__ void pp_commit(const PairArgs& a, TileXY t, int gt, const PPHalo& hr, unsigned char* rin) {
   float sc[8], sh[8];
   unpack_aff(hr.aff, sc, sh);
@@ -1089,7 +1099,7 @@ __device__ __forceinline__ void pp_commit(const PairArgs& a, TileXY t, int gt, c
     const int y = pi / IW, x = pi - y * IW;
     const int gy = t.ty0 - 2 + y, gx = t.tx0 - 2 + x;
     u32x4 pk = (u32x4){0u, 0u, 0u, 0u};
-    if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+    if (INT || (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         pk[j] = relu_bf16x2(pack2bf(fmaf(lo_bf(hr.h[i][j]), sc[2 * j], sh[2 * j]),
@@ -1184,7 +1194,7 @@ __device__ __forceinline__ void pp_issue_skip(const PairArgs& a, TileXY t, int g
 }
 
 // actB(+ skip) -> h (bf16) in the region, zero outside the image; h pixel (ry, rx) of the 18 x 34 region
-template <bool X2>
+template <bool X2, bool INT>
 __device__ __forceinline__ void pp_epi_a(const PairArgs& a, TileXY t, const f32x4 (&acc)[2][ppk::APT],
                                          unsigned char* rh, const float4 (&s)[2], const float4 (&sh)[2],
                                          const PPSkip& sk, int gw, int lrow, int kq) {
@@ -1213,7 +1223,7 @@ __device__ __forceinline__ void pp_epi_a(const PairArgs& a, TileXY t, const f32x
         v0 += lo_bf(xv[0]); v1 += hi_bf(xv[0]); v2 += lo_bf(xv[1]); v3 += hi_bf(xv[1]);
       }
       u32x2 st = (u32x2){0u, 0u};
-      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
+      if (INT || (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)) {
         st[0] = relu_bf16x2(pack2bf(fmaf(v0, s[ct].x, sh[ct].x), fmaf(v1, s[ct].y, sh[ct].y)));
         st[1] = relu_bf16x2(pack2bf(fmaf(v2, s[ct].z, sh[ct].z), fmaf(v3, s[ct].w, sh[ct].w)));
       }
@@ -1283,6 +1293,29 @@ __device__ __forceinline__ void pp_issue_res(const PairArgs& a, TileXY t, int gw
 // bias + residual -> wave-private staging (swizzled like h) -> 16-byte coalesced NHWC stores
 __device__ __forceinline__ void pp_epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[2][ppk::BPT], const PPRes& r,
                                          unsigned char* ws, int gw, int lrow, int kq, bool act) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      a.out + (size_t)t.n * a.H * a.W * 32, (short)0, a.H * a.W * 64, 0x00020000);
+  if constexpr (PP_VAR & 16) {
+    // direct: 8-byte buffer stores from the accumulator layout (lane = 4 channels of one pixel; a
+    // 16-lane row covers 16 pixels x 8 B, the four kq rows and the two ct halves fill each pixel's
+    // 64 B in L2), no LDS staging round trip; 16 stores (PP_NST)
+#pragma unroll
+    for (int pt = 0; pt < ppk::BPT; ++pt) {
+      const int py = t.ty0 + 4 * gw + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+      const bool ok = act && py < a.H && px < a.W;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        u32x2 rv = r.rv[pt][ct];
+        asm volatile("" : "+v"(rv));
+        u32x2 st;
+        st[0] = pack2bf(acc[ct][pt][0] + r.bias[ct].x + lo_bf(rv[0]), acc[ct][pt][1] + r.bias[ct].y + hi_bf(rv[0]));
+        st[1] = pack2bf(acc[ct][pt][2] + r.bias[ct].z + lo_bf(rv[1]), acc[ct][pt][3] + r.bias[ct].w + hi_bf(rv[1]));
+        const int off = ok ? ((py * a.W + px) * 32 + ct * 16 + kq * 4) * 2 : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b64(st, rs, off, 0, 0);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     const int ow = lrow * 64 + ((((2 * ct) | (kq >> 1)) ^ ((lrow >> 1) & 3)) << 4) + (kq & 1) * 8;
@@ -1305,8 +1338,6 @@ __device__ __forceinline__ void pp_epi_b(const PairArgs& a, TileXY t, const f32x
   // this group's) gets an out-of-range offset and the range check drops it, so exactly PP_EPI_STORES
   // stores are issued on every path and the next P1's halo wait can be a counted vmcnt.  One unit in
   // flight at a time (the next halo's registers are live through this phase).
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      a.out + (size_t)t.n * a.H * a.W * 32, (short)0, a.H * a.W * 64, 0x00020000);
   const int py0 = t.ty0 + 4 * gw, px0 = t.tx0 + (lane >> 2);
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
@@ -1373,7 +1404,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
       tstamp = tn;
     }
   };
-  constexpr int NST = HEAD ? 32 : 8;  // buffer stores per P5 (counted wait in P1)
+  constexpr int NST = HEAD ? 32 : ((PP_VAR & 16) ? 16 : 8);  // buffer stores per P5 (counted wait in P1)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid0 = threadIdx.x;
   const int total = a.N * a.tiles_x * a.tiles_y;
@@ -1411,6 +1442,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
     // big register sets, which the allocator handled badly), only the global stores are predicated.
     const bool act = t < t1;
     const TileXY cur = tile_xy(a, act ? t : t1 - 1);
+    const bool inner = pp_interior(a, cur);  // tile-uniform: bounds-free commit / epilogue A
     f32x4 acc_a[2][ppk::APT];
     float4 sb[2], tb[2];
     PPSkip sk;
@@ -1419,15 +1451,20 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
       // P1: input chunk c -> activated image.  For c = 0 in flight: the halo (issued in P4), then
       // exactly the previous P5's NST buffer stores; the counted wait retires the halo only (the
       // builtin, so the compiler's own wait tracking sees it and adds no vmcnt(0) behind the stores).
-      if (c == 0) __builtin_amdgcn_s_waitcnt((NST & 0xf) | (0x7 << 4) | (0xf << 8) | ((NST >> 4) << 14));
+      constexpr int NW = (PP_VAR & 2) ? 0 : NST;
+      if (c == 0) __builtin_amdgcn_s_waitcnt((NW & 0xf) | (0x7 << 4) | (0xf << 8) | ((NW >> 4) << 14));
       int gc = gt0;
       asm volatile("" : "+v"(gc));  // per chunk: the unit addresses are recomputed, not kept across P2
-      pp_commit(a, cur, gc, halo, reg);
+      if (inner) pp_commit<true>(a, cur, gc, halo, reg);
+      else pp_commit<false>(a, cur, gc, halo, reg);
       pre(2 * c);
       __syncthreads();
       post(2 * c);
       // P2: stage A over chunk c (the next chunk's halo, or the epilogue operands, in flight)
-      if (c + 1 < NCA) pp_issue_halo<INMODE, CIN>(a, cur, c + 1, gt, halo);
+      if (c + 1 < NCA) {
+        if (inner) pp_issue_halo<INMODE, CIN, true>(a, cur, c + 1, gt, halo);
+        else pp_issue_halo<INMODE, CIN>(a, cur, c + 1, gt, halo);
+      }
       if (c == NCA - 1) {
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
@@ -1442,9 +1479,9 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
 #pragma unroll
           for (int j = 0; j < ppk::APT; ++j) acc_a[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(1);
       pp_mma_a(acc_a, reg, wl + c * 32 * ppk::WSTR, gw, lrow, kq);
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(0);
       pre(2 * c + 1);
       __syncthreads();
       post(2 * c + 1);
@@ -1452,7 +1489,15 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
     // P3: epilogue A -> h
     int g3 = gt0;
     asm volatile("" : "+v"(g3));
-    pp_epi_a<X2>(a, cur, acc_a, reg, sb, tb, sk, gw, g3 & 15, (g3 & 63) >> 4);
+    if (inner) pp_epi_a<X2, true>(a, cur, acc_a, reg, sb, tb, sk, gw, g3 & 15, (g3 & 63) >> 4);
+    else pp_epi_a<X2, false>(a, cur, acc_a, reg, sb, tb, sk, gw, g3 & 15, (g3 & 63) >> 4);
+    PPRes res;
+    if constexpr (PP_VAR & 1) pp_issue_res<RES>(a, cur, gw, g3 & 15, (g3 & 63) >> 4, res);
+    if constexpr (PP_VAR & 8) {  // the group's next halo two slots ahead of its commit
+      const TileXY nx = tile_xy(a, min(t + 2, t1 - 1));
+      if (pp_interior(a, nx)) pp_issue_halo<INMODE, CIN, true>(a, nx, 0, g3, halo);
+      else pp_issue_halo<INMODE, CIN>(a, nx, 0, g3, halo);
+    }
     pre(2 * NCA);
     __syncthreads();
     post(2 * NCA);
@@ -1463,15 +1508,14 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
     asm volatile("" : "+v"(g4));
     const int lrow4 = g4 & 15, kq4 = (g4 & 63) >> 4;
     f32x4 acc_b[2][ppk::BPT];
-    PPRes res;
-    pp_issue_res<RES>(a, cur, gw, lrow4, kq4, res);
+    if constexpr (!(PP_VAR & 1)) pp_issue_res<RES>(a, cur, gw, lrow4, kq4, res);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < ppk::BPT; ++j) acc_b[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(1);
     pp_mma_b(acc_b, reg, wb, gw, lrow4, kq4);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(0);
     pre(2 * NCA + 1);
     __syncthreads();
     post(2 * NCA + 1);
@@ -1481,10 +1525,16 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
     int g5 = gt0;
     asm volatile("" : "+v"(g5));
     const int lrow5 = g5 & 15, kq5 = (g5 & 63) >> 4;
-    pp_issue_halo<INMODE, CIN>(a, tile_xy(a, min(t + 2, t1 - 1)), 0, g5, halo);
+    auto next_halo = [&]() {
+      const TileXY nx = tile_xy(a, min(t + 2, t1 - 1));
+      if (pp_interior(a, nx)) pp_issue_halo<INMODE, CIN, true>(a, nx, 0, g5, halo);
+      else pp_issue_halo<INMODE, CIN>(a, nx, 0, g5, halo);
+    };
+    if constexpr (!(PP_VAR & 10)) next_halo();
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (HEAD) pp_epi_head(a, cur, acc_b, res, hr, gw, lrow5, kq5, act);
     else pp_epi_b(a, cur, acc_b, res, reg + gw * ppk::OUTW_B, gw, lrow5, kq5, act);
+    if constexpr (PP_VAR & 2) next_halo();
     pre(2 * NCA + 2);
     __syncthreads();
     post(2 * NCA + 2);
