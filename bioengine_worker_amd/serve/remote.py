@@ -48,11 +48,20 @@ class RemoteReplica(ReplicaBase):
         self.node_id = node.node_id
 
     async def start(self):
-        res = await self.node.service.start_replica(
-            tag=self.tag, app=self.app, dep=self.dep, payload=cloudpickle.dumps((self.cls, self.args, self.kwargs)),
-            gpu_ids=self.gpu_ids, env=self.env)
-        self.pid = res.get("pid")
+        # The node counts as busy from the moment a replica is placed on it, not once the start RPC
+        # returns: a slow start (replica imports on a loaded host) otherwise leaves it looking idle
+        # and the SLURM idle scale-down stops the node under the starting replica.
         self.node.replicas.add(self.tag)
+        self.node.last_busy = time.time()
+        try:
+            res = await self.node.service.start_replica(
+                tag=self.tag, app=self.app, dep=self.dep, payload=cloudpickle.dumps((self.cls, self.args, self.kwargs)),
+                gpu_ids=self.gpu_ids, env=self.env)
+        except BaseException:
+            self.node.replicas.discard(self.tag)
+            self.node.last_busy = time.time()
+            raise
+        self.pid = res.get("pid")
         self.state = RUNNING
 
     async def call(self, method: str, args, kwargs, model_id: str = ""):

@@ -1035,19 +1035,26 @@ int launch_pair(PairArgs a, int grid_cap, hipStream_t s) {
 #ifndef PP_VAR
 #define PP_VAR 1  // tuning variants (tools/build_native.py --variant ... --vflags=-DPP_VAR=n)
 #endif
+#ifndef PP_GW
+#define PP_GW 4  // waves per group (4: one per SIMD, 8: two per SIMD, 128 VGPRs)
+#endif
 namespace ppk {
-constexpr int GW = 4, GT = GW * 64;     // waves / threads per group
+constexpr int GW = PP_GW, GT = GW * 64;  // waves / threads per group
+constexpr int NTP = 2 * GT;              // threads per workgroup
+constexpr int RPW = TH / GW;             // stage-B output rows per wave
 constexpr int IN_B = IPIX * 64;         // 46080
 constexpr int H_B = RPIX * 64;          // 39168
-constexpr int OUTW_B = 4 * TW * 64;     // 8192: one wave's 4 x 32 output pixels
+constexpr int OUTW_B = RPW * TW * 64;   // one wave's RPW x 32 output pixels
 constexpr int RB = IN_B;                // one group's region
 constexpr int WSTR = 9 * 32 + 16;       // 304: weight row stride (elements; 8 (mod 16) dwords)
 constexpr int W_B = 32 * WSTR * 2;      // one conv's panel, bytes
-constexpr int APT = 10, BPT = 8;        // pixel tiles per wave: stage A (39 in 40 slots), stage B
+constexpr int APT = 40 / GW, BPT = 32 / GW;  // pixel tiles per wave: stage A (39 in 40 slots), stage B
+constexpr int TLAST0 = GW * (APT - 1);        // stage-A tile index of a wave's last slot, minus gw
 constexpr int HU = IPIX * 4;            // 16-byte halo units per tile
 constexpr int HUPT = (HU + GT - 1) / GT;
 static_assert(H_B <= RB && GW * OUTW_B <= RB, "ping-pong region overlays");
 static_assert(APT * GW >= RPT && (APT - 1) * GW <= 2 * RH && BPT * GW * 16 == TH * TW, "tile maps");
+static_assert(GW == 4 || GW == 8, "group size");
 }  // namespace ppk
 
 struct PPHalo {
@@ -1121,11 +1128,25 @@ __device__ __forceinline__ void pp_mma_a(f32x4 (&acc)[2][ppk::APT], const unsign
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr)
       A0[dx][pr] = b0 + dx * 64 + ((kq ^ (((((lrow + dx) >> 2) ^ par ^ pr) & 1) << 1)) << 4);
-  int ry9 = 8 * gw + (lrow >> 1), rx9 = 32 + (lrow & 1);
-  if (ry9 >= RH) { ry9 = 0; rx9 = 0; }  // padding lanes: valid data, never stored
-  int E[2];
+  // the wave's last slot: a row tile (8-wave groups, gw < 4) or an edge / padding tile
+  int L[3][2];
+  const int tl = gw + ppk::TLAST0;  // wave-uniform
+  if (tl < 2 * RH) {
+    const int ryl = tl >> 1, rxl = (tl & 1) * 16 + lrow;
 #pragma unroll
-  for (int pr = 0; pr < 2; ++pr) E[pr] = (ry9 * IW + rx9) * 64 + ((kq ^ ((((ry9 & 1) ^ pr) & 1) << 1)) << 4);
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+        L[dx][pr] = (ryl * IW + rxl + dx) * 64 + ((kq ^ (((((lrow + dx) >> 2) ^ ryl ^ pr) & 1) << 1)) << 4);
+  } else {
+    int ry9 = (tl - 2 * RH) * 8 + (lrow >> 1), rx9 = 32 + (lrow & 1);
+    if (ry9 >= RH) { ry9 = 0; rx9 = 0; }  // padding lanes: valid data, never stored
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+        L[dx][pr] = (ry9 * IW + rx9 + dx) * 64 + ((kq ^ ((((ry9 & 1) ^ pr) & 1) << 1)) << 4);
+  }
   auto frags = [&](int ks, bf16x8 (&af)[2], bf16x8 (&bf)[ppk::APT]) {
     const int dy = ks / 3, dx = ks % 3;
 #pragma unroll
@@ -1133,8 +1154,8 @@ __device__ __forceinline__ void pp_mma_a(f32x4 (&acc)[2][ppk::APT], const unsign
       af[ct] = *reinterpret_cast<const bf16x8*>(wa + (ct * 16 + lrow) * ppk::WSTR + ks * 32 + kq * 8);
 #pragma unroll
     for (int j = 0; j < ppk::APT - 1; ++j)
-      bf[j] = *reinterpret_cast<const bf16x8*>(rin + A0[dx][dy & 1] + j * 2 * IW * 64 + dy * IW * 64);
-    bf[ppk::APT - 1] = *reinterpret_cast<const bf16x8*>(rin + E[dy & 1] + dx * 64 + dy * IW * 64);
+      bf[j] = *reinterpret_cast<const bf16x8*>(rin + A0[dx][dy & 1] + j * (ppk::GW / 2) * IW * 64 + dy * IW * 64);
+    bf[ppk::APT - 1] = *reinterpret_cast<const bf16x8*>(rin + L[dx][dy & 1] + dy * IW * 64);
   };
   // one pixel-fragment set, rolling reload: each pixel fragment of K-step ks + 1 is read right after
   // its last MFMA of step ks (80 accumulator VGPRs leave no room for a second set); the two weight
@@ -1156,9 +1177,9 @@ __device__ __forceinline__ void pp_mma_a(f32x4 (&acc)[2][ppk::APT], const unsign
       }
       if (more) {
         if (j < ppk::APT - 1)
-          bf[j] = *reinterpret_cast<const bf16x8*>(rin + A0[dx][dy & 1] + j * 2 * IW * 64 + dy * IW * 64);
+          bf[j] = *reinterpret_cast<const bf16x8*>(rin + A0[dx][dy & 1] + j * (ppk::GW / 2) * IW * 64 + dy * IW * 64);
         else
-          bf[j] = *reinterpret_cast<const bf16x8*>(rin + E[dy & 1] + dx * 64 + dy * IW * 64);
+          bf[j] = *reinterpret_cast<const bf16x8*>(rin + L[dx][dy & 1] + dy * IW * 64);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1174,16 +1195,29 @@ struct PPSkip {
   u32x2 xv[ppk::APT][2];
 };
 
+// the h pixel (ry, rx) of a wave's last stage-A slot: a row tile (8-wave groups, gw < 4) or an
+// edge / padding tile; false for padding lanes
+__device__ __forceinline__ bool pp_last(int gw, int lrow, int& ry, int& rx) {
+  const int tl = gw + ppk::TLAST0;
+  if (tl < 2 * RH) {
+    ry = tl >> 1;
+    rx = (tl & 1) * 16 + lrow;
+    return true;
+  }
+  ry = (tl - 2 * RH) * 8 + (lrow >> 1);
+  rx = 32 + (lrow & 1);
+  return ry < RH;
+}
+
 __device__ __forceinline__ void pp_issue_skip(const PairArgs& a, TileXY t, int gw, int lrow, int kq, PPSkip& sk) {
 #pragma unroll
   for (int j = 0; j < ppk::APT; ++j) {
     int ry, rx;
     if (j < ppk::APT - 1) {
-      ry = (gw >> 1) + 2 * j;
+      ry = (gw >> 1) + (ppk::GW / 2) * j;
       rx = (gw & 1) * 16 + lrow;
     } else {
-      ry = 8 * gw + (lrow >> 1);
-      rx = 32 + (lrow & 1);
+      pp_last(gw, lrow, ry, rx);
     }
     // clamped, unconditional: pp_epi_a stores zero outside the image and nothing for padding lanes
     const int gy = min(max(t.ty0 - 1 + ry, 0), a.H - 1), gx = min(max(t.tx0 - 1 + rx, 0), a.W - 1);
@@ -1206,13 +1240,11 @@ __device__ __forceinline__ void pp_epi_a(const PairArgs& a, TileXY t, const f32x
     for (int j = 0; j < ppk::APT; ++j) {
       int ry, rx, off;
       if (j < ppk::APT - 1) {
-        ry = (gw >> 1) + 2 * j;
+        ry = (gw >> 1) + (ppk::GW / 2) * j;
         rx = (gw & 1) * 16 + lrow;
-        off = hw + j * 2 * RW * 64;
+        off = hw + j * (ppk::GW / 2) * RW * 64;
       } else {
-        ry = 8 * gw + (lrow >> 1);
-        rx = 32 + (lrow & 1);
-        if (ry >= RH) continue;
+        if (!pp_last(gw, lrow, ry, rx)) continue;
         off = (ry * RW + rx) * 64 + ((hc ^ ((rx >> 1) & 3)) << 4) + (kq & 1) * 8;
       }
       const int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
@@ -1232,12 +1264,12 @@ __device__ __forceinline__ void pp_epi_a(const PairArgs& a, TileXY t, const f32x
   }
 }
 
-// stage B: wave gw owns output rows 4 gw .. 4 gw + 3; pixel tile pt = row (pt >> 1), half (pt & 1)
+// stage B: wave gw owns output rows RPW gw .. RPW gw + RPW - 1; pixel tile pt = row (pt >> 1), half (pt & 1)
 __device__ __forceinline__ void pp_mma_b(f32x4 (&acc)[2][ppk::BPT], const unsigned char* rh, const bf16_t* wb, int gw,
                                          int lrow, int kq) {
   int B0[3];
 #pragma unroll
-  for (int dx = 0; dx < 3; ++dx) B0[dx] = ((4 * gw) * RW + lrow + dx) * 64 + ((kq ^ (((lrow + dx) >> 1) & 3)) << 4);
+  for (int dx = 0; dx < 3; ++dx) B0[dx] = ((ppk::RPW * gw) * RW + lrow + dx) * 64 + ((kq ^ (((lrow + dx) >> 1) & 3)) << 4);
   auto frags = [&](int ks, bf16x8 (&af)[2], bf16x8 (&bf)[ppk::BPT]) {
     const int dy = ks / 3, dx = ks % 3;
 #pragma unroll
@@ -1280,7 +1312,7 @@ template <int RES>
 __device__ __forceinline__ void pp_issue_res(const PairArgs& a, TileXY t, int gw, int lrow, int kq, PPRes& r) {
 #pragma unroll
   for (int pt = 0; pt < ppk::BPT; ++pt) {
-    const int py = min(t.ty0 + 4 * gw + (pt >> 1), a.H - 1), px = min(t.tx0 + (pt & 1) * 16 + lrow, a.W - 1);
+    const int py = min(t.ty0 + ppk::RPW * gw + (pt >> 1), a.H - 1), px = min(t.tx0 + (pt & 1) * 16 + lrow, a.W - 1);
     const bf16_t* rp = RES == 1 ? a.res + (((size_t)t.n * a.H + py) * a.W + px) * 32 + kq * 4
                                 : a.res + (((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1)) * 32 + kq * 4;
 #pragma unroll
@@ -1301,7 +1333,7 @@ __device__ __forceinline__ void pp_epi_b(const PairArgs& a, TileXY t, const f32x
     // 64 B in L2), no LDS staging round trip; 16 stores (PP_NST)
 #pragma unroll
     for (int pt = 0; pt < ppk::BPT; ++pt) {
-      const int py = t.ty0 + 4 * gw + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+      const int py = t.ty0 + ppk::RPW * gw + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
       const bool ok = act && py < a.H && px < a.W;
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
@@ -1338,9 +1370,9 @@ __device__ __forceinline__ void pp_epi_b(const PairArgs& a, TileXY t, const f32x
   // this group's) gets an out-of-range offset and the range check drops it, so exactly PP_EPI_STORES
   // stores are issued on every path and the next P1's halo wait can be a counted vmcnt.  One unit in
   // flight at a time (the next halo's registers are live through this phase).
-  const int py0 = t.ty0 + 4 * gw, px0 = t.tx0 + (lane >> 2);
+  const int py0 = t.ty0 + ppk::RPW * gw, px0 = t.tx0 + (lane >> 2);
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
+  for (int it = 0; it < 2 * ppk::RPW; ++it) {
     const int py = py0 + (it >> 1), px = px0 + (it & 1) * 16;
     const u32x4 v = *reinterpret_cast<const u32x4*>(ws + rd + it * 1024);
     const int off = (act && py < a.H && px < a.W) ? ((py * a.W + px) * 32 + (lane & 3) * 8) * 2 : 0x7ffffff0;
@@ -1369,7 +1401,7 @@ __device__ __forceinline__ void pp_epi_head(const PairArgs& a, TileXY t, const f
       bw[2 * ct + 1] = relu_bf16x2(pack2bf(fmaf(lo_bf(o1), hr.s[ct].z, hr.t[ct].z), fmaf(hi_bf(o1), hr.s[ct].w, hr.t[ct].w)));
     }
     const f32x4 y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hr.w, *reinterpret_cast<const bf16x8*>(&bw), zero, 0, 0, 0);
-    const int py = t.ty0 + 4 * gw + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
+    const int py = t.ty0 + ppk::RPW * gw + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
     const bool ok = act && py < a.H && px < a.W;
     const float bb[4] = {hr.b.x, hr.b.y, hr.b.z, hr.b.w};
 #pragma unroll
@@ -1384,7 +1416,7 @@ __device__ __forceinline__ void pp_epi_head(const PairArgs& a, TileXY t, const f
 // NCA input chunks of 32 channels (Cin = 32 NCA), INMODE 0 (full resolution) or 1 (nearest 2x up),
 // X2: + skip operand on stage A's output, RES 1 (full) or 2 (up2 of a half-resolution map).
 template <int NCA, int INMODE, bool X2, int RES, bool HEAD, bool STAMP = false>
-__global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
+__global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_kernel(PairArgs a) {
   constexpr int CIN = 32 * NCA;
   // STAMP (diagnostics, tools/pp_phase_profile.py): wave 0 of each group accumulates s_memtime
   // cycles of every phase's own work and of its wait at the closing barrier, [grid][2 groups][16]
@@ -1404,7 +1436,8 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
       tstamp = tn;
     }
   };
-  constexpr int NST = HEAD ? 32 : ((PP_VAR & 16) ? 16 : 8);  // buffer stores per P5 (counted wait in P1)
+  // buffer stores per P5 (counted wait in P1)
+  constexpr int NST = HEAD ? 4 * ppk::BPT : ((PP_VAR & 16) ? 2 * ppk::BPT : 2 * ppk::RPW);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid0 = threadIdx.x;
   const int total = a.N * a.tiles_x * a.tiles_y;
@@ -1414,14 +1447,14 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
   bf16_t* wl = reinterpret_cast<bf16_t*>(smem + 2 * ppk::RB);
   // NCA stage-A panels then the stage-B panel, [32 rows][304] each (from the packed [Cout][NCA][288]
   // and [Cout][1][288] layouts)
-  for (int u = tid0; u < (NCA + 1) * 32 * 36; u += NT) {
+  for (int u = tid0; u < (NCA + 1) * 32 * 36; u += ppk::NTP) {
     const int pnl = u / (32 * 36), q = u % (32 * 36), r = q / 36, k8 = q % 36;
     const bf16_t* src = pnl < NCA ? a.wa + ((size_t)r * NCA + pnl) * 288 + k8 * 8 : a.wb + (size_t)r * 288 + k8 * 8;
     *reinterpret_cast<u32x4*>(wl + pnl * 32 * ppk::WSTR + r * ppk::WSTR + k8 * 8) = *reinterpret_cast<const u32x4*>(src);
   }
   const bf16_t* wb = wl + NCA * 32 * ppk::WSTR;
   // wave-uniform values in SGPRs (readfirstlane): the group / wave-in-group branches stay scalar
-  const int grp = __builtin_amdgcn_readfirstlane(tid0 >> 8);  // waves 0-3 | 4-7 (w and w + 4 share a SIMD)
+  const int grp = __builtin_amdgcn_readfirstlane(tid0 / ppk::GT);  // waves 0..GW-1 | GW..2GW-1 (w, w + GW share a SIMD)
   const int gt0 = tid0 & (ppk::GT - 1);
   unsigned char* reg = smem + grp * ppk::RB;
   HeadRegs hr;
@@ -1541,7 +1574,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pair_pp_kernel(PairArgs a) {
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   if constexpr (STAMP) {
-    if ((tid0 & 255) < 16) {  // wave 0 of each group: lane k stores slot k (lane-indexed vector store)
+    if ((tid0 & (ppk::GT - 1)) < 16) {  // wave 0 of each group: lane k stores slot k (lane-indexed vector store)
       const int k = tid0 & 15;
       unsigned long long v = 0;
 #pragma unroll
@@ -1584,10 +1617,10 @@ int launch_pair_pp(PairArgs a, int grid_cap, hipStream_t s) {
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_st = true;
     }
-    hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, true>), dim3(g), dim3(NT), lds, s, a);
+    hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, true>), dim3(g), dim3(ppk::NTP), lds, s, a);
     return BE_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD>), dim3(g), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD>), dim3(g), dim3(ppk::NTP), lds, s, a);
   return BE_CHECK_LAUNCH();
 }
 }  // namespace
