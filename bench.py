@@ -517,8 +517,9 @@ def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int, force_dp: 
 def bench_cpsam_infer(dev, batch: int = 8, steps: int = 4, lat_n: int = 10) -> dict:
     """Cellpose-SAM inference -- the reference app's default ``infer`` model
     (apps/cellpose-finetuning/main.py:4966-5144, bf16 Transformer :126-127): 512x512x3 images through
-    cellpose 4's 256-tile / 0.1-overlap path (9 tiles per image), the ViT-L/8 engine on the in-house
-    GEMMs replayed from its HIP graph, taper blend, dynamics (niter 200), flow QC and fill holes.
+    cellpose 4's 256-tile / 0.1-overlap path (9 tiles per image), the ViT-L/8 engine (HIP attention,
+    rel-pos, LayerNorm, bias-GELU; hipBLASLt linear layers after the A/B against the in-house GEMM)
+    replayed from its HIP graph, taper blend, dynamics (niter 200), flow QC and fill holes.
     Random-init weights, synthetic images."""
     from bioengine_worker_amd.cellpose.pipeline import CellposeRunner, EvalParams, synthetic_cells
     from bioengine_worker_amd.models.cpsam import CPSAM

@@ -31,6 +31,7 @@ import os
 
 from ..ops.conv import PackedConv, fused_conv2d
 from ..ops.transformer import add_layernorm, attention_ref, bias_gelu_, flash_attention
+from ..ops.vit_train import relpos_fwd
 
 
 def get_rel_pos(q_size: int, k_size: int, rel_pos: torch.Tensor) -> torch.Tensor:
@@ -203,6 +204,9 @@ class CPSAMEngine:
                 qkv_b=bf(blk.attn.qkv.bias), proj_w=bf(blk.attn.proj.weight), proj_b=bf(blk.attn.proj.bias),
                 Rh=f32(get_rel_pos(g, g, blk.attn.rel_pos_h.detach())),
                 Rw=f32(get_rel_pos(g, g, blk.attn.rel_pos_w.detach())),
+                # the [2g-1, c] tables themselves for the MFMA rel-pos kernel (gather inside)
+                tab_h=f32(blk.attn.rel_pos_h) if blk.attn.rel_pos_h.shape[0] == 2 * g - 1 else None,
+                tab_w=f32(blk.attn.rel_pos_w) if blk.attn.rel_pos_w.shape[0] == 2 * g - 1 else None,
                 n2w=f32(blk.norm2.weight), n2b=f32(blk.norm2.bias), l1_w=bf(blk.mlp.lin1.weight),
                 l1_b=f32(blk.mlp.lin1.bias), l2_w=bf(blk.mlp.lin2.weight), l2_b=bf(blk.mlp.lin2.bias)))
         self.neck0 = bf(e.neck[0].weight.reshape(e.neck[0].weight.shape[0], -1))
@@ -217,11 +221,18 @@ class CPSAMEngine:
     #: batch 8: lib 99.7 img/s, mt 84.4 / 84.8 (profiles/r05/cpsam/infer_mt_vs_lib_s23.jsonl): the
     #: in-house GEMM trails hipBLASLt by 10-15 % per forward shape, so the library stays the default.
     GEMM = os.environ.get("BE_CPSAM_INFER_GEMM", "lib")
+    #: rel-pos terms: "hip" (relpos.hip MFMA kernel, default) or "torch" (fp32 einsums; A/B only)
+    RELPOS = os.environ.get("BE_CPSAM_RELPOS", "hip")
 
     def _gemms(self):
-        if self.GEMM == "lib":
+        if self.GEMM in ("lib", "hyb"):
             def lin(x, w, b=None):
                 return F.linear(x, w, b)
+
+            if self.GEMM == "hyb":  # lin1 on the macro-tile GEMM with bias + exact GELU fused
+                from ..ops import gemm_mt
+
+                return lin, gemm_mt.linear_gelu_only
 
             def lin_gelu(x, w, b):
                 return bias_gelu_(F.linear(x, w), b)
@@ -245,7 +256,13 @@ class CPSAMEngine:
         for i, b in enumerate(blocks):
             qkv = lin(h.view(B * N, D), b["qkv_w"], b["qkv_b"]).view(B, N, 3, Hh, D // Hh)
             q = qkv[:, :, 0]
-            rel_h, rel_w = rel_pos_terms(q, b["Rh"], b["Rw"], g, g)
+            if b["tab_h"] is not None and b["tab_w"] is not None and q.is_cuda and self.RELPOS == "hip":
+                # relpos.hip (the training engine's kernel): q . R on MFMA straight from the strided
+                # q view; the fp32 einsums it replaces were ~21 % of the forward's kernel time
+                # (q.float() copies, permuted outputs, fp32 library GEMMs; profiles/r05/kt/cpi_stats.txt)
+                rel_h, rel_w = relpos_fwd(q, b["tab_h"], b["tab_w"])
+            else:
+                rel_h, rel_w = rel_pos_terms(q, b["Rh"], b["Rw"], g, g)
             a = flash_attention(q, qkv[:, :, 1], qkv[:, :, 2], (D // Hh) ** -0.5, rel_h, rel_w).view(B * N, D)
             y = lin(a, b["proj_w"], b["proj_b"]).view(B, N, D)
             h2 = add_layernorm(t, y, None, b["n2w"], b["n2b"])
