@@ -191,11 +191,13 @@ def _plan_launch(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps
     B, nlab = bbox.shape[:2]
     dev = bbox.device
     n = B * nlab
-    split = kind == 0 and counts is not None
+    split = kind in (0, 2) and counts is not None
     if split:
         assert counts.shape == (B, nlab) and counts.dtype == torch.int32
         px_counts = counts.contiguous()
-    nb = len(caps) + 1 + int(split)
+    # kind 2 (needs counts): the compact work-queue buckets (wave jobs, workgroup jobs) in front of
+    # kind 0's buckets, which keep the masks the queue kernel cannot take
+    nb = len(caps) + 1 + int(split) + (2 if kind == 2 and split else 0)
     jobs = torch.empty(nb, max(n, 1), 4, dtype=torch.int64, device=dev)
     bucket_n = torch.zeros(nb, dtype=torch.int32, device=dev)
     tot = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -207,6 +209,14 @@ def _plan_launch(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps
                  len(caps), _native.ptr(jobs), _native.ptr(bucket_n), _native.ptr(tot), _native.ptr(niter_img),
                  _native.stream(dev))
     return jobs, bucket_n, tot, niter_img
+
+
+#: compact work-queue diffusion (be_cp_diffuse_q) for the masks it can take; 0 = the LDS-box buckets
+DIFFUSE_QUEUE = os.environ.get("BE_DIFFUSE_QUEUE", "1") != "0"
+
+
+def _diffuse_plan_kind() -> int:
+    return 2 if DIFFUSE_QUEUE else 0
 
 
 def _diffuse_lds_bytes(ly, lx):
@@ -405,8 +415,11 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
     if nlab <= 1:
         return mu, (torch.zeros(B, nlab, device=dev) if dp is not None else None), counts
     if plan is None:
-        plan = _plan_finish([_plan_launch(mask_bboxes(M, nlab), None, 0, DIFFUSE_CAPS, counts)])[0]
+        plan = _plan_finish([_plan_launch(mask_bboxes(M, nlab), None, _diffuse_plan_kind(), DIFFUSE_CAPS, counts)])[0]
     slices, ssize, niter_img = plan
+    qjobs = None
+    if len(slices) == len(DIFFUSE_BUCKETS) + 4:  # kind 2: queue buckets first
+        qjobs, slices = slices[:2], slices[2:]
     if niter is not None:
         niter_img = torch.full((B,), niter, dtype=torch.int32, device=dev)
     bj = slices[-1]
@@ -428,6 +441,12 @@ def masks_to_flows_gpu(M: torch.Tensor, dp: torch.Tensor | None = None, niter: i
             ready.record(torch.cuda.current_stream(dev))
     else:
         release = None
+    if qjobs is not None and (qjobs[0].shape[0] or qjobs[1].shape[0]):
+        # one persistent launch over every mask the compact kernel takes (nearly all of them),
+        # queued first: the box-bucket kernels below then only see the rare leftovers
+        qws = torch.empty(2, dtype=torch.int32, device=dev)
+        _native.call("be_cp_diffuse_q", _native.ptr(Mc), _native.ptr(qjobs[0]), qjobs[0].shape[0], _native.ptr(qjobs[1]),
+                     qjobs[1].shape[0], H, W, _native.ptr(niter_img), _native.ptr(L), _native.ptr(qws), st)
     if bj.shape[0]:
         # first, on an idle device: the centre kernel runs alone (~0.07 ms instead of ~0.36 ms
         # among the bucket kernels), then the cooperative tiled sweep -- the critical path -- is
@@ -564,7 +583,7 @@ def compute_masks_gpu(y: torch.Tensor, niter: int = 200, cellprob_threshold: flo
     # masks below min_size are dropped whatever their flow error: the QC diffusion skips them (the
     # plan still takes cellpose's per-image niter over ALL masks, so the kept masks' flows are
     # unchanged)
-    plans = _plan_finish(([_plan_launch(bbox, fill_keep, 0, DIFFUSE_CAPS, counts)] if qc else [])
+    plans = _plan_finish(([_plan_launch(bbox, fill_keep, _diffuse_plan_kind(), DIFFUSE_CAPS, counts)] if qc else [])
                          + [_plan_launch(bbox, fill_keep, 1, [LDS_FILL_BYTES])])
     if qc:
         _, err, _ = masks_to_flows_gpu(M, dp=y, nlab=nlab, counts=counts, plan=plans[0], want_mu=False)

@@ -569,6 +569,230 @@ __global__ __launch_bounds__(MT) void fill_holes_kernel(const int* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Compact heat diffusion on one persistent work queue (flow QC and training targets, every mask
+// of <= DQ_BCAP pixels).  The box-shaped kernels above keep the mask's whole bounding box in LDS,
+// and the masks of the headline batch fill 14 % of their boxes (tools/mask_census.py), so most of
+// their LDS and threads hold zeros; they also ran as six launches per batch on three streams, each
+// with its own tail.  Here a mask is its pixel list only: raster-ordered ranks, heat values
+// indexed by rank (+ one zero slot that stands for every non-mask neighbour), and per pixel the
+// byte offsets of its 3x3 neighbours, found once by binary search over the sorted list and then
+// kept in registers for all iterations.  Masks of <= 256 pixels are one WAVE's job (no barrier at
+// all: the wave's LDS accesses are ordered), larger ones a workgroup's; each wave / workgroup
+// pulls its next job from a global counter, so the chip stays full until the queue drains.
+// Sums are formed in the sparse sweep's order (rows of 3, then the 3 row sums) and the centre
+// source is stored as T + 1 at the centre (the dense sweep's cur[ce] += 1), the unshifted value
+// kept in the owner's register: results are bit-identical to diffuse_kernel.
+constexpr int DQ_T = 512, DQ_K = 4;
+constexpr int DQ_WCAP = 64 * DQ_K, DQ_WHX = 256;   // wave jobs: pixels, box width + 2
+constexpr int DQ_BCAP = DQ_T * DQ_K, DQ_BHX = 1024;  // workgroup jobs
+template <int CAP, int HX>
+struct DQL {
+  static constexpr int T_B = 2 * (CAP + 1) * 8;  // two heat buffers, slot CAP = the zero slot
+  static constexpr int BYTES = T_B + CAP * 4 + HX * 4 + 64;
+};
+using DQW = DQL<DQ_WCAP, DQ_WHX>;
+using DQB = DQL<DQ_BCAP, DQ_BHX>;
+constexpr int DQ_LDS = 8 * DQW::BYTES > DQB::BYTES ? 8 * DQW::BYTES : DQB::BYTES;
+static_assert(DQ_T == 512 && DQW::BYTES % 16 == 0 && DQ_LDS <= 64 * 1024, "diffuse queue LDS layout");
+
+// smallest bin i with sum(h[0..i]) > k (one wave)
+__device__ __forceinline__ int dq_kth(const int* h, int n, int k, int lane) {
+  int acc = 0;
+  for (int b0 = 0; b0 < n; b0 += 64) {
+    int inc = b0 + lane < n ? h[b0 + lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    const unsigned long long bal = __ballot(acc + inc > k);
+    if (bal) return b0 + __ffsll((unsigned long long)bal) - 1;
+    acc += __shfl(inc, 63, 64);
+  }
+  return n - 1;
+}
+
+template <int NTH, int CAP, int HX>
+__device__ __forceinline__ void dq_job(const MaskJob& J, const int* __restrict__ M, int H, int W,
+                                       const int* __restrict__ niter_img, double* __restrict__ Lout, unsigned char* lds,
+                                       int t) {
+  constexpr int K = CAP / NTH;
+  double* T0 = reinterpret_cast<double*>(lds);
+  double* T1 = T0 + CAP + 1;
+  int* list = reinterpret_cast<int*>(T1 + CAP + 1);
+  int* hx = list + CAP;
+  unsigned long long* best = reinterpret_cast<unsigned long long*>(hx + HX);
+  float* med = reinterpret_cast<float*>(best + 1);
+  int* wc = reinterpret_cast<int*>(med + 2);  // NTH / 64 wave counts (workgroup jobs)
+  auto sync = [&]() {
+    if constexpr (NTH == 64) {  // one wave: its LDS accesses complete in order; compiler ordering only
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
+  const int lane = t & 63;
+  const int RX = J.lx + 2;
+  const int ncell = J.ly * J.lx;
+  const int* Mb = M + (size_t)J.b * H * W;
+  for (int i = t; i < RX; i += NTH) hx[i] = 0;
+  if (t == 0) *best = ~0ull;
+  sync();
+  // the mask's pixels in raster order (ranks = ballot prefix counts), x histogram for the median
+  int P = 0;
+  for (int c0 = 0; c0 < ncell; c0 += NTH) {
+    const int c = c0 + t;
+    int cy = 0, cx = 0;
+    bool m = false;
+    if (c < ncell) {
+      cy = c / J.lx;
+      cx = c - cy * J.lx;
+      m = Mb[(size_t)(J.y0 + cy) * W + J.x0 + cx] == J.lab;
+    }
+    const unsigned long long bal = __ballot(m);
+    int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+    int tot = __popcll(bal);
+    if constexpr (NTH > 64) {
+      if (lane == 0) wc[t >> 6] = tot;
+      sync();
+      int pre = 0;
+      tot = 0;
+#pragma unroll
+      for (int w = 0; w < NTH / 64; ++w) {
+        const int x = wc[w];
+        pre += w < (t >> 6) ? x : 0;
+        tot += x;
+      }
+      rank += pre;
+    }
+    if (m && P + rank < CAP) {
+      list[P + rank] = (cy + 1) * RX + cx + 1;
+      atomicAdd(&hx[cx + 1], 1);
+    }
+    P += tot;
+    if constexpr (NTH > 64) sync();  // wc is rewritten by the next chunk
+  }
+  P = min(P, CAP);  // (the planner sized the job from the exact pixel count)
+  sync();
+  if (P == 0) return;
+  // exact medians in padded-box coordinates (numpy: mean of the two middle values); the list is
+  // raster-ordered, so its ry are sorted
+  if (t < 64) {
+    const int k1 = (P - 1) / 2, k2 = P / 2;
+    const int y1 = list[k1] / RX, y2 = list[k2] / RX;
+    const int x1 = dq_kth(hx, RX, k1, lane), x2 = dq_kth(hx, RX, k2, lane);
+    if (lane == 0) {
+      med[0] = 0.5f * (float)(y1 + y2);
+      med[1] = 0.5f * (float)(x1 + x2);
+    }
+  }
+  sync();
+  int myr[K], off[K][9];
+  bool own[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int r = t + j * NTH;
+    own[j] = r < P;
+    myr[j] = own[j] ? r : CAP;
+    if (own[j]) {
+      const int e = list[r];
+      const float dy = (float)(e / RX) - med[0], dx = (float)(e % RX) - med[1];
+      const float d = dx * dx + dy * dy;  // exact: half-integer coordinates
+      atomicMin(best, ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)r);  // ties: raster order
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        if (k == 4) { off[j][k] = r * 8; continue; }
+        const int e2 = e + (k / 3 - 1) * RX + (k % 3 - 1);
+        int lo = 0, hi = P;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (list[mid] < e2) lo = mid + 1;
+          else hi = mid;
+        }
+        off[j][k] = (lo < P && list[lo] == e2 ? lo : CAP) * 8;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) off[j][k] = CAP * 8;
+    }
+  }
+  for (int i = t; i < P; i += NTH) { T0[i] = 0.0; T1[i] = 0.0; }
+  if (t == 0) { T0[CAP] = 0.0; T1[CAP] = 0.0; }
+  sync();
+  const int cidx = (int)(*best & 0xffffffffu);
+  if (t == 0) T0[cidx] = 1.0;  // S = T + e_c: the centre source of the first sweep
+  sync();
+  const int niter = niter_img[J.b];
+  const int nsl = (P + NTH - 1) / NTH;  // slots in use (uniform)
+  double* cur = T0;
+  double* nxt = T1;
+  double tc = 0.0;  // the centre's own (unshifted) value, in its owner's register
+  for (int it = 0; it < niter; ++it) {
+    const unsigned char* cb = reinterpret_cast<const unsigned char*>(cur);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j < nsl) {
+        double v[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) v[k] = *reinterpret_cast<const double*>(cb + off[j][k]);
+        const double hp = v[0] + v[1] + v[2];
+        const double hc = v[3] + v[4] + v[5];
+        const double hn = v[6] + v[7] + v[8];
+        const double tn = (hp + hc + hn) * (1.0 / 9.0);
+        const bool isc = myr[j] == cidx;
+        if (isc) tc = tn;
+        if (own[j]) nxt[myr[j]] = isc ? tn + 1.0 : tn;
+      }
+    }
+    sync();
+    double* tt = cur; cur = nxt; nxt = tt;
+  }
+  double* Lb = Lout + (size_t)J.b * H * W;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (!own[j]) continue;
+    const int e = list[myr[j]];
+    const int ry = e / RX, rx = e - ry * RX;
+    const double val = myr[j] == cidx ? tc : cur[myr[j]];
+    Lb[(size_t)(J.y0 + ry - 1) * W + (J.x0 + rx - 1)] = log1p(val);
+  }
+  sync();  // the LDS slot is reused by the next job
+}
+
+// q[0] / q[1]: workgroup / wave job cursors (zeroed by the launcher).  Workgroup jobs first (all
+// waves), then every wave drains the wave-job queue on its own; every wave exits once both cursors
+// pass their counts.
+__global__ __launch_bounds__(DQ_T) void diffuse_q_kernel(const int* __restrict__ M, const MaskJob* __restrict__ wjobs,
+                                                         int nw, const MaskJob* __restrict__ bjobs, int nb, int H, int W,
+                                                         const int* __restrict__ niter_img, double* __restrict__ Lout,
+                                                         unsigned* __restrict__ q) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int sj;
+  const int t = threadIdx.x;
+  for (;;) {
+    if (t == 0) sj = (int)atomicAdd(q, 1u);
+    __syncthreads();
+    const int j = sj;
+    __syncthreads();
+    if (j >= nb) break;
+    const MaskJob J = bjobs[j];
+    dq_job<DQ_T, DQ_BCAP, DQ_BHX>(J, M, H, W, niter_img, Lout, smem, t);
+  }
+  const int lane = t & 63;
+  unsigned char* slot = smem + (t >> 6) * DQW::BYTES;
+  for (;;) {
+    int j = 0;
+    if (lane == 0) j = (int)atomicAdd(q + 1, 1u);
+    j = __builtin_amdgcn_readfirstlane(__shfl(j, 0, 64));
+    if (j >= nw) break;
+    const MaskJob J = wjobs[j];
+    dq_job<64, DQ_WCAP, DQ_WHX>(J, M, H, W, niter_img, Lout, slot, lane);
+  }
+}
+
 // LDS variant with a block size matched to the masks (the launcher buckets small masks by their
 // LDS need, so a 20x20 mask no longer reserves the 48 KiB of the largest one).  dv = rows per work
 // item of the sliding-window sweep: 4 gives each mask twice the lanes and half the serial LDS
@@ -645,6 +869,35 @@ int be_cp_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, co
     fprintf(stderr, "be_cp_diffuse_nt(njobs=%d, lds=%d, threads=%d, dv=%d): %s\n", njobs, lds_bytes, threads, dv,
             hipGetErrorString(e));
   return (int)e;
+}
+
+// Compact work-queue diffusion (see diffuse_q_kernel): wjobs = masks of <= 256 pixels with box
+// width + 2 <= 256, bjobs = <= 2048 pixels, box width + 2 <= 1024 (plan kind 2 buckets 0 / 1);
+// q: >= 8 bytes of device memory (the two job cursors).
+int be_cp_diffuse_q(const int* M, const void* wjobs, int nw, const void* bjobs, int nb, int H, int W, const int* niter_img,
+                    double* Lout, unsigned* q, hipStream_t s) {
+  if (nw + nb == 0) return 0;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  const int want = max(nb, (nw + 7) / 8);
+  const int grid = max(1, min(want, 3 * ncu));  // 3 workgroups (49 KiB LDS each) per CU
+  (void)hipMemsetAsync(q, 0, 8, s);
+  hipLaunchKernelGGL(diffuse_q_kernel, dim3(grid), dim3(DQ_T), DQ_LDS, s, M, (const MaskJob*)wjobs, nw,
+                     (const MaskJob*)bjobs, nb, H, W, niter_img, Lout, q);
+  return BE_CHECK_LAUNCH();
+}
+
+int be_cp_diffuse_q_caps(int* out4) {
+  out4[0] = DQ_WCAP;
+  out4[1] = DQ_WHX;
+  out4[2] = DQ_BCAP;
+  out4[3] = DQ_BHX;
+  return 0;
 }
 
 int be_cp_diffuse_tile_params(int* out3) {
@@ -749,11 +1002,28 @@ __global__ __launch_bounds__(256) void plan_masks_kernel(const int* __restrict__
   const int y0 = bb[0], y1 = bb[1], x0 = bb[2], x1 = bb[3];
   if (lab == 0 || y1 < 0) return;
   const int ly = y1 - y0 + 1, lx = x1 - x0 + 1;
+  // kind 2 = kind 0 with the compact work-queue buckets in front: 0 = wave jobs, 1 = workgroup
+  // jobs (diffuse_q_kernel), 2.. = kind 0's buckets for the masks those cannot take
+  const int q2 = kind == 2 ? 2 : 0;
+  if (kind == 2) kind = 0;
   if (kind == 0) atomicMax(niter_img + b, 2 * (ly + lx + 2));  // 2 * ((y1-y0)+(x1-x0)+4)
   if (valid && !valid[i]) return;
   const long long RY = ly + 2, RX = lx + 2, R = RY * RX;
   const long long need = kind == 0 ? 16 * R + 4 * (RY + RX) + R + 16 : R;
   int k = 0;
+  if (q2 && cnts) {
+    const long long c = cnts[i];
+    int kq = -1;
+    if (c <= DQ_WCAP && RX <= DQ_WHX) kq = 0;
+    else if (c <= DQ_BCAP && RX <= DQ_BHX) kq = 1;
+    if (kq >= 0) {
+      const int slot = atomicAdd(counts + kq, 1);
+      MaskJob J;
+      J.b = b; J.lab = lab; J.y0 = y0; J.x0 = x0; J.ly = ly; J.lx = lx; J.scratch = -1;
+      jobs[(size_t)kq * n + slot] = J;
+      return;
+    }
+  }
   while (k < ncap && need > caps.v[k]) ++k;
   // kind 0 with pixel counts: a too-big-for-LDS mask that the sparse sweep can take (box fill
   // < 60 %, <= SPARSE_BIG_PX pixels) goes to bucket ncap (one workgroup, heat field in global
@@ -767,6 +1037,7 @@ __global__ __launch_bounds__(256) void plan_masks_kernel(const int* __restrict__
     const long long sz = kind == 0 ? 2 * R + (RY + RX + 1) / 2 + (R + 7) / 8 + 2 : R;
     scr = (long long)atomicAdd(scratch_total, (unsigned long long)sz);
   }
+  k += q2;
   const int slot = atomicAdd(counts + k, 1);
   MaskJob J;
   J.b = b;

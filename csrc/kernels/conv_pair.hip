@@ -1312,6 +1312,10 @@ template <int RES>
 __device__ __forceinline__ void pp_issue_res(const PairArgs& a, TileXY t, int gw, int lrow, int kq, PPRes& r) {
 #pragma unroll
   for (int pt = 0; pt < ppk::BPT; ++pt) {
+    if constexpr (RES == 0) {  // the stem: its residual is the in-kernel projection
+      r.rv[pt][0] = r.rv[pt][1] = (u32x2){0u, 0u};
+      continue;
+    }
     const int py = min(t.ty0 + ppk::RPW * gw + (pt >> 1), a.H - 1), px = min(t.tx0 + (pt & 1) * 16 + lrow, a.W - 1);
     const bf16_t* rp = RES == 1 ? a.res + (((size_t)t.n * a.H + py) * a.W + px) * 32 + kq * 4
                                 : a.res + (((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1)) * 32 + kq * 4;
@@ -1323,6 +1327,7 @@ __device__ __forceinline__ void pp_issue_res(const PairArgs& a, TileXY t, int gw
 }
 
 // bias + residual -> wave-private staging (swizzled like h) -> 16-byte coalesced NHWC stores
+template <int RES>
 __device__ __forceinline__ void pp_epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[2][ppk::BPT], const PPRes& r,
                                          unsigned char* ws, int gw, int lrow, int kq, bool act) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1354,7 +1359,7 @@ __device__ __forceinline__ void pp_epi_b(const PairArgs& a, TileXY t, const f32x
 #pragma unroll
     for (int pt = 0; pt < ppk::BPT; ++pt) {
       u32x2 rv = r.rv[pt][ct];
-      asm volatile("" : "+v"(rv));  // keeps the bf16 unpacking here, not hoisted next to the loads in P4
+      if constexpr (RES != 0) asm volatile("" : "+v"(rv));  // keeps the bf16 unpacking here, not hoisted next to the loads in P4
       u32x2 st;
       st[0] = pack2bf(acc[ct][pt][0] + r.bias[ct].x + lo_bf(rv[0]), acc[ct][pt][1] + r.bias[ct].y + hi_bf(rv[0]));
       st[1] = pack2bf(acc[ct][pt][2] + r.bias[ct].z + lo_bf(rv[1]), acc[ct][pt][3] + r.bias[ct].w + hi_bf(rv[1]));
@@ -1413,11 +1418,151 @@ __device__ __forceinline__ void pp_epi_head(const PairArgs& a, TileXY t, const f
   }
 }
 
+// ---- stem (Cin = 8 + the 1x1 projection) on the ping-pong kernel -------------------------------
+// In: the 20 x 36 halo of actA(x) at 8 channels per pixel, padded to 24 elements (48 B: sixteen
+// consecutive pixels hit 16 distinct 16-byte slots); P: actP(x) at the 16 x 32 centre pixels,
+// unpadded 16-byte pixels (a fragment read is 256 contiguous bytes), read by stage B's projection K
+// step; h and the output staging as the 32-channel path.  Total 122 KiB: the same ~32 KiB of a CU's
+// LDS stays free for the mask-stage kernels that run beside the network (the first build padded P
+// to 48 B, took 154 KiB and slowed the pipelined headline although the stem call itself was faster).
+namespace pps {
+constexpr int PST = 24;                      // In pixel stride (elements)
+constexpr int PSP = 8;                       // P pixel stride (elements)
+constexpr int KPA = 96, WSTRA = KPA + 16;    // stage-A K: 9 taps x 8 channels, 4 taps per 32-deep step
+constexpr int WSTRP = 48;                    // projection weight row stride
+constexpr int IN_B = IPIX * PST * 2;         // 34560
+constexpr int P_B = TH * TW * PSP * 2;       // 8192
+constexpr int R_B = ppk::H_B > IN_B ? ppk::H_B : IN_B;  // In / h / output staging overlay
+constexpr int RB = R_B + P_B;                // one group's region
+constexpr int WA_B = 32 * WSTRA * 2, WB_B = 32 * ppk::WSTR * 2, WP_B = 32 * WSTRP * 2;
+constexpr int LDS = 2 * RB + WA_B + WB_B + WP_B;
+constexpr int HUPT = (IPIX + ppk::GT - 1) / ppk::GT;  // one 16-byte unit (8 channels) per pixel
+static_assert(LDS <= 128 * 1024 && ppk::GW * ppk::OUTW_B <= R_B, "stem ping-pong LDS budget");
+}  // namespace pps
+
+struct PPHalo8 {
+  u32x4 h[pps::HUPT];
+  float4 aff[4], paff[4];
+};
+
+template <bool INT = false>
+__device__ __forceinline__ void pp8_issue_halo(const PairArgs& a, TileXY t, int gt, PPHalo8& hr) {
+  hr.aff[0] = *reinterpret_cast<const float4*>(a.sa);
+  hr.aff[1] = *reinterpret_cast<const float4*>(a.sa + 4);
+  const float* tr = a.ta + (size_t)t.n * a.ta_ns;
+  hr.aff[2] = *reinterpret_cast<const float4*>(tr);
+  hr.aff[3] = *reinterpret_cast<const float4*>(tr + 4);
+  hr.paff[0] = *reinterpret_cast<const float4*>(a.sp);
+  hr.paff[1] = *reinterpret_cast<const float4*>(a.sp + 4);
+  hr.paff[2] = *reinterpret_cast<const float4*>(a.tp);
+  hr.paff[3] = *reinterpret_cast<const float4*>(a.tp + 4);
+#pragma unroll
+  for (int i = 0; i < pps::HUPT; ++i) {  // clamped, unconditional (exact vmcnt counts)
+    const int pi = min(gt + i * ppk::GT, IPIX - 1);
+    const int y = pi / IW, x = pi - y * IW;
+    const int gy = INT ? t.ty0 - 2 + y : min(max(t.ty0 - 2 + y, 0), a.H - 1);
+    const int gx = INT ? t.tx0 - 2 + x : min(max(t.tx0 - 2 + x, 0), a.W - 1);
+    hr.h[i] = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + gy) * a.Ws + gx) * 8);
+  }
+}
+
+template <bool INT>
+__device__ __forceinline__ void pp8_commit(const PairArgs& a, TileXY t, int gt, const PPHalo8& hr, unsigned char* rin,
+                                           unsigned char* preg) {
+  float sc[8], sh[8], ps[8], pt[8];
+  unpack_aff(hr.aff, sc, sh);
+  unpack_aff(hr.paff, ps, pt);
+#pragma unroll
+  for (int i = 0; i < pps::HUPT; ++i) {
+    const int pi = gt + i * ppk::GT;
+    if (pi >= IPIX) continue;
+    const int iy = pi / IW, ix = pi - iy * IW;
+    const int gy = t.ty0 - 2 + iy, gx = t.tx0 - 2 + ix;
+    const bool in = INT || (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(hr.h[i][j]); v[2 * j + 1] = hi_bf(hr.h[i][j]); }
+    u32x4 pk = (u32x4){0u, 0u, 0u, 0u};
+    if (in) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        pk[j] = relu_bf16x2(pack2bf(fmaf(v[2 * j], sc[2 * j], sh[2 * j]), fmaf(v[2 * j + 1], sc[2 * j + 1], sh[2 * j + 1])));
+    }
+    *reinterpret_cast<u32x4*>(rin + pi * pps::PST * 2) = pk;
+    if (iy >= 2 && iy < TH + 2 && ix >= 2 && ix < TW + 2) {
+      u32x4 pp = (u32x4){0u, 0u, 0u, 0u};
+      if (in) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          pp[j] = pack2bf(fmaf(v[2 * j], ps[2 * j], pt[2 * j]), fmaf(v[2 * j + 1], ps[2 * j + 1], pt[2 * j + 1]));
+      }
+      *reinterpret_cast<u32x4*>(preg + ((iy - 2) * TW + (ix - 2)) * pps::PSP * 2) = pp;
+    }
+  }
+}
+
+// stage A of the stem: 3 K steps of 4 taps x 8 channels (lane kq: tap 4 ks + kq; taps >= 9 have zero
+// weights and read the tap-0 pixel)
+__device__ __forceinline__ void pp8_mma_a(f32x4 (&acc)[2][ppk::APT], const unsigned char* rin, const bf16_t* wa, int gw,
+                                          int lrow, int kq) {
+  int toff[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    int tap = ks * 4 + kq;
+    if (tap >= 9) tap = 0;
+    toff[ks] = ((tap / 3) * IW + tap % 3) * pps::PST * 2;
+  }
+  const int b0 = ((gw >> 1) * IW + (gw & 1) * 16 + lrow) * pps::PST * 2;
+  int ryl, rxl;
+  if (!pp_last(gw, lrow, ryl, rxl)) { ryl = 0; rxl = 0; }
+  const int bl = (ryl * IW + rxl) * pps::PST * 2;
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    bf16x8 af[2], bf[ppk::APT];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+      af[ct] = *reinterpret_cast<const bf16x8*>(wa + (ct * 16 + lrow) * pps::WSTRA + ks * 32 + kq * 8);
+#pragma unroll
+    for (int j = 0; j < ppk::APT - 1; ++j)
+      bf[j] = *reinterpret_cast<const bf16x8*>(rin + b0 + toff[ks] + j * (ppk::GW / 2) * IW * pps::PST * 2);
+    bf[ppk::APT - 1] = *reinterpret_cast<const bf16x8*>(rin + bl + toff[ks]);
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int j = 0; j < ppk::APT; ++j)
+        acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[j], acc[ct][j], 0, 0, 0);
+  }
+}
+
+// the stem's 1x1 projection as one more K step into stage B's accumulators (k >= 8: zero weights)
+__device__ __forceinline__ void pp8_mma_p(f32x4 (&acc)[2][ppk::BPT], const unsigned char* preg, const bf16_t* wp, int gw,
+                                          int lrow, int kq) {
+  bf16x8 af[2], bf[ppk::BPT];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) af[ct] = *reinterpret_cast<const bf16x8*>(wp + (ct * 16 + lrow) * pps::WSTRP + kq * 8);
+#pragma unroll
+  for (int pt = 0; pt < ppk::BPT; ++pt) {
+    const int oy = ppk::RPW * gw + (pt >> 1), ox = (pt & 1) * 16 + lrow;
+    bf[pt] = *reinterpret_cast<const bf16x8*>(preg + (oy * TW + ox) * pps::PSP * 2);
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int pt = 0; pt < ppk::BPT; ++pt)
+      acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[pt], acc[ct][pt], 0, 0, 0);
+}
+
+template <bool STEM> struct PPHaloOf { using T = PPHalo; };
+template <> struct PPHaloOf<true> { using T = PPHalo8; };
+
 // NCA input chunks of 32 channels (Cin = 32 NCA), INMODE 0 (full resolution) or 1 (nearest 2x up),
 // X2: + skip operand on stage A's output, RES 1 (full) or 2 (up2 of a half-resolution map).
-template <int NCA, int INMODE, bool X2, int RES, bool HEAD, bool STAMP = false>
+// STEM: Cin = 8 with the 1x1 projection as the residual (NCA 1, INMODE 0, RES 0; regions pps::).
+template <int NCA, int INMODE, bool X2, int RES, bool HEAD, bool STEM = false, bool STAMP = false>
 __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_kernel(PairArgs a) {
+  static_assert(!STEM || (NCA == 1 && INMODE == 0 && !X2 && RES == 0 && !HEAD), "stem configuration");
   constexpr int CIN = 32 * NCA;
+  constexpr int RB = STEM ? pps::RB : ppk::RB;
   // STAMP (diagnostics, tools/pp_phase_profile.py): wave 0 of each group accumulates s_memtime
   // cycles of every phase's own work and of its wait at the closing barrier, [grid][2 groups][16]
   unsigned long long ph_work[7] = {0, 0, 0, 0, 0, 0, 0}, ph_wait[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -1444,23 +1589,47 @@ __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_k
   const int t0 = (int)(((long long)blockIdx.x * total) / gridDim.x);
   const int t1 = (int)(((long long)(blockIdx.x + 1) * total) / gridDim.x);
   if (t0 >= t1) return;  // workgroup-uniform
-  bf16_t* wl = reinterpret_cast<bf16_t*>(smem + 2 * ppk::RB);
-  // NCA stage-A panels then the stage-B panel, [32 rows][304] each (from the packed [Cout][NCA][288]
-  // and [Cout][1][288] layouts)
-  for (int u = tid0; u < (NCA + 1) * 32 * 36; u += ppk::NTP) {
-    const int pnl = u / (32 * 36), q = u % (32 * 36), r = q / 36, k8 = q % 36;
-    const bf16_t* src = pnl < NCA ? a.wa + ((size_t)r * NCA + pnl) * 288 + k8 * 8 : a.wb + (size_t)r * 288 + k8 * 8;
-    *reinterpret_cast<u32x4*>(wl + pnl * 32 * ppk::WSTR + r * ppk::WSTR + k8 * 8) = *reinterpret_cast<const u32x4*>(src);
+  bf16_t* wl = reinterpret_cast<bf16_t*>(smem + 2 * RB);
+  const bf16_t* wb = wl + (STEM ? 32 * pps::WSTRA : NCA * 32 * ppk::WSTR);
+  const bf16_t* wp = wb + 32 * ppk::WSTR;  // STEM: the projection panel [32][48]
+  if constexpr (STEM) {  // [32][96] stage A, [32][288] stage B, [32][32] projection
+    for (int u = tid0; u < 32 * (12 + 36 + 4); u += ppk::NTP) {
+      const int r = u / 52, q = u % 52;
+      const bf16_t* src;
+      bf16_t* dst;
+      if (q < 12) { src = a.wa + (size_t)r * 96 + q * 8; dst = wl + r * pps::WSTRA + q * 8; }
+      else if (q < 48) { src = a.wb + (size_t)r * 288 + (q - 12) * 8; dst = const_cast<bf16_t*>(wb) + r * ppk::WSTR + (q - 12) * 8; }
+      else { src = a.wp + (size_t)r * 32 + (q - 48) * 8; dst = const_cast<bf16_t*>(wp) + r * pps::WSTRP + (q - 48) * 8; }
+      *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+    }
+  } else {
+    // NCA stage-A panels then the stage-B panel, [32 rows][304] each (from the packed [Cout][NCA][288]
+    // and [Cout][1][288] layouts)
+    for (int u = tid0; u < (NCA + 1) * 32 * 36; u += ppk::NTP) {
+      const int pnl = u / (32 * 36), q = u % (32 * 36), r = q / 36, k8 = q % 36;
+      const bf16_t* src = pnl < NCA ? a.wa + ((size_t)r * NCA + pnl) * 288 + k8 * 8 : a.wb + (size_t)r * 288 + k8 * 8;
+      *reinterpret_cast<u32x4*>(wl + pnl * 32 * ppk::WSTR + r * ppk::WSTR + k8 * 8) = *reinterpret_cast<const u32x4*>(src);
+    }
   }
-  const bf16_t* wb = wl + NCA * 32 * ppk::WSTR;
   // wave-uniform values in SGPRs (readfirstlane): the group / wave-in-group branches stay scalar
   const int grp = __builtin_amdgcn_readfirstlane(tid0 / ppk::GT);  // waves 0..GW-1 | GW..2GW-1 (w, w + GW share a SIMD)
   const int gt0 = tid0 & (ppk::GT - 1);
-  unsigned char* reg = smem + grp * ppk::RB;
+  unsigned char* reg = smem + grp * RB;
   HeadRegs hr;
   if constexpr (HEAD) load_head(a, tid0 & 15, (tid0 & 63) >> 4, hr);
-  PPHalo halo;
-  pp_issue_halo<INMODE, CIN>(a, tile_xy(a, min(t0 + grp, t1 - 1)), 0, gt0, halo);
+  typename PPHaloOf<STEM>::T halo;
+  // chunk 0 of a tile's input halo -> registers
+  auto issue0 = [&](TileXY nx, int gtv) {
+    if constexpr (STEM) {
+      if (pp_interior(a, nx)) pp8_issue_halo<true>(a, nx, gtv, halo);
+      else pp8_issue_halo<false>(a, nx, gtv, halo);
+    } else {
+      if (pp_interior(a, nx)) pp_issue_halo<INMODE, CIN, true>(a, nx, 0, gtv, halo);
+      else pp_issue_halo<INMODE, CIN>(a, nx, 0, gtv, halo);
+    }
+  };
+  if constexpr (STEM) pp8_issue_halo<false>(a, tile_xy(a, min(t0 + grp, t1 - 1)), gt0, halo);
+  else pp_issue_halo<INMODE, CIN>(a, tile_xy(a, min(t0 + grp, t1 - 1)), 0, gt0, halo);
   __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xf << 8));  // vmcnt(0): see the counted wait in P1
   __syncthreads();  // weights resident
   if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger: group 1 runs one phase behind
@@ -1488,15 +1657,22 @@ __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_k
       if (c == 0) __builtin_amdgcn_s_waitcnt((NW & 0xf) | (0x7 << 4) | (0xf << 8) | ((NW >> 4) << 14));
       int gc = gt0;
       asm volatile("" : "+v"(gc));  // per chunk: the unit addresses are recomputed, not kept across P2
-      if (inner) pp_commit<true>(a, cur, gc, halo, reg);
-      else pp_commit<false>(a, cur, gc, halo, reg);
+      if constexpr (STEM) {
+        if (inner) pp8_commit<true>(a, cur, gc, halo, reg, reg + pps::R_B);
+        else pp8_commit<false>(a, cur, gc, halo, reg, reg + pps::R_B);
+      } else {
+        if (inner) pp_commit<true>(a, cur, gc, halo, reg);
+        else pp_commit<false>(a, cur, gc, halo, reg);
+      }
       pre(2 * c);
       __syncthreads();
       post(2 * c);
       // P2: stage A over chunk c (the next chunk's halo, or the epilogue operands, in flight)
-      if (c + 1 < NCA) {
-        if (inner) pp_issue_halo<INMODE, CIN, true>(a, cur, c + 1, gt, halo);
-        else pp_issue_halo<INMODE, CIN>(a, cur, c + 1, gt, halo);
+      if constexpr (!STEM) {
+        if (c + 1 < NCA) {
+          if (inner) pp_issue_halo<INMODE, CIN, true>(a, cur, c + 1, gt, halo);
+          else pp_issue_halo<INMODE, CIN>(a, cur, c + 1, gt, halo);
+        }
       }
       if (c == NCA - 1) {
 #pragma unroll
@@ -1513,7 +1689,8 @@ __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_k
           for (int j = 0; j < ppk::APT; ++j) acc_a[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
       if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(1);
-      pp_mma_a(acc_a, reg, wl + c * 32 * ppk::WSTR, gw, lrow, kq);
+      if constexpr (STEM) pp8_mma_a(acc_a, reg, wl, gw, lrow, kq);
+      else pp_mma_a(acc_a, reg, wl + c * 32 * ppk::WSTR, gw, lrow, kq);
       if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(0);
       pre(2 * c + 1);
       __syncthreads();
@@ -1526,11 +1703,7 @@ __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_k
     else pp_epi_a<X2, false>(a, cur, acc_a, reg, sb, tb, sk, gw, g3 & 15, (g3 & 63) >> 4);
     PPRes res;
     if constexpr (PP_VAR & 1) pp_issue_res<RES>(a, cur, gw, g3 & 15, (g3 & 63) >> 4, res);
-    if constexpr (PP_VAR & 8) {  // the group's next halo two slots ahead of its commit
-      const TileXY nx = tile_xy(a, min(t + 2, t1 - 1));
-      if (pp_interior(a, nx)) pp_issue_halo<INMODE, CIN, true>(a, nx, 0, g3, halo);
-      else pp_issue_halo<INMODE, CIN>(a, nx, 0, g3, halo);
-    }
+    if constexpr (PP_VAR & 8) issue0(tile_xy(a, min(t + 2, t1 - 1)), g3);  // two slots ahead of its commit
     pre(2 * NCA);
     __syncthreads();
     post(2 * NCA);
@@ -1548,6 +1721,7 @@ __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_k
       for (int j = 0; j < ppk::BPT; ++j) acc_b[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(1);
     pp_mma_b(acc_b, reg, wb, gw, lrow4, kq4);
+    if constexpr (STEM) pp8_mma_p(acc_b, reg + pps::R_B, wp, gw, lrow4, kq4);
     if constexpr (!(PP_VAR & 4)) __builtin_amdgcn_s_setprio(0);
     pre(2 * NCA + 1);
     __syncthreads();
@@ -1558,15 +1732,11 @@ __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_k
     int g5 = gt0;
     asm volatile("" : "+v"(g5));
     const int lrow5 = g5 & 15, kq5 = (g5 & 63) >> 4;
-    auto next_halo = [&]() {
-      const TileXY nx = tile_xy(a, min(t + 2, t1 - 1));
-      if (pp_interior(a, nx)) pp_issue_halo<INMODE, CIN, true>(a, nx, 0, g5, halo);
-      else pp_issue_halo<INMODE, CIN>(a, nx, 0, g5, halo);
-    };
+    auto next_halo = [&]() { issue0(tile_xy(a, min(t + 2, t1 - 1)), g5); };
     if constexpr (!(PP_VAR & 10)) next_halo();
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (HEAD) pp_epi_head(a, cur, acc_b, res, hr, gw, lrow5, kq5, act);
-    else pp_epi_b(a, cur, acc_b, res, reg + gw * ppk::OUTW_B, gw, lrow5, kq5, act);
+    else pp_epi_b<RES>(a, cur, acc_b, res, reg + gw * ppk::OUTW_B, gw, lrow5, kq5, act);
     if constexpr (PP_VAR & 2) next_halo();
     pre(2 * NCA + 2);
     __syncthreads();
@@ -1591,9 +1761,9 @@ __global__ __launch_bounds__(ppk::NTP, ppk::GW == 4 ? 2 : 4) void conv_pair_pp_k
 unsigned long long* g_pp_stamps = nullptr;  // diagnostics: be_conv_pair_pp_set_stamps
 int g_pp_stamps_cap = 0;
 
-template <int NCA, int INMODE, bool X2, int RES, bool HEAD>
+template <int NCA, int INMODE, bool X2, int RES, bool HEAD, bool STEM = false>
 int launch_pair_pp(PairArgs a, int grid_cap, hipStream_t s) {
-  constexpr int lds = 2 * ppk::RB + (NCA + 1) * ppk::W_B;
+  constexpr int lds = STEM ? pps::LDS : 2 * ppk::RB + (NCA + 1) * ppk::W_B;
   static_assert(lds <= 160 * 1024, "ping-pong LDS budget");
   a.tiles_x = (a.W + TW - 1) / TW;
   a.tiles_y = (a.H + TH - 1) / TH;
@@ -1604,7 +1774,7 @@ int launch_pair_pp(PairArgs a, int grid_cap, hipStream_t s) {
   a.stamps = nullptr;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, STEM>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr_set = true;
   }
@@ -1613,14 +1783,14 @@ int launch_pair_pp(PairArgs a, int grid_cap, hipStream_t s) {
     a.stamps = g_pp_stamps;
     static bool attr_st = false;
     if (!attr_st) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, true>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, STEM, true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_st = true;
     }
-    hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, true>), dim3(g), dim3(ppk::NTP), lds, s, a);
+    hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, STEM, true>), dim3(g), dim3(ppk::NTP), lds, s, a);
     return BE_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD>), dim3(g), dim3(ppk::NTP), lds, s, a);
+  hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, STEM>), dim3(g), dim3(ppk::NTP), lds, s, a);
   return BE_CHECK_LAUNCH();
 }
 }  // namespace
@@ -1634,6 +1804,12 @@ static int g_pair_grid = [] {
 // BE_PAIR_PP (default 1): the level-0 32 -> 32 half-blocks (+ the head) on the ping-pong kernel
 static int g_pair_pp = [] {
   const char* e = getenv("BE_PAIR_PP");
+  return e ? atoi(e) : 1;
+}();
+
+// BE_PAIR_PP_STEM (default 1): the stem (8 -> 32 + projection) on the ping-pong kernel as well
+static int g_pair_pp_stem = [] {
+  const char* e = getenv("BE_PAIR_PP_STEM");
   return e ? atoi(e) : 1;
 }();
 
@@ -1703,8 +1879,11 @@ int be_conv_pair(const void* x, const void* x2, const float* sa, const float* ta
   if ((resmode != 0) != (res != nullptr)) return -21;
   if (proj && (!sp || !tp || !wp)) return -22;
   const int g = g_pair_grid;
-  if (CM == 32 && Cin == 8 && inmode == 0 && !hx2 && proj && resmode == 0)
+  if (CM == 32 && Cin == 8 && inmode == 0 && !hx2 && proj && resmode == 0) {
+    if (g_pair_pp_stem && pp_ok(a, g) && Hs == H && Ws == W)
+      return launch_pair_pp<1, 0, false, 0, false, true>(a, g, stream);
     return launch_pair<8, 32, 0, false, true, 0, 1>(a, g, stream);
+  }
   if (CM == 32 && Cin == 32 && inmode == 0 && !hx2 && !proj && resmode == 1) {
     if (pp_ok(a, g) && Hs == H && Ws == W) return launch_pair_pp<1, 0, false, 1, false>(a, g, stream);
     return launch_pair<32, 32, 0, false, false, 1, 1>(a, g, stream);

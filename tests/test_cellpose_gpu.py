@@ -218,9 +218,10 @@ def test_normalize99_radix_select_matches_sort_and_numpy(gpu, shape, kind):
 
 
 @pytest.mark.gpu
-def test_sparse_diffusion_bit_identical_to_dense(gpu):
-    """The sparse pixel-list sweep (default for thin / irregular masks) gives exactly the dense
-    sweep's flows: same sums in the same order, centre source folded into the reads."""
+def test_sparse_diffusion_bit_identical_to_dense(gpu, monkeypatch):
+    """The sparse pixel-list sweep (thin / irregular masks) and the compact work-queue kernel
+    (diffuse_q_kernel, the default) give exactly the dense sweep's flows: same sums in the same
+    order, centre source folded into the reads."""
     import os
 
     from bioengine_worker_amd.cellpose import gpu as cg
@@ -236,13 +237,17 @@ def test_sparse_diffusion_bit_identical_to_dense(gpu):
                 M[b, y, x] = lab
                 y = int(np.clip(y + rng.integers(-1, 2), 1, 198))
                 x = int(np.clip(x + rng.integers(-1, 2), 1, 218))
+    M[1, 150:190, 5:50] = lab + 1  # a 1800-pixel blob: a workgroup job of the queue kernel
     Mt = torch.from_numpy(M).to(gpu)
     old = os.environ.get("BE_DIFFUSE_VARIANT")
     try:
+        monkeypatch.setattr(cg, "DIFFUSE_QUEUE", False)
         os.environ["BE_DIFFUSE_VARIANT"] = "3"
         dense, _, _ = cg.masks_to_flows_gpu(Mt)
         os.environ["BE_DIFFUSE_VARIANT"] = "0"
         sparse, _, _ = cg.masks_to_flows_gpu(Mt)
+        monkeypatch.setattr(cg, "DIFFUSE_QUEUE", True)
+        queued, _, _ = cg.masks_to_flows_gpu(Mt)
     finally:
         if old is None:
             os.environ.pop("BE_DIFFUSE_VARIANT", None)
@@ -251,6 +256,31 @@ def test_sparse_diffusion_bit_identical_to_dense(gpu):
     torch.cuda.synchronize()
     assert dense.abs().sum() > 0
     assert torch.equal(dense, sparse)
+    assert torch.equal(dense, queued)
+
+
+@pytest.mark.gpu
+def test_diffusion_queue_plan_buckets(gpu):
+    """Plan kind 2: masks of <= 256 pixels (box width + 2 <= 256) are wave jobs, <= 2048 pixels
+    workgroup jobs, the rest keep kind 0's buckets; every present mask lands in exactly one."""
+    from bioengine_worker_amd.cellpose import gpu as cg
+
+    M = torch.zeros(2, 300, 320, dtype=torch.int32)
+    M[0, 5:15, 5:20] = 1      # 150 px: wave
+    M[0, 20:60, 5:50] = 2     # 1800 px: workgroup
+    M[0, 70:290, 5:300] = 3   # 64900 px: kind-0 buckets
+    M[1, 5:6, 2:300] = 1      # 298 px thin line: workgroup (pixels > 256)
+    M[1, 10:11, 2:4] = 2      # 2 px: wave
+    M = M.to(gpu)
+    nlab = 4
+    counts = cg.label_counts(M, nlab)
+    bbox = cg.mask_bboxes(M, nlab)
+    got, _, _ = cg._plan_finish([cg._plan_launch(bbox, None, 2, cg.DIFFUSE_CAPS, counts)])[0]
+    assert len(got) == len(cg.DIFFUSE_BUCKETS) + 4
+    key = lambda t: sorted((int(r[0]) & 0xFFFFFFFF, int(r[0]) >> 32) for r in t.cpu())
+    assert key(got[0]) == [(0, 1), (1, 2)]
+    assert key(got[1]) == [(0, 2), (1, 1)]
+    assert sum(len(key(g)) for g in got[2:]) == 1
 
 
 @pytest.mark.gpu

@@ -213,3 +213,64 @@ def test_conv_pair_head_matches_reference(gpu, hw, nh):
     assert out.shape == (3, nh, H, W) and torch.isfinite(out).all()
     err = (out - ref).abs().max().item()
     assert err < 1.5e-2 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES[:4])
+@pytest.mark.parametrize("hw", [(48, 96), (30, 44)])
+def test_conv_pair_pingpong_matches_reference(gpu, case, hw):
+    """The ping-pong kernel (conv_pair_pp_kernel: the stem, the 32->32 pairs, the 64->32 up pair) runs
+    only when every workgroup has two tiles or more: a 5-workgroup grid forces it at test sizes.  Odd
+    per-workgroup ranges exercise the idle group's dummy tile; (48, 96) has bounds-free interior tiles,
+    (30, 44) partial edge tiles only."""
+    from bioengine_worker_amd.ops import _native
+
+    cin, cm, inmode, has_x2, proj, res, ta2d, tb2d = case
+    H, W = hw
+    if inmode == "up2" and (H % 2 or W % 2):
+        pytest.skip("up2 needs even output")
+    spec, raw = _spec(cin, cm, inmode, proj, seed=9)
+    x, x2, r, ta, tb_raw = _inputs(case, 3, H, W, seed=10)
+    tb = None if tb_raw is None else cp.fold_bias(tb_raw, spec.sb, raw[1])
+    ref = cp.conv_pair_ref(x, spec, ta=ta, tb=tb, x2=x2, res=r, res_mode=res).float()
+    d = lambda t: None if t is None else t.to(gpu)
+    gspec = cp.PairSpec(pa=spec.pa.to(gpu), pb=spec.pb.to(gpu), sa=d(spec.sa), ta=d(spec.ta), sb=d(spec.sb),
+                        tb=d(spec.tb), bias=d(spec.bias), inmode=inmode,
+                        pp=None if spec.pp is None else spec.pp.to(gpu), sp=d(spec.sp), tp=d(spec.tp))
+    try:
+        _native.call("be_conv_pair_set_grid", 5)
+        out = cp.conv_pair(d(x), gspec, ta=d(ta), tb=d(tb), x2=d(x2), res=d(r), res_mode=res).float().cpu()
+    finally:
+        _native.call("be_conv_pair_set_grid", 0)
+    assert torch.isfinite(out).all()
+    err = (out - ref).abs()
+    tol = 1.5e-2 * max(1.0, ref.abs().max().item())
+    assert err.max().item() < tol, f"max err {err.max().item()} (tol {tol}); at {torch.nonzero(err == err.max())[0].tolist()}"
+
+
+@pytest.mark.gpu
+def test_conv_pair_head_pingpong_matches_reference(gpu):
+    """The fused output head on the ping-pong kernel (5-workgroup grid, see above)."""
+    from bioengine_worker_amd.ops import _native
+
+    H, W, nh = 48, 96, 3
+    case = (32, 32, "none", False, False, "full", True, True)
+    spec, raw = _spec(32, 32, "none", False, seed=11)
+    x, _, r, ta, tb_raw = _inputs(case, 3, H, W, seed=12)
+    tb = cp.fold_bias(tb_raw, spec.sb, raw[1])
+    g = torch.Generator().manual_seed(13)
+    head = cp.HeadSpec.build(1 + 0.1 * torch.randn(32, generator=g), 0.1 * torch.randn(32, generator=g),
+                             torch.randn(nh, 32, 1, 1, generator=g) / 32 ** 0.5, 0.1 * torch.randn(nh, generator=g))
+    ref = cp.head_ref(cp.conv_pair_ref(x, spec, ta=ta, tb=tb, res=r, res_mode="full"), head)
+    d = lambda t: None if t is None else t.to(gpu)
+    gspec = cp.PairSpec(pa=spec.pa.to(gpu), pb=spec.pb.to(gpu), sa=d(spec.sa), ta=d(spec.ta), sb=d(spec.sb),
+                        tb=d(spec.tb), bias=d(spec.bias), inmode="none")
+    ghead = cp.HeadSpec(s=d(head.s), t=d(head.t), w=d(head.w), b=d(head.b), nh=nh, wh=d(head.wh))
+    try:
+        _native.call("be_conv_pair_set_grid", 5)
+        out = cp.conv_pair_head(d(x), gspec, ghead, ta=d(ta), tb=d(tb), res=d(r)).cpu()
+    finally:
+        _native.call("be_conv_pair_set_grid", 0)
+    assert torch.isfinite(out).all()
+    err = (out - ref).abs().max().item()
+    assert err < 1.5e-2 * max(1.0, ref.abs().max().item()), err

@@ -14,9 +14,11 @@ import torch  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1,2", help="BE_DIFFUSE_VARIANT values, or dv=8,4,2 for BE_DIFFUSE_DV")
+    ap.add_argument("--variants", default="0,1,2",
+                    help="BE_DIFFUSE_VARIANT values, dv8,dv4,.. for BE_DIFFUSE_DV, q1 / q0 for the work-queue kernel on / off")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
+    from bioengine_worker_amd.cellpose import gpu as cg
     from bioengine_worker_amd.cellpose.gpu import compute_masks_gpu, follow_and_label, masks_to_flows_gpu
     from bioengine_worker_amd.cellpose.pipeline import CellposeRunner, EvalParams, synthetic_cells
 
@@ -26,12 +28,16 @@ def main():
     _, y, _ = runner.eval(imgs, EvalParams(compute_masks=False))
     y = y.float().contiguous()
     M = follow_and_label(y, 200, 0.0, 0.4)
+    if isinstance(M, tuple):
+        M = M[0]
     ref = None
     res = {}
     for rep in range(a.reps + 1):
         for v in a.variants.split(","):
             if v.startswith("dv"):
                 os.environ["BE_DIFFUSE_DV"] = v[2:]
+            elif v.startswith("q"):
+                cg.DIFFUSE_QUEUE = v[1:] == "1"
             else:
                 os.environ["BE_DIFFUSE_VARIANT"] = v
             torch.cuda.synchronize()
