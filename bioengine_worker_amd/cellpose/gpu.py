@@ -197,7 +197,7 @@ def _plan_launch(bbox: torch.Tensor, valid: torch.Tensor | None, kind: int, caps
         px_counts = counts.contiguous()
     # kind 2 (needs counts): the compact work-queue buckets (wave jobs, workgroup jobs) in front of
     # kind 0's buckets, which keep the masks the queue kernel cannot take
-    nb = len(caps) + 1 + int(split) + (2 if kind == 2 and split else 0)
+    nb = len(caps) + 1 + int(split) + (2 if kind == 2 and split else 0) + (2 if kind == 3 else 0)
     jobs = torch.empty(nb, max(n, 1), 4, dtype=torch.int64, device=dev)
     bucket_n = torch.zeros(nb, dtype=torch.int32, device=dev)
     tot = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -217,6 +217,14 @@ DIFFUSE_QUEUE = os.environ.get("BE_DIFFUSE_QUEUE", "1") != "0"
 
 def _diffuse_plan_kind() -> int:
     return 2 if DIFFUSE_QUEUE else 0
+
+
+#: one-wave hole filling (be_cp_fill_holes_wave) for boxes up to 64 x 64 with the ring; 0 = LDS kernel only
+FILL_WAVE = os.environ.get("BE_FILL_WAVE", "1") != "0"
+
+
+def _fill_plan_kind() -> int:
+    return 3 if FILL_WAVE else 1
 
 
 def _diffuse_lds_bytes(ly, lx):
@@ -250,8 +258,9 @@ def _diffuse_buckets(dv: int):
 _DEBUG_STATS = os.environ.get("BIOENGINE_MASK_STATS", "0") == "1"
 
 
-#: flow-following launch: XCD-ordered + block-compacted (default) or the plain pixel-per-lane one
-FOLLOW_FLOWS_ENTRY = os.environ.get("BIOENGINE_FOLLOW_ENTRY", "be_cp_follow_flows_xcd")
+#: flow-following launch: LDS-staged flow window per 32 x 32 tile (default), XCD-ordered +
+#: block-compacted L2 gathers, or the plain pixel-per-lane one (all bit-identical)
+FOLLOW_FLOWS_ENTRY = os.environ.get("BIOENGINE_FOLLOW_ENTRY", "be_cp_follow_flows_lds")
 
 _SIDE_STREAMS: dict = {}
 #: LDS buckets run on their own HIP streams so their launch tails (a few CUs finishing the
@@ -490,7 +499,7 @@ def fill_holes_gpu(M: torch.Tensor, min_size: int = 15, nlab: int | None = None)
     if min_size > 0:
         keep &= counts >= min_size
     keep[:, 0] = False
-    plan = _plan_masks(mask_bboxes(M, nlab), keep, 1, [LDS_FILL_BYTES])
+    plan = _plan_masks(mask_bboxes(M, nlab), keep, _fill_plan_kind(), [LDS_FILL_BYTES])
     return _fill_run(M, _rank_lut(keep), nlab, plan)
 
 
@@ -506,12 +515,20 @@ def _fill_run(M: torch.Tensor, lut: torch.Tensor, nlab: int, plan) -> torch.Tens
     B, H, W = M.shape
     dev = M.device
     out = torch.zeros_like(M)
-    (sj, bj), ssize, _ = plan
-    if sj.shape[0] + bj.shape[0] == 0:
+    slices, ssize, _ = plan
+    wjs = []
+    if len(slices) == 4:  # kind 3: the one-wave buckets (<= 64 x 64, <= 256 x 128 boxes) first
+        wjs, slices = slices[:2], slices[2:]
+    sj, bj = slices
+    if sj.shape[0] + bj.shape[0] + sum(w.shape[0] for w in wjs) == 0:
         return out
     scratch = torch.empty(max(ssize, 1), dtype=torch.uint8, device=dev)
     st = _native.stream(dev)
     Mc = M.contiguous()
+    for big, wj in enumerate(wjs):
+        if wj.shape[0]:
+            _native.call("be_cp_fill_holes_wave", _native.ptr(Mc), _native.ptr(wj), wj.shape[0], H, W, _native.ptr(lut), nlab,
+                         _native.ptr(out), big, st)
     if sj.shape[0]:
         _native.call("be_cp_fill_holes", _native.ptr(Mc), _native.ptr(sj), sj.shape[0], H, W, _native.ptr(lut), nlab,
                      _native.ptr(scratch), _native.ptr(out), LDS_FILL_BYTES, st)
@@ -584,7 +601,7 @@ def compute_masks_gpu(y: torch.Tensor, niter: int = 200, cellprob_threshold: flo
     # plan still takes cellpose's per-image niter over ALL masks, so the kept masks' flows are
     # unchanged)
     plans = _plan_finish(([_plan_launch(bbox, fill_keep, _diffuse_plan_kind(), DIFFUSE_CAPS, counts)] if qc else [])
-                         + [_plan_launch(bbox, fill_keep, 1, [LDS_FILL_BYTES])])
+                         + [_plan_launch(bbox, fill_keep, _fill_plan_kind(), [LDS_FILL_BYTES])])
     if qc:
         _, err, _ = masks_to_flows_gpu(M, dp=y, nlab=nlab, counts=counts, plan=plans[0], want_mu=False)
         qc_keep = (counts > 0) & ~(err / counts.clamp(min=1).float() > flow_threshold)

@@ -17,6 +17,7 @@ definition (tests/test_em_*.py).
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable
 
 import numpy as np
@@ -204,6 +205,10 @@ def watershed(neg_dist: np.ndarray, markers: np.ndarray, mask: np.ndarray, conn:
     return out
 
 
+#: relax only the tiles whose neighbourhood changed in the previous sweep (BE_WS_ACTIVE=0: every tile)
+WS_ACTIVE_TILES = os.environ.get("BE_WS_ACTIVE", "1") != "0"
+
+
 def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor | None = None,
                   max_local: int = 32, check_every: int = 4, max_sweeps: int = 100000) -> torch.Tensor:
     """Marker watershed of ``elev`` ([H, W] or [D, H, W] fp32, device) with 4/6-connectivity as the
@@ -225,11 +230,24 @@ def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor 
     st = _native.stream(dev)
     _native.call("be_ws_init", _native.ptr(e), _native.ptr(mk), _native.ptr(m), n, _native.ptr(key), _native.ptr(flags), st)
     sweeps = 0
+    if WS_ACTIVE_TILES:
+        # active-tile sweeps: only tiles whose neighbourhood changed in the previous sweep run
+        import ctypes
+
+        lib = _native.hip()
+        lib.be_ws_tiles.restype = ctypes.c_longlong
+        nt = int(lib.be_ws_tiles(D, H, W))
+        dirty = [torch.ones(nt, dtype=torch.uint8, device=dev), torch.empty(nt, dtype=torch.uint8, device=dev)]
     while sweeps < max_sweeps:
         changed.zero_()
         for _ in range(check_every):
-            _native.call("be_ws_relax", _native.ptr(e), _native.ptr(flags), _native.ptr(key), D, H, W, max_local,
-                         _native.ptr(changed), st)
+            if WS_ACTIVE_TILES:
+                _native.call("be_ws_relax_active", _native.ptr(e), _native.ptr(flags), _native.ptr(key), D, H, W, max_local,
+                             _native.ptr(changed), _native.ptr(dirty[0]), _native.ptr(dirty[1]), st)
+                dirty.reverse()
+            else:
+                _native.call("be_ws_relax", _native.ptr(e), _native.ptr(flags), _native.ptr(key), D, H, W, max_local,
+                             _native.ptr(changed), st)
         sweeps += check_every
         if int(changed.item()) == 0:
             break
@@ -260,7 +278,7 @@ def edt3d(mask: torch.Tensor) -> torch.Tensor:
     m = mask.to(torch.uint8).contiguous()
     dist = torch.empty(D, H, W, dtype=torch.float32, device=dev)
     tmp = torch.empty_like(dist)
-    v = torch.empty(D * H * W, dtype=torch.int32, device=dev)
+    v = torch.empty(D * H * W + D * max(H, W), dtype=torch.int32, device=dev)  # tail: fallback line flags
     z = torch.empty(D * H * W + D * max(H, W), dtype=torch.float64, device=dev)
     _native.call("be_edt3d", _native.ptr(m), _native.ptr(dist), _native.ptr(tmp), _native.ptr(v), _native.ptr(z), D, H, W,
                  _native.stream(dev))

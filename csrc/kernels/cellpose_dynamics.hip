@@ -205,6 +205,108 @@ __global__ __launch_bounds__(256) void follow_flows_xcd_pool_kernel(const float2
   }
 }
 
+// follow_flows with the flow field staged in LDS.  The XCD kernel above is bound by the latency
+// of its dependent L2 gathers (position -> 4 bilinear corners -> next position, 200 times).  Here a
+// workgroup owns a 32 x 32 pixel tile and stages the 64 x 64 window around it (16-pixel margin,
+// zeros outside the image = ldflow's padding) in LDS once; a step whose 2 x 2 corner block lies in
+// the window reads LDS (the (y, x) / (y + 1, x) pairs are one ds_read2_b64 each), a step outside it
+// (a particle that travelled > 16 px past the tile) reads global memory as before.  Same float
+// operations in the same order: results are bit-identical to follow_flows_kernel.
+// FT = 32 (1,024 pixels, four per thread at most) for batches; FT = 16 (one pixel per thread, a
+// 48 x 48 window) when the 32-pixel tiles would not give every CU several workgroups: at batch 1
+// the 32-pixel tiles ran each thread's pixels one after another and cost 0.3 ms of latency.
+constexpr int FM = 16;
+
+template <int FT>
+__global__ __launch_bounds__(256) void follow_flows_lds_kernel(const float2* __restrict__ flow2,
+                                                               const uint8_t* __restrict__ fg, int* __restrict__ hist,
+                                                               int* __restrict__ pos, int B, int H, int W, int niter,
+                                                               int tiles_x, int tiles_y) {
+  constexpr int FWN = FT + 2 * FM, NP = FT * FT / 256;  // passes of 256 pixels
+  constexpr int LG = FT == 32 ? 5 : 4;
+  __shared__ float2 win[FWN * FWN];
+  __shared__ short list[FT * FT];
+  __shared__ int wcount[4 * NP];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);  // an XCD walks consecutive tiles of one image
+  const int tpi = tiles_x * tiles_y;
+  const int b = blk / tpi, q = blk - b * tpi;
+  const int ty0 = (q / tiles_x) * FT, tx0 = (q % tiles_x) * FT;
+  const size_t HW = (size_t)H * W;
+  const uint8_t* fgb = fg + b * HW;
+  int* posb = pos + b * HW;
+  unsigned long long m[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {  // pass k: 256 pixels of whole tile rows (coalesced)
+    const int p = k * 256 + tid;
+    const int y = ty0 + (p >> LG), x = tx0 + (p & (FT - 1));
+    const bool in = y < H && x < W;
+    const bool f = in && fgb[(size_t)y * W + x];
+    if (in && !f) posb[(size_t)y * W + x] = -1;
+    m[k] = __ballot(f);
+    if (lane == 0) wcount[k * 4 + wv] = __popcll(m[k]);
+  }
+  __syncthreads();
+  int total = 0;
+#pragma unroll
+  for (int i = 0; i < 4 * NP; ++i) total += wcount[i];
+  if (total == 0) return;  // workgroup-uniform
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    int base = 0;
+    for (int i = 0; i < k * 4 + wv; ++i) base += wcount[i];
+    if ((m[k] >> lane) & 1ull) list[base + __popcll(m[k] & ((1ull << lane) - 1ull))] = (short)(k * 256 + tid);
+  }
+  const float2* fl = flow2 + b * HW;
+  const int wy0 = ty0 - FM, wx0 = tx0 - FM;
+  for (int i = tid; i < FWN * FWN; i += 256) {
+    const int gy = wy0 + i / FWN, gx = wx0 + i % FWN;
+    win[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? fl[(size_t)gy * W + gx] : make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  const float sy_scale = (H > 1) ? (float)H / (float)(H - 1) : 0.f;
+  const float sx_scale = (W > 1) ? (float)W / (float)(W - 1) : 0.f;
+  const float ymax = (float)(H - 1), xmax = (float)(W - 1);
+  const int Wp = W + 2 * RPAD;
+  for (int e = tid; e < total; e += 256) {
+    const int p = list[e];
+    const int y = ty0 + (p >> LG), x = tx0 + (p & (FT - 1));
+    float py = (float)y, px = (float)x;
+    for (int t = 0; t < niter; ++t) {
+      const float sy = py * sy_scale - 0.5f;
+      const float sx = px * sx_scale - 0.5f;
+      const float fy = floorf(sy), fx = floorf(sx);
+      const int y0 = (int)fy, x0 = (int)fx;
+      const float wy = sy - fy, wx = sx - fx;
+      const int ly = y0 - wy0, lx = x0 - wx0;
+      float2 a, bq, c, d;
+      if ((unsigned)ly < (unsigned)(FWN - 1) && (unsigned)lx < (unsigned)(FWN - 1)) {
+        const float2* w = win + ly * FWN + lx;
+        a = w[0];
+        bq = w[1];
+        c = w[FWN];
+        d = w[FWN + 1];
+      } else {
+        a = ldflow(fl, H, W, y0, x0);
+        bq = ldflow(fl, H, W, y0, x0 + 1);
+        c = ldflow(fl, H, W, y0 + 1, x0);
+        d = ldflow(fl, H, W, y0 + 1, x0 + 1);
+      }
+      const float w00 = (1.f - wy) * (1.f - wx), w01 = (1.f - wy) * wx, w10 = wy * (1.f - wx), w11 = wy * wx;
+      const float dy = a.x * w00 + bq.x * w01 + c.x * w10 + d.x * w11;
+      const float dx = a.y * w00 + bq.y * w01 + c.y * w10 + d.y * w11;
+      py = fminf(fmaxf(py + dy, 0.f), ymax);
+      px = fminf(fmaxf(px + dx, 0.f), xmax);
+    }
+    int iy = (int)py + RPAD, ix = (int)px + RPAD;
+    iy = min(max(iy, 0), H + RPAD - 1);
+    ix = min(max(ix, 0), W + RPAD - 1);
+    const int lin = iy * Wp + ix;
+    posb[(size_t)y * W + x] = lin;
+    atomicAdd(hist + (size_t)b * (H + 2 * RPAD) * Wp + lin, 1);
+  }
+}
+
 // Seeds: h > 10 and h == max over the 5x5 neighbourhood (zero outside).
 __global__ __launch_bounds__(256) void seeds_kernel(const int* __restrict__ hist, int B, int Hp, int Wp,
                                                     long long* __restrict__ keys, int* __restrict__ nseeds, int cap) {
@@ -292,18 +394,36 @@ __global__ __launch_bounds__(256) void expand_kernel(const int* __restrict__ his
   }
 }
 
-// Per-pixel label from its end point; count pixels per label.
+// Per-pixel label from its end point; count pixels per label.  A thread takes LL consecutive pixels
+// of one image row-major run and issues one counter atomic per run of equal labels (neighbouring
+// pixels share their label: one atomic per pixel on a few hundred counters per image serialised
+// in L2, 0.25 ms per batch of 32).
+constexpr int LL = 8;
 __global__ __launch_bounds__(256) void label_lookup_kernel(const int* __restrict__ pos, const int* __restrict__ M1, int B,
                                                            int HW, int HWp, int* __restrict__ M0, int* __restrict__ counts,
                                                            int nlab) {
+  const int segs = (HW + LL - 1) / LL;
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= (long long)B * HW) return;
-  const int b = (int)(gid / HW);
-  const int p = pos[gid];
-  int lab = 0;
-  if (p >= 0) lab = M1[(size_t)b * HWp + p];
-  M0[gid] = lab;
-  if (lab > 0) atomicAdd(counts + (size_t)b * nlab + lab, 1);
+  if (gid >= (long long)B * segs) return;
+  const int b = (int)(gid / segs);
+  const int p0 = (int)(gid % segs) * LL, p1 = min(p0 + LL, HW);
+  const int* pb = pos + (size_t)b * HW;
+  const int* mb = M1 + (size_t)b * HWp;
+  int* ob = M0 + (size_t)b * HW;
+  int* cb = counts + (size_t)b * nlab;
+  int cur = 0, run = 0;
+  for (int q = p0; q < p1; ++q) {
+    const int p = pb[q];
+    const int lab = p >= 0 ? mb[p] : 0;
+    ob[q] = lab;
+    if (lab != cur) {
+      if (cur > 0) atomicAdd(cb + cur, run);
+      cur = lab;
+      run = 0;
+    }
+    ++run;
+  }
+  if (cur > 0) atomicAdd(cb + cur, run);
 }
 
 // flow2 = (dY, dX) * (cellprob > thr) / 5 from a [B, 3, H, W] network output; fg mask.
@@ -371,6 +491,26 @@ int be_cp_follow_flows_xcd_pool(const void* flow2, const void* fg, int* hist, in
   return BE_CHECK_LAUNCH();
 }
 
+// LDS-window launch (see follow_flows_lds_kernel): one 256-thread workgroup per 32 x 32 tile.
+int be_cp_follow_flows_lds(const void* flow2, const void* fg, int* hist, int* pos, int B, int H, int W, int niter,
+                           hipStream_t s) {
+  if ((long long)B * H * W == 0) return 0;
+  const long long t32 = (long long)B * ((W + 31) / 32) * ((H + 31) / 32);
+  const char* ft = getenv("BE_FOLLOW_TILE");  // 16 / 32 forces a tile size (tests, A/B)
+  const int force = ft ? atoi(ft) : 0;
+  if (force == 32 || (force != 16 && t32 >= 2048)) {  // >= 8 workgroups per CU
+    const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32;
+    hipLaunchKernelGGL(follow_flows_lds_kernel<32>, dim3((unsigned)t32), dim3(256), 0, s, (const float2*)flow2,
+                       (const uint8_t*)fg, hist, pos, B, H, W, niter, tiles_x, tiles_y);
+  } else {
+    const int tiles_x = (W + 15) / 16, tiles_y = (H + 15) / 16;
+    const long long nblk = (long long)B * tiles_x * tiles_y;
+    hipLaunchKernelGGL(follow_flows_lds_kernel<16>, dim3((unsigned)nblk), dim3(256), 0, s, (const float2*)flow2,
+                       (const uint8_t*)fg, hist, pos, B, H, W, niter, tiles_x, tiles_y);
+  }
+  return BE_CHECK_LAUNCH();
+}
+
 int be_cp_seeds(const int* hist, int B, int Hp, int Wp, long long* keys, int* nseeds, int cap, hipStream_t s) {
   const long long n = (long long)B * Hp * Wp;
   hipLaunchKernelGGL(seeds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hist, B, Hp, Wp, keys, nseeds, cap);
@@ -388,7 +528,8 @@ int be_cp_expand(const int* hist, const long long* keys_sorted, const int* nseed
 
 int be_cp_label_lookup(const int* pos, const int* M1, int B, int HW, int HWp, int* M0, int* counts, int nlab,
                        hipStream_t s) {
-  const long long n = (long long)B * HW;
+  const long long n = (long long)B * ((HW + LL - 1) / LL);
+  if (n == 0) return 0;
   hipLaunchKernelGGL(label_lookup_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pos, M1, B, HW, HWp, M0, counts,
                      nlab);
   return BE_CHECK_LAUNCH();

@@ -793,6 +793,132 @@ __global__ __launch_bounds__(DQ_T) void diffuse_q_kernel(const int* __restrict__
   }
 }
 
+// Hole filling of a mask whose box (+1 ring) fits NS * 64 rows x NWD * 64 columns: one WAVE, no
+// LDS, no barriers.  Box row r lives in lane r % 64, slot r / 64, as NWD 64-bit words (bit x of the
+// row = column x); "outside" grows from the ring through the cells that are not this label: within
+// a row by carry propagation (adding the seed bits to the row's free bits clears every free run
+// upward of a seed, carrying across words; the bit-reversed sum does the same downward), across
+// rows through the neighbour lanes, until no lane changes.  Same 4-connectivity and writes as
+// fill_holes_kernel (which keeps the larger boxes).  <1, 1>: boxes <= 64 x 64 (nearly all masks);
+// <4, 2>: <= 256 rows x 128 columns (the long tail the one-workgroup LDS kernel spent 0.44 ms on).
+template <int NS, int NWD>
+__global__ __launch_bounds__(256) void fill_holes_bits_kernel(const int* __restrict__ M, const MaskJob* __restrict__ jobs,
+                                                              int njobs, int H, int W, const int* __restrict__ lut, int nlab,
+                                                              int* __restrict__ out) {
+  using u64 = unsigned long long;
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= njobs) return;  // wave-uniform
+  const MaskJob J = jobs[j];
+  const int RY = J.ly + 2, RX = J.lx + 2;
+  const int* Mb = M + (size_t)J.b * H * W;
+  u64 full[NWD];
+#pragma unroll
+  for (int w = 0; w < NWD; ++w) {
+    const int nbits = min(max(RX - 64 * w, 0), 64);
+    full[w] = nbits >= 64 ? ~0ull : ((1ull << nbits) - 1ull);
+  }
+  u64 mrow[NS][NWD];
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int w = 0; w < NWD; ++w) mrow[k][w] = 0ull;
+  for (int r = 1; r <= J.ly; ++r) {
+#pragma unroll
+    for (int w = 0; w < NWD; ++w) {
+      const int col = 64 * w + lane;
+      const bool m = col >= 1 && col <= J.lx && Mb[(size_t)(J.y0 + r - 1) * W + J.x0 + col - 1] == J.lab;
+      const u64 bal = __ballot(m);
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        if (k == (r >> 6) && lane == (r & 63)) mrow[k][w] = bal;
+    }
+  }
+  u64 fr[NS][NWD], o[NS][NWD];
+  const int wl = (RX - 1) >> 6;  // word of the last column
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int row = 64 * k + lane;
+    const bool rowin = row < RY;
+    const bool ringrow = row == 0 || row == RY - 1;
+#pragma unroll
+    for (int w = 0; w < NWD; ++w) {
+      fr[k][w] = rowin ? (~mrow[k][w] & full[w]) : 0ull;
+      u64 ring = ringrow ? full[w] : 0ull;
+      if (w == 0) ring |= 1ull;
+      if (w == wl) ring |= 1ull << ((RX - 1) & 63);
+      o[k][w] = ring & fr[k][w];
+    }
+  }
+  for (;;) {
+    u64 h[NS][NWD];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      u64 up[NWD], dn[NWD], rf[NWD], ro[NWD];
+      unsigned long long carry = 0ull;
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) {  // multi-word add fr + o
+        const u64 t = fr[k][w] + o[k][w];
+        const u64 sum = t + carry;
+        carry = (t < fr[k][w]) || (sum < t) ? 1ull : 0ull;
+        up[w] = fr[k][w] & ~sum;
+      }
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) {  // bit reversal of the whole row (word order swapped)
+        rf[w] = __builtin_bitreverse64(fr[k][NWD - 1 - w]);
+        ro[w] = __builtin_bitreverse64(o[k][NWD - 1 - w]);
+      }
+      carry = 0ull;
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) {
+        const u64 t = rf[w] + ro[w];
+        const u64 sum = t + carry;
+        carry = (t < rf[w]) || (sum < t) ? 1ull : 0ull;
+        dn[NWD - 1 - w] = __builtin_bitreverse64(rf[w] & ~sum);
+      }
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) h[k][w] = o[k][w] | up[w] | dn[w];
+    }
+    bool ch = false;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) {
+        u64 above = __shfl_up(h[k][w], 1, 64), below = __shfl_down(h[k][w], 1, 64);
+        if (k > 0) {
+          const u64 prev = __shfl(h[k > 0 ? k - 1 : 0][w], 63, 64);
+          if (lane == 0) above = prev;
+        }
+        if (k + 1 < NS) {
+          const u64 next = __shfl(h[k + 1 < NS ? k + 1 : k][w], 0, 64);
+          if (lane == 63) below = next;
+        }
+        const u64 n = h[k][w] | ((above | below) & fr[k][w]);
+        ch |= n != o[k][w];
+        o[k][w] = n;
+      }
+    }
+    if (!__any(ch)) break;
+  }
+  const int newlab = lut[(size_t)J.b * nlab + J.lab];
+  int* ob = out + (size_t)J.b * H * W;
+  for (int r = 1; r <= J.ly; ++r) {
+#pragma unroll
+    for (int w = 0; w < NWD; ++w) {
+      u64 iv = 0ull, mv = 0ull;
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        if (k == (r >> 6)) { iv = ~o[k][w] & full[w]; mv = mrow[k][w]; }
+      const u64 in_r = __shfl(iv, r & 63, 64), m_r = __shfl(mv, r & 63, 64);
+      const int col = 64 * w + lane;
+      if (col >= 1 && col <= J.lx && ((in_r >> lane) & 1ull)) {
+        const size_t idx = (size_t)(J.y0 + r - 1) * W + J.x0 + col - 1;
+        if (((m_r >> lane) & 1ull) || Mb[idx] == 0) atomicMax(ob + idx, newlab);
+      }
+    }
+  }
+}
+
 // LDS variant with a block size matched to the masks (the launcher buckets small masks by their
 // LDS need, so a 20x20 mask no longer reserves the 48 KiB of the largest one).  dv = rows per work
 // item of the sliding-window sweep: 4 gives each mask twice the lanes and half the serial LDS
@@ -968,6 +1094,19 @@ int be_cp_fill_holes(const int* M, const void* jobs, int njobs, int H, int W, co
   return BE_CHECK_LAUNCH();
 }
 
+// One-wave hole filling (plan kind 3): big = 0: boxes (+ ring) <= 64 x 64 (bucket 0), big = 1:
+// <= 256 rows x 128 columns (bucket 1).  4 waves per workgroup.
+int be_cp_fill_holes_wave(const int* M, const void* jobs, int njobs, int H, int W, const int* lut, int nlab, int* out,
+                          int big, hipStream_t s) {
+  if (njobs == 0) return 0;
+  const dim3 g((unsigned)((njobs + 3) / 4));
+  if (big)
+    hipLaunchKernelGGL((fill_holes_bits_kernel<4, 2>), g, dim3(256), 0, s, M, (const MaskJob*)jobs, njobs, H, W, lut, nlab, out);
+  else
+    hipLaunchKernelGGL((fill_holes_bits_kernel<1, 1>), g, dim3(256), 0, s, M, (const MaskJob*)jobs, njobs, H, W, lut, nlab, out);
+  return BE_CHECK_LAUNCH();
+}
+
 int be_cp_mask_job_bytes() { return (int)sizeof(MaskJob); }
 
 // Job planning for the per-mask kernels in one launch (replaces ~80 small torch ops and their host
@@ -1004,8 +1143,21 @@ __global__ __launch_bounds__(256) void plan_masks_kernel(const int* __restrict__
   const int ly = y1 - y0 + 1, lx = x1 - x0 + 1;
   // kind 2 = kind 0 with the compact work-queue buckets in front: 0 = wave jobs, 1 = workgroup
   // jobs (diffuse_q_kernel), 2.. = kind 0's buckets for the masks those cannot take
-  const int q2 = kind == 2 ? 2 : 0;
+  // kind 3 = kind 1 with the one-wave hole-filling buckets in front: 0 = box + ring <= 64 x 64,
+  // 1 = <= 256 rows x 128 columns
+  const int q2 = kind == 2 ? 2 : (kind == 3 ? 2 : 0);
   if (kind == 2) kind = 0;
+  if (kind == 3) {
+    kind = 1;
+    const int kw = (ly + 2 <= 64 && lx + 2 <= 64) ? 0 : ((ly + 2 <= 256 && lx + 2 <= 128) ? 1 : -1);
+    if (!(valid && !valid[i]) && kw >= 0) {
+      const int slot = atomicAdd(counts + kw, 1);
+      MaskJob J;
+      J.b = b; J.lab = lab; J.y0 = y0; J.x0 = x0; J.ly = ly; J.lx = lx; J.scratch = -1;
+      jobs[(size_t)kw * n + slot] = J;
+      return;
+    }
+  }
   if (kind == 0) atomicMax(niter_img + b, 2 * (ly + lx + 2));  // 2 * ((y1-y0)+(x1-x0)+4)
   if (valid && !valid[i]) return;
   const long long RY = ly + 2, RX = lx + 2, R = RY * RX;

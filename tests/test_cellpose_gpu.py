@@ -145,6 +145,47 @@ def test_fill_holes_gpu(gpu):
 
 
 @pytest.mark.gpu
+def test_fill_holes_wave_kernel_matches_lds_kernel_and_oracle(gpu, monkeypatch):
+    """One-wave bit-row hole filling (boxes + ring <= 64 x 64, and <= 256 x 128) vs the LDS
+    flood-fill kernel and the numpy oracle, on rings, nested labels, boxes at the size limits of
+    each kernel, multi-slot rows, islands and random blobs."""
+    from bioengine_worker_amd.cellpose import gpu as cg
+
+    rng = np.random.default_rng(7)
+    M = np.zeros((2, 200, 240), np.int32)
+    yy, xx = np.mgrid[0:200, 0:240]
+    M[0][((yy - 40) ** 2 + (xx - 40) ** 2 < 30 ** 2) & ((yy - 40) ** 2 + (xx - 40) ** 2 >= 12 ** 2)] = 1  # ring, 61 px box
+    M[0][(yy - 40) ** 2 + (xx - 40) ** 2 < 4 ** 2] = 2  # another label inside the hole
+    M[0, 100:162, 5:67] = 3  # 62 x 62 box: the largest one-wave box
+    M[0, 110:150, 15:55] = 0  # its hole
+    M[0, 120:125, 30:35] = 4
+    M[0, 100:163, 100:110] = 5  # 63 rows (65 with the ring): the 256 x 128 bit-row kernel
+    M[0, 120:130, 103:107] = 0
+    M[0, 30:160, 205:235] = 8  # 130 rows: three row slots per lane
+    M[0, 40:150, 210:230] = 0
+    M[0, 60:70, 215:220] = 8   # an island inside its own hole
+    M[0, 170:198, 5:235] = 9   # 230 columns: the LDS kernel
+    M[0, 175:190, 10:200] = 0
+    M[0, 10:20, 150:230] = 6
+    M[0, 12:18, 152:160] = 0
+    M[0, 14:16, 170:200] = 0
+    lab = 7
+    for _ in range(60):  # random blobs with holes
+        cy, cx, r = rng.integers(10, 190), rng.integers(10, 230), rng.integers(3, 12)
+        blob = ((yy - cy) ** 2 + (xx - cx) ** 2 < r * r) & (rng.random((200, 240)) > 0.15)
+        M[1][blob] = lab
+        lab += 1
+    Mt = torch.from_numpy(M).to(gpu)
+    monkeypatch.setattr(cg, "FILL_WAVE", False)
+    lds = cg.fill_holes_gpu(Mt, min_size=15).cpu().numpy()
+    monkeypatch.setattr(cg, "FILL_WAVE", True)
+    wave = cg.fill_holes_gpu(Mt, min_size=15).cpu().numpy()
+    np.testing.assert_array_equal(wave, lds)
+    for b in range(2):
+        np.testing.assert_array_equal(wave[b], ref.fill_holes_and_remove_small_masks(M[b], 15))
+
+
+@pytest.mark.gpu
 def test_tiles_gather_blend_roundtrip(gpu):
     from bioengine_worker_amd.cellpose.gpu import TilePlan
 
@@ -181,10 +222,13 @@ def test_follow_flows_launch_variants_identical(gpu, monkeypatch):
         ys.append(np.concatenate([dP, cp[None]], 0))
     y = torch.from_numpy(np.stack(ys)).to(gpu)
     outs = []
-    for entry in ("be_cp_follow_flows", "be_cp_follow_flows_xcd", "be_cp_follow_flows_xcd_pool"):
-        monkeypatch.setattr(cg, "FOLLOW_FLOWS_ENTRY", entry)
+    for entry in ("be_cp_follow_flows", "be_cp_follow_flows_xcd", "be_cp_follow_flows_xcd_pool", "be_cp_follow_flows_lds",
+                  "be_cp_follow_flows_lds:32"):
+        name, _, tile = entry.partition(":")
+        monkeypatch.setattr(cg, "FOLLOW_FLOWS_ENTRY", name)
+        monkeypatch.setenv("BE_FOLLOW_TILE", tile or "0")
         outs.append(cg.compute_masks_gpu(y).cpu())
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
 @pytest.mark.gpu

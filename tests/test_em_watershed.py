@@ -129,6 +129,22 @@ def test_edt3d_matches_scipy(gpu):
 
 
 @pytest.mark.gpu
+def test_edt3d_bounded_search_and_fallback_lines(gpu):
+    """The per-voxel bounded search (thin objects) and the flagged-line envelope fallback (objects
+    thicker than its 64-voxel cap, and a column block with no background at all along z) both give
+    scipy's exact transform."""
+    from scipy import ndimage
+
+    m = np.zeros((40, 180, 200), bool)
+    m[:, 10:170, 20:190] = True        # every z-column of this block is foreground: INF after the z pass
+    m[5:35, 60:65, 30:35] = False      # ... except a few background holes
+    m[3:8, 2:6, 2:6] = True            # thin object
+    got = mito.edt3d(torch.from_numpy(m).to(gpu)).cpu().numpy()
+    want = ndimage.distance_transform_edt(m)
+    assert np.abs(got - want).max() < 1e-3
+
+
+@pytest.mark.gpu
 def test_blend3d_gpu_matches_oracle(gpu):
     torch.manual_seed(0)
     v = torch.rand(19, 45, 37)
@@ -176,3 +192,26 @@ def test_analyze_volume_split_touching_gpu(gpu):
     plain = vol_mod.analyze_volume(torch.from_numpy(m).to(gpu), vol_mod.probability_identity, tile=32, overlap=8,
                                    min_voxels=50, norm_range=(0.0, 1.0))
     assert out["n_instances"] == 2 and plain["n_instances"] == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim", [2, 3])
+def test_watershed_active_tiles_identical_to_full_sweeps(gpu, dim, monkeypatch):
+    """The active-tile sweeps (only tiles whose neighbourhood changed) reach the same unique
+    fixpoint as relaxing every tile every sweep."""
+    rng = np.random.default_rng(11)
+    shape = (150, 170) if dim == 2 else (24, 90, 100)
+    m = rng.random(shape) > 0.35
+    m = torch.from_numpy(m).to(gpu)
+    dist = mito.edt(m) if dim == 2 else mito.edt3d(m)
+    elev = -dist + 0.01 * torch.from_numpy(rng.random(shape).astype(np.float32)).to(gpu)
+    markers = torch.zeros(shape, dtype=torch.int32)
+    flat = markers.view(-1)
+    flat[torch.from_numpy(rng.choice(flat.numel(), 40, replace=False))] = torch.arange(1, 41, dtype=torch.int32)
+    markers = markers.to(gpu)
+    outs = []
+    for active in (False, True):
+        monkeypatch.setattr(mito, "WS_ACTIVE_TILES", active)
+        outs.append(mito.watershed_gpu(elev, markers, m).cpu())
+    assert int(outs[0].max()) > 0
+    assert torch.equal(outs[0], outs[1])

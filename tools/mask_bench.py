@@ -15,7 +15,8 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="0,1,2",
-                    help="BE_DIFFUSE_VARIANT values, dv8,dv4,.. for BE_DIFFUSE_DV, q1 / q0 for the work-queue kernel on / off")
+                    help="BE_DIFFUSE_VARIANT values, dv8,dv4,.. for BE_DIFFUSE_DV, q1 / q0 (diffusion queue), fw1 / fw0 (one-wave fill), "
+                         "fe:<entry> (follow-flows launch), base (all defaults), r04 (the round-4 stage)")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     from bioengine_worker_amd.cellpose import gpu as cg
@@ -38,6 +39,14 @@ def main():
                 os.environ["BE_DIFFUSE_DV"] = v[2:]
             elif v.startswith("q"):
                 cg.DIFFUSE_QUEUE = v[1:] == "1"
+            elif v.startswith("fw"):
+                cg.FILL_WAVE = v[2:] == "1"
+            elif v.startswith("fe:"):
+                cg.FOLLOW_FLOWS_ENTRY = v[3:]
+            elif v == "base":  # every default on
+                cg.DIFFUSE_QUEUE, cg.FILL_WAVE, cg.FOLLOW_FLOWS_ENTRY = True, True, "be_cp_follow_flows_lds"
+            elif v == "r04":  # the round-4 mask stage
+                cg.DIFFUSE_QUEUE, cg.FILL_WAVE, cg.FOLLOW_FLOWS_ENTRY = False, False, "be_cp_follow_flows_xcd"
             else:
                 os.environ["BE_DIFFUSE_VARIANT"] = v
             torch.cuda.synchronize()
