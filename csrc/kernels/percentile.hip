@@ -53,16 +53,43 @@ __global__ __launch_bounds__(kThreads) void pct_hist_kernel(const float* __restr
   const float* row = x + (size_t)r * n;
   const long long c0 = (long long)blockIdx.x * chunk;
   const long long c1 = c0 + chunk < n ? c0 + chunk : n;
+  // Each thread counts runs of equal digits in registers and issues one LDS atomic per run: image
+  // rows are smooth, so a thread's successive elements (256 apart) mostly share the top digit, and
+  // one atomic per element serialised every wave on a handful of bins (0.22 ms per 32-image batch).
   if (pass == 0) {
-    for (long long i = c0 + threadIdx.x; i < c1; i += kThreads) atomicAdd(&h[0][fkey(row[i]) >> 24], 1u);
+    uint32_t cd = 0, cc = 0;
+    for (long long i = c0 + threadIdx.x; i < c1; i += kThreads) {
+      const uint32_t d = fkey(row[i]) >> 24;
+      if (d != cd) {
+        if (cc) atomicAdd(&h[0][cd], cc);
+        cd = d;
+        cc = 0;
+      }
+      ++cc;
+    }
+    if (cc) atomicAdd(&h[0][cd], cc);
   } else {
+    uint32_t cd[kT], cc[kT];
+#pragma unroll
+    for (int t = 0; t < kT; ++t) { cd[t] = 0; cc[t] = 0; }
     for (long long i = c0 + threadIdx.x; i < c1; i += kThreads) {
       const uint32_t k = fkey(row[i]);
       const uint32_t d = (k >> shift) & 255u;
 #pragma unroll
-      for (int t = 0; t < kT; ++t)
-        if (((k ^ pre[t]) & hi_mask) == 0) atomicAdd(&h[t][d], 1u);
+      for (int t = 0; t < kT; ++t) {
+        if (((k ^ pre[t]) & hi_mask) == 0) {
+          if (d != cd[t]) {
+            if (cc[t]) atomicAdd(&h[t][cd[t]], cc[t]);
+            cd[t] = d;
+            cc[t] = 0;
+          }
+          ++cc[t];
+        }
+      }
     }
+#pragma unroll
+    for (int t = 0; t < kT; ++t)
+      if (cc[t]) atomicAdd(&h[t][cd[t]], cc[t]);
   }
   __syncthreads();
   uint32_t* g = hist + (size_t)r * kT * 256;
