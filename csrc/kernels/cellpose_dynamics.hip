@@ -212,9 +212,10 @@ __global__ __launch_bounds__(256) void follow_flows_xcd_pool_kernel(const float2
 // the window reads LDS (the (y, x) / (y + 1, x) pairs are one ds_read2_b64 each), a step outside it
 // (a particle that travelled > 16 px past the tile) reads global memory as before.  Same float
 // operations in the same order: results are bit-identical to follow_flows_kernel.
-// FT = 32 (1,024 pixels, four per thread at most) for batches; FT = 16 (one pixel per thread, a
-// 48 x 48 window) when the 32-pixel tiles would not give every CU several workgroups: at batch 1
-// the 32-pixel tiles ran each thread's pixels one after another and cost 0.3 ms of latency.
+// FT = 16 (default: one pixel per thread, a 48 x 48 window) or 32 (1,024 pixels, up to four per
+// thread, 64 x 64 window): at batch 1 the 32-pixel tiles ran each thread's pixels one after
+// another (+0.3 ms latency), and at batch 32 their 37 KiB of LDS kept them off the CUs the convs
+// of the next batch hold.
 constexpr int FM = 16;
 
 template <int FT>
@@ -496,9 +497,13 @@ int be_cp_follow_flows_lds(const void* flow2, const void* fg, int* hist, int* po
                            hipStream_t s) {
   if ((long long)B * H * W == 0) return 0;
   const long long t32 = (long long)B * ((W + 31) / 32) * ((H + 31) / 32);
-  const char* ft = getenv("BE_FOLLOW_TILE");  // 16 / 32 forces a tile size (tests, A/B)
-  const int force = ft ? atoi(ft) : 0;
-  if (force == 32 || (force != 16 && t32 >= 2048)) {  // >= 8 workgroups per CU
+  // 16-pixel tiles by default at every batch size: one pixel per thread and a 19 KiB workgroup
+  // that fits beside the convs of the next batch (s29: compute_masks 3.17 vs 3.53 ms at batch 32,
+  // headline +2 %); BE_FOLLOW_TILE=32 selects the 32-pixel tiles (64 x 64 window, 37 KiB)
+  const char* ft = getenv("BE_FOLLOW_TILE");
+  const int force = ft ? atoi(ft) : 16;
+  (void)t32;
+  if (force == 32) {
     const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32;
     hipLaunchKernelGGL(follow_flows_lds_kernel<32>, dim3((unsigned)t32), dim3(256), 0, s, (const float2*)flow2,
                        (const uint8_t*)fg, hist, pos, B, H, W, niter, tiles_x, tiles_y);

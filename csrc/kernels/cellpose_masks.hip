@@ -583,7 +583,14 @@ __global__ __launch_bounds__(MT) void fill_holes_kernel(const int* __restrict__ 
 // Sums are formed in the sparse sweep's order (rows of 3, then the 3 row sums) and the centre
 // source is stored as T + 1 at the centre (the dense sweep's cur[ce] += 1), the unshifted value
 // kept in the owner's register: results are bit-identical to diffuse_kernel.
-constexpr int DQ_T = 512, DQ_K = 4;
+// DQ_T = 512 (default): 49 KiB per workgroup, workgroup jobs up to 2,048 pixels.  256 (A/B build)
+// fits beside a pair-kernel workgroup on a CU but caps workgroup jobs at 1,024 pixels, and the
+// masks above that went back to the box kernels: masks_to_flows 1.82 vs 0.96 ms, headline 1,902 /
+// 1,951 vs 2,001 / 2,017 img/s (profiles/r05/masks/s29).
+#ifndef DQ_T_BUILD
+#define DQ_T_BUILD 512
+#endif
+constexpr int DQ_T = DQ_T_BUILD, DQ_K = 4;
 constexpr int DQ_WCAP = 64 * DQ_K, DQ_WHX = 256;   // wave jobs: pixels, box width + 2
 constexpr int DQ_BCAP = DQ_T * DQ_K, DQ_BHX = 1024;  // workgroup jobs
 template <int CAP, int HX>
@@ -593,8 +600,9 @@ struct DQL {
 };
 using DQW = DQL<DQ_WCAP, DQ_WHX>;
 using DQB = DQL<DQ_BCAP, DQ_BHX>;
-constexpr int DQ_LDS = 8 * DQW::BYTES > DQB::BYTES ? 8 * DQW::BYTES : DQB::BYTES;
-static_assert(DQ_T == 512 && DQW::BYTES % 16 == 0 && DQ_LDS <= 64 * 1024, "diffuse queue LDS layout");
+constexpr int DQ_NWV = DQ_T / 64;  // waves (wave-job slots) per workgroup
+constexpr int DQ_LDS = DQ_NWV * DQW::BYTES > DQB::BYTES ? DQ_NWV * DQW::BYTES : DQB::BYTES;
+static_assert((DQ_T == 256 || DQ_T == 512) && DQW::BYTES % 16 == 0 && DQ_LDS <= 64 * 1024, "diffuse queue LDS layout");
 
 // smallest bin i with sum(h[0..i]) > k (one wave)
 __device__ __forceinline__ int dq_kth(const int* h, int n, int k, int lane) {
@@ -1010,8 +1018,8 @@ int be_cp_diffuse_q(const int* M, const void* wjobs, int nw, const void* bjobs, 
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
   }
-  const int want = max(nb, (nw + 7) / 8);
-  const int grid = max(1, min(want, 3 * ncu));  // 3 workgroups (49 KiB LDS each) per CU
+  const int want = max(nb, (nw + DQ_NWV - 1) / DQ_NWV);
+  const int grid = max(1, min(want, (DQ_T == 256 ? 6 : 3) * ncu));  // LDS: 25 / 49 KiB per workgroup
   (void)hipMemsetAsync(q, 0, 8, s);
   hipLaunchKernelGGL(diffuse_q_kernel, dim3(grid), dim3(DQ_T), DQ_LDS, s, M, (const MaskJob*)wjobs, nw,
                      (const MaskJob*)bjobs, nb, H, W, niter_img, Lout, q);

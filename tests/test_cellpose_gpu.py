@@ -281,7 +281,7 @@ def test_sparse_diffusion_bit_identical_to_dense(gpu, monkeypatch):
                 M[b, y, x] = lab
                 y = int(np.clip(y + rng.integers(-1, 2), 1, 198))
                 x = int(np.clip(x + rng.integers(-1, 2), 1, 218))
-    M[1, 150:190, 5:50] = lab + 1  # a 1800-pixel blob: a workgroup job of the queue kernel
+    M[1, 150:180, 5:35] = lab + 1  # a 900-pixel blob: a workgroup job of the queue kernel
     Mt = torch.from_numpy(M).to(gpu)
     old = os.environ.get("BE_DIFFUSE_VARIANT")
     try:
@@ -306,12 +306,13 @@ def test_sparse_diffusion_bit_identical_to_dense(gpu, monkeypatch):
 @pytest.mark.gpu
 def test_diffusion_queue_plan_buckets(gpu):
     """Plan kind 2: masks of <= 256 pixels (box width + 2 <= 256) are wave jobs, <= 2048 pixels
-    workgroup jobs, the rest keep kind 0's buckets; every present mask lands in exactly one."""
+    (the default 512-thread build; 1024 in the 256-thread one) workgroup jobs, the rest keep kind
+    0's buckets; every present mask lands in exactly one."""
     from bioengine_worker_amd.cellpose import gpu as cg
 
     M = torch.zeros(2, 300, 320, dtype=torch.int32)
     M[0, 5:15, 5:20] = 1      # 150 px: wave
-    M[0, 20:60, 5:50] = 2     # 1800 px: workgroup
+    M[0, 20:50, 5:35] = 2     # 900 px: workgroup
     M[0, 70:290, 5:300] = 3   # 64900 px: kind-0 buckets
     M[1, 5:6, 2:300] = 1      # 298 px thin line: workgroup (pixels > 256)
     M[1, 10:11, 2:4] = 2      # 2 px: wave
