@@ -591,6 +591,13 @@ __global__ __launch_bounds__(MT) void fill_holes_kernel(const int* __restrict__ 
 #define DQ_T_BUILD 512
 #endif
 constexpr int DQ_T = DQ_T_BUILD, DQ_K = 4;
+#ifndef DQ_DPP
+// 1: horizontal neighbours by DPP from the adjacent lanes (3 LDS reads per pixel instead of 9).
+// Measured slower (s32: masks_to_flows 1.12 vs 0.97 ms, batch-1 2.03 vs 1.82 ms): the sweep is
+// bound by its dependent latency, not LDS bandwidth, and the DPP moves + the divergent run-edge
+// reads lengthen the chain.  Kept as an A/B build.
+#define DQ_DPP 0
+#endif
 constexpr int DQ_WCAP = 64 * DQ_K, DQ_WHX = 256;   // wave jobs: pixels, box width + 2
 constexpr int DQ_BCAP = DQ_T * DQ_K, DQ_BHX = 1024;  // workgroup jobs
 template <int CAP, int HX>
@@ -603,6 +610,21 @@ using DQB = DQL<DQ_BCAP, DQ_BHX>;
 constexpr int DQ_NWV = DQ_T / 64;  // waves (wave-job slots) per workgroup
 constexpr int DQ_LDS = DQ_NWV * DQW::BYTES > DQB::BYTES ? DQ_NWV * DQW::BYTES : DQB::BYTES;
 static_assert((DQ_T == 256 || DQ_T == 512) && DQW::BYTES % 16 == 0 && DQ_LDS <= 64 * 1024, "diffuse queue LDS layout");
+
+// lane l <- lane l - 1 (prev) / l + 1 (next) of a double, across the whole wave (DPP wave_shr /
+// wave_shl: VALU, no LDS traffic); the end lanes get 0
+__device__ __forceinline__ double dq_from_prev(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dq_from_next(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 // smallest bin i with sum(h[0..i]) > k (one wave)
 __device__ __forceinline__ int dq_kth(const int* h, int n, int k, int lane) {
@@ -733,6 +755,18 @@ __device__ __forceinline__ void dq_job(const MaskJob& J, const int* __restrict__
   const int cidx = (int)(*best & 0xffffffffu);
   if (t == 0) T0[cidx] = 1.0;  // S = T + e_c: the centre source of the first sweep
   sync();
+  // DQ_DPP builds: horizontal neighbours from the adjacent lanes: ranks are raster-ordered and lane l - 1 of the
+  // same slot holds rank r - 1, so when the left pixel is rank r - 1 the left column (up-left,
+  // left, down-left) is exactly lane l - 1's own column, which it reads anyway; likewise on the
+  // right.  A sweep then reads 3 values per pixel from LDS (its column) and takes the other 6 by
+  // DPP, reading them itself only where a row run starts or ends (or at the wave's end lanes).
+  // The 9 values and the order they are summed in are unchanged.
+  bool lok[K], rok[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    lok[j] = own[j] && lane > 0 && off[j][3] == (myr[j] - 1) * 8;
+    rok[j] = own[j] && lane < 63 && off[j][5] == (myr[j] + 1) * 8;
+  }
   const int niter = niter_img[J.b];
   const int nsl = (P + NTH - 1) / NTH;  // slots in use (uniform)
   double* cur = T0;
@@ -744,8 +778,25 @@ __device__ __forceinline__ void dq_job(const MaskJob& J, const int* __restrict__
     for (int j = 0; j < K; ++j) {
       if (j < nsl) {
         double v[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) v[k] = *reinterpret_cast<const double*>(cb + off[j][k]);
+        v[1] = *reinterpret_cast<const double*>(cb + off[j][1]);
+        v[4] = *reinterpret_cast<const double*>(cb + off[j][4]);
+        v[7] = *reinterpret_cast<const double*>(cb + off[j][7]);
+        const double l1 = dq_from_prev(v[1]), l4 = dq_from_prev(v[4]), l7 = dq_from_prev(v[7]);
+        const double r1 = dq_from_next(v[1]), r4 = dq_from_next(v[4]), r7 = dq_from_next(v[7]);
+        if (DQ_DPP && lok[j]) {
+          v[0] = l1; v[3] = l4; v[6] = l7;
+        } else {
+          v[0] = *reinterpret_cast<const double*>(cb + off[j][0]);
+          v[3] = *reinterpret_cast<const double*>(cb + off[j][3]);
+          v[6] = *reinterpret_cast<const double*>(cb + off[j][6]);
+        }
+        if (DQ_DPP && rok[j]) {
+          v[2] = r1; v[5] = r4; v[8] = r7;
+        } else {
+          v[2] = *reinterpret_cast<const double*>(cb + off[j][2]);
+          v[5] = *reinterpret_cast<const double*>(cb + off[j][5]);
+          v[8] = *reinterpret_cast<const double*>(cb + off[j][8]);
+        }
         const double hp = v[0] + v[1] + v[2];
         const double hc = v[3] + v[4] + v[5];
         const double hn = v[6] + v[7] + v[8];
