@@ -224,8 +224,13 @@ __global__ __launch_bounds__(256) void follow_flows_lds_kernel(const float2* __r
                                                                int* __restrict__ pos, int B, int H, int W, int niter,
                                                                int tiles_x, int tiles_y) {
   constexpr int FWN = FT + 2 * FM, NP = FT * FT / 256;  // passes of 256 pixels
+  // window row stride FWN + 1 float2 (odd in 8-byte units): with FWN, rows y and y + 2 (stride
+  // 96 dwords = 32 mod 64 banks) or every row (FWN = 64: 128 dwords) shared their banks, and a
+  // wave's corner reads -- lanes spread over the tile's rows -- measured 10 bank conflicts per LDS
+  // instruction (profiles/r05/pmc/s35)
+  constexpr int FWS = FWN + 1;
   constexpr int LG = FT == 32 ? 5 : 4;
-  __shared__ float2 win[FWN * FWN];
+  __shared__ float2 win[FWN * FWS];
   __shared__ short list[FT * FT];
   __shared__ int wcount[4 * NP];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -261,8 +266,9 @@ __global__ __launch_bounds__(256) void follow_flows_lds_kernel(const float2* __r
   const float2* fl = flow2 + b * HW;
   const int wy0 = ty0 - FM, wx0 = tx0 - FM;
   for (int i = tid; i < FWN * FWN; i += 256) {
-    const int gy = wy0 + i / FWN, gx = wx0 + i % FWN;
-    win[i] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? fl[(size_t)gy * W + gx] : make_float2(0.f, 0.f);
+    const int wy = i / FWN, wx = i % FWN;
+    const int gy = wy0 + wy, gx = wx0 + wx;
+    win[wy * FWS + wx] = (gy >= 0 && gy < H && gx >= 0 && gx < W) ? fl[(size_t)gy * W + gx] : make_float2(0.f, 0.f);
   }
   __syncthreads();
   const float sy_scale = (H > 1) ? (float)H / (float)(H - 1) : 0.f;
@@ -282,11 +288,11 @@ __global__ __launch_bounds__(256) void follow_flows_lds_kernel(const float2* __r
       const int ly = y0 - wy0, lx = x0 - wx0;
       float2 a, bq, c, d;
       if ((unsigned)ly < (unsigned)(FWN - 1) && (unsigned)lx < (unsigned)(FWN - 1)) {
-        const float2* w = win + ly * FWN + lx;
+        const float2* w = win + ly * FWS + lx;
         a = w[0];
         bq = w[1];
-        c = w[FWN];
-        d = w[FWN + 1];
+        c = w[FWS];
+        d = w[FWS + 1];
       } else {
         a = ldflow(fl, H, W, y0, x0);
         bq = ldflow(fl, H, W, y0, x0 + 1);
