@@ -112,10 +112,19 @@ def compact_labels(roots: torch.Tensor) -> tuple[torch.Tensor, int]:
 
 def _keep_large(roots: torch.Tensor, min_size: int) -> torch.Tensor:
     """Foreground voxels whose component (CCL root index, -1 = background) has >= ``min_size``
-    voxels.  Sizes come from one sort (``unique`` with counts): counting with atomics into the root
-    slots serialises on large components -- millions of adds to one address took 5 s on a
-    128 x 2048^2 EM volume."""
+    voxels.  GPU: run-length atomics (one add per run of equal roots along x) into a per-root
+    counter -- plain per-voxel atomics serialised on large components (millions of adds to one
+    address took 5 s on a 128 x 2048^2 volume), and the sort-based ``unique`` that replaced them
+    took 0.25 s per 256 x 2048^2 slab.  CPU: ``unique`` with counts."""
     flat = roots.reshape(-1)
+    if COMP_KEEP_GPU and flat.is_cuda and flat.dtype == torch.int32 and flat.numel() < 2 ** 31:
+        # run-length atomics into a per-root counter (be_component_keep), no sort
+        rc = flat.contiguous()
+        counts = torch.empty(rc.numel(), dtype=torch.int32, device=rc.device)
+        out = torch.empty(rc.numel(), dtype=torch.uint8, device=rc.device)
+        _native.call("be_component_keep", _native.ptr(rc), rc.numel(), _native.ptr(counts), int(min_size), _native.ptr(out),
+                     _native.stream(rc.device))
+        return out.view(torch.bool).reshape(roots.shape)
     fg = flat >= 0
     _, inv, cnt = torch.unique(flat[fg], return_inverse=True, return_counts=True)
     keep = torch.zeros(flat.shape, dtype=torch.bool, device=roots.device)
@@ -143,7 +152,7 @@ def edt(mask: torch.Tensor) -> torch.Tensor:
     dev = m.device
     dist = torch.empty(H, W, dtype=torch.float32, device=dev)
     g = torch.empty(H, W, dtype=torch.int32, device=dev)
-    v = torch.empty(H, W, dtype=torch.int32, device=dev)
+    v = torch.empty(H * W + H, dtype=torch.int32, device=dev)  # tail: fallback row flags
     z = torch.empty(H, W + 1, dtype=torch.float64, device=dev)
     _native.call("be_edt", _native.ptr(m), _native.ptr(dist), _native.ptr(g), _native.ptr(v), _native.ptr(z), 1, H, W,
                  _native.stream(dev))
@@ -204,6 +213,12 @@ def watershed(neg_dist: np.ndarray, markers: np.ndarray, mask: np.ndarray, conn:
     _native.rt_call("be_rt_watershed", vp(img), vp(mk), vp(ms), D, H, W, conn, vp(out))
     return out
 
+
+#: component sizes by run-length atomics (BE_COMP_KEEP=0: torch.unique sort)
+COMP_KEEP_GPU = os.environ.get("BE_COMP_KEEP", "1") != "0"
+
+#: closing on bit-packed rows (BE_MORPH_BITS=0: the per-pixel window kernel)
+MORPH_BITS = os.environ.get("BE_MORPH_BITS", "1") != "0"
 
 #: relax only the tiles whose neighbourhood changed in the previous sweep (BE_WS_ACTIVE=0: every tile)
 WS_ACTIVE_TILES = os.environ.get("BE_WS_ACTIVE", "1") != "0"
@@ -364,8 +379,13 @@ def closing_per_slice(binary: torch.Tensor, r: int) -> torch.Tensor:
         b = binary.cpu().numpy()
         return torch.from_numpy(np.stack([ndimage.binary_closing(b[z], structure=disk) for z in range(D)]))
     m8 = binary.to(torch.uint8).contiguous()
-    tmp, out = torch.empty_like(m8), torch.empty_like(m8)
     st = _native.stream(binary.device)
+    if MORPH_BITS and r < 64:  # bit-packed rows (be_closing_disk_bits), same result
+        out = torch.empty_like(m8)
+        bits = torch.empty(2 * D * H * ((W + 63) // 64), dtype=torch.int64, device=binary.device)
+        _native.call("be_closing_disk_bits", _native.ptr(m8), _native.ptr(out), _native.ptr(bits), D, H, W, r, 0, st)
+        return out.bool()
+    tmp, out = torch.empty_like(m8), torch.empty_like(m8)
     _native.call("be_morph_disk", _native.ptr(m8), _native.ptr(tmp), D, H, W, r, 0, 0, st)
     _native.call("be_morph_disk", _native.ptr(tmp), _native.ptr(out), D, H, W, r, 1, 0, st)
     return out.bool()

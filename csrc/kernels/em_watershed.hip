@@ -256,9 +256,66 @@ __global__ void edt3_axis(const float* __restrict__ fin, float* __restrict__ fou
   }
 }
 
+// ---------------------------------------------------------------- component size filter
+// Sizes of CCL components (root = a voxel index, -1 = background) by run-length atomics: a thread
+// walks CS_RUN consecutive voxels and adds once per run of equal roots, and a wave whose lanes all
+// end on the same root (the inside of a large component) adds their runs with ONE atomic.  Plain
+// per-voxel atomics serialised on the counters of large components (5 s per 128 x 2048^2), and so
+// did 32-voxel runs without the wave combine (0.76 s per 256 x 2048^2, s38); the torch.unique
+// sort this replaces took 0.25 s.
+constexpr int CS_RUN = 256;
+
+__global__ __launch_bounds__(256) void comp_count_kernel(const int* __restrict__ roots, long long n, int* __restrict__ counts) {
+  const long long seg = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long i0 = seg * CS_RUN;
+  const long long i1 = i0 + CS_RUN < n ? i0 + CS_RUN : n;
+  int cur = -1, run = 0;
+  for (long long i = i0; i < i1; ++i) {
+    const int r = roots[i];
+    if (r != cur) {
+      if (cur >= 0) atomicAdd(counts + cur, run);
+      cur = r;
+      run = 0;
+    }
+    ++run;
+  }
+  // pending run: one atomic per wave when every lane holds the same root
+  const int lane = threadIdx.x & 63;
+  const int c0 = __shfl(cur, 0, 64);
+  if (__all(cur == c0)) {
+    int sum = run;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0 && c0 >= 0) atomicAdd(counts + c0, sum);
+  } else if (cur >= 0) {
+    atomicAdd(counts + cur, run);
+  }
+}
+
+__global__ __launch_bounds__(256) void comp_keep_kernel(const int* __restrict__ roots, long long n,
+                                                        const int* __restrict__ counts, int min_size,
+                                                        unsigned char* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int r = roots[i];
+  out[i] = (r >= 0 && counts[r] >= min_size) ? 1 : 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+// out[i] = 1 where voxel i's component (roots: CCL root voxel index, -1 background, all < n) has
+// >= min_size voxels.  counts: n ints of scratch.
+int be_component_keep(const int* roots, long long n, int* counts, int min_size, unsigned char* out, hipStream_t s) {
+  if (n == 0) return 0;
+  (void)hipMemsetAsync(counts, 0, (size_t)n * sizeof(int), s);
+  const long long nseg = (n + CS_RUN - 1) / CS_RUN;
+  hipLaunchKernelGGL(comp_count_kernel, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, s, roots, n, counts);
+  hipLaunchKernelGGL(comp_keep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, roots, n, counts, min_size, out);
+  return BE_CHECK_LAUNCH();
+}
+
 
 // Marker watershed on elev (e.g. -EDT) restricted to mask (uint8, optional), markers int32 (>0),
 // D = 1 for 2-D.  key: [n] uint64 scratch, flags: [n] uint8 scratch, changed: 1 int (device).

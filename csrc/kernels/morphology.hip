@@ -82,6 +82,78 @@ __global__ void morph_disk(const unsigned char* __restrict__ in, unsigned char* 
   out[gid] = res ? 1 : 0;
 }
 
+// Bit-packed disk morphology: 64 pixels of a row per 64-bit word.  A footprint row dy covers
+// dx in [-w, w], w = floor(sqrt(r^2 - dy^2)); its contribution to a word is the OR (dilation) /
+// AND (erosion) of the word shifted by every dx, with the neighbouring words supplying the bits
+// that cross the word edge.  Pixels outside the image read as border_value, exactly like
+// morph_disk -- whose per-pixel loop over the (2r+1)^2 window took 0.13 s for the closing of a
+// 256 x 2048^2 slab; this costs ~2 bit operations per pixel.
+__device__ __forceinline__ unsigned long long mb_word(const unsigned long long* __restrict__ row, int k, int nwd, int W,
+                                                      bool row_in, int border) {
+  const unsigned long long bv = border ? ~0ull : 0ull;
+  if (!row_in || k < 0 || k >= nwd) return bv;
+  unsigned long long w = row[k];
+  const int valid = W - 64 * k;  // pixels of this word inside the image
+  if (valid < 64) {
+    const unsigned long long m = (1ull << valid) - 1ull;
+    w = (w & m) | (bv & ~m);
+  }
+  return w;
+}
+
+__global__ __launch_bounds__(256) void pack_bits_kernel(const unsigned char* __restrict__ in, unsigned long long* __restrict__ out,
+                                                        long long rows, int W, int nwd) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= rows * nwd) return;
+  const long long row = g / nwd;
+  const int k = (int)(g % nwd);
+  const unsigned char* p = in + row * W + 64 * k;
+  const int n = min(64, W - 64 * k);
+  unsigned long long w = 0;
+  for (int i = 0; i < n; ++i) w |= (unsigned long long)(p[i] != 0) << i;
+  out[g] = w;
+}
+
+__global__ __launch_bounds__(256) void unpack_bits_kernel(const unsigned long long* __restrict__ in, unsigned char* __restrict__ out,
+                                                          long long rows, int W, int nwd) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= rows * W) return;
+  const long long row = g / W;
+  const int x = (int)(g % W);
+  out[g] = (unsigned char)((in[row * nwd + (x >> 6)] >> (x & 63)) & 1ull);
+}
+
+__global__ __launch_bounds__(256) void morph_disk_bits_kernel(const unsigned long long* __restrict__ in,
+                                                              unsigned long long* __restrict__ out, int B, int H, int W,
+                                                              int nwd, int r, int op, int border) {
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (long long)B * H * nwd) return;
+  const int k = (int)(g % nwd);
+  const long long by = g / nwd;
+  const int y = (int)(by % H);
+  const unsigned long long* base = in + (by - y) * nwd;  // slice start
+  unsigned long long acc = op == 1 ? ~0ull : 0ull;
+  for (int dy = -r; dy <= r; ++dy) {
+    int w = 0;
+    while ((w + 1) * (w + 1) + dy * dy <= r * r) ++w;
+    const int yy = y + dy;
+    const bool rin = yy >= 0 && yy < H;
+    const unsigned long long* row = base + (long long)(rin ? yy : 0) * nwd;
+    const unsigned long long p = mb_word(row, k - 1, nwd, W, rin, border);
+    const unsigned long long c = mb_word(row, k, nwd, W, rin, border);
+    const unsigned long long n = mb_word(row, k + 1, nwd, W, rin, border);
+    unsigned long long v = c;
+    for (int s = 1; s <= w; ++s) {
+      // bit x of the result needs pixel x + s (from c, then n) and pixel x - s (from c, then p)
+      const unsigned long long right = (c >> s) | (n << (64 - s));
+      const unsigned long long left = (c << s) | (p >> (64 - s));
+      v = op == 1 ? (v & right & left) : (v | right | left);
+    }
+    acc = op == 1 ? (acc & v) : (acc | v);
+  }
+  out[g] = acc;
+}
+
 // column pass: g[y, x] = (distance along y to the nearest background pixel)^2 (int), or -1 = none
 __global__ void edt_cols(const unsigned char* __restrict__ fg, int* __restrict__ g, int B, int H, int W) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -105,10 +177,38 @@ __global__ void edt_cols(const unsigned char* __restrict__ fg, int* __restrict__
 
 // row pass: out[y, x] = sqrt(min_x' g[y, x'] + (x - x')^2) (lower envelope of parabolas, fp64
 // intersections so 4k+ rows stay exact); v int / z double scratch [B*H, W] / [B*H, W+1]
+// Row pass, one thread per PIXEL: d(q) = min_p (q - p)^2 + g(p), searched outwards from q until
+// r^2 reaches the best value (every farther site is at least r^2): a few steps for thin EM
+// foreground, neighbouring threads on neighbouring addresses.  A pixel whose search passes
+// EDT2_RCAP flags its row, and edt_rows (the lower envelope) redoes exactly those rows -- as
+// be_edt3d does; squared distances are exact integers, so the transform is unchanged.
+constexpr int EDT2_RCAP = 64;
+__global__ __launch_bounds__(256) void edt_rows_bf(const int* __restrict__ g, float* __restrict__ out, int B, int H, int W,
+                                                   unsigned char* __restrict__ only) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long long)B * H * W) return;
+  const long long row = gid / W;
+  const int q = (int)(gid - row * W);
+  const int* f = g + row * W;
+  const int NONE = 0x7fffffff;
+  int best = f[q] < 0 ? NONE : f[q];
+  const int rmax = max(q, W - 1 - q);
+  int r = 1;
+  for (; r <= rmax && r <= EDT2_RCAP; ++r) {
+    const int r2 = r * r;
+    if (r2 >= best) break;
+    if (q - r >= 0 && f[q - r] >= 0) best = min(best, r2 + f[q - r]);
+    if (q + r < W && f[q + r] >= 0) best = min(best, r2 + f[q + r]);
+  }
+  if (r > EDT2_RCAP && r <= rmax && r * r < best) only[row] = 1;
+  out[gid] = best == NONE ? 3.4e38f : (float)sqrt((double)best);
+}
+
 __global__ void edt_rows(const int* __restrict__ g, float* __restrict__ out, int* __restrict__ vbuf,
-                         double* __restrict__ zbuf, int B, int H, int W) {
+                         double* __restrict__ zbuf, int B, int H, int W, const unsigned char* __restrict__ only = nullptr) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (long long)B * H) return;
+  if (only && !only[gid]) return;
   const int* f = g + gid * W;
   float* o = out + gid * W;
   int* v = vbuf + gid * W;
@@ -195,11 +295,35 @@ int be_morph_disk(const void* in, void* out, int B, int H, int W, int r, int op,
   return BE_CHECK_LAUNCH();
 }
 
-// fg uint8 [B, H, W] -> dist f32 [B, H, W]; scratch: g int [B*H*W], v int [B*H*W], z f64 [B*H*(W+1)]
+// Closing (dilation then erosion) of B slices [H, W] uint8 with a radius-r disk on the bit-packed
+// form; bits: 2 * B * H * ceil(W / 64) uint64 of scratch.  Same result as two be_morph_disk calls.
+// r < 64 (a shift never crosses more than one word).
+int be_closing_disk_bits(const void* in, void* out, unsigned long long* bits, int B, int H, int W, int r, int border_value,
+                         hipStream_t s) {
+  const long long rows = (long long)B * H;
+  if (rows * W == 0) return 0;
+  if (r < 0 || r >= 64) return -1;
+  const int nwd = (W + 63) / 64;
+  const long long nw = rows * nwd;
+  unsigned long long* a = bits;
+  unsigned long long* b = bits + nw;
+  hipLaunchKernelGGL(pack_bits_kernel, dim3(nblk(nw)), dim3(256), 0, s, (const unsigned char*)in, a, rows, W, nwd);
+  hipLaunchKernelGGL(morph_disk_bits_kernel, dim3(nblk(nw)), dim3(256), 0, s, a, b, B, H, W, nwd, r, 0, border_value);
+  hipLaunchKernelGGL(morph_disk_bits_kernel, dim3(nblk(nw)), dim3(256), 0, s, b, a, B, H, W, nwd, r, 1, border_value);
+  hipLaunchKernelGGL(unpack_bits_kernel, dim3(nblk(rows * W)), dim3(256), 0, s, a, (unsigned char*)out, rows, W, nwd);
+  return BE_CHECK_LAUNCH();
+}
+
+// fg uint8 [B, H, W] -> dist f32 [B, H, W]; scratch: g int [B*H*W], v int [B*H*W + B*H] (the
+// tail holds the per-row fallback flags), z f64 [B*H*(W+1)]
 int be_edt(const void* fg, float* dist, int* g, int* v, double* z, int B, int H, int W, hipStream_t s) {
-  if ((long long)B * H * W == 0) return 0;
+  const long long n = (long long)B * H * W;
+  if (n == 0) return 0;
+  unsigned char* only = reinterpret_cast<unsigned char*>(v + n);
   hipLaunchKernelGGL(edt_cols, dim3(nblk((long long)B * W)), dim3(256), 0, s, (const unsigned char*)fg, g, B, H, W);
-  hipLaunchKernelGGL(edt_rows, dim3(nblk((long long)B * H)), dim3(256), 0, s, g, dist, v, z, B, H, W);
+  (void)hipMemsetAsync(only, 0, (size_t)B * H, s);
+  hipLaunchKernelGGL(edt_rows_bf, dim3(nblk(n)), dim3(256), 0, s, g, dist, B, H, W, only);
+  hipLaunchKernelGGL(edt_rows, dim3(nblk((long long)B * H)), dim3(256), 0, s, g, dist, v, z, B, H, W, only);
   return BE_CHECK_LAUNCH();
 }
 

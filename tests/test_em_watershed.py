@@ -215,3 +215,55 @@ def test_watershed_active_tiles_identical_to_full_sweeps(gpu, dim, monkeypatch):
         outs.append(mito.watershed_gpu(elev, markers, m).cpu())
     assert int(outs[0].max()) > 0
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+def test_component_size_filter_gpu_matches_sort(gpu):
+    """be_component_keep (run-length atomics) keeps exactly the components the sort-based
+    ``unique`` count keeps, including one component spanning most of the volume."""
+    from bioengine_worker_amd.em.volume import ccl3d
+
+    rng = np.random.default_rng(3)
+    m = rng.random((20, 70, 90)) > 0.55
+    m[2:18, 5:65, 5:85] |= rng.random((16, 60, 80)) > 0.2  # large connected blob
+    roots = ccl3d(torch.from_numpy(m).to(gpu))
+    got = mito._keep_large(roots, 40).cpu()
+    want = mito._keep_large(roots.cpu(), 40)
+    assert got.any() and (~got & torch.from_numpy(m)).any()
+    assert torch.equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,r", [((3, 50, 70), 4), ((2, 33, 130), 2), ((1, 40, 64), 5), ((2, 20, 200), 9)])
+def test_closing_bits_matches_window_kernel_and_scipy(gpu, monkeypatch, shape, r):
+    """Bit-packed disk closing (be_closing_disk_bits: word-edge shifts, partial last words, image
+    borders) == the per-pixel window kernel == scipy's binary_closing per slice."""
+    from scipy import ndimage
+
+    rng = np.random.default_rng(r)
+    m = rng.random(shape) > 0.6
+    t = torch.from_numpy(m).to(gpu)
+    monkeypatch.setattr(mito, "MORPH_BITS", True)
+    bits = mito.closing_per_slice(t, r).cpu()
+    monkeypatch.setattr(mito, "MORPH_BITS", False)
+    win = mito.closing_per_slice(t, r).cpu()
+    assert torch.equal(bits, win)
+    yy, xx = np.mgrid[-r:r + 1, -r:r + 1]
+    disk = (yy ** 2 + xx ** 2) <= r ** 2
+    want = np.stack([ndimage.binary_closing(m[z], structure=disk) for z in range(shape[0])])
+    assert np.array_equal(bits.numpy(), want)
+
+
+@pytest.mark.gpu
+def test_edt2d_bounded_search_and_fallback_rows(gpu):
+    """2-D EDT: the per-pixel bounded row search (thin objects) and the envelope fallback rows
+    (a blob wider than the 64-pixel cap, rows with no background at all) match scipy."""
+    from scipy import ndimage
+
+    rng = np.random.default_rng(4)
+    m = rng.random((300, 333)) > 0.3
+    m[20:290, 10:320] = True   # blob: distances up to ~135
+    m[0:5, :] = True           # rows touching the top edge with background only below
+    got = mito.edt(torch.from_numpy(m).to(gpu)).cpu().numpy()
+    want = ndimage.distance_transform_edt(m)
+    assert np.abs(got - want).max() < 1e-3
