@@ -218,11 +218,12 @@ def test_watershed_active_tiles_identical_to_full_sweeps(gpu, dim, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_component_size_filter_gpu_matches_sort(gpu):
-    """be_component_keep (run-length atomics) keeps exactly the components the sort-based
-    ``unique`` count keeps, including one component spanning most of the volume."""
+def test_component_size_filter_gpu_matches_sort(gpu, monkeypatch):
+    """be_component_keep (run-length atomics; BE_COMP_KEEP=1) keeps exactly the components the
+    sort-based ``unique`` count keeps, including one component spanning most of the volume."""
     from bioengine_worker_amd.em.volume import ccl3d
 
+    monkeypatch.setattr(mito, "COMP_KEEP_GPU", True)
     rng = np.random.default_rng(3)
     m = rng.random((20, 70, 90)) > 0.55
     m[2:18, 5:65, 5:85] |= rng.random((16, 60, 80)) > 0.2  # large connected blob
