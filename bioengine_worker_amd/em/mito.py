@@ -112,10 +112,10 @@ def compact_labels(roots: torch.Tensor) -> tuple[torch.Tensor, int]:
 
 def _keep_large(roots: torch.Tensor, min_size: int) -> torch.Tensor:
     """Foreground voxels whose component (CCL root index, -1 = background) has >= ``min_size``
-    voxels.  GPU: run-length atomics (one add per run of equal roots along x) into a per-root
-    counter -- plain per-voxel atomics serialised on large components (millions of adds to one
-    address took 5 s on a 128 x 2048^2 volume), and the sort-based ``unique`` that replaced them
-    took 0.25 s per 256 x 2048^2 slab.  CPU: ``unique`` with counts."""
+    voxels.  GPU: per-chunk LDS hash maps, one global atomic per root and chunk
+    (``be_component_keep``) -- plain per-voxel atomics serialised on large components (millions of
+    adds to one address took 5 s on a 128 x 2048^2 volume), and the sort-based ``unique`` took
+    0.25 s per 256 x 2048^2 slab.  CPU: ``unique`` with counts."""
     flat = roots.reshape(-1)
     if COMP_KEEP_GPU and flat.is_cuda and flat.dtype == torch.int32 and flat.numel() < 2 ** 31:
         # run-length atomics into a per-root counter (be_component_keep), no sort
@@ -214,10 +214,10 @@ def watershed(neg_dist: np.ndarray, markers: np.ndarray, mask: np.ndarray, conn:
     return out
 
 
-#: BE_COMP_KEEP=1: component sizes by run-length atomics (be_component_keep).  Measured slower than
-#: the torch.unique sort on the 256 x 2048^2 slab (remove_small 0.50 vs 0.25 s, s39), so the sort
-#: stays the default.
-COMP_KEEP_GPU = os.environ.get("BE_COMP_KEEP", "0") == "1"
+#: component sizes in per-chunk LDS hash maps (be_component_keep; BE_COMP_KEEP=0: the torch.unique
+#: sort): remove_small 0.19 vs 0.25 s per 256 x 2048^2 slab (s41; the first, run-length version
+#: took 0.50 s, s39)
+COMP_KEEP_GPU = os.environ.get("BE_COMP_KEEP", "1") != "0"
 
 #: closing on bit-packed rows (BE_MORPH_BITS=0: the per-pixel window kernel)
 MORPH_BITS = os.environ.get("BE_MORPH_BITS", "1") != "0"
