@@ -882,15 +882,27 @@ __global__ __launch_bounds__(256) void fill_holes_bits_kernel(const int* __restr
   for (int k = 0; k < NS; ++k)
 #pragma unroll
     for (int w = 0; w < NWD; ++w) mrow[k][w] = 0ull;
-  for (int r = 1; r <= J.ly; ++r) {
+  // rows in batches of 8: the 8 x NWD loads of a batch are in flight together (a tall box loaded
+  // row by row waited for each load before the next)
+  for (int r0 = 1; r0 <= J.ly; r0 += 8) {
+    bool mv[8][NWD];
 #pragma unroll
-    for (int w = 0; w < NWD; ++w) {
-      const int col = 64 * w + lane;
-      const bool m = col >= 1 && col <= J.lx && Mb[(size_t)(J.y0 + r - 1) * W + J.x0 + col - 1] == J.lab;
-      const u64 bal = __ballot(m);
+    for (int q = 0; q < 8; ++q)
 #pragma unroll
-      for (int k = 0; k < NS; ++k)
-        if (k == (r >> 6) && lane == (r & 63)) mrow[k][w] = bal;
+      for (int w = 0; w < NWD; ++w) {
+        const int r = r0 + q, col = 64 * w + lane;
+        mv[q][w] = r <= J.ly && col >= 1 && col <= J.lx && Mb[(size_t)(J.y0 + r - 1) * W + J.x0 + col - 1] == J.lab;
+      }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = r0 + q;
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) {
+        const u64 bal = __ballot(mv[q][w]);
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+          if (k == (r >> 6) && lane == (r & 63)) mrow[k][w] = bal;
+      }
     }
   }
   u64 fr[NS][NWD], o[NS][NWD];
