@@ -186,28 +186,63 @@ class EntryDeployment:
                    additional_requirements: Optional[List[str]] = Field(None, description="Extra pip requirements for the test; installed from the local wheelhouse, test run in an isolated task."),
                    skip_cache: Optional[bool] = Field(False, description="Re-download and re-test."),
                    publish_test_report: Optional[bool] = Field(False, description="Upload the report to the artifact.")) -> Dict:
-        """Run the package's test (test inputs -> outputs) on the GPU runtime; reports are cached
-        per package modification time."""
+        """Run the package's test (test inputs -> outputs) on the GPU runtime.  Reports carry
+        ``tested_at`` and ``env`` rows; the cached report is reused while the package and the
+        BioImage.IO implementation versions are unchanged; publishing uploads ``test_report.json``
+        and the manifest ``test_summary`` (bioengine_worker_amd/bioimageio/report.py)."""
+        import traceback
+
+        from bioengine_worker_amd.bioimageio import report as rep
+
         await self._check_runtime_available()
         lease = await self.model_cache.get_model_package(model_id, stage=stage, skip_cache=skip_cache)
         async with lease:
             cache = lease.source / ".test_cache.json"
+            report = None
             if cache.exists() and not skip_cache:
-                c = json.loads(cache.read_text())
-                if c.get("latest_remote_modified") == lease.latest_remote_modified:
-                    return c["report"]
-            report = await self.runtime_deployment.test.remote(rdf_path=str(lease.rdf_path),
-                                                               additional_requirements=additional_requirements)
-            cache.write_text(json.dumps({"latest_remote_modified": lease.latest_remote_modified,
-                                         "additional_requirements": additional_requirements, "report": report},
-                                        default=str))
+                try:
+                    c = json.loads(cache.read_text())
+                    if rep.cached_report_valid(c, lease.latest_remote_modified):
+                        report = c["test_report"]
+                except (OSError, ValueError) as e:
+                    logger.warning("unreadable cached test report for %s: %s", model_id, e)
+            if report is None:
+                tested_at = time.time()
+                cacheable = True
+                try:
+                    report = await self.runtime_deployment.test.remote(
+                        rdf_path=str(lease.rdf_path), additional_requirements=additional_requirements)
+                except Exception:  # noqa: BLE001 -- a failed run still yields a (failed) report
+                    cacheable = False
+                    try:
+                        import yaml
+
+                        kind = yaml.safe_load(lease.rdf_path.read_text()).get("type")
+                    except Exception:  # noqa: BLE001
+                        kind = None
+                    report = rep.fallback_report(model_id, str(lease.rdf_path), kind, traceback.format_exc())
+                report = rep.finalize_report(report, tested_at)
+                if cacheable:
+                    cache.write_text(json.dumps({"latest_remote_modified": lease.latest_remote_modified,
+                                                 "additional_requirements": additional_requirements,
+                                                 "test_report": report}, default=str))
         if publish_test_report and self.artifact_manager is not None:
-            aid = f"bioimage-io/{model_id}"
+            import httpx
+
+            async def http_get(url):
+                async with httpx.AsyncClient(timeout=30) as c:
+                    r = await c.get(url)
+                    r.raise_for_status()
+                    return r.text
+
+            async def http_put(url, body):
+                async with httpx.AsyncClient(timeout=30) as c:
+                    (await c.put(url, content=body)).raise_for_status()
+
             try:
-                await self.artifact_manager.edit(aid, stage=True, manifest={"test_summary": {"status": report["status"]}})
-                await self.artifact_manager.commit(aid)
+                await rep.publish_report(self.artifact_manager, f"bioimage-io/{model_id}", report, http_get, http_put)
             except Exception as e:  # noqa: BLE001
-                report["publish_error"] = str(e)
+                report = dict(report, publish_error=str(e))
         return report
 
     @schema_method

@@ -13,6 +13,7 @@ from pathlib import Path
 import numpy as np
 import torch
 
+from .report import env_rows
 from .runner import PredictionPipeline
 from .spec import format_summary, load_rdf, tensors, validate_format
 
@@ -72,5 +73,5 @@ def test_model(source, device=None, weights_format: str | None = None) -> dict:
     return {"name": "bioimageio format validation and model test", "status": status, "type": rdf.get("type"),
             "id": rdf.get("id"), "format_version": rdf.get("format_version"), "details": details,
             "summary": format_summary(v), "duration_s": round(time.time() - t0, 3),
-            "env": {"bioengine_worker_amd": "0.1.0", "torch": torch.__version__, "python": platform.python_version(),
-                    "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"}}
+            "env": env_rows({"torch": torch.__version__, "python": platform.python_version(),
+                             "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"})}

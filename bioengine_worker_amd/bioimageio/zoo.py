@@ -189,7 +189,24 @@ class ModelCache:
             return False  # just created; its owner record follows the mkdir
         if not _owner_stale(info, DOWNLOAD_TIMEOUT_S, mt):
             return False
-        shutil.rmtree(marker, ignore_errors=True)
+        # Atomic reclaim: rename the stale marker to a tombstone unique to this waiter.  Of several
+        # waiters that judged the same marker stale, only one rename succeeds; the others see it gone
+        # (and then race on the mkdir, which is atomic).  A rmtree of the marker path itself could
+        # delete a FRESH marker another waiter had just reclaimed and re-created.
+        tomb = marker.with_name(f"{marker.name}.stale.{os.getpid()}.{uuid.uuid4().hex[:8]}")
+        try:
+            os.rename(marker, tomb)
+        except OSError:
+            return True  # someone else reclaimed (or the owner finished): retry the mkdir
+        # the renamed directory must still be the one judged stale: a marker re-created between the
+        # check and the rename carries a different owner record -- put it back untouched
+        if _read_owner(tomb / "owner.json") != info:
+            try:
+                os.rename(tomb, marker)
+                return False
+            except OSError:
+                pass  # a third marker exists now; the tombstone is ours to drop
+        shutil.rmtree(tomb, ignore_errors=True)
         return True
 
     async def get_model_package(self, model_id: str, stage: bool = False, skip_cache: bool = False,

@@ -281,29 +281,52 @@ class CPSAMEngine:
         o = o.view(B, g, g, self.nout, ps, ps).permute(0, 3, 1, 4, 2, 5).reshape(B, self.nout, g * ps, g * ps)
         return o
 
+    #: tile-count buckets of :meth:`graphed`: a batch is zero-padded up to the next one, so a server
+    #: seeing images of many sizes keeps at most len(GRAPH_BUCKETS) graphs (each holds a private
+    #: memory pool with the whole forward's intermediates) instead of one per exact tile count
+    GRAPH_BUCKETS = (1, 2, 4, 8, 16, 32, 64)
+    #: capture attempts per bucket before that bucket stays eager for the process
+    GRAPH_MAX_TRIES = 3
+    #: BE_CPSAM_GRAPH=0 turns graph replay off (every call runs the eager forward)
+    GRAPH = os.environ.get("BE_CPSAM_GRAPH", "1") != "0"
+
     @torch.no_grad()
     def graphed(self, x: torch.Tensor) -> torch.Tensor:
-        """:meth:`__call__` replayed from a HIP graph captured once per tile count (static input
-        buffer; the output is a fresh copy).  Falls back to the eager forward off-GPU."""
-        if not (x.is_cuda and self.device.type == "cuda"):
-            return self(x)
+        """:meth:`__call__` replayed from a HIP graph per tile-count bucket (static input buffer,
+        zero-padded to the bucket; the output is a fresh copy).  Falls back to the eager forward
+        off-GPU, above the largest bucket, with BE_CPSAM_GRAPH=0, and when a capture fails (counted
+        per bucket: after GRAPH_MAX_TRIES failures the bucket stays eager)."""
         B = x.shape[0]
+        if not (x.is_cuda and self.device.type == "cuda") or not self.GRAPH or B > self.GRAPH_BUCKETS[-1]:
+            return self(x)
+        bucket = next(b for b in self.GRAPH_BUCKETS if b >= B)
         graphs = self.__dict__.setdefault("_graphs", {})
-        ent = graphs.get(B)
+        key = (bucket, tuple(x.shape[1:]))
+        ent = graphs.get(key)
+        if isinstance(ent, int):  # earlier capture attempts failed
+            if ent >= self.GRAPH_MAX_TRIES:
+                return self(x)
+            ent = None
         if ent is None:
-            xs = torch.empty((B,) + tuple(x.shape[1:]), device=self.device, dtype=torch.bfloat16)
-            xs.copy_(x)
+            xs = torch.zeros((bucket,) + tuple(x.shape[1:]), device=self.device, dtype=torch.bfloat16)
+            xs[:B].copy_(x)
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side):
                 self(xs)  # lazy state (kernel attributes, workspaces) outside the capture
             torch.cuda.current_stream(self.device).wait_stream(side)
             gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr, capture_error_mode="thread_local"):
-                out = self(xs)
-            ent = graphs[B] = (gr, xs, out)
+            try:
+                with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+                    out = self(xs)
+            except Exception:  # noqa: BLE001 -- counted; the request itself runs eagerly
+                graphs[key] = int(graphs.get(key) or 0) + 1
+                return self(x)
+            ent = graphs[key] = (gr, xs, out)
         gr, xs, out = ent
-        xs.copy_(x)
+        xs[:B].copy_(x)
+        if B < bucket:
+            xs[B:].zero_()
         gr.replay()
-        return out.clone()
+        return out[:B].clone()
 

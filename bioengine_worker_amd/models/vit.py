@@ -187,11 +187,15 @@ class ViTEngine:
                 fc2_b=bf(blk.mlp.fc2.bias), g2=ls(blk.ls2)))
         self.nw, self.nb = f32(net.norm.weight), f32(net.norm.bias)
         if precision == "fp8":
-            # e4m3 weights with per-output-channel scales; the bf16 copies are dropped.  qkv reads the
-            # LayerNorm's per-token e4m3 and has no fused epilogue, so it runs wherever its plain GEMM is
-            # fastest (BE_VIT_QKV_GEMM; hipBLASLt by default: 43.0 vs 60.9 us at batch 64,
-            # profiles/r03/fp8/fp8_bench_s23.jsonl); proj / fc1 / fc2 keep the HIP kernel for the
-            # MX-fp8 hand-offs its epilogues fuse
+            # e4m3 weights with per-output-channel scales; the bf16 copies are dropped.  Every
+            # projection, qkv included, runs on the HIP block-scaled MX-fp8 GEMM by default: qkv reads
+            # the MX-fp8 (E8M0 scale per 32 channels) that the fused add+LayerNorm+quantise kernel
+            # writes.  Round 5 measured 16,300 img/s against 16,449 for hipBLASLt _scaled_mm on
+            # per-token e4m3 (within 1 %), cosine 0.993 vs bf16 (profiles/r05/vit/vit_qkv_mx_ab_s23.jsonl).
+            # BE_VIT_QKV_GEMM=lib selects the hipBLASLt arm.  Embeddings from the two arms differ at
+            # the quantisation level, so a search index ingested before round 5 (qkv on hipBLASLt)
+            # carries slightly different vectors than one ingested now; re-ingest, or pin the arm
+            # the index was built with.
             qkv_gemm = os.environ.get("BE_VIT_QKV_GEMM", fp8_gemm)
             for b in self.blocks:
                 for name in ("qkv", "proj", "fc1", "fc2"):

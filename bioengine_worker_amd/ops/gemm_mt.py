@@ -98,9 +98,17 @@ _ws: dict = {}
 _cnt: dict = {}
 
 
+def _stream_key(dev: torch.device) -> tuple:
+    """Split-K scratch is private to a (device, stream) pair: two split-K launches in flight on two
+    streams (the CPSAM step's side-stream weight gradients beside a main-stream one) would otherwise
+    overwrite each other's slabs and bump the same tile counters.  Work on ONE stream is ordered, so
+    it can share."""
+    return (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+
+
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
     """fp32 split-K slab workspace, grown but never freed: a captured HIP graph keeps its address."""
-    key = dev.index
+    key = _stream_key(dev)
     cur = _ws.get(key)
     if cur is None or cur[-1].numel() * 4 < nbytes:
         t = torch.empty((nbytes + 3) // 4, device=dev, dtype=torch.float32)
@@ -110,10 +118,11 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
 
 
 def _counters(dev: torch.device) -> torch.Tensor:
-    c = _cnt.get(dev.index)
+    key = _stream_key(dev)
+    c = _cnt.get(key)
     if c is None:
         # per-tile arrival counters; the last arriving slice resets its tile's counter to 0
-        c = _cnt[dev.index] = torch.zeros(65536, device=dev, dtype=torch.int32)
+        c = _cnt[key] = torch.zeros(65536, device=dev, dtype=torch.int32)
     return c
 
 

@@ -998,12 +998,12 @@ template <int T, int DV>
 static void launch_diffuse_nt(const int* M, const void* jobs, int njobs, int H, int W, const int* niter_img, double* Lout,
                               int lds_bytes, int variant, hipStream_t s) {
   if (lds_bytes > 64 * 1024) {  // > 64 KiB of dynamic LDS (up to the 160 KiB of a CU) needs the opt-in
-    static int attr = 0;
-    if (attr < lds_bytes) {
+    static int attr[BE_MAX_DEV] = {};
+    if (attr[be_cur_dev()] < lds_bytes) {
       const hipError_t ae = hipFuncSetAttribute(reinterpret_cast<const void*>(diffuse_kernel<true, T, DV>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
       if (ae != hipSuccess) fprintf(stderr, "be_cp_diffuse_nt: hipFuncSetAttribute(%d): %s\n", lds_bytes, hipGetErrorString(ae));
-      attr = lds_bytes;
+      attr[be_cur_dev()] = lds_bytes;
     }
   }
   hipLaunchKernelGGL((diffuse_kernel<true, T, DV>), dim3(njobs), dim3(T), lds_bytes, s, M, (const MaskJob*)jobs, H, W,

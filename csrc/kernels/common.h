@@ -64,3 +64,25 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }
 
 #define BE_CHECK_LAUNCH() ((int)hipGetLastError())
+
+// ---- per-device host state ---------------------------------------------------------------------
+// A process may drive several GPUs (the 3-D EM slab path, multi-GPU replicas in one process): the
+// one-time kernel attributes (hipFuncSetAttribute is per device) and the zero pages the implicit-GEMM
+// loaders read for conv padding must be kept per device, never once per process.
+#define BE_MAX_DEV 64
+inline int be_cur_dev() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return (d < 0 || d >= BE_MAX_DEV) ? 0 : d;
+}
+
+// Zero-filled device buffer of `bytes` on the current device, allocated once per (device, slot).
+inline const bf16_t* be_zero_page(int slot, size_t bytes) {
+  static bf16_t* pages[4][BE_MAX_DEV] = {};
+  bf16_t*& z = pages[slot & 3][be_cur_dev()];
+  if (!z) {
+    if (hipMalloc((void**)&z, bytes) != hipSuccess) { z = nullptr; return nullptr; }
+    if (hipMemset(z, 0, bytes) != hipSuccess) return nullptr;
+  }
+  return z;
+}

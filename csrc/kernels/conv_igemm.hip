@@ -308,24 +308,17 @@ int launch_ig(IgArgs a, hipStream_t s) {
   if (lds > 160 * 1024) return -22;
   const long long nblk = (long long)a.tiles * a.cob;
   if (nblk >= (1LL << 31)) return -23;
-  static bool attr_set = false;
-  if (!attr_set) {
+  static bool attr_set[BE_MAX_DEV] = {};
+  if (!attr_set[be_cur_dev()]) {
     (void)hipFuncSetAttribute((const void*)conv3_igemm_kernel<WM, WN, HIMAX, NSTAGE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
+    attr_set[be_cur_dev()] = true;
   }
   hipLaunchKernelGGL((conv3_igemm_kernel<WM, WN, HIMAX, NSTAGE>), dim3((unsigned)nblk), dim3(C::NT), lds, s, a);
   return BE_CHECK_LAUNCH();
 }
 
-static const bf16_t* zero_page() {
-  static bf16_t* z = nullptr;
-  if (!z) {
-    if (hipMalloc((void**)&z, 1 << 20) != hipSuccess) return nullptr;
-    if (hipMemset(z, 0, 1 << 20) != hipSuccess) return nullptr;
-  }
-  return z;
-}
+static const bf16_t* zero_page() { return be_zero_page(0, 1 << 20); }
 
 }  // namespace
 

@@ -943,12 +943,12 @@ int launch_pair_l(PairArgs a, int g, hipStream_t s) {
   constexpr bool seps = (VAR & 16) != 0 && C::RESW && !HEAD;
   constexpr size_t lds = C::LDS + (seps ? (size_t)C::R_OUT * sizeof(bf16_t) : 0);
   static_assert(lds <= 160 * 1024, "LDS budget (separate output staging)");
-  static bool attr_set = false;
-  if (!attr_set) {
+  static bool attr_set[BE_MAX_DEV] = {};
+  if (!attr_set[be_cur_dev()]) {
     hipFuncSetAttribute(
         reinterpret_cast<const void*>(&conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, VAR>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
+    attr_set[be_cur_dev()] = true;
   }
   hipLaunchKernelGGL((conv_pair_kernel<CK, CM, INMODE, X2, PROJ, RES, NCA, HEAD, STAMP, VAR>), dim3(g), dim3(NT), lds, s,
                      a);
@@ -1772,20 +1772,20 @@ int launch_pair_pp(PairArgs a, int grid_cap, hipStream_t s) {
   if (g > tiles) g = tiles;
   if (g < 1) return 0;
   a.stamps = nullptr;
-  static bool attr_set = false;
-  if (!attr_set) {
+  static bool attr_set[BE_MAX_DEV] = {};
+  if (!attr_set[be_cur_dev()]) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, STEM>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr_set = true;
+    attr_set[be_cur_dev()] = true;
   }
   if (g_pp_stamps != nullptr) {
     if (g > g_pp_stamps_cap) return -30;
     a.stamps = g_pp_stamps;
-    static bool attr_st = false;
-    if (!attr_st) {
+    static bool attr_st[BE_MAX_DEV] = {};
+    if (!attr_st[be_cur_dev()]) {
       hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, STEM, true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_st = true;
+      attr_st[be_cur_dev()] = true;
     }
     hipLaunchKernelGGL((conv_pair_pp_kernel<NCA, INMODE, X2, RES, HEAD, STEM, true>), dim3(g), dim3(ppk::NTP), lds, s, a);
     return BE_CHECK_LAUNCH();

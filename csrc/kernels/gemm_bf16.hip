@@ -270,12 +270,12 @@ template <int TA, int TB, int WM, int WN, int FM, int FN, int EPI>
 int launch_gemm(GArgs a, hipStream_t s) {
   constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   constexpr size_t LDS = 3 * (size_t)(BM + BN) * BK * 2;
-  static bool attr = false;
-  if (!attr) {
+  static bool attr[BE_MAX_DEV] = {};
+  if (!attr[be_cur_dev()]) {
     if (hipFuncSetAttribute((const void*)gemm_bf16_kernel<TA, TB, WM, WN, FM, FN, EPI>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS) != hipSuccess)
       return -30;
-    attr = true;
+    attr[be_cur_dev()] = true;
   }
   if ((TA == 1 && a.M % BM) || (TB == 1 && a.N % BN)) return -31;  // transposed tiles are read whole
   a.tiles_n = (a.N + BN - 1) / BN;

@@ -441,12 +441,12 @@ int launch_mt(MArgs a, hipStream_t s) {
   constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   constexpr int LDS = NST * (BM + BN) * 128;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
+  static bool attr[BE_MAX_DEV] = {};
+  if (!attr[be_cur_dev()]) {
     if (hipFuncSetAttribute((const void*)gemm_mt_kernel<WM, WN, FM, FN, NST, EPI, TA, TB>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return -30;
-    attr = true;
+    attr[be_cur_dev()] = true;
   }
   // M/N-contiguous images: [64][BM | BN] k-row tiles of whole 16-byte chunks, power-of-two widths
   static_assert((TA == 0 || (BM & (BM - 1)) == 0) && (TB == 0 || (BN & (BN - 1)) == 0), "swizzled k-row tiles");
@@ -492,14 +492,7 @@ int launch_conv(MArgs a, int cfg, hipStream_t s) {
   return -32;
 }
 
-const bf16_t* conv_zero_page() {
-  static bf16_t* z = nullptr;
-  if (!z) {
-    if (hipMalloc((void**)&z, 4096) != hipSuccess) return nullptr;
-    if (hipMemset(z, 0, 4096) != hipSuccess) return nullptr;
-  }
-  return z;
-}
+const bf16_t* conv_zero_page() { return be_zero_page(1, 4096); }
 
 }  // namespace
 

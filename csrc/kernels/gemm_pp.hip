@@ -368,12 +368,12 @@ int launch_pp(PArgs a, hipStream_t s) {
   constexpr int BM = 16 * FM * WM, BN = 16 * FN * WN;
   constexpr int LDS = NSLOT * (BM + BN) * 64;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
+  static bool attr[BE_MAX_DEV] = {};
+  if (!attr[be_cur_dev()]) {
     if (hipFuncSetAttribute((const void*)gemm_pp_kernel<WM, WN, FM, FN, EPI, TA, TB>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS) != hipSuccess)
       return -30;
-    attr = true;
+    attr[be_cur_dev()] = true;
   }
   if ((TB == 1 && a.N % BN) || (TA == 1 && a.M % BM)) return -33;  // k-row tiles are read whole
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -406,14 +406,7 @@ __global__ __launch_bounds__(256) void pp_slab_sum_kernel(const float* __restric
   }
 }
 
-const bf16_t* zero_page() {
-  static bf16_t* z = nullptr;
-  if (!z) {
-    if (hipMalloc((void**)&z, 4096) != hipSuccess) return nullptr;
-    if (hipMemset(z, 0, 4096) != hipSuccess) return nullptr;
-  }
-  return z;
-}
+const bf16_t* zero_page() { return be_zero_page(2, 4096); }
 
 }  // namespace
 
