@@ -32,21 +32,46 @@ import torch
 import torch.distributed as dist
 
 
-class FlatParams:
-    """Re-home a module's trainable parameters into flat fp32 param / grad buffers."""
+def bucket_bounds(sizes: list[int], cap: int, multiple: int = 4) -> tuple[list[int], list[tuple[int, int, list[int]]]]:
+    """Parameter offsets and gradient buckets (start, end, member indices) for parameters of the
+    given element counts in gradient-arrival order.  Every parameter segment is padded to 4 elements
+    (16 B, so vector kernels never straddle parameters); a bucket closes at the first parameter
+    boundary past ``cap`` elements and its end is padded up to ``multiple`` elements (the sharded
+    optimizer needs every bucket to split into world equal, 4-aligned chunks)."""
+    offsets, buckets = [], []
+    off, start, members = 0, 0, []
+    for i, n in enumerate(sizes):
+        offsets.append(off)
+        off += (n + 3) // 4 * 4
+        members.append(i)
+        if off - start >= cap:
+            off = (off + multiple - 1) // multiple * multiple
+            buckets.append((start, off, members))
+            start, members = off, []
+    if members:
+        off = (off + multiple - 1) // multiple * multiple
+        buckets.append((start, off, members))
+    return offsets, buckets
 
-    def __init__(self, module: torch.nn.Module, device: torch.device | str | None = None):
+
+class FlatParams:
+    """Re-home a module's trainable parameters into flat fp32 param / grad buffers.
+
+    ``bucket_mb`` / ``bucket_multiple``: lay the buffers out for gradient buckets of that size whose
+    ends are padded to a multiple of ``bucket_multiple`` elements (:class:`ShardedAdamW` passes
+    4 x world); the layout is then recorded in :attr:`buckets` and every reducer uses it."""
+
+    def __init__(self, module: torch.nn.Module, device: torch.device | str | None = None,
+                 bucket_mb: float | None = None, bucket_multiple: int = 4):
         params = [p for p in module.parameters() if p.requires_grad]
         params = list(reversed(params))  # gradient-arrival order
         self.params = params
         device = torch.device(device) if device is not None else params[0].device
         n = sum(p.numel() for p in params)
-        # pad every segment to 4 elements (16 B) so vector kernels never straddle params
-        self.offsets = []
-        off = 0
-        for p in params:
-            self.offsets.append(off)
-            off += (p.numel() + 3) // 4 * 4
+        cap = max(1, int(bucket_mb * 1024 * 1024 / 4)) if bucket_mb is not None else 1 << 62
+        self.offsets, bks = bucket_bounds([p.numel() for p in params], cap, bucket_multiple)
+        self.buckets = bks if bucket_mb is not None else None
+        off = bks[-1][1] if bks else 0
         self.numel = off
         self.flat = torch.zeros(off, dtype=torch.float32, device=device)
         self.grad = torch.zeros(off, dtype=torch.float32, device=device)
@@ -74,17 +99,15 @@ class BucketedAllReduce:
         self.active = self.world > 1 or (force and dist.is_initialized())
         self.comm_dtype = comm_dtype
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
-        # bucket boundaries on parameter boundaries, in gradient-arrival order
-        self.buckets: list[tuple[int, int, list[int]]] = []
-        start, members = 0, []
-        for i, (p, o) in enumerate(zip(fp.params, fp.offsets)):
-            end = o + (p.numel() + 3) // 4 * 4
-            members.append(i)
-            if end - start >= cap:
-                self.buckets.append((start, end, members))
-                start, members = end, []
-        if members:
-            self.buckets.append((start, fp.numel, members))
+        # bucket boundaries on parameter boundaries, in gradient-arrival order (the layout the
+        # FlatParams was built for, if it was built for one)
+        if getattr(fp, "buckets", None) is not None:
+            self.buckets = [(s, e, list(m)) for (s, e, m) in fp.buckets]
+        else:
+            _, self.buckets = bucket_bounds([p.numel() for p in fp.params], cap)
+            if self.buckets:
+                s, _, m = self.buckets[-1]
+                self.buckets[-1] = (s, fp.numel, m)
         self.param_bucket = {}
         for bi, (_, _, mem) in enumerate(self.buckets):
             for i in mem:
