@@ -489,16 +489,18 @@ def bench_model_runner_cpu(reps: int = 10) -> dict:
                                             "threads": torch.get_num_threads()}}
 
 
-def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int, force_dp: bool = False):
+def bench_train_cpsam(args, world, rank, dev, batch: int, steps: int, force_dp: bool = False, zero: bool = False):
     """Cellpose-SAM (ViT-L/8, 256x256 crops) fine-tune steps -- the reference app's own training
     workload -- on the HIP CPSAM engine; with world > 1 data-parallel over RCCL (bucketed fp32
     gradients, all-reduces overlapped with the segmented-graph backward).  ``force_dp`` runs that
-    data-parallel path on one GPU over a 1-rank group (its overhead vs the single-GPU graph)."""
+    data-parallel path on one GPU over a 1-rank group (its overhead vs the single-GPU graph).
+    ``zero``: the ZeRO-1 optimizer (bucketed reduce-scatter, AdamW on the rank's chunk, all-gather;
+    parallel/ddp.py ShardedAdamW) instead of all-reduce + full AdamW."""
     from bioengine_worker_amd.models.cpsam import CPSAM
     from bioengine_worker_amd.train.cellpose_train import TrainConfig, build_trainer, synthetic_train_batch
 
     cfg = TrainConfig(batch_size=batch, bsize=256, lr=1e-5, weight_decay=1e-4, bucket_mb=64.0, comm_bf16=False,
-                      force_dp_path=force_dp)
+                      force_dp_path=force_dp, zero_adamw=zero)
     trainer = build_trainer(cfg, device=dev, world_size=world, rank=rank, net=CPSAM().randomize_(0))
     data = synthetic_train_batch(batch, 256, device=dev, seed=rank)
     for _ in range(3):
@@ -747,6 +749,10 @@ def main():
                                             "engine": "HIP fwd/bwd engine, HIP-graph step" if world == 1 else
                                             "HIP fwd/bwd engine, segmented HIP-graph step, RCCL bucketed fp32 all-reduce overlapped",
                                             "parallelism": f"dp{world}"}
+            if world > 1:  # the ZeRO-1 optimizer on the same DP step
+                spz, msz = bench_train_cpsam(args, world, rank, dev, args.cpsam_batch, args.train_steps, zero=True)
+                out["finetune_cpsam_zero_samples_per_sec"] = round(spz, 2)
+                out["finetune_cpsam_zero_ms"] = round(msz, 3)
             if world == 1:
                 sps1, ms1 = bench_train_cpsam(args, world, rank, dev, 1, args.train_steps)
                 out["finetune_cpsam_batch1_samples_per_sec"] = round(sps1, 2)  # the reference's batch size
@@ -762,6 +768,8 @@ def main():
                 try:
                     _, msd = bench_train_cpsam(args, world, rank, dev, 1, args.train_steps, force_dp=True)
                     out["finetune_cpsam_dp_path_ms_b1"] = round(msd, 3)
+                    _, msz = bench_train_cpsam(args, world, rank, dev, 1, args.train_steps, force_dp=True, zero=True)
+                    out["finetune_cpsam_zero_dp_path_ms_b1"] = round(msz, 3)
                 finally:
                     dist.destroy_process_group()
         except Exception as e:  # noqa: BLE001

@@ -234,3 +234,135 @@ def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
         else:
             dist.init_process_group(backend)
     return world, rank, local
+
+
+class ShardedAdamW:
+    """ZeRO-1 data-parallel AdamW over a :class:`FlatParams` laid out for padded buckets.
+
+    Per gradient bucket (same buckets, hooks and readiness interface as :class:`BucketedAllReduce`,
+    so the segmented-graph step drives either): a ``reduce_scatter`` leaves rank r the summed
+    gradient of chunk r of the bucket only; AdamW updates that chunk (1/world of the parameters, so
+    the optimizer's HBM stream is cut by the world size); an ``all_gather`` then re-assembles the
+    updated fp32 parameters of the bucket on every rank (and the bf16 compute mirror, when given, is
+    refreshed from them).  Bytes on the wire equal one all-reduce (reduce-scatter + all-gather are
+    its two halves); with ``comm_dtype=bfloat16`` the gradient half moves bf16.
+
+    The moments live in full-size buffers, but a rank only updates its own chunks: call
+    :meth:`sync_moments` before reading them (checkpoints).  Works on gloo (CPU tests) and RCCL.
+    """
+
+    def __init__(self, fp: FlatParams, m: torch.Tensor, v: torch.Tensor, group=None, comm_dtype=None,
+                 force: bool = False):
+        self.fp, self.m, self.v = fp, m, v
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.active = self.world > 1 or (force and dist.is_initialized())
+        self.comm_dtype = comm_dtype
+        if fp.buckets is None:
+            raise ValueError("ShardedAdamW needs FlatParams(..., bucket_mb=..., bucket_multiple=4 * world)")
+        self.buckets = [(s, e, list(mem)) for (s, e, mem) in fp.buckets]
+        for s, e, _ in self.buckets:
+            if (e - s) % (4 * self.world):
+                raise ValueError(f"bucket [{s}, {e}) does not split into {self.world} 4-aligned chunks")
+        self.param_bucket = {i: bi for bi, (_, _, mem) in enumerate(self.buckets) for i in mem}
+        self._index = {id(p): i for i, p in enumerate(fp.params)}
+        self._inplace = dist.is_initialized() and dist.get_backend(group) == "nccl"
+        self._hooks = []
+        if self.active:
+            for i, p in enumerate(fp.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.reset()
+
+    # -- the BucketedAllReduce readiness interface
+    def chunk(self, bi: int) -> tuple[int, int]:
+        s, e, _ = self.buckets[bi]
+        L = (e - s) // self.world
+        return s + self.rank * L, s + (self.rank + 1) * L
+
+    def bucket_of(self, p) -> int:
+        return self.param_bucket[self._index[id(p)]]
+
+    def reset(self):
+        self.pending = [len(m) for (_, _, m) in self.buckets]
+        self._order = []
+
+    def launch_bucket(self, bi: int) -> None:
+        if self.active and self.pending[bi] > 0:
+            self.pending[bi] = 0
+            self._launch(bi)
+
+    def mark_ready(self, params) -> None:
+        if not self.active:
+            return
+        for p in params:
+            bi = self.param_bucket[self._index[id(p)]]
+            self.pending[bi] -= 1
+            if self.pending[bi] == 0:
+                self._launch(bi)
+
+    def _make_hook(self, i: int):
+        def hook(_p):
+            bi = self.param_bucket[i]
+            self.pending[bi] -= 1
+            if self.pending[bi] == 0:
+                self._launch(bi)
+        return hook
+
+    def _launch(self, bi: int):
+        s, e, _ = self.buckets[bi]
+        cs, ce = self.chunk(bi)
+        full, own = self.fp.grad[s:e], self.fp.grad[cs:ce]
+        if self.comm_dtype is not None and self.comm_dtype != torch.float32:
+            src = full.to(self.comm_dtype)
+            out = torch.empty(ce - cs, dtype=self.comm_dtype, device=full.device)
+        else:
+            src = full if self._inplace else full.clone()
+            out = own
+        w = dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._order.append((bi, w, out, src))
+
+    def step(self, lr: float, step: int, weight_decay: float = 0.0, mirror: torch.Tensor | None = None,
+             betas=(0.9, 0.999), eps: float = 1e-8) -> None:
+        """Finish the gradient reduce-scatters (launching buckets that never filled), update the own
+        chunk of every bucket as soon as ITS collective is done, and gather the parameters back."""
+        from ..ops import train_ops
+
+        for bi, n in enumerate(self.pending):
+            if n > 0:
+                self.pending[bi] = 0
+                self._launch(bi)
+        scale = 1.0 / self.world
+        gathers = []
+        for bi, w, out, _src in self._order:
+            w.wait()
+            s, e, _ = self.buckets[bi]
+            cs, ce = self.chunk(bi)
+            if out.data_ptr() != self.fp.grad[cs:ce].data_ptr():
+                self.fp.grad[cs:ce].copy_(out.float())
+            train_ops.adamw_flat_(self.fp.flat[cs:ce], self.fp.grad[cs:ce], self.m[cs:ce], self.v[cs:ce], lr=lr,
+                                  step=step, betas=betas, eps=eps, weight_decay=weight_decay, grad_scale=scale)
+            own = self.fp.flat[cs:ce]
+            g = dist.all_gather_into_tensor(self.fp.flat[s:e], own if self._inplace else own.clone(),
+                                            group=self.group, async_op=True)
+            gathers.append((g, s, e))
+        for g, s, e in gathers:
+            g.wait()
+            if mirror is not None and mirror.data_ptr() != self.fp.flat.data_ptr():
+                mirror[s:e].copy_(self.fp.flat[s:e])
+        self.reset()
+
+    def sync_moments(self) -> None:
+        """All-gather every bucket's moment chunks, so m / v are whole on every rank (checkpoint)."""
+        if not self.active:
+            return
+        for bi, (s, e, _) in enumerate(self.buckets):
+            cs, ce = self.chunk(bi)
+            for t in (self.m, self.v):
+                own = t[cs:ce]
+                dist.all_gather_into_tensor(t[s:e], own if self._inplace else own.clone(), group=self.group)
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -27,7 +27,7 @@ import torch.distributed as dist
 
 from ..models.cpnet import CPnet
 from ..ops import train_ops
-from ..parallel.ddp import BucketedAllReduce, FlatParams, broadcast_params
+from ..parallel.ddp import BucketedAllReduce, FlatParams, ShardedAdamW, broadcast_params
 
 
 @dataclass
@@ -76,6 +76,10 @@ class TrainConfig:
     # complete; each bucket's all-reduce is issued right after its segment replays, so RCCL traffic
     # overlaps the remaining backward while the step stays launch-free
     cpsam_dp_graph: bool = True
+    # data-parallel optimizer: False = bucketed all-reduce + AdamW over all parameters on every rank;
+    # True = ZeRO-1 (parallel/ddp.py ShardedAdamW): bucketed reduce-scatter, AdamW on the rank's
+    # 1/world chunk of every bucket, all-gather of the updated parameters
+    zero_adamw: bool = False
 
 
 def lr_schedule(learning_rate: float, n_epochs: int) -> np.ndarray:
@@ -105,13 +109,19 @@ class CellposeTrainer:
         self.net = net.to(self.device).train()
         if self.device.type == "cuda" and not self.is_cpsam:
             self.net = self.net.to(memory_format=torch.channels_last)
-        self.fp = FlatParams(self.net, self.device)
+        zero = cfg.zero_adamw and (world_size > 1 or cfg.force_dp_path)
+        self.fp = FlatParams(self.net, self.device, bucket_mb=cfg.bucket_mb if zero else None,
+                             bucket_multiple=4 * world_size)
         if world_size > 1:
             broadcast_params(self.fp, 0, group)
-        self.ar = BucketedAllReduce(self.fp, group=group, bucket_mb=cfg.bucket_mb,
-                                    comm_dtype=torch.bfloat16 if cfg.comm_bf16 else None, force=cfg.force_dp_path)
         self.m = torch.zeros_like(self.fp.flat)
         self.v = torch.zeros_like(self.fp.flat)
+        comm = torch.bfloat16 if cfg.comm_bf16 else None
+        if zero:
+            self.ar = ShardedAdamW(self.fp, self.m, self.v, group=group, comm_dtype=comm, force=cfg.force_dp_path)
+        else:
+            self.ar = BucketedAllReduce(self.fp, group=group, bucket_mb=cfg.bucket_mb, comm_dtype=comm,
+                                        force=cfg.force_dp_path)
         self.step_count = 0
         self.epoch = 0  # completed epochs (exact resume point)
         self.lr = cfg.lr
@@ -171,6 +181,8 @@ class CellposeTrainer:
             loss = self.forward_loss(x, lbl)
         with trace.span("train.backward", cuda=True):
             loss.backward()
+        if self._sharded_update():
+            return loss.detach()
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
@@ -195,6 +207,8 @@ class CellposeTrainer:
                 loss = self._graph_step(eng, x, lbl)  # ar.finish() then all-reduces every bucket
             else:
                 loss = eng.loss_and_backward(x, lbl, on_params_ready=self.ar.mark_ready if self.ar.active else None)
+        if self._sharded_update():
+            return loss
         with trace.span("train.grad_allreduce_finish", cuda=True):
             gscale = self.ar.finish()
         self.step_count += 1
@@ -235,6 +249,8 @@ class CellposeTrainer:
             else:
                 loss = eng.loss_and_backward(x, lbl, keep,
                                              on_params_ready=self.ar.mark_ready if self.ar.active else None)
+        if self._sharded_update(eng.mirror if eng.mirror is not self.fp.flat else None):
+            return loss
         if self.ar.active and not fused_opt and self.cfg.cpsam_bucket_adamw:
             # per-bucket AdamW, each on its own bucket's all-reduce completion: the update of the
             # buckets the backward finished first overlaps the last buckets' collectives
@@ -253,6 +269,17 @@ class CellposeTrainer:
             train_ops.adamw_flat_(self.fp.flat, self.fp.grad, self.m, self.v, lr=self.lr, step=self.step_count,
                                   weight_decay=self.cfg.weight_decay, grad_scale=gscale, p_bf16=mirror)
         return loss
+
+    def _sharded_update(self, mirror=None) -> bool:
+        """ZeRO-1 optimizer step (ShardedAdamW): True when it ran (the caller's AdamW is skipped)."""
+        if not (isinstance(self.ar, ShardedAdamW) and self.ar.active):
+            return False
+        from ..profiling import trace
+
+        self.step_count += 1
+        with trace.span("train.reduce_scatter_adamw_allgather", cuda=True):
+            self.ar.step(lr=self.lr, step=self.step_count, weight_decay=self.cfg.weight_decay, mirror=mirror)
+        return True
 
     def _adamw_range(self, s: int, e: int, grad_scale: float, mirror) -> None:
         """AdamW over flat elements [s, e) (bucket boundaries are 4-element aligned)."""
@@ -484,6 +511,8 @@ class CellposeTrainer:
         self.ar.remove()
         self.world, self.rank = int(world_size), int(rank)
         self.fp.zero_grad()
+        # a shrunk world keeps the plain all-reduce path: the padded ZeRO bucket layout was cut for
+        # the old world size (moment chunks a lost rank owned since the last checkpoint are stale)
         self.ar = BucketedAllReduce(self.fp, group=group, bucket_mb=self.cfg.bucket_mb,
                                     comm_dtype=torch.bfloat16 if self.cfg.comm_bf16 else None)
         self._graph = self._graph_io = None
@@ -501,6 +530,8 @@ class CellposeTrainer:
 
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:
+        if isinstance(self.ar, ShardedAdamW):
+            self.ar.sync_moments()  # each rank updated only its own chunks
         return {"flat": self.fp.flat.detach().cpu(), "m": self.m.cpu(), "v": self.v.cpu(), "step": self.step_count,
                 "epoch": self.epoch, "lr": self.lr, "rng": self.gen.get_state(), "cfg": asdict(self.cfg),
                 "buffers": {k: v.cpu() for k, v in self.net.named_buffers()}}
