@@ -401,7 +401,7 @@ def bench_em_volume(args, world, rank, dev) -> dict:
 def bench_em_volume3d(args, world, rank, dev) -> dict:
     """BASELINE config 4 as real 3-D tiled inference: each rank's z-slab through a
     BioImage.IO 3-D U-Net (16-32-64-128, Conv3d 3x3x3 + BN + ReLU on the one-launch implicit-GEMM
-    kernel after the graph pass), 128 x 128 x 32 tiles with 16 / 8 voxels of overlap blended by the
+    kernel after the graph pass), 64 x 256 x 256 tiles with 8 / 16 voxels of overlap blended by the
     separable Gaussian window (be_blend_gather), then the same sharded post-processing and rank-0
     gather as the 2-D line.  Slab size per rank from --em3d-z / --em3d-yx (the 2048^3 volume at N = 8
     is --em3d-z 256 --em3d-yx 2048: same code, longer run)."""
@@ -428,7 +428,11 @@ def bench_em_volume3d(args, world, rank, dev) -> dict:
         np.save(npy, synthetic_slab(z0, z0 + Z, YX, YX, dev).cpu().numpy())
         src = VolumeSource(str(npy))
         warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
-        kw = dict(tile=128, overlap=16, batch=4, tile_z=32, overlap_z=8, split_touching=True)
+        # 64 x 256^2 tiles, 4 per call: 350 vs 239 M voxel/s for the 32 x 128^2 tiles of round 5 on a
+        # 64 x 2048^2 slab (profiles/r06/em3d/tile_sweep_s4_s5.txt: fewer, larger launches, and the
+        # z overlap costs 8 of 64 slices instead of 8 of 32)
+        kw = dict(tile=getattr(args, "em3d_tile", 256), overlap=16, batch=getattr(args, "em3d_batch", 4),
+                  tile_z=getattr(args, "em3d_tile_z", 64), overlap_z=8, split_touching=True)
         warm = torch.from_numpy(src.read(0, min(Z, 40))).to(dev)[:, :256, :256].contiguous()
         analyze_volume(warm, None, predict3d=predict3d, norm_range=(90.0, 210.0), **kw)
         del warm
@@ -448,7 +452,8 @@ def bench_em_volume3d(args, world, rank, dev) -> dict:
         timings["gather_rank0"] = round(t_gather, 4)
         out = {"em_volume3d_voxels_per_sec": round(Z * world * YX * YX / dt, 1),
                "em_volume3d_config": {"volume": [Z * world, YX, YX], "slab_per_gpu": [Z, YX, YX],
-                                      "tile": [32, 128, 128], "overlap": [8, 16, 16], "tiles_per_call": 4,
+                                      "tile": [kw["tile_z"], kw["tile"], kw["tile"]], "overlap": [8, 16, 16],
+                                      "tiles_per_call": kw["batch"],
                                       "model": "BioImage.IO 3-D U-Net 16-32-64-128 (random init, graph pass, "
                                                "implicit-GEMM 3x3x3 conv)",
                                       "split_touching": True, "gather": "rank0", "seconds": round(dt, 3),
@@ -639,8 +644,8 @@ def main():
     ap.add_argument("--em-yx", type=int, default=2048)
     ap.add_argument("--em-tile-batch", type=int, default=32, help="512^2 tiles per U-Net call (EM volume line)")
     ap.add_argument("--no-em", action="store_true", help="skip the EM volume line")
-    ap.add_argument("--em3d-z", type=int, default=32, help="z-slices per GPU of the 3-D U-Net EM line")
-    ap.add_argument("--em3d-yx", type=int, default=512)
+    ap.add_argument("--em3d-z", type=int, default=256, help="z-slices per GPU of the 3-D U-Net EM line (2048^3 at N=8)")
+    ap.add_argument("--em3d-yx", type=int, default=2048)
     ap.add_argument("--trace", default=None, metavar="PATH",
                     help="after the timed steps, run one more traced step and write a Chrome trace (rank 0)")
     args = ap.parse_args()

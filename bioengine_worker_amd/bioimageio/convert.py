@@ -19,7 +19,10 @@
    conv's input prologue (:class:`HipNormConv2d`, per-image affine from fp32 statistics);
 6. ``ConvTranspose2d(k=2, s=2)`` becomes a 1x1 MFMA conv + depth-to-space
    (:class:`HipConvTranspose2x2`) and ``Conv2d(k=2, s=2)`` space-to-depth + a 1x1 MFMA conv
-   (:class:`HipConvStride2x2`).
+   (:class:`HipConvStride2x2`); in 3-D, ``ConvTranspose3d(k=2, s=2)`` becomes a 1x1x1 MFMA conv to
+   8*Cout + the ``vol3d.hip`` depth-to-space scatter (:class:`HipConvTranspose3x2`) and
+   ``MaxPool3d(2)`` the ``vol3d.hip`` NDHWC pooling kernel (:class:`HipMaxPool3d`), so a 3-D U-Net
+   runs no library convolution.
 
 TorchScript-only weights go through :mod:`.ts_convert` (frozen graph rewrite).  Convolutions that
 do not match (3x3 strided, dilated, grouped, 5x5, ...) stay on MIOpen.
@@ -31,7 +34,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.conv import PackedConv, fused_conv2d
-from ..ops.conv3d import PackedConv3d, fused_conv3d
+from ..ops.conv3d import PackedConv3d, depth2space3d, fused_conv3d, maxpool3d_ndhwc
 
 
 def _eligible(c: nn.Module) -> bool:
@@ -41,9 +44,12 @@ def _eligible(c: nn.Module) -> bool:
 
 
 def _eligible3d(c: nn.Module) -> bool:
+    # 3x3x3 needs Cout % 4 (implicit-GEMM tiles); a 1x1x1 with a ragged Cout (a segmentation head)
+    # runs the 2-D kernel's fp32 NCHW-output epilogue instead
     return (type(c) is nn.Conv3d and c.kernel_size in ((1, 1, 1), (3, 3, 3)) and c.stride == (1, 1, 1)
             and c.dilation == (1, 1, 1) and c.groups == 1 and c.padding_mode == "zeros"
-            and c.padding == tuple(k // 2 for k in c.kernel_size) and c.out_channels % 4 == 0)
+            and c.padding == tuple(k // 2 for k in c.kernel_size)
+            and (c.out_channels % 4 == 0 or c.kernel_size == (1, 1, 1)))
 
 
 _CONV = (nn.Conv2d, nn.Conv3d)
@@ -108,7 +114,9 @@ class HipConv3d(nn.Module):
         super().__init__()
         self.cin, self.cout = conv.in_channels, conv.out_channels
         self.post_relu = post_relu
-        self.pc = PackedConv3d(conv.weight.detach().float(), None if conv.bias is None else conv.bias.detach().float())
+        self.nchw_out = self.cout % 4 != 0  # 1x1x1 head: fp32 NCDHW straight from the epilogue
+        self.pc = PackedConv3d(conv.weight.detach().float(), None if conv.bias is None else conv.bias.detach().float(),
+                               cout_pad_to=16 if self.nchw_out else None)
         self._dev = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -120,10 +128,14 @@ class HipConv3d(nn.Module):
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
-        C = x.shape[1]
+        N, C, D, H, W = x.shape
         xh = x.to(torch.bfloat16).permute(0, 2, 3, 4, 1)  # NDHWC (a view for channels_last_3d inputs)
         if C != self.pc.cin_pad:
             xh = F.pad(xh, (0, self.pc.cin_pad - C))
+        if self.nchw_out:  # [N*D, Cout, H, W] fp32 -> NCDHW view
+            y = fused_conv2d(xh.contiguous().view(N * D, H, W, self.pc.cin_pad), self.pc.taps[0], out_nchw_f32=True,
+                             cout_valid=self.cout, post_relu=self.post_relu)
+            return y.view(N, D, self.cout, H, W).permute(0, 2, 1, 3, 4)
         y = fused_conv3d(xh.contiguous(), self.pc, post_relu=self.post_relu)  # [N, D, H, W, Cout]
         return y.permute(0, 4, 1, 2, 3)  # channels_last_3d view, no copy
 
@@ -226,6 +238,64 @@ class HipConvTranspose2x2(nn.Module):
         return f"{self.cin}, {self.cout}, k=2, s=2 (1x1 MFMA + depth-to-space)"
 
 
+class HipConvTranspose3x2(nn.Module):
+    """ConvTranspose3d(k=2, stride=2) as a 1x1x1 MFMA conv to 8*Cout channels (one per output
+    sub-voxel) followed by the depth-to-space scatter of ``vol3d.hip``: each output voxel
+    (2z+dz, 2y+dy, 2x+dx) is W[:, :, dz, dy, dx]^T x[z, y, x] + b."""
+
+    def __init__(self, ct: nn.ConvTranspose3d):
+        super().__init__()
+        w = ct.weight.detach().float()  # [Cin, Cout, 2, 2, 2]
+        self.cin, self.cout = w.shape[0], w.shape[1]
+        w1 = w.permute(2, 3, 4, 1, 0).reshape(8 * self.cout, self.cin, 1, 1)  # row (4dz+2dy+dx)*Cout + co
+        b1 = None if ct.bias is None else ct.bias.detach().float().repeat(8)
+        self.__dict__["ref"] = ct  # CPU oracle only: not a registered submodule (no library op in the tree)
+        self.pc = PackedConv.from_weight(w1, b1)
+        self._dev = None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            return self.ref.to(x.device).float()(x.float()).to(x.dtype)
+        if self._dev != x.device:
+            self.pc.to(x.device)
+            self._dev = x.device
+        N, C, D, H, W = x.shape
+        xh = x.to(torch.bfloat16).permute(0, 2, 3, 4, 1)
+        if C != self.pc.cin_pad:
+            xh = F.pad(xh, (0, self.pc.cin_pad - C))
+        y = fused_conv2d(xh.contiguous().view(N * D, H, W, self.pc.cin_pad), self.pc)  # [N*D, H, W, 8*Cout]
+        out = depth2space3d(y.view(N, D, H, W, 8 * self.cout), self.cout)  # [N, 2D, 2H, 2W, Cout]
+        return out.permute(0, 4, 1, 2, 3)
+
+    def extra_repr(self) -> str:
+        return f"{self.cin}, {self.cout}, k=2, s=2 (1x1x1 MFMA + depth-to-space)"
+
+
+class HipMaxPool3d(nn.Module):
+    """MaxPool3d(2) on NDHWC bf16 (``vol3d.hip``): one 16-byte load per 8 channels per window voxel."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda or x.shape[1] % 8:
+            return F.max_pool3d(x, 2)
+        y = maxpool3d_ndhwc(x.to(torch.bfloat16).permute(0, 2, 3, 4, 1).contiguous())
+        return y.permute(0, 4, 1, 2, 3)
+
+
+def _ct3_ok(m) -> bool:
+    return (type(m) is nn.ConvTranspose3d and m.kernel_size == (2, 2, 2) and m.stride == (2, 2, 2)
+            and m.padding == (0, 0, 0) and m.output_padding == (0, 0, 0) and m.dilation == (1, 1, 1)
+            and m.groups == 1)
+
+
+def _mp3_ok(m) -> bool:
+    def two(v):
+        return v in (2, (2, 2, 2))
+
+    return (type(m) is nn.MaxPool3d and two(m.kernel_size) and two(m.stride if m.stride is not None else 2)
+            and m.padding in (0, (0, 0, 0)) and m.dilation in (1, (1, 1, 1)) and not m.ceil_mode
+            and not m.return_indices)
+
+
 class HipConvStride2x2(nn.Module):
     """Conv2d(k=2, stride=2) (strided-conv downsampling) as space-to-depth + a 1x1 MFMA conv over
     4*Cin channels: out[y, x] = sum_{dy,dx} W[:, :, dy, dx] x[2y+dy, 2x+dx]."""
@@ -316,6 +386,16 @@ def _rewrite(mod: nn.Module, stats: dict) -> None:
                     stats["conv_transpose"] += 1
                     i += 1
                     continue
+                if _ct3_ok(m):
+                    child._modules[k] = HipConvTranspose3x2(m)
+                    stats["conv_transpose"] += 1
+                    i += 1
+                    continue
+                if _mp3_ok(m):
+                    child._modules[k] = HipMaxPool3d()
+                    stats["pool3d"] += 1
+                    i += 1
+                    continue
                 if _s2_ok(m):
                     relu = i + 1 < len(items) and isinstance(items[i + 1][1], nn.ReLU)
                     child._modules[k] = HipConvStride2x2(m, post_relu=relu)
@@ -349,6 +429,12 @@ def _rewrite(mod: nn.Module, stats: dict) -> None:
         elif _ct2x2_ok(child):
             setattr(mod, name, HipConvTranspose2x2(child))
             stats["conv_transpose"] += 1
+        elif _ct3_ok(child):
+            setattr(mod, name, HipConvTranspose3x2(child))
+            stats["conv_transpose"] += 1
+        elif _mp3_ok(child):
+            setattr(mod, name, HipMaxPool3d())
+            stats["pool3d"] += 1
         elif _s2_ok(child):
             setattr(mod, name, HipConvStride2x2(child))
             stats["strided"] += 1
@@ -365,7 +451,7 @@ def optimize_for_mi355x(model: nn.Module, device=None) -> tuple[nn.Module, dict]
     """In-place graph pass (model must be in eval mode).  Returns (model, stats)."""
     model.eval()
     stats = {"convs": 0, "bn_folded": 0, "relu_fused": 0, "skipped": 0, "norm_fused": 0, "norm_unfused": 0,
-             "conv_transpose": 0, "strided": 0}
+             "conv_transpose": 0, "strided": 0, "pool3d": 0}
     _rewrite(model, stats)
     if device is not None:
         model.to(device)

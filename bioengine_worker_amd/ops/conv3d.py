@@ -110,3 +110,28 @@ def fused_conv3d(x: torch.Tensor, pc: PackedConv3d, post_relu: bool = False) -> 
         if post_relu:
             on[-1].relu_()  # the last slice has no z+1 tap: its ReLU is the only pass left
     return out
+
+
+def maxpool3d_ndhwc(x: torch.Tensor) -> torch.Tensor:
+    """MaxPool3d(2) (floor mode) of NDHWC [N, D, H, W, C] -> [N, D/2, H/2, W/2, C] (``vol3d.hip``)."""
+    N, D, H, W, C = x.shape
+    if not x.is_cuda:
+        y = F.max_pool3d(x.permute(0, 4, 1, 2, 3).float(), 2)
+        return y.permute(0, 2, 3, 4, 1).to(x.dtype).contiguous()
+    assert x.dtype == torch.bfloat16 and x.is_contiguous() and C % 8 == 0
+    out = torch.empty(N, D // 2, H // 2, W // 2, C, device=x.device, dtype=x.dtype)
+    _native.call("be_maxpool3d_ndhwc", _native.ptr(x), _native.ptr(out), N, D, H, W, C, _native.stream(x.device))
+    return out
+
+
+def depth2space3d(y: torch.Tensor, cout: int) -> torch.Tensor:
+    """[N, D, H, W, 8 cout] (channel (4 dz + 2 dy + dx) * cout + c) -> [N, 2D, 2H, 2W, cout]."""
+    N, D, H, W, C8 = y.shape
+    assert C8 == 8 * cout
+    if not y.is_cuda or cout % 8:
+        return (y.view(N, D, H, W, 2, 2, 2, cout).permute(0, 1, 4, 2, 5, 3, 6, 7)
+                .reshape(N, 2 * D, 2 * H, 2 * W, cout).contiguous())
+    assert y.dtype == torch.bfloat16 and y.is_contiguous()
+    out = torch.empty(N, 2 * D, 2 * H, 2 * W, cout, device=y.device, dtype=y.dtype)
+    _native.call("be_depth2space3d", _native.ptr(y), _native.ptr(out), N, D, H, W, cout, _native.stream(y.device))
+    return out

@@ -58,6 +58,8 @@ elif _GEMM == "hip":
 else:
     from ..ops import gemm_auto as gemm
 from ..ops import vit_train as vt
+from ..ops.conv import PackedConv, fused_conv2d
+from ..ops.conv_train import conv_wgrad
 from ..parallel.ddp import FlatParams
 
 #: smallest token count m at which the <= 192-tile weight gradients run split-K 4 (A/B knob; at batch 1,
@@ -123,6 +125,9 @@ class _Blk:
 class CPSAMTrainEngine:
     """Forward + backward of :class:`CPSAM` at a fixed batch shape ``[B, 3, bsize, bsize]``."""
 
+    #: the neck's 3x3 conv (fwd, dgrad, wgrad) on the NHWC MFMA / implicit-GEMM HIP kernels
+    #: (BE_CPSAM_NECK=miopen: the library convolution it replaces, A/B only)
+    NECK_HIP = os.environ.get("BE_CPSAM_NECK", "hip") != "miopen"
 
     def __init__(self, net: CPSAM, fp: FlatParams, B: int, device, eps: float = 1e-6,
                  side_wgrad: bool | None = None):
@@ -165,6 +170,9 @@ class CPSAMTrainEngine:
             self.blocks.append(b)
         self.neck = e.neck
         self.outc = net.out
+        nw = self.neck[2].weight.detach().float()
+        self._neck_pc = PackedConv.from_weight(nw).to(self.device)                                 # forward
+        self._neck_pcT = PackedConv.from_weight(nw.flip(2, 3).transpose(0, 1).contiguous()).to(self.device)  # dgrad
         g = self.g
         ar = torch.arange(g, device=self.device)
         self.rel_idx = (ar[:, None] - ar[None, :] + (g - 1)).long()  # get_rel_pos index at q == k size
@@ -279,8 +287,14 @@ class CPSAMTrainEngine:
         n0 = gemm.linear(t, W(self.neck[0].weight).reshape(256, D))
         _, n1, sn1 = vt.ln_fwd(n0, self.neck[1].weight, self.neck[1].bias, eps=self.eps)
         n1i = n1.view(B, g, g, 256).permute(0, 3, 1, 2)  # NCHW view of NHWC memory (channels_last)
-        n2 = F.conv2d(n1i, W(self.neck[2].weight), padding=1)
-        n2r = n2.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
+        if self.NECK_HIP and n1.is_cuda and n1.dtype == torch.bfloat16:
+            # the 3x3 neck conv on the NHWC MFMA kernel (conv2d_nhwc.hip), weights re-packed from the
+            # bf16 mirror every step (a few device copies; graph-capturable)
+            self._neck_pc.refresh(W(self.neck[2].weight).float())
+            n2r = fused_conv2d(n1.view(B, g, g, 256), self._neck_pc).view(B * N, 256)
+        else:
+            n2 = F.conv2d(n1i, W(self.neck[2].weight), padding=1)
+            n2r = n2.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
         _, n3, sn3 = vt.ln_fwd(n2r, self.neck[3].weight, self.neck[3].bias, eps=self.eps)
         o = gemm.linear(n3, W(self.outc.weight).reshape(self.outc.weight.shape[0], 256), W(self.outc.bias))
         yout = o.view(B, g, g, self.nout, ps, ps).permute(0, 3, 1, 4, 2, 5).reshape(B, self.nout, g * ps, g * ps)
@@ -333,12 +347,23 @@ class CPSAMTrainEngine:
         dn3 = gemm.mm(do, outw)
         _, dn2, _, _, _ = vt.ln_bwd(dn3, s["n2r"], s["sn3"], self.neck[3].weight, want_dx=False, want_dxb=True,
                                     out_dw=self.neck[3].weight.grad, out_db=self.neck[3].bias.grad)
-        dn2i = dn2.view(B, g, g, 256).permute(0, 3, 1, 2)
         cw = W(self.neck[2].weight)
-        dn1i, dcw, _ = torch.ops.aten.convolution_backward(dn2i, s["n1i"], cw, None, [1, 1], [1, 1], [1, 1], False,
-                                                           [0, 0], 1, [True, True, False])
-        self.neck[2].weight.grad.copy_(dcw)
-        dn1 = dn1i.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
+        if self.NECK_HIP and dn2.is_cuda and dn2.dtype == torch.bfloat16 and s["n1"].dtype == torch.bfloat16:
+            # data gradient = 3x3 conv of dy with the flipped, transposed weights (same MFMA kernel);
+            # weight gradient = the implicit-GEMM wgrad kernel (conv_train.hip), accumulated into a
+            # zeroed slice of the flat gradient
+            dn2h = dn2.reshape(B, g, g, 256).contiguous()
+            self._neck_pcT.refresh(cw.float().flip(2, 3).transpose(0, 1).contiguous())
+            dn1 = fused_conv2d(dn2h, self._neck_pcT).view(B * N, 256)
+            gw = self.neck[2].weight.grad
+            gw.zero_()
+            conv_wgrad(s["n1"].view(B, g, g, 256).contiguous(), dn2h, ks=3, cin_valid=256, cout_valid=256, dw=gw)
+        else:
+            dn2i = dn2.view(B, g, g, 256).permute(0, 3, 1, 2)
+            dn1i, dcw, _ = torch.ops.aten.convolution_backward(dn2i, s["n1i"], cw, None, [1, 1], [1, 1], [1, 1], False,
+                                                               [0, 0], 1, [True, True, False])
+            self.neck[2].weight.grad.copy_(dcw)
+            dn1 = dn1i.permute(0, 2, 3, 1).reshape(B * N, 256).contiguous()
         _, dn0, _, _, _ = vt.ln_bwd(dn1, s["n0"], s["sn1"], self.neck[1].weight, want_dx=False, want_dxb=True,
                                     out_dw=self.neck[1].weight.grad, out_db=self.neck[1].bias.grad)
         n0w = W(self.neck[0].weight).reshape(256, D)

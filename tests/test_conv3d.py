@@ -40,10 +40,13 @@ def test_graph_pass_3d_structure_and_cpu_numerics(pkg3d):
     with torch.no_grad():
         ref = net(x)
     net2, stats = optimize_for_mi355x(net)
-    # 7 conv blocks x 2 Conv3d(3x3x3) with BN + ReLU; the 1-channel 1x1x1 head stays on MIOpen
-    assert stats["convs"] == 14 and stats["bn_folded"] == 14 and stats["relu_fused"] == 14
-    assert stats["skipped"] == 1
-    assert sum(isinstance(m, HipConv3d) for m in net2.modules()) == 14
+    # 7 conv blocks x 2 Conv3d(3x3x3) with BN + ReLU, the 1-channel 1x1x1 head (fp32 NCDHW epilogue),
+    # 3 ConvTranspose3d(2, 2) and the MaxPool3d(2): no library convolution or pooling is left
+    assert stats["convs"] == 15 and stats["bn_folded"] == 14 and stats["relu_fused"] == 14
+    assert stats["skipped"] == 0 and stats["conv_transpose"] == 3 and stats["pool3d"] == 1
+    assert sum(isinstance(m, HipConv3d) for m in net2.modules()) == 15
+    lib = (torch.nn.Conv3d, torch.nn.ConvTranspose3d, torch.nn.MaxPool3d)
+    assert not [m for m in net2.modules() if type(m) in lib]
     with torch.no_grad():
         y = net2(x.bfloat16()).float()
     assert (y - ref).abs().max() < 0.05
@@ -86,7 +89,7 @@ def test_graph_pass_unet3d_matches_fp32(gpu, pkg3d):
     with torch.no_grad():
         ref = net.to(gpu)(x.to(gpu)).float().cpu()
     net2, stats = optimize_for_mi355x(net, gpu)
-    assert stats["convs"] == 14
+    assert stats["convs"] == 15 and stats["conv_transpose"] == 3 and stats["pool3d"] == 1
     with torch.no_grad():
         y = net2(x.to(gpu).bfloat16().contiguous(memory_format=torch.channels_last_3d)).float().cpu()
     assert (y - ref).abs().max() < 0.05, (y - ref).abs().max()
@@ -127,3 +130,56 @@ def test_conv3d_igemm_single_rounding(gpu, N, D, H, W, Cin, Cout, monkeypatch):
     err = (y - ref).abs()
     # one bf16 rounding of the output (2^-8 relative) plus fp32 summation-order noise
     assert (err <= ref.abs() * 2 ** -8 + 1e-4 * ref.abs().max()).all(), err.max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,D,H,W,Cin,Cout", [(1, 6, 10, 12, 64, 32), (2, 3, 5, 7, 128, 64), (1, 4, 8, 8, 32, 16)])
+def test_conv_transpose3d_matches_fp32(gpu, N, D, H, W, Cin, Cout):
+    """ConvTranspose3d(k=2, s=2) = 1x1x1 MFMA conv to 8*Cout + vol3d.hip depth-to-space, against the
+    fp32 torch op on the same bf16-rounded operands."""
+    from bioengine_worker_amd.bioimageio.convert import HipConvTranspose3x2
+
+    g = torch.Generator().manual_seed(N * 100 + D + Cin)
+    ct = torch.nn.ConvTranspose3d(Cin, Cout, 2, stride=2)
+    with torch.no_grad():
+        ct.weight.copy_(torch.randn(ct.weight.shape, generator=g) * 0.1)
+        ct.bias.copy_(torch.randn(Cout, generator=g))
+    x = torch.randn(N, Cin, D, H, W, generator=g)
+    xb = x.bfloat16().float()
+    with torch.no_grad():
+        ref = F.conv_transpose3d(xb, ct.weight.bfloat16().float(), ct.bias, stride=2)
+        mod = HipConvTranspose3x2(ct)
+        y = mod(x.to(gpu).bfloat16().contiguous(memory_format=torch.channels_last_3d)).float().cpu()
+    assert y.shape == ref.shape
+    err = ((y - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(1, 6, 10, 12, 16), (2, 7, 9, 5, 64), (1, 4, 64, 64, 32)])
+def test_maxpool3d_and_depth2space_exact(gpu, shape):
+    from bioengine_worker_amd.ops.conv3d import depth2space3d, maxpool3d_ndhwc
+
+    N, D, H, W, C = shape
+    x = torch.randn(shape).bfloat16()
+    y = maxpool3d_ndhwc(x.to(gpu)).cpu()
+    ref = F.max_pool3d(x.float().permute(0, 4, 1, 2, 3), 2).permute(0, 2, 3, 4, 1).bfloat16()
+    assert torch.equal(y, ref)  # max of bf16 values is exact
+    z = torch.randn(N, D, H, W, 8 * C).bfloat16()
+    d = depth2space3d(z.to(gpu), C).cpu()
+    assert torch.equal(d, depth2space3d(z, C))  # CPU path: reshape / permute
+    assert torch.equal(d[0, 1, 0, 1], z[0, 0, 0, 0, 5 * C: 6 * C])  # sub-voxel (dz, dy, dx) = (1, 0, 1)
+
+
+@pytest.mark.gpu
+def test_head_1x1x1_small_cout(gpu):
+    from bioengine_worker_amd.bioimageio.convert import HipConv3d
+
+    conv = torch.nn.Conv3d(16, 3, 1)
+    x = torch.randn(2, 16, 5, 12, 20)
+    with torch.no_grad():
+        ref = conv(x.bfloat16().float())
+        mod = HipConv3d(conv)
+        y = mod(x.to(gpu).bfloat16().contiguous(memory_format=torch.channels_last_3d)).float().cpu()
+    assert y.shape == ref.shape
+    assert (y - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
