@@ -37,16 +37,6 @@
 
 namespace {
 
-constexpr int TW = 32, TH = 16, NW = 8, NT = NW * 64;
-constexpr int RW = TW + 2, RH = TH + 2, RPIX = RW * RH;  // h region 34 x 18 = 612 px
-constexpr int IW = TW + 4, IH = TH + 4, IPIX = IW * IH;  // A input halo 36 x 20 = 720 px
-constexpr int RPT = (RPIX + 15) / 16;                    // 39 pixel tiles of 16
-constexpr int APT = (RPT + NW - 1) / NW;                 // 5 per wave
-constexpr int KPB = 288;                                 // B K per 32-channel chunk (9 taps x 32)
-constexpr int WSTRB = KPB + 16;
-constexpr int PSTRP = 24;                                // proj region pixel stride (8 channels)
-constexpr int WSTRP = 48;
-
 struct PairArgs {
   const bf16_t* x;   // [N, Hs, Ws, Cin]
   const bf16_t* x2;  // [N, H, W, CM] skip added to convA's output (X2)
@@ -73,850 +63,16 @@ struct PairArgs {
   unsigned long long* stamps;
 };
 
-template <int CK_, int CM_, int INMODE, bool X2, bool PROJ, int RES, int NCA>
-struct PC {
-  static constexpr int CK = CK_, CM = CM_;
-  static constexpr bool PROJ_ = PROJ;
-  static constexpr int KPA = ((9 * CK + 31) / 32) * 32;
-  static constexpr int KSA = KPA / 32;
-  static constexpr int WSTRA = KPA + 16;
-  static constexpr int PSTRI = CK == 8 ? 24 : CK + 16;
-  static constexpr int CGI = CK / 8;
-  static constexpr int PSTRM = CM + 16;
-  static constexpr int NCT = CM / 16;
-  static constexpr int NCB = CM / 32;
-  static constexpr bool RESW = CM == 32;  // every weight panel resident in LDS
-  static constexpr int HU = IPIX * CGI;   // 16-byte halo units per A chunk
-  static constexpr int HUPT = (HU + NT - 1) / NT;
-  static constexpr int WA_ELEMS = CM * WSTRA;
-  static constexpr int WB_ELEMS = CM * WSTRB;
-  static constexpr int WU = CM * KPB / 8;  // streaming: 16-byte units per weight chunk
-  static constexpr int WUPT = RESW ? 1 : (WU + NT - 1) / NT;
-  static constexpr int OUT_WAVE = 2 * TW * CM;
-  static constexpr int R_IN = IPIX * PSTRI, R_H = RPIX * PSTRM, R_OUT = NW * OUT_WAVE;
-  static constexpr int RREG0 = R_IN > R_H ? R_IN : R_H;
-  static constexpr int RREG = RREG0 > R_OUT ? RREG0 : R_OUT;
-  static constexpr int PREG = PROJ ? TH * TW * PSTRP : 0;
-  static constexpr int WREG = RESW ? NCA * WA_ELEMS + NCB * WB_ELEMS + (PROJ ? CM * WSTRP : 0) : WB_ELEMS;
-  static constexpr size_t LDS = (size_t)(RREG + PREG + WREG) * sizeof(bf16_t);
-  static constexpr int CPP = NCT * 2;  // 16-byte output chunks per pixel
-  // prefetch the residual / skip operands at tile start (registers permitting)
-  static constexpr bool PF = CM == 32;
-  static constexpr int OSH = CM == 32 ? 1 : 0;
-  static_assert(NT % CGI == 0, "a thread's channel group must not change across halo units");
-  static_assert(CK == 8 || (PSTRI / 2) % 16 == 8, "input pixel stride must be 8 (mod 16) dwords");
-  static_assert((PSTRM / 2) % 16 == 8, "h pixel stride must be 8 (mod 16) dwords");
-  static_assert((WSTRA / 2) % 16 == 8 && (WSTRB / 2) % 16 == 8, "weight row stride must be 8 (mod 16) dwords");
-  static_assert(!PROJ || (CK == 8 && NCA == 1 && RESW), "in-kernel projection only for the 8-channel stem");
-  static_assert(RESW || CK == 32, "streamed weight chunks assume equal A/B chunk geometry");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-};
-
-struct TileXY {
-  int n, ty0, tx0;
-};
-
-__device__ __forceinline__ TileXY tile_xy(const PairArgs& a, int t) {
-  const int tpi = a.tiles_x * a.tiles_y;
-  TileXY r;
-  r.n = t / tpi;
-  const int q = t - r.n * tpi;
-  r.ty0 = (q / a.tiles_x) * TH;
-  r.tx0 = (q % a.tiles_x) * TW;
-  return r;
-}
-
-// Stage-A pixel tile T (0..38) of the 18 x 34 h region -> this lane's region pixel (ry, rx).
-// Tiles 0..35 are the two 16-pixel halves of columns 0..31 of each region row, so the 16 lanes of an
-// MFMA operand read consecutive pixels of ONE halo row (ds_read_b128 conflict-free for the 8 (mod 16)
-// dword pixel stride); tiles 36..38 take the two edge columns 32..33 of 8 rows each.  (A linear
-// pixel order wraps rows inside ~half of the tiles: measured ~1.8 conflict cycles per LDS op.)
-__device__ __forceinline__ bool apix(int T, int lrow, int& ry, int& rx) {
-  if (T < 2 * RH) {
-    ry = T >> 1;
-    rx = (T & 1) * 16 + lrow;
-    return true;
-  }
-  ry = (T - 2 * RH) * 8 + (lrow >> 1);
-  rx = 2 * 16 + (lrow & 1);
-  const bool ok = ry < RH;
-  if (!ok) { ry = 0; rx = 0; }  // padding lanes: read valid data, never stored
-  return ok;
-}
-static_assert(RW == 2 * 16 + 2 && 2 * RH + (RH + 7) / 8 == RPT, "stage-A tile map covers the 18 x 34 region");
-
-// 16-byte halo unit u -> (halo pixel, 8-channel group).  For 32-channel chunks, 8 consecutive lanes
-// take 4 pixels x 2 channel groups: their ds_write_b128 then cover 8 distinct 16-byte slots of the
-// 32-bank write row (the plain pixel-major order is 2-way conflicted at the 24-dword pixel stride),
-// and 16 lanes still read 256 contiguous bytes of global memory.  The channel group of a thread is
-// the same for u and u + NT (NT % 16 == 0), which the affine prefetch relies on.
-template <int CGI>
-__device__ __forceinline__ void unit_pc(int u, int& pix, int& cg) {
-  if constexpr (CGI == 4) {
-    pix = (u >> 4) * 4 + ((u >> 1) & 3);
-    cg = ((u >> 3) & 1) * 2 + (u & 1);
-  } else {
-    pix = u / CGI;
-    cg = u % CGI;
-  }
-}
-static_assert(NT % 16 == 0, "unit_pc keeps a thread's channel group across units");
-
-// ---- A input halo: global -> registers (raw, in-transform applied) --------------------------------
-template <typename C>
-struct HaloRegs {
-  u32x4 h[C::HUPT];
-  float4 aff[C::PF ? 4 : 1];        // actA scale (2) + shift (2) of this thread's 8 channels
-  float4 paff[C::PROJ_ ? 4 : 1];    // actP
-};
-
-template <typename C, int INMODE, bool PROJ>
-__device__ __forceinline__ void issue_halo(const PairArgs& a, TileXY t, int ch, int tid, HaloRegs<C>& hr) {
-  const int c0 = ch * C::CGI * 8;
-  if constexpr (C::PF) {  // the thread's channel group is the same for every unit: its affine rides along
-    int pix0, cg0;
-    unit_pc<C::CGI>(tid, pix0, cg0);
-    const int c = c0 + cg0 * 8;
-    hr.aff[0] = *reinterpret_cast<const float4*>(a.sa + c);
-    hr.aff[1] = *reinterpret_cast<const float4*>(a.sa + c + 4);
-    const float* tr = a.ta + (size_t)t.n * a.ta_ns + c;
-    hr.aff[2] = *reinterpret_cast<const float4*>(tr);
-    hr.aff[3] = *reinterpret_cast<const float4*>(tr + 4);
-    if constexpr (PROJ) {
-      hr.paff[0] = *reinterpret_cast<const float4*>(a.sp + c);
-      hr.paff[1] = *reinterpret_cast<const float4*>(a.sp + c + 4);
-      hr.paff[2] = *reinterpret_cast<const float4*>(a.tp + c);
-      hr.paff[3] = *reinterpret_cast<const float4*>(a.tp + c + 4);
-    }
-  }
-  u32x4 (&hraw)[C::HUPT] = hr.h;
-  // CM = 32 (PF): unconditional loads (unit and coordinates clamped to valid memory): commit_halo
-  // zeroes what lies outside the image and skips units past HU, so only the addresses need to stay in
-  // bounds.  With no branch around them the compiler counts these loads exactly, and its later vmcnt
-  // waits (the epilogues) no longer drain the next tile's halo along with the operands they need.
-  // (CM = 64 keeps the branches: the clamps cost it registers it does not have.)
-  constexpr bool CL = C::PF;
-#pragma unroll
-  for (int i = 0; i < C::HUPT; ++i) {
-    const int u = CL ? min(tid + i * NT, C::HU - 1) : tid + i * NT;
-    u32x4 r = (u32x4){0u, 0u, 0u, 0u};
-    if (CL || u < C::HU) {
-      int pix, cg;
-      unit_pc<C::CGI>(u, pix, cg);
-      int gy = t.ty0 - 2 + pix / IW, gx = t.tx0 - 2 + pix % IW;
-      if (CL) {
-        gy = min(max(gy, 0), a.H - 1);
-        gx = min(max(gx, 0), a.W - 1);
-      }
-      if (CL || (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W)) {
-        const int c = c0 + cg * 8;
-        if (INMODE == 0) {
-          r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + gy) * a.Ws + gx) * a.Cin + c);
-        } else if (INMODE == 1) {
-          r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)t.n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * a.Cin + c);
-        } else {
-          const bf16_t* base = a.x + (((size_t)t.n * a.Hs + 2 * gy) * a.Ws + 2 * gx) * a.Cin + c;
-          const u32x4 r0 = *reinterpret_cast<const u32x4*>(base);
-          const u32x4 r1 = *reinterpret_cast<const u32x4*>(base + a.Cin);
-          const u32x4 q0 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin);
-          const u32x4 q1 = *reinterpret_cast<const u32x4*>(base + (size_t)a.Ws * a.Cin + a.Cin);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {  // max of bf16 values is exact in bf16
-            const float lo = fmaxf(fmaxf(lo_bf(r0[j]), lo_bf(r1[j])), fmaxf(lo_bf(q0[j]), lo_bf(q1[j])));
-            const float hi = fmaxf(fmaxf(hi_bf(r0[j]), hi_bf(r1[j])), fmaxf(hi_bf(q0[j]), hi_bf(q1[j])));
-            r[j] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
-          }
-        }
-      }
-    }
-    hraw[i] = r;
-  }
-}
-
-// activated halo -> LDS (conv zero padding applies AFTER the activation); the stem also writes
-// actP of the centre pixels for the in-kernel projection
-__device__ __forceinline__ void unpack_aff(const float4 (&f)[4], float (&sc)[8], float (&sh)[8]) {
-  sc[0] = f[0].x; sc[1] = f[0].y; sc[2] = f[0].z; sc[3] = f[0].w; sc[4] = f[1].x; sc[5] = f[1].y; sc[6] = f[1].z; sc[7] = f[1].w;
-  sh[0] = f[2].x; sh[1] = f[2].y; sh[2] = f[2].z; sh[3] = f[2].w; sh[4] = f[3].x; sh[5] = f[3].y; sh[6] = f[3].z; sh[7] = f[3].w;
-}
-
-// CM = 64, EARLY build: this chunk's actA affine loaded before the barrier that precedes the commit
-template <typename C>
-__device__ __forceinline__ void load_aff(const PairArgs& a, TileXY t, int ch, int tid, float4 (&f)[4]) {
-  int pix0, cg0;
-  unit_pc<C::CGI>(tid, pix0, cg0);
-  const int c = ch * C::CGI * 8 + cg0 * 8;
-  f[0] = *reinterpret_cast<const float4*>(a.sa + c);
-  f[1] = *reinterpret_cast<const float4*>(a.sa + c + 4);
-  const float* tr = a.ta + (size_t)t.n * a.ta_ns + c;
-  f[2] = *reinterpret_cast<const float4*>(tr);
-  f[3] = *reinterpret_cast<const float4*>(tr + 4);
-}
-
-template <typename C, bool PROJ, bool DRAIN = false>
-__device__ __forceinline__ void commit_halo(const PairArgs& a, TileXY t, int ch, int tid, const HaloRegs<C>& hr,
-                                            bf16_t* rin, bf16_t* preg, const float4 (*aff_pre)[4] = nullptr) {
-  float sc[8], sh[8];
-  if constexpr (C::PF) {
-    unpack_aff(hr.aff, sc, sh);
-  } else if (aff_pre) {
-    unpack_aff(*aff_pre, sc, sh);
-  } else {  // CM = 64: no registers to spare across the MFMA stage; read the (L2-hot) affine here
-    int pix0, cg0;
-    unit_pc<C::CGI>(tid, pix0, cg0);
-    const int c = ch * C::CGI * 8 + cg0 * 8;
-    float4 f[4];
-    f[0] = *reinterpret_cast<const float4*>(a.sa + c);
-    f[1] = *reinterpret_cast<const float4*>(a.sa + c + 4);
-    const float* tr = a.ta + (size_t)t.n * a.ta_ns + c;
-    f[2] = *reinterpret_cast<const float4*>(tr);
-    f[3] = *reinterpret_cast<const float4*>(tr + 4);
-    unpack_aff(f, sc, sh);
-  }
-  float ps[8], pt[8];
-  if constexpr (PROJ) unpack_aff(hr.paff, ps, pt);
-  // DRAIN (LATEEPI builds, nothing but the halo in flight): every halo register is consumed here, so
-  // one unconditional wait instead of the compiler's waits
-  // inside the per-unit bounds branches, whose skipped paths left the halo loads "pending" in its
-  // tracking and made it wait again, for loads issued later, further down the tile.
-  // (the builtin, not inline asm: the compiler's wait tracking sees it)
-  if constexpr (DRAIN) __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xf << 8));  // vmcnt(0)
-  const u32x4 (&hraw)[C::HUPT] = hr.h;
-#pragma unroll
-  for (int i = 0; i < C::HUPT; ++i) {
-    const int u = tid + i * NT;
-    if (u >= C::HU) continue;
-    int pix, cg;
-    unit_pc<C::CGI>(u, pix, cg);
-    const int iy = pix / IW, ix = pix % IW;
-    const int gy = t.ty0 - 2 + iy, gx = t.tx0 - 2 + ix;
-    const bool in = gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf(hraw[i][j]); v[2 * j + 1] = hi_bf(hraw[i][j]); }
-    u32x4 pk = (u32x4){0u, 0u, 0u, 0u};
-    if (in) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        pk[j] = relu_bf16x2(pack2bf(fmaf(v[2 * j], sc[2 * j], sh[2 * j]), fmaf(v[2 * j + 1], sc[2 * j + 1], sh[2 * j + 1])));
-    }
-    *reinterpret_cast<u32x4*>(rin + pix * C::PSTRI + cg * 8) = pk;
-    if (PROJ && iy >= 2 && iy < TH + 2 && ix >= 2 && ix < TW + 2) {
-      u32x4 pp = (u32x4){0u, 0u, 0u, 0u};
-      if (in) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          pp[j] = pack2bf(fmaf(v[2 * j], ps[2 * j], pt[2 * j]), fmaf(v[2 * j + 1], ps[2 * j + 1], pt[2 * j + 1]));
-      }
-      *reinterpret_cast<u32x4*>(preg + ((iy - 2) * TW + (ix - 2)) * PSTRP) = pp;
-    }
-  }
-}
-
-// ---- weights ---------------------------------------------------------------------------------
-// Streaming (CM = 64): stage s of a tile is A chunk s (s < NCA) or B chunk s - NCA; both are
-// [CM][288] panels of the packed [Cout][nchunk][288] layouts.
-template <typename C, int NCA>
-__device__ __forceinline__ void issue_w(const PairArgs& a, int s, int tid, u32x4 (&wraw)[C::WUPT]) {
-  const bf16_t* src;
-  int nch, ch;
-  if (s < NCA) { src = a.wa; nch = NCA; ch = s; } else { src = a.wb; nch = C::NCB; ch = s - NCA; }
-#pragma unroll
-  for (int i = 0; i < C::WUPT; ++i) {
-    const int u = tid + i * NT;
-    if (u < C::WU) {
-      const int r = u / (KPB / 8), k8 = u % (KPB / 8);
-      // 32-bit offsets off a uniform base (global_load ... saddr): loop-invariant 64-bit per-unit
-      // addresses kept live across tiles were what spilled
-      const uint32_t off = (uint32_t)((r * nch + ch) * KPB + k8 * 8);
-      wraw[i] = *reinterpret_cast<const u32x4*>(src + off);
-    }
-  }
-}
-
-template <typename C>
-__device__ __forceinline__ void commit_w(int tid, const u32x4 (&wraw)[C::WUPT], bf16_t* wl) {
-#pragma unroll
-  for (int i = 0; i < C::WUPT; ++i) {
-    const int u = tid + i * NT;
-    if (u < C::WU) {
-      const int r = u / (KPB / 8), k8 = u % (KPB / 8);
-      *reinterpret_cast<u32x4*>(wl + r * WSTRB + k8 * 8) = wraw[i];
-    }
-  }
-}
-
-// Resident (CM = 32): every panel copied once per workgroup: A chunks, B chunk(s), projection.
-template <typename C, bool PROJ, int NCA>
-__device__ __forceinline__ void load_resident(const PairArgs& a, int tid, bf16_t* wl) {
-  for (int u = tid; u < NCA * 32 * (C::KPA / 8); u += NT) {  // CM == 32 rows
-    const int ch = u / (32 * (C::KPA / 8)), q = u % (32 * (C::KPA / 8));
-    const int r = q / (C::KPA / 8), k8 = q % (C::KPA / 8);
-    *reinterpret_cast<u32x4*>(wl + ch * C::WA_ELEMS + r * C::WSTRA + k8 * 8) =
-        *reinterpret_cast<const u32x4*>(a.wa + ((size_t)r * NCA + ch) * C::KPA + k8 * 8);
-  }
-  bf16_t* wlb = wl + NCA * C::WA_ELEMS;
-  for (int u = tid; u < C::NCB * 32 * (KPB / 8); u += NT) {
-    const int ch = u / (32 * (KPB / 8)), q = u % (32 * (KPB / 8));
-    const int r = q / (KPB / 8), k8 = q % (KPB / 8);
-    *reinterpret_cast<u32x4*>(wlb + ch * C::WB_ELEMS + r * WSTRB + k8 * 8) =
-        *reinterpret_cast<const u32x4*>(a.wb + ((size_t)r * C::NCB + ch) * KPB + k8 * 8);
-  }
-  if (PROJ) {
-    bf16_t* wlp = wlb + C::NCB * C::WB_ELEMS;
-    for (int u = tid; u < 32 * 4; u += NT) {
-      const int r = u / 4, k8 = u % 4;
-      *reinterpret_cast<u32x4*>(wlp + r * WSTRP + k8 * 8) = *reinterpret_cast<const u32x4*>(a.wp + (size_t)r * 32 + k8 * 8);
-    }
-  }
-}
-
-// ---- stage A: h region (612 px, linear order) from the input halo ---------------------------------
-template <typename C, bool ROLL = false>
-__device__ __forceinline__ void mma_a(f32x4 (&acc)[C::NCT][APT], const bf16_t* rin, const bf16_t* wl, int wave,
-                                      int lrow, int kq) {
-  int base[APT];
-#pragma unroll
-  for (int j = 0; j < APT; ++j) {
-    int ry, rx;
-    apix(wave + j * NW, lrow, ry, rx);
-    base[j] = (ry * IW + rx) * C::PSTRI + (C::CK == 8 ? 0 : kq * 8);
-  }
-  auto frags = [&](int ks, bf16x8 (&af)[C::NCT], bf16x8 (&bf)[APT]) {
-    int off;
-    if constexpr (C::CK == 8) {  // 4 taps x 8 channels per K step; K padding (tap >= 9) has zero weights
-      int tap = ks * 4 + kq;
-      if (tap >= 9) tap = 0;
-      off = ((tap / 3) * IW + tap % 3) * C::PSTRI;
-    } else {
-      off = ((ks / 3) * IW + ks % 3) * C::PSTRI;
-    }
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct)
-      af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTRA + ks * 32 + kq * 8);
-#pragma unroll
-    for (int j = 0; j < APT; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(rin + base[j] + off);
-  };
-  if constexpr (C::NCT * APT <= 10) {  // registers to spare: explicit fragment double buffer
-    bf16x8 af[2][C::NCT], bf[2][APT];
-    frags(0, af[0], bf[0]);
-#pragma unroll
-    for (int ks = 0; ks < C::KSA; ++ks) {
-      const int cur = ks & 1;
-      if (ks + 1 < C::KSA) frags(ks + 1, af[cur ^ 1], bf[cur ^ 1]);
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct)
-#pragma unroll
-        for (int j = 0; j < APT; ++j)
-          acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bf[cur][j], acc[ct][j], 0, 0, 0);
-    }
-  } else if constexpr (ROLL) {
-    // CM = 64, rolling reload: one fragment set, and each fragment of K-step ks+1 is read into its
-    // register right after its last MFMA of step ks (pixel fragments after their 4-MFMA group,
-    // weight fragments during the last group), so the reads run under the remaining MFMAs of ks
-    // instead of being exposed at the top of every step, with no extra registers
-    bf16x8 af[C::NCT], bf[APT];
-    frags(0, af, bf);
-#pragma unroll
-    for (int ks = 0; ks < C::KSA; ++ks) {
-      const bool more = ks + 1 < C::KSA;
-      const int kn = more ? ks + 1 : ks;
-      const int offn = ((kn / 3) * IW + kn % 3) * C::PSTRI;
-#pragma unroll
-      for (int j = 0; j < APT; ++j) {
-#pragma unroll
-        for (int ct = 0; ct < C::NCT; ++ct) {
-          acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[j], acc[ct][j], 0, 0, 0);
-          if (j == APT - 1 && more)
-            af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * C::WSTRA + kn * 32 + kq * 8);
-        }
-        if (more) bf[j] = *reinterpret_cast<const bf16x8*>(rin + base[j] + offn);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  } else {  // CM = 64: 80 accumulator VGPRs; single fragment set, the scheduler overlaps the reads
-#pragma unroll
-    for (int ks = 0; ks < C::KSA; ++ks) {
-      bf16x8 af[C::NCT], bf[APT];
-      frags(ks, af, bf);
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct)
-#pragma unroll
-        for (int j = 0; j < APT; ++j)
-          acc[ct][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[j], acc[ct][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // keep later steps' ds_reads from being hoisted (spills)
-    }
-  }
-}
-
-// Per-tile epilogue operands, issued at the START of the tile so their latency hides behind the
-// A-stage MFMAs (loading them in the epilogues left ~1 us of dependent global-load latency exposed
-// per phase: 1 block of 8 waves per CU has nothing else to run meanwhile).
-template <typename C, bool X2, int RES, bool PF>
-struct EpiRegs {
-  float4 sb[PF ? C::NCT : 1], tb[PF ? C::NCT : 1], bias[PF ? C::NCT : 1];
-  u32x2 xv[X2 && PF ? APT : 1][C::NCT];
-  u32x2 rv[RES && PF ? 4 : 1][C::NCT];
-};
-
-template <typename C, bool X2>
-__device__ __forceinline__ u32x2 load_x2(const PairArgs& a, TileXY t, int j, int ct, int wave, int lrow, int kq) {
-  // CM = 32: clamped, unconditional load (see issue_halo): epi_a stores zero outside the image and
-  // nothing for padding lanes, so only the address must stay valid
-  int ry, rx;
-  const bool ok = apix(wave + j * NW, lrow, ry, rx);
-  int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
-  u32x2 v = (u32x2){0u, 0u};
-  if constexpr (C::PF) {
-    gy = min(max(gy, 0), a.H - 1);
-    gx = min(max(gx, 0), a.W - 1);
-    if (X2) v = *reinterpret_cast<const u32x2*>(a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * C::CM + ct * 16 + kq * 4);
-  } else if (X2 && ok && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
-    v = *reinterpret_cast<const u32x2*>(a.x2 + (((size_t)t.n * a.H + gy) * a.W + gx) * C::CM + ct * 16 + kq * 4);
-  }
-  return v;
-}
-
-template <typename C, int RES>
-__device__ __forceinline__ u32x2 load_res(const PairArgs& a, TileXY t, int pt, int ct, int wave, int lrow, int kq) {
-  // CM = 32: clamped, unconditional load (see issue_halo): pixels outside the image are never stored
-  int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
-  if constexpr (C::PF) {
-    py = min(py, a.H - 1);
-    px = min(px, a.W - 1);
-  } else if (py >= a.H || px >= a.W) {
-    return (u32x2){0u, 0u};
-  }
-  if (RES == 0) return (u32x2){0u, 0u};
-  size_t pix;
-  if (RES == 1) pix = ((size_t)t.n * a.H + py) * a.W + px;
-  else pix = ((size_t)t.n * (a.H >> 1) + (py >> 1)) * (a.W >> 1) + (px >> 1);
-  return *reinterpret_cast<const u32x2*>(a.res + pix * C::CM + ct * 16 + kq * 4);
-}
-
-template <typename C, bool X2, int RES, bool PF>
-__device__ __forceinline__ void issue_epi(const PairArgs& a, TileXY t, int wave, int lrow, int kq,
-                                          EpiRegs<C, X2, RES, PF>& e) {
-  if constexpr (PF) {
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct) {
-      const int c = ct * 16 + kq * 4;
-      e.sb[ct] = *reinterpret_cast<const float4*>(a.sb + c);
-      e.tb[ct] = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
-      e.bias[ct] = *reinterpret_cast<const float4*>(a.bias + c);
-    }
-  }
-  if constexpr (PF && X2) {
-#pragma unroll
-    for (int j = 0; j < APT; ++j)
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct) e.xv[j][ct] = load_x2<C, X2>(a, t, j, ct, wave, lrow, kq);
-  }
-  if constexpr (PF && RES != 0) {
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-      for (int ct = 0; ct < C::NCT; ++ct) e.rv[pt][ct] = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
-  }
-}
-
-// CM = 64, EPIA build: actB's scale / shift (and the skip operand) of the stage-A epilogue loaded
-// before the barrier that precedes it, in flight while the slower waves finish their MFMAs
-template <typename C, bool X2>
-struct EpiA {
-  float4 s[C::NCT], sh[C::NCT];
-  u32x2 xv[X2 ? APT : 1][C::NCT];
-};
-
-template <typename C, bool X2>
-__device__ __forceinline__ void issue_epia(const PairArgs& a, TileXY t, int wave, int lrow, int kq, EpiA<C, X2>& p) {
-#pragma unroll
-  for (int ct = 0; ct < C::NCT; ++ct) {
-    const int c = ct * 16 + kq * 4;
-    p.s[ct] = *reinterpret_cast<const float4*>(a.sb + c);
-    p.sh[ct] = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
-    if constexpr (X2) {
-#pragma unroll
-      for (int j = 0; j < APT; ++j) p.xv[j][ct] = load_x2<C, X2>(a, t, j, ct, wave, lrow, kq);
-    }
-  }
-}
-
-// actB(+skip) of stage A's accumulators -> h (bf16) in LDS; zero outside the image
-template <typename C, bool X2, int RES, bool PF>
-__device__ __forceinline__ void epi_a(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][APT], bf16_t* rh,
-                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq,
-                                      const EpiA<C, X2>* pre = nullptr) {
-#pragma unroll
-  for (int ct = 0; ct < C::NCT; ++ct) {
-    const int c = ct * 16 + kq * 4;
-    float4 s, sh;
-    if constexpr (PF) {
-      s = e.sb[ct];
-      sh = e.tb[ct];
-    } else if (pre) {
-      s = pre->s[ct];
-      sh = pre->sh[ct];
-    } else {
-      s = *reinterpret_cast<const float4*>(a.sb + c);
-      sh = *reinterpret_cast<const float4*>(a.tb + (size_t)t.n * a.tb_ns + c);
-    }
-    u32x2 xv[APT];
-#pragma unroll
-    for (int j = 0; j < APT; ++j) {
-      if constexpr (PF && X2) xv[j] = e.xv[j][ct];
-      else if (X2 && pre) xv[j] = pre->xv[j][ct];
-      else xv[j] = load_x2<C, X2>(a, t, j, ct, wave, lrow, kq);
-    }
-#pragma unroll
-    for (int j = 0; j < APT; ++j) {
-      int ry, rx;
-      if (!apix(wave + j * NW, lrow, ry, rx)) continue;
-      const int p = ry * RW + rx;
-      const int gy = t.ty0 - 1 + ry, gx = t.tx0 - 1 + rx;
-      u32x2 st = (u32x2){0u, 0u};
-      if (gy >= 0 && gy < a.H && gx >= 0 && gx < a.W) {
-        float v0 = acc[ct][j][0], v1 = acc[ct][j][1], v2 = acc[ct][j][2], v3 = acc[ct][j][3];
-        if (X2) {
-          v0 += lo_bf(xv[j][0]); v1 += hi_bf(xv[j][0]); v2 += lo_bf(xv[j][1]); v3 += hi_bf(xv[j][1]);
-        }
-        st[0] = relu_bf16x2(pack2bf(fmaf(v0, s.x, sh.x), fmaf(v1, s.y, sh.y)));
-        st[1] = relu_bf16x2(pack2bf(fmaf(v2, s.z, sh.z), fmaf(v3, s.w, sh.w)));
-      }
-      *reinterpret_cast<u32x2*>(rh + p * C::PSTRM + c) = st;
-    }
-  }
-}
-
-// ---- stage B: 16x32 output tile from h ----------------------------------------------------------
-template <typename C>
-__device__ __forceinline__ void mma_b(f32x4 (&acc)[C::NCT][4], const bf16_t* rh, const bf16_t* wl, int cb, int wave,
-                                      int lrow, int kq) {
-  int base[4];
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    const int oy = 2 * wave + (pt >> 1), ox = (pt & 1) * 16 + lrow;
-    base[pt] = (oy * RW + ox) * C::PSTRM + cb * 32 + kq * 8;
-  }
-  auto frags = [&](int ks, bf16x8 (&af)[C::NCT], bf16x8 (&bf)[4]) {
-    const int off = ((ks / 3) * RW + ks % 3) * C::PSTRM;
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct)
-      af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * WSTRB + ks * 32 + kq * 8);
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt) bf[pt] = *reinterpret_cast<const bf16x8*>(rh + base[pt] + off);
-  };
-  bf16x8 af[2][C::NCT], bf[2][4];
-  frags(0, af[0], bf[0]);
-#pragma unroll
-  for (int ks = 0; ks < 9; ++ks) {
-    const int cur = ks & 1;
-    if (ks + 1 < 9) frags(ks + 1, af[cur ^ 1], bf[cur ^ 1]);
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct)
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt)
-        acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][ct], bf[cur][pt], acc[ct][pt], 0, 0, 0);
-  }
-}
-
-// 1x1 projection of the stem (8 input channels = one 32-deep K step, k >= 8 zero weights)
-template <typename C>
-__device__ __forceinline__ void mma_p(f32x4 (&acc)[C::NCT][4], const bf16_t* preg, const bf16_t* wl, int wave, int lrow,
-                                      int kq) {
-  bf16x8 af[C::NCT], bf[4];
-#pragma unroll
-  for (int ct = 0; ct < C::NCT; ++ct) af[ct] = *reinterpret_cast<const bf16x8*>(wl + (ct * 16 + lrow) * WSTRP + kq * 8);
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    const int oy = 2 * wave + (pt >> 1), ox = (pt & 1) * 16 + lrow;
-    bf[pt] = *reinterpret_cast<const bf16x8*>(preg + (oy * TW + ox) * PSTRP);
-  }
-#pragma unroll
-  for (int ct = 0; ct < C::NCT; ++ct)
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-      acc[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bf[pt], acc[ct][pt], 0, 0, 0);
-}
-
-template <typename C>
-__device__ __forceinline__ int stage_off(int p, int co) {
-  return p * (C::NCT * 16) + ((co >> 3) ^ ((p >> C::OSH) & (C::CPP - 1))) * 8 + (co & 7);
-}
-
-// bias + residual, staged through LDS, 16-byte coalesced NHWC stores
-template <typename C, int RES>
-struct LateEpi {  // CM = 64 (no tile-start prefetch): residual + bias issued right after stage B's MFMAs
-  u32x2 rv[4][C::NCT];
-  float4 bias[C::NCT];
-};
-
-template <typename C, int RES>
-__device__ __forceinline__ void issue_late(const PairArgs& a, TileXY t, int wave, int lrow, int kq, LateEpi<C, RES>& l) {
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct) l.rv[pt][ct] = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
-#pragma unroll
-  for (int ct = 0; ct < C::NCT; ++ct) l.bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
-}
-
-template <typename C, bool X2, int RES, bool PF, bool LATE = false>
-__device__ __forceinline__ void epi_b(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][4], bf16_t* stage,
-                                      const EpiRegs<C, X2, RES, PF>& e, int wave, int lrow, int kq,
-                                      const LateEpi<C, RES>* late = nullptr) {
-  u32x2 rv[4][C::NCT];
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct) {
-      if constexpr (PF && RES != 0) rv[pt][ct] = e.rv[pt][ct];
-      else if constexpr (LATE) rv[pt][ct] = late->rv[pt][ct];
-      else rv[pt][ct] = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
-    }
-  float4 bias[C::NCT];
-#pragma unroll
-  for (int ct = 0; ct < C::NCT; ++ct) {
-    if constexpr (PF) bias[ct] = e.bias[ct];
-    else if constexpr (LATE) bias[ct] = late->bias[ct];
-    else bias[ct] = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
-  }
-  bf16_t* ws = stage + wave * C::OUT_WAVE;
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    const int p = (pt >> 1) * TW + (pt & 1) * 16 + lrow;
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct) {
-      u32x2 st;
-      st[0] = pack2bf(acc[ct][pt][0] + bias[ct].x + lo_bf(rv[pt][ct][0]), acc[ct][pt][1] + bias[ct].y + hi_bf(rv[pt][ct][0]));
-      st[1] = pack2bf(acc[ct][pt][2] + bias[ct].z + lo_bf(rv[pt][ct][1]), acc[ct][pt][3] + bias[ct].w + hi_bf(rv[pt][ct][1]));
-      *reinterpret_cast<u32x2*>(ws + stage_off<C>(p, ct * 16 + kq * 4)) = st;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int lane = lrow + 16 * kq;
-#pragma unroll
-  for (int it = 0; it < 2 * TW * C::CPP / 64; ++it) {
-    const int q = it * 64 + lane;
-    const int p = q / C::CPP, c = q % C::CPP;
-    const int py = t.ty0 + 2 * wave + p / TW, px = t.tx0 + p % TW;
-    const u32x4 v = *reinterpret_cast<const u32x4*>(ws + stage_off<C>(p, c * 8));
-    if (py < a.H && px < a.W) *reinterpret_cast<u32x4*>(a.out + (((size_t)t.n * a.H + py) * a.W + px) * C::CM + c * 8) = v;
-  }
-}
-
-// HEAD epilogue (CM = 32): out = bf16(acc + bias + res) as the per-layer path would store it, then the
-// output layer's pre-activation and 1x1 conv as ONE 16x16x32 MFMA per 16 pixels straight from the
-// registers: this lane's B fragment is its 8 channels {4kq..4kq+3, 16+4kq..16+4kq+3} of pixel lrow
-// (the host packs Wh's k axis in that order), so the 32-channel map never goes to HBM and the
-// separate head launch (a full re-read of it) disappears.  Lane (lrow, kq) ends with output
-// channels 4kq..4kq+3 of pixel lrow; rows >= nh are zero-weight padding.
-struct HeadRegs {
-  float4 s[2], t[2];
-  bf16x8 w;
-  float4 b;
-};
-
-__device__ __forceinline__ void load_head(const PairArgs& a, int lrow, int kq, HeadRegs& hr) {
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    hr.s[ct] = *reinterpret_cast<const float4*>(a.sh + ct * 16 + kq * 4);
-    hr.t[ct] = *reinterpret_cast<const float4*>(a.th + ct * 16 + kq * 4);
-  }
-  hr.w = *reinterpret_cast<const bf16x8*>(a.wh + lrow * 32 + kq * 8);
-  hr.b = *reinterpret_cast<const float4*>(a.bh + kq * 4);
-}
-
-template <typename C, bool X2, int RES, bool PF>
-__device__ __forceinline__ void epi_head(const PairArgs& a, TileXY t, const f32x4 (&acc)[C::NCT][4],
-                                         const EpiRegs<C, X2, RES, PF>& e, const HeadRegs& hr, int wave, int lrow,
-                                         int kq) {
-  static_assert(C::NCT == 2, "head fusion is for the 32-channel level");
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    u32x4 bw;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      u32x2 rv;
-      if constexpr (PF && RES != 0) rv = e.rv[pt][ct];
-      else rv = load_res<C, RES>(a, t, pt, ct, wave, lrow, kq);
-      float4 bias;
-      if constexpr (PF) bias = e.bias[ct];
-      else bias = *reinterpret_cast<const float4*>(a.bias + ct * 16 + kq * 4);
-      const uint32_t o0 = pack2bf(acc[ct][pt][0] + bias.x + lo_bf(rv[0]), acc[ct][pt][1] + bias.y + hi_bf(rv[0]));
-      const uint32_t o1 = pack2bf(acc[ct][pt][2] + bias.z + lo_bf(rv[1]), acc[ct][pt][3] + bias.w + hi_bf(rv[1]));
-      bw[2 * ct] = relu_bf16x2(pack2bf(fmaf(lo_bf(o0), hr.s[ct].x, hr.t[ct].x), fmaf(hi_bf(o0), hr.s[ct].y, hr.t[ct].y)));
-      bw[2 * ct + 1] = relu_bf16x2(pack2bf(fmaf(lo_bf(o1), hr.s[ct].z, hr.t[ct].z), fmaf(hi_bf(o1), hr.s[ct].w, hr.t[ct].w)));
-    }
-    const f32x4 y = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hr.w, *reinterpret_cast<const bf16x8*>(&bw), zero, 0, 0, 0);
-    const int py = t.ty0 + 2 * wave + (pt >> 1), px = t.tx0 + (pt & 1) * 16 + lrow;
-    if (py < a.H && px < a.W) {
-      const float bb[4] = {hr.b.x, hr.b.y, hr.b.z, hr.b.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int co = kq * 4 + i;
-        if (co < a.nh) a.hout[(((size_t)t.n * a.nh + co) * a.H + py) * a.W + px] = y[i] + bb[i];
-      }
-    }
-  }
-}
-
-// VAR (CM = 64 A/B): bit 0 = LATE (BE_PAIR_LATE_EPI): the output epilogue's residual and bias loads
-// are issued right after stage B's MFMAs, in flight across the barrier before the epilogue; bit 1 =
-// ROLL (BE_PAIR_ROLL): stage A's rolling fragment reload (see mma_a); bit 2 = EARLY
-// (BE_PAIR_EARLY_AFF): each chunk's actA affine loaded before the barrier ahead of its halo commit.
-template <int CK, int CM, int INMODE, bool X2, bool PROJ, int RES, int NCA, bool HEAD = false, bool STAMP = false,
-          int VAR = 0>
-__global__ __launch_bounds__(NT, 2) void conv_pair_kernel(PairArgs a) {
-  constexpr bool LATE = (VAR & 1) != 0;
-  constexpr bool ROLL = (VAR & 2) != 0;
-  constexpr bool EARLY = (VAR & 4) != 0;
-  constexpr bool EPIA = (VAR & 8) != 0;
-  using C0 = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
-  // BE_PAIR_TOPEPI=1 -> the round-4 order (A/B); NCA = 2 keeps it (its skip operand prefetch on top
-  // of the next chunk's halo spills), with exact vmcnt counts now that the loads are unconditional
-  constexpr bool LATEEPI = (VAR & 32) == 0 && NCA == 1 && C0::PF;
-  // SEPS (CM = 32, BE_PAIR_SEPS): output staging in its own LDS region (wave-private slots) after the
-  // weights, so the next tile's halo commit never overlays it and needs no barrier of its own: the
-  // barrier ahead of the output epilogue already fences stage B's reads of h
-  using C = PC<CK, CM, INMODE, X2, PROJ, RES, NCA>;
-  constexpr bool SEPS = (VAR & 16) != 0 && C::RESW && !HEAD;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* R = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* P = R + C::RREG;
-  bf16_t* WL = P + C::PREG;
-  bf16_t* S = WL + C::WREG;  // SEPS only (the launch adds R_OUT elements of LDS)
-  const int tid0 = threadIdx.x;
-  const int total = a.N * a.tiles_x * a.tiles_y;
-  // contiguous tile range per workgroup (tiles sharing halo rows run back to back on one CU)
-  const int t0 = (int)(((long long)blockIdx.x * total) / gridDim.x);
-  const int t1 = (int)(((long long)(blockIdx.x + 1) * total) / gridDim.x);
-  if (t0 >= t1) return;
-  if constexpr (C::RESW) load_resident<C, PROJ, NCA>(a, tid0, WL);
-
-  HeadRegs hr;
-  if constexpr (HEAD) load_head(a, tid0 & 15, (tid0 & 63) >> 4, hr);
-  HaloRegs<C> hraw;
-  u32x4 wraw[C::WUPT];
-  issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t0), 0, tid0, hraw);
-  if constexpr (!C::RESW) issue_w<C, NCA>(a, 0, tid0, wraw);
-  unsigned long long ph[5] = {0, 0, 0, 0, 0};
-  unsigned long long tprev = STAMP ? __builtin_amdgcn_s_memtime() : 0;
-  auto stamp = [&](int k) {
-    if constexpr (STAMP) {
-      const unsigned long long tn = __builtin_amdgcn_s_memtime();
-      ph[k] += tn - tprev;
-      tprev = tn;
-    }
-  };
-
-  for (int t = t0; t < t1; ++t) {
-    // Opaque per-iteration copy of the thread id: without it LICM hoists every per-unit halo /
-    // weight / LDS address out of the tile loop and the CM = 64 variants spill (~100 B/lane).
-    int tid = tid0;
-    asm volatile("" : "+v"(tid));
-    const int lane = tid & 63, wave = tid >> 6, lrow = lane & 15, kq = lane >> 4;
-    const TileXY cur = tile_xy(a, t);
-    EpiRegs<C, X2, RES, C::PF> ep;
-    // LATEEPI (default): the epilogue operands are issued after the last halo commit, not at the
-    // top of the tile: loads issued ahead of the commit sit behind the halo registers in the
-    // in-order vmcnt queue, and the commit's wait for its halo then also waited for them (~1 L2 / HBM
-    // round trip per tile).  They are first needed by epi_a, after stage A's MFMAs.
-    if constexpr (!LATEEPI) issue_epi<C, X2, RES, C::PF>(a, cur, wave, lrow, kq, ep);
-    f32x4 acc_a[C::NCT][APT];
-#pragma unroll
-    for (int i = 0; i < C::NCT; ++i)
-#pragma unroll
-      for (int j = 0; j < APT; ++j) acc_a[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    // ---- stage A: NCA input chunks ----
-    auto chunk = [&](const int c) {
-      if constexpr (EARLY && !C::PF) {
-        float4 aff[4];
-        load_aff<C>(a, cur, c, tid, aff);  // in flight across the barrier
-        __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
-        commit_halo<C, PROJ>(a, cur, c, tid, hraw, R, P, &aff);
-      } else {
-        if (!(SEPS && c == 0)) __syncthreads();  // previous readers of R (last tile's output staging / previous chunk) are done
-        commit_halo<C, PROJ, LATEEPI>(a, cur, c, tid, hraw, R, P);
-      }
-      if constexpr (!C::RESW) commit_w<C>(tid, wraw, WL);
-      __syncthreads();
-      stamp(0);
-      if (LATEEPI && c == NCA - 1) issue_epi<C, X2, RES, C::PF>(a, cur, wave, lrow, kq, ep);
-      if (c + 1 < NCA) issue_halo<C, INMODE, PROJ>(a, cur, c + 1, tid, hraw);
-      else if (t + 1 < t1) issue_halo<C, INMODE, PROJ>(a, tile_xy(a, t + 1), 0, tid, hraw);
-      if constexpr (!C::RESW) issue_w<C, NCA>(a, c + 1, tid, wraw);
-      mma_a<C, ROLL>(acc_a, R, C::RESW ? WL + c * C::WA_ELEMS : WL, wave, lrow, kq);
-      stamp(1);
-    };
-    // CM = 32: unrolled, so each chunk's vmcnt waits are counted on its own path (the rolled loop
-    // merges chunk 0's, with the epilogue operands in flight, into every chunk's)
-    if constexpr (C::PF) {
-#pragma unroll
-      for (int c = 0; c < NCA; ++c) chunk(c);
-    } else {
-#pragma unroll 1
-      for (int c = 0; c < NCA; ++c) chunk(c);
-    }
-    if constexpr (EPIA && !C::PF && !X2) {  // with the skip operand too it spills (320 B)
-      EpiA<C, X2> pa;
-      issue_epia<C, X2>(a, cur, wave, lrow, kq, pa);
-      __syncthreads();  // every wave is done with the input halo and the A weights
-      epi_a<C, X2, RES, C::PF>(a, cur, acc_a, R, ep, wave, lrow, kq, &pa);
-    } else {
-      __syncthreads();  // every wave is done with the input halo and the A weights
-      epi_a<C, X2, RES, C::PF>(a, cur, acc_a, R, ep, wave, lrow, kq);
-    }
-    stamp(2);
-    // ---- stage B: CM/32 chunks of h ----
-    f32x4 acc_b[C::NCT][4];
-#pragma unroll
-    for (int i = 0; i < C::NCT; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc_b[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int cb = 0; cb < C::NCB; ++cb) {
-      if constexpr (!C::RESW) {
-        if (cb > 0) __syncthreads();  // previous chunk's weights consumed
-        commit_w<C>(tid, wraw, WL);
-        __syncthreads();
-        const int s = NCA + cb + 1;  // next stage: next B chunk or the next tile's A chunk 0
-        if (s < NCA + C::NCB) issue_w<C, NCA>(a, s, tid, wraw);
-        else if (t + 1 < t1) issue_w<C, NCA>(a, 0, tid, wraw);
-      } else {
-        __syncthreads();  // h complete
-      }
-      mma_b<C>(acc_b, R, C::RESW ? WL + NCA * C::WA_ELEMS + cb * C::WB_ELEMS : WL, cb, wave, lrow, kq);
-    }
-    if constexpr (PROJ) mma_p<C>(acc_b, P, WL + NCA * C::WA_ELEMS + C::NCB * C::WB_ELEMS, wave, lrow, kq);
-    stamp(3);
-    if constexpr (HEAD) {
-      epi_head<C, X2, RES, C::PF>(a, cur, acc_b, ep, hr, wave, lrow, kq);  // registers only: no LDS staging
-    } else if constexpr (LATE && !C::PF && RES != 0) {
-      LateEpi<C, RES> late;
-      issue_late<C, RES>(a, cur, wave, lrow, kq, late);
-      __syncthreads();  // every wave is done reading h before the output staging overlays it
-      epi_b<C, X2, RES, C::PF, true>(a, cur, acc_b, R, ep, wave, lrow, kq, &late);
-    } else {
-      __syncthreads();  // every wave is done reading h before the output staging overlays it
-      epi_b<C, X2, RES, C::PF>(a, cur, acc_b, SEPS ? S : R, ep, wave, lrow, kq);
-    }
-    stamp(4);
-  }
-  if constexpr (STAMP) {
-    if (tid0 < 64) {  // wave 0: lane k stores slot k (a lane-indexed vector store)
-      unsigned long long v = 0;
-#pragma unroll
-      for (int k = 0; k < 5; ++k)
-        if (tid0 == k) v = ph[k];
-      if (tid0 == 7) v = (unsigned long long)(t1 - t0);
-      if (tid0 < 8) a.stamps[(size_t)blockIdx.x * 8 + tid0] = v;
-    }
-  }
-}
+// The one-group kernel and its helpers, once per tile geometry (conv_pair_onegroup.inc).
+namespace g32 {
+constexpr int TW = 32, TH = 16, NW = 8;
+#include "conv_pair_onegroup.inc"
+}  // namespace g32
+namespace g12 {
+constexpr int TW = 16, TH = 12, NW = 4;
+#include "conv_pair_onegroup.inc"
+}  // namespace g12
+using namespace g32;  // the ping-pong kernel and the launchers below use the 16 x 32 geometry
 
 unsigned long long* g_pair_stamps = nullptr;  // diagnostics: be_conv_pair_set_stamps
 int g_pair_stamps_cap = 0;                    // workgroups the stamp buffer holds
@@ -1807,6 +963,41 @@ static int g_pair_pp = [] {
   return e ? atoi(e) : 1;
 }();
 
+// BE_PAIR_G12 (A/B): the level-1 (CM = 64) half-blocks on the 12 x 16-tile geometry -- 4 waves and
+// <= 79 KB of LDS per workgroup, so two workgroups share each CU and one's halo / epilogue phases run
+// beside the other's MFMAs (the one-group 16 x 32 kernel leaves the MFMA pipe idle through them:
+// profiles/r04/conv/pair_phases.jsonl).  BE_PAIR_G12_GRID: workgroups (default 512).
+static int g_pair_g12 = [] {
+  const char* e = getenv("BE_PAIR_G12");
+  return e ? atoi(e) : 0;
+}();
+static int g_pair_g12_grid = [] {
+  const char* e = getenv("BE_PAIR_G12_GRID");
+  return e ? atoi(e) : 512;
+}();
+
+template <int CK, int CM, int INMODE, bool X2, int RES, int NCA>
+int launch_pair12(PairArgs a, hipStream_t s) {
+  using C = g12::PC<CK, CM, INMODE, X2, false, RES, NCA>;
+  constexpr size_t lds = C::LDS;
+  static_assert(2 * lds <= 160 * 1024, "two workgroups per CU");
+  a.tiles_x = (a.W + g12::TW - 1) / g12::TW;
+  a.tiles_y = (a.H + g12::TH - 1) / g12::TH;
+  const int tiles = a.N * a.tiles_x * a.tiles_y;
+  int g = g_pair_g12_grid > 0 ? g_pair_g12_grid : 512;
+  if (g > tiles) g = tiles;
+  if (g < 1) return 0;
+  a.stamps = nullptr;
+  constexpr auto kern = &g12::conv_pair_kernel<CK, CM, INMODE, X2, false, RES, NCA, false, false, 7>;
+  static bool attr_set[BE_MAX_DEV] = {};
+  if (!attr_set[be_cur_dev()]) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set[be_cur_dev()] = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(g), dim3(g12::NT), lds, s, a);
+  return BE_CHECK_LAUNCH();
+}
+
 // BE_PAIR_PP_STEM (default 1): the stem (8 -> 32 + projection) on the ping-pong kernel as well
 static int g_pair_pp_stem = [] {
   const char* e = getenv("BE_PAIR_PP_STEM");
@@ -1894,11 +1085,11 @@ int be_conv_pair(const void* x, const void* x2, const float* sa, const float* ta
     return launch_pair<32, 32, 1, true, false, 2, 2>(a, g, stream);
   }
   if (CM == 64 && Cin == 32 && inmode == 2 && !hx2 && !proj && resmode == 1)
-    return launch_pair<32, 64, 2, false, false, 1, 1>(a, g, stream);
+    return g_pair_g12 ? launch_pair12<32, 64, 2, false, 1, 1>(a, stream) : launch_pair<32, 64, 2, false, false, 1, 1>(a, g, stream);
   if (CM == 64 && Cin == 64 && inmode == 0 && !hx2 && !proj && resmode == 1)
-    return launch_pair<32, 64, 0, false, false, 1, 2>(a, g, stream);
+    return g_pair_g12 ? launch_pair12<32, 64, 0, false, 1, 2>(a, stream) : launch_pair<32, 64, 0, false, false, 1, 2>(a, g, stream);
   if (CM == 64 && Cin == 128 && inmode == 1 && hx2 && !proj && resmode == 2)
-    return launch_pair<32, 64, 1, true, false, 2, 4>(a, g, stream);
+    return g_pair_g12 ? launch_pair12<32, 64, 1, true, 2, 4>(a, stream) : launch_pair<32, 64, 1, true, false, 2, 4>(a, g, stream);
   return -23;
 }
 

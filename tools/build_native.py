@@ -69,7 +69,7 @@ def _key(src: Path, flags: list[str]) -> str:
     h = hashlib.sha1()
     h.update(" ".join(flags).encode())
     h.update(src.read_bytes())
-    for hdr in sorted(src.parent.glob("*.h")):
+    for hdr in sorted(list(src.parent.glob("*.h")) + list(src.parent.glob("*.inc"))):
         h.update(hdr.read_bytes())
     return h.hexdigest()[:16]
 
