@@ -68,8 +68,11 @@ class FlatParams:
         self.params = params
         device = torch.device(device) if device is not None else params[0].device
         n = sum(p.numel() for p in params)
+        # without a bucket layout the buffer keeps the plain 4-element padding: its size must not
+        # depend on the world size (checkpoints move between worlds, e.g. after an elastic shrink)
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4)) if bucket_mb is not None else 1 << 62
-        self.offsets, bks = bucket_bounds([p.numel() for p in params], cap, bucket_multiple)
+        self.offsets, bks = bucket_bounds([p.numel() for p in params], cap,
+                                          bucket_multiple if bucket_mb is not None else 4)
         self.buckets = bks if bucket_mb is not None else None
         off = bks[-1][1] if bks else 0
         self.numel = off
