@@ -56,12 +56,17 @@ class PackedConv3d:
             self.kpad = (27 * self.cin_pad + 63) // 64 * 64
             self.w_mt = F.pad(w, (0, self.kpad - 27 * self.cin_pad)).to(torch.bfloat16).contiguous()
             self.b_mt = (self.bias if self.bias is not None else torch.zeros(cout)).float().contiguous()
+            # z-tap stacked 2-D weights for be_conv3d_ztaps: W'[co][dz * cin_pad + c][ky][kx]
+            wz = F.pad(self.w, (0, 0, 0, 0, 0, 0, 0, self.cin_pad - cin)).permute(0, 2, 1, 3, 4)
+            self.ztap = PackedConv.from_weight(wz.reshape(cout, 3 * self.cin_pad, 3, 3), self.bias,
+                                               cin_pad=3 * self.cin_pad)
 
     def to(self, device) -> "PackedConv3d":
         for t in self.taps:
             t.to(device)
         if self.ks == 3:
             self.w_mt, self.b_mt = self.w_mt.to(device), self.b_mt.to(device)
+            self.ztap.to(device)
         self.w = self.w.to(device)
         if self.bias is not None:
             self.bias = self.bias.to(device)
@@ -91,7 +96,15 @@ def fused_conv3d(x: torch.Tensor, pc: PackedConv3d, post_relu: bool = False) -> 
     if pc.ks == 1:
         y = fused_conv2d(x.view(N * D, H, W, C), pc.taps[0], post_relu=post_relu)
         return y.view(N, D, H, W, pc.cout)
-    if os.environ.get("BE_CONV3D", "igemm") != "taps" and pc.cout % 4 == 0:
+    mode = os.environ.get("BE_CONV3D", "igemm")
+    taps_maxcin = int(os.environ.get("BE_CONV3D_TAPS_MAXCIN", "0"))  # A/B: narrow layers on the taps path
+    if mode == "ztaps" and pc.cout % 4 == 0 and pc.ztap.cin_pad == 3 * C and C % pc.ztap.ck == 0:
+        out = torch.empty(N, D, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
+        zt = pc.ztap
+        _native.call("be_conv3d_ztaps", _native.ptr(x), _native.ptr(zt.wp), _native.ptr(zt.bias), _native.ptr(out),
+                     N, D, H, W, C, pc.cout, zt.ck, zt.tco, int(post_relu), 4, _native.stream(x.device))
+        return out
+    if mode != "taps" and pc.cout % 4 == 0 and C > taps_maxcin:
         out = torch.empty(N, D, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
         cfg = 5 if pc.cout <= 32 else (6 if pc.cout <= 64 else 4)
         _native.call("be_conv3d_mt", _native.ptr(x), _native.ptr(pc.w_mt), _native.ptr(pc.b_mt), _native.ptr(out),

@@ -80,6 +80,9 @@ struct ConvArgs {
   const float* qscale;
   const float* qshift;
   int qshift_ns;
+  // INMODE 3 (3x3x3 conv as ONE 2-D launch over the N * zD slices): the K axis stacks the three
+  // depth taps, stacked channel dz * zC + c = channel c of slice z + dz - 1 (zero outside the volume)
+  int zD, zC;
 };
 
 // Block order of the one-block-per-tile kernel.  Tile-major (grid x = tile, y = cout block) sends
@@ -159,6 +162,11 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
         const int c = c0 + cg * 8;
         if (INMODE == 0) {
           r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + gy) * a.Ws + gx) * a.Cin + c);
+        } else if (INMODE == 3) {
+          const int dz = c / a.zC - 1, cz = c - (dz + 1) * a.zC;  // zC % CK == 0: one slice per chunk
+          const int zz = n % a.zD + dz;
+          if (zz >= 0 && zz < a.zD)
+            r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)(n + dz) * a.Hs + gy) * a.Ws + gx) * a.zC + cz);
         } else if (INMODE == 1) {
           r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * a.Cin + c);
         } else {
@@ -656,6 +664,16 @@ int dispatch_tco(int tco, int inmode, bool x2, int nw, const ConvArgs& a, hipStr
 
 }  // namespace
 
+template <int CK>
+int dispatch_ztaps(int tco, int nw, const ConvArgs& a, hipStream_t s) {
+  switch (tco) {
+    case 16: return dispatch_nw<3, CK, 16, 3, false>(nw, a, s);
+    case 32: return dispatch_nw<3, CK, 32, 3, false>(nw, a, s);
+    case 64: return dispatch_nw<3, CK, 64, 3, false>(nw, a, s);
+  }
+  return -2;
+}
+
 static int g_persist_blocks = 0;  // tuning override (0 = heuristic)
 
 extern "C" {
@@ -695,6 +713,25 @@ int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const flo
     if (ck == 64) return dispatch_tco<1, 64>(tco, inmode, x2p, nw, a, stream);
   }
   return -12;
+}
+
+// 3x3x3 / stride 1 / zero-pad 1 conv of x NDHWC bf16 [N][D][H][W][zC] as ONE launch of the 2-D
+// LDS-staged kernel over the N * D slices, K = 3 depth taps x zC stacked channels x 9 in-plane taps
+// (w: the 2-D packed layout of W'[co][dz * zC + c][ky][kx] = W[co][c][dz][ky][kx]); fp32 accumulation
+// over all 27 taps, one bf16 rounding, bias (+ ReLU) in the epilogue.  The halo of every slice tap
+// is staged in LDS once per output tile, so the narrow layers of a 3-D U-Net read each input voxel
+// ~3x from L2 instead of 27x (the implicit-GEMM gather of be_conv3d_mt).
+int be_conv3d_ztaps(const void* x, const void* w, const float* bias, void* out, int N, int D, int H, int W, int zC,
+                    int Cout, int ck, int tco, int relu, int nw, hipStream_t stream) {
+  if (zC % ck != 0 || Cout % 4 != 0 || (ck != 8 && ck != 32)) return -10;
+  ConvArgs a = {};
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = bias; a.out = out;
+  a.N = N * D; a.H = H; a.W = W; a.Hs = H; a.Ws = W; a.Cin = 3 * zC; a.Cout = Cout; a.cout_valid = Cout;
+  a.nchunk = 3 * zC / ck; a.KP = be_conv2d_packed_kp(3, ck);
+  a.prelu = relu ? 2 : 0;
+  a.persist_blocks = g_persist_blocks;
+  a.zD = D; a.zC = zC;
+  return ck == 8 ? dispatch_ztaps<8>(tco, nw, a, stream) : dispatch_ztaps<32>(tco, nw, a, stream);
 }
 
 }  // extern "C"

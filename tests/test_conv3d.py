@@ -183,3 +183,25 @@ def test_head_1x1x1_small_cout(gpu):
         y = mod(x.to(gpu).bfloat16().contiguous(memory_format=torch.channels_last_3d)).float().cpu()
     assert y.shape == ref.shape
     assert (y - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,D,H,W,Cin,Cout", [(1, 8, 40, 72, 32, 64), (2, 5, 33, 20, 16, 32), (1, 6, 20, 36, 16, 16),
+                                              (1, 4, 24, 40, 128, 64)])
+def test_conv3d_ztaps_single_rounding(gpu, N, D, H, W, Cin, Cout, monkeypatch):
+    """BE_CONV3D=ztaps: the 3x3x3 conv as ONE launch of the LDS-staged 2-D kernel with the depth taps
+    stacked on K, fp32 accumulation over all 27 taps, one bf16 rounding (same bound as the igemm)."""
+    monkeypatch.setenv("BE_CONV3D", "ztaps")
+    g = torch.Generator().manual_seed(N * 1000 + D * 10 + Cin)
+    w = torch.randn(Cout, Cin, 3, 3, 3, generator=g) / (27 * Cin) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    pc = PackedConv3d(w, b).to(gpu)
+    x = torch.randn(N, D, H, W, pc.cin_pad, generator=g)
+    x[..., Cin:] = 0
+    xb = x.to(gpu).bfloat16().contiguous()
+    for relu in (False, True):
+        y = fused_conv3d(xb, pc, post_relu=relu).float().cpu()
+        ref = F.conv3d(x.bfloat16().float()[..., :Cin].permute(0, 4, 1, 2, 3), w.bfloat16().float(), b, padding=1)
+        ref = (torch.relu(ref) if relu else ref).permute(0, 2, 3, 4, 1)
+        err = (y - ref).abs().max().item()
+        assert err <= 2 ** -7 * ref.abs().max().item() + 1e-3, err

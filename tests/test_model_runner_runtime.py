@@ -112,8 +112,11 @@ def test_model_runner_runtime_batching_health_and_requirements(tmp_path, monkeyp
         # ---- additional_requirements: isolated test task with a wheelhouse-installed extra package
         plain = await app.test(model_id="needs-dep")  # the package's own import fails without it
         assert plain["status"] == "failed"
-        with pytest.raises(Exception, match="bioengine-testdep"):  # no wheelhouse: unsatisfiable
-            await app.test(model_id="needs-dep", additional_requirements=["bioengine-testdep==0.1.0"], skip_cache=True)
+        # no wheelhouse: unsatisfiable.  As upstream (entry_deployment.py:1651-1701) a test run that
+        # raises yields a failed fallback report carrying the traceback, not an exception
+        bad = await app.test(model_id="needs-dep", additional_requirements=["bioengine-testdep==0.1.0"], skip_cache=True)
+        assert bad["status"] == "failed" and "bioengine-testdep" in str(bad["details"]), bad
+        assert "tested_at" in bad and any(r[0] == "bioengine" for r in bad["env"])
         monkeypatch.setenv("BIOENGINE_WHEELHOUSE", str(wheelhouse))
         rep = await app.test(model_id="needs-dep", additional_requirements=["bioengine-testdep==0.1.0"],
                              skip_cache=True)
