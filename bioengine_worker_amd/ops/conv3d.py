@@ -1,10 +1,13 @@
 """3-D convolution (1x1x1 / 3x3x3, stride 1, "same" zero padding) on the framework's MFMA kernels.
 
-3x3x3 convs run as ONE implicit-GEMM launch over the whole batch (``be_conv3d_mt`` in
-``csrc/kernels/gemm_mt.hip``): M = N*D*H*W output voxels, N = Cout, K = 27 taps x Cin (tap-major),
-each DMA lane fetching its voxel's tap-shifted 8-channel chunk (the zero page at the volume faces),
-fp32 accumulation across all 27 taps and one bf16 rounding of the output, bias + ReLU in the
-epilogue.  The older depth-tap decomposition below (``BE_CONV3D=taps``) is kept as the A/B path.
+3x3x3 convs run as ONE launch of the LDS-staged 2-D conv kernel over the N*D slices with the three
+depth taps stacked on K (``be_conv3d_ztaps`` in ``csrc/kernels/conv2d_nhwc.hip``, INMODE 3: stacked
+channel dz*Cin + c is channel c of slice z+dz-1, zero outside the volume): fp32 accumulation across all
+27 taps, one bf16 rounding, bias + ReLU in the epilogue, and each input voxel staged ~3x per output
+tile instead of gathered 27x from L2.  ``BE_CONV3D=igemm`` selects the one-launch implicit GEMM
+(``be_conv3d_mt`` in ``gemm_mt.hip``, the round-5 default, also the fallback when the stacked layout
+does not apply, e.g. a 1-channel input); the older three-launch depth-tap decomposition below
+(``BE_CONV3D=taps``) is kept as an A/B path.
 
 Depth-tap decomposition (A/B path):
 
@@ -96,7 +99,11 @@ def fused_conv3d(x: torch.Tensor, pc: PackedConv3d, post_relu: bool = False) -> 
     if pc.ks == 1:
         y = fused_conv2d(x.view(N * D, H, W, C), pc.taps[0], post_relu=post_relu)
         return y.view(N, D, H, W, pc.cout)
-    mode = os.environ.get("BE_CONV3D", "igemm")
+    # ztaps (default): one launch of the LDS-staged 2-D kernel with the depth taps stacked on K --
+    # 492 vs 351 M voxel/s for the one-launch implicit GEMM on the 3-D EM line (profiles/r06/em3d/
+    # conv3d_path_ab_s8.txt): the narrow 3-D U-Net layers were bound by the igemm's 27x per-tap L2
+    # gather.  igemm / taps: the previous default / the three-launch decomposition (A/B)
+    mode = os.environ.get("BE_CONV3D", "ztaps")
     taps_maxcin = int(os.environ.get("BE_CONV3D_TAPS_MAXCIN", "0"))  # A/B: narrow layers on the taps path
     if mode == "ztaps" and pc.cout % 4 == 0 and pc.ztap.cin_pad == 3 * C and C % pc.ztap.ck == 0:
         out = torch.empty(N, D, H, W, pc.cout, device=x.device, dtype=torch.bfloat16)
