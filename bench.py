@@ -365,13 +365,14 @@ def bench_em_volume(args, world, rank, dev) -> dict:
         # the memory-mapped slab is read-only; torch only reads it (straight into the H2D copy)
         warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
         warm = torch.from_numpy(src.read(0, 4)).to(dev)  # graph pass, kernels, allocator
-        analyze_volume(warm, predict, 512, 64, args.em_tile_batch, split_touching=True, norm_range=(90.0, 210.0))
+        tile, ov = getattr(args, "em_tile", 512), getattr(args, "em_overlap", 64)
+        analyze_volume(warm, predict, tile, ov, args.em_tile_batch, split_touching=True, norm_range=(90.0, 210.0))
         del warm
         _barrier(world)
         t0 = time.perf_counter()
         slab = torch.from_numpy(src.read(0, Z)).to(dev)
         t_read = time.perf_counter()
-        res = analyze_volume(slab, predict, 512, 64, args.em_tile_batch, group=None, z_offset=z0, timings=True,
+        res = analyze_volume(slab, predict, tile, ov, args.em_tile_batch, group=None, z_offset=z0, timings=True,
                              split_touching=True)
         tg = time.perf_counter()
         full = gather_to_rank0(res["labels_slab_t"])
@@ -384,8 +385,8 @@ def bench_em_volume(args, world, rank, dev) -> dict:
         timings["read_h2d"] = round(t_read - t0, 4)
         timings["gather_rank0"] = round(t_gather, 4)
         out = {"em_volume_voxels_per_sec": round(vox / dt, 1),
-               "em_volume_config": {"volume": [Z * world, YX, YX], "slab_per_gpu": [Z, YX, YX], "tile": 512,
-                                    "overlap": 64, "tiles_per_call": args.em_tile_batch,
+               "em_volume_config": {"volume": [Z * world, YX, YX], "slab_per_gpu": [Z, YX, YX], "tile": tile,
+                                    "overlap": ov, "tiles_per_call": args.em_tile_batch,
                                     "model": "BioImage.IO 2-D U-Net 32-64-128-256 (random init, graph pass)",
                                     "source": "memory-mapped .npy slab per rank", "split_touching": True,
                                     "gather": "rank0 (dist.gather of int32 labels)", "seconds": round(dt, 3),
