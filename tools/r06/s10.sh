@@ -11,3 +11,5 @@ for l in open("gpurun_out/r06/s10/sweep.jsonl"):
         d = json.loads(l); c = d["em_volume_config"]; t = c["stage_timings_s_rank0"]
         print(c["tile"], c["overlap"], c["tiles_per_call"], round(d["em_volume_voxels_per_sec"] / 1e6, 1), "Mvox/s", t["inference"], t["label"], t["stats"], d["max_memory_allocated_gb"])
 PY
+timeout -k 10 300 python -u tools/gemm_infer_ab.py > gpurun_out/r06/s10/gemm_infer_ab.jsonl 2>&1 || { tail -20 gpurun_out/r06/s10/gemm_infer_ab.jsonl; exit 1; }
+grep '"impl"' gpurun_out/r06/s10/gemm_infer_ab.jsonl

@@ -67,8 +67,24 @@ async def main_async(a) -> list[dict]:
                 return await handle.infer.remote(**kw)
 
         app = _H()
+    timeline = getattr(a, "timeline", None)
+    gc_events: list = []
+    if timeline:  # GC pauses of this process (hub + worker + router + clients share its event loop)
+        import gc
+
+        _gc_t0 = {}
+
+        def _gc_cb(phase, info):
+            if phase == "start":
+                _gc_t0["t"] = time.perf_counter()
+            else:
+                gc_events.append((_gc_t0.get("t", 0.0), time.perf_counter() - _gc_t0.get("t", 0.0), info["generation"],
+                                  info["collected"]))
+
+        gc.callbacks.append(_gc_cb)
     for conc in a.concurrency:
         lat: list[float] = []
+        starts: list[float] = []
         stop = time.perf_counter() + a.seconds
 
         async def client(cid):
@@ -77,6 +93,7 @@ async def main_async(a) -> list[dict]:
                 t = time.perf_counter()
                 out = await app.infer(input_arrays=[imgs[k % 16]], model=a.model)
                 lat.append(time.perf_counter() - t)
+                starts.append(t)
                 assert out[0]["output"].shape == (a.size, a.size)
                 k += conc
 
@@ -99,6 +116,14 @@ async def main_async(a) -> list[dict]:
             pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(120)
             Path(a.profile).write_text(buf.getvalue())
         ms = np.array(lat) * 1e3
+        if timeline:
+            thr = float(np.percentile(ms, 99))
+            slow = sorted((round(st - t0, 4), round(l * 1e3, 2)) for st, l in zip(starts, lat) if l * 1e3 >= thr)
+            gcs = [(round(t - t0, 4), round(d * 1e3, 2), g, c) for t, d, g, c in gc_events if t >= t0 and d > 0.002]
+            with open(timeline, "a") as fh:
+                fh.write(json.dumps({"concurrency": conc, "phase_s": round(dt, 3), "p99_ms": round(thr, 2),
+                                     "slow_start_s_and_ms": slow[:200], "gc_pauses_over_2ms_s_ms_gen_collected": gcs})
+                         + "\n")
         r = {"concurrency": conc, "requests": len(lat), "imgs_per_s": round(len(lat) / dt, 1),
              "p50_ms": round(float(np.percentile(ms, 50)), 2), "p95_ms": round(float(np.percentile(ms, 95)), 2),
              "p99_ms": round(float(np.percentile(ms, 99)), 2), "image": [a.size, a.size, 2], "gpus": a.gpus,
@@ -127,6 +152,9 @@ def main():
     ap.add_argument("--layer", default="hub", choices=["hub", "handle"],
                     help="hub: client -> hub RPC -> app service -> router (default); handle: router directly")
     ap.add_argument("--model", default="cyto3", help="built-in model served (headline: cyto3 CPnet)")
+    ap.add_argument("--timeline", default=None, metavar="PATH",
+                    help="append, per concurrency level, the start times of the requests at or above p99 and the "
+                         "GC pauses (> 2 ms) of the benchmark process")
     ap.add_argument("--profile", default=None, metavar="PATH",
                     help="cProfile the worker-side event loop during the highest-concurrency phase")
     a = ap.parse_args()
