@@ -22,6 +22,7 @@ import json
 import os
 import shutil
 import socket
+import asyncio
 import subprocess
 import time
 from pathlib import Path
@@ -182,9 +183,10 @@ class NodeCluster:
     def check_connection(self) -> bool:
         return self.is_ready
 
-    def node_state(self) -> dict:
+    def node_state(self, gpus: list[dict] | None = None) -> dict:
         r = self.resources
-        gpus = gpu_telemetry(r.gpu_ids) if r.gpu_ids else []
+        if gpus is None:
+            gpus = gpu_telemetry(r.gpu_ids) if r.gpu_ids else []
         tot_gm = sum(g["total_memory"] or 0 for g in gpus) if gpus else (0 if not r.gpu_ids else "NA")
         used_gm = sum(g["used_memory"] or 0 for g in gpus) if gpus else (0 if not r.gpu_ids else "NA")
         accel = "NA"
@@ -196,8 +198,8 @@ class NodeCluster:
                 "total_object_store_memory": 0, "used_object_store_memory": 0, "accelerator_type": accel,
                 "slurm_job_id": None, "gpus": gpus, "hostname": self.hostname}
 
-    def monitor(self) -> dict:
-        nodes = {f"head-{self.hostname}": self.node_state()}
+    def monitor(self, gpus: list[dict] | None = None) -> dict:
+        nodes = {f"head-{self.hostname}": self.node_state(gpus)}
         nodes.update(self.remote_nodes)
         if self.controller is not None:
             nodes.update({nid: n.status() for nid, n in self.controller.remote_nodes.items()})
@@ -224,6 +226,13 @@ class NodeCluster:
 
     async def monitor_cluster(self):
         await self.discover_nodes()
-        self.monitor()
+        # The SMI query is a ~100-150 ms subprocess.  Run on the event loop it stalled the hub, router
+        # and app bridges that share this loop once per monitoring interval: every request in flight
+        # at that moment waited it out (the c = 64 router p99 of ~150 ms against a ~30 ms p50,
+        # profiles/r06/serve/timeline_s11.txt).  The query runs in a worker thread; the snapshot is
+        # assembled back on the loop.
+        r = self.resources
+        gpus = await asyncio.to_thread(gpu_telemetry, r.gpu_ids) if r.gpu_ids else []
+        self.monitor(gpus)
         if self.slurm is not None:
             await self.slurm.check_scaling(self.status)

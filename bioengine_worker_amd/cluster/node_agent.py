@@ -71,8 +71,9 @@ class NodeAgent:
         return self._head
 
     # ------------------------------------------------------------------ service methods
-    def get_resources(self) -> dict:
-        gpus = gpu_telemetry(self.gpu_ids) if self.gpu_ids else []
+    async def get_resources(self) -> dict:
+        # the SMI subprocess off the event loop (it would stall this agent's replica RPCs)
+        gpus = await asyncio.to_thread(gpu_telemetry, self.gpu_ids) if self.gpu_ids else []
         return {"node_id": self.node_id, "hostname": socket.gethostname(), "num_cpus": self.num_cpus,
                 "gpu_ids": self.gpu_ids, "slurm_job_id": self.slurm_job_id,
                 "gpu_memory": sum((g.get("total_memory") or 0) for g in gpus),
