@@ -335,7 +335,7 @@ def bench_em_volume(args, world, rank, dev) -> dict:
     2048 x 2048 synthetic EM volume (256 slices per GPU = the 2048^3 volume at N=8), written as its own
     ``.npy`` and read back memory-mapped like the app's gang job reads a volume source
     (``em.volume.VolumeSource``).  Timed, max over ranks: slab read + H2D, percentiles (all-reduced),
-    slice-wise 512/64 tiled 2-D U-Net inference (graph pass onto the HIP convs) with blending, the
+    slice-wise 768/64 tiled 2-D U-Net inference (graph pass onto the HIP convs) with blending, the
     sharded touching-object split (remove small, closing, EDT, peaks, marker watershed; halo exchange
     over RCCL at N > 1), global instance statistics, and ``dist.gather`` of the int32 label volume
     onto rank 0 (reference: ``apps/fibsem-mito-analysis/analysis_deployment.py:108-176``, which is 2-D
@@ -364,8 +364,14 @@ def bench_em_volume(args, world, rank, dev) -> dict:
         src = VolumeSource(str(npy))
         # the memory-mapped slab is read-only; torch only reads it (straight into the H2D copy)
         warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
-        warm = torch.from_numpy(src.read(0, 4)).to(dev)  # graph pass, kernels, allocator
-        tile, ov = getattr(args, "em_tile", 512), getattr(args, "em_overlap", 64)
+        # 768^2 tiles (stride 704: 3 x 3 per 2048^2 slice, 5.3 M px of U-Net work) beat 512^2 (5 x 5,
+        # 6.6 M px): 565 vs 520 M voxel/s on a 64 x 2048^2 slab, profiles/r06/em2d/sweep_s10.txt
+        tile, ov = getattr(args, "em_tile", 768), getattr(args, "em_overlap", 64)
+        # One untimed pass over the whole slab, like a training bench's warm-up steps: the first pass
+        # at full size pays ~0.5 s of one-time costs (allocator growth for the multi-GB stage
+        # buffers, the first large radix sort / nonzero) that a 4-slice warm-up does not cover
+        # (sweep_s10.txt: stats 0.36 -> 0.02 s, peaks 0.10 -> 0.014 s, normalize 0.08 -> 0.002 s).
+        warm = torch.from_numpy(src.read(0, Z)).to(dev)
         analyze_volume(warm, predict, tile, ov, args.em_tile_batch, split_touching=True, norm_range=(90.0, 210.0))
         del warm
         _barrier(world)
@@ -434,7 +440,7 @@ def bench_em_volume3d(args, world, rank, dev) -> dict:
         # z overlap costs 8 of 64 slices instead of 8 of 32)
         kw = dict(tile=getattr(args, "em3d_tile", 256), overlap=16, batch=getattr(args, "em3d_batch", 4),
                   tile_z=getattr(args, "em3d_tile_z", 64), overlap_z=8, split_touching=True)
-        warm = torch.from_numpy(src.read(0, min(Z, 40))).to(dev)[:, :256, :256].contiguous()
+        warm = torch.from_numpy(src.read(0, Z)).to(dev)  # one untimed full-slab pass (see the 2-D line)
         analyze_volume(warm, None, predict3d=predict3d, norm_range=(90.0, 210.0), **kw)
         del warm
         _barrier(world)
@@ -643,7 +649,7 @@ def main():
     ap.add_argument("--cpsam-batch", type=int, default=8, help="256x256 crops per step per GPU (Cellpose-SAM)")
     ap.add_argument("--em-z", type=int, default=256, help="z-slices per GPU of the EM volume line (2048^3 at N=8)")
     ap.add_argument("--em-yx", type=int, default=2048)
-    ap.add_argument("--em-tile-batch", type=int, default=32, help="512^2 tiles per U-Net call (EM volume line)")
+    ap.add_argument("--em-tile-batch", type=int, default=16, help="768^2 tiles per U-Net call (EM volume line)")
     ap.add_argument("--no-em", action="store_true", help="skip the EM volume line")
     ap.add_argument("--em3d-z", type=int, default=256, help="z-slices per GPU of the 3-D U-Net EM line (2048^3 at N=8)")
     ap.add_argument("--em3d-yx", type=int, default=2048)
