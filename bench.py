@@ -227,7 +227,9 @@ def bench_cell_like(runner, imgs, p, steps=3):
 def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
     """Requests through the full serving stack (tools/serve_bench.py): hub RPC -> app service ->
     router -> GPU-pinned process replica (shared-memory ring) -> @serve.batch continuous batching ->
-    HIP pipeline -> back; one 512x512 image per request, H2D/D2H inside every request."""
+    HIP pipeline -> back; one 512x512 image per request, H2D/D2H inside every request.  Each
+    concurrency level runs a 0.5 s ramp (all clients fire at once) before its measured window; the
+    ramp's requests are reported as served_ramp_requests_c* and folded into served_p99_ms_c*_incl_ramp."""
     import argparse as _ap
     import asyncio
 
@@ -244,6 +246,8 @@ def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
         out[f"served_p50_ms_c{c}"] = r["p50_ms"]
         out[f"served_p95_ms_c{c}"] = r["p95_ms"]
         out[f"served_p99_ms_c{c}"] = r["p99_ms"]
+        out[f"served_p99_ms_c{c}_incl_ramp"] = r.get("p99_ms_incl_ramp")
+        out[f"served_ramp_requests_c{c}"] = r.get("ramp_requests")
     return out
 
 

@@ -237,6 +237,13 @@ class CPSAMEngine:
             def lin_gelu(x, w, b):
                 return bias_gelu_(F.linear(x, w), b)
             return lin, lin_gelu
+        if self.GEMM == "ltgelu":  # hipBLASLt GELU_BIAS epilogue (tanh-approximated GELU); A/B
+            def lin(x, w, b=None):
+                return F.linear(x, w, b)
+
+            def lin_gelu(x, w, b):
+                return torch._addmm_activation(b, x, w.t(), use_gelu=True)
+            return lin, lin_gelu
         from ..ops import gemm_mt
 
         return gemm_mt.linear, gemm_mt.linear_gelu_only
