@@ -288,35 +288,42 @@ class CPSAMEngine:
         o = o.view(B, g, g, self.nout, ps, ps).permute(0, 3, 1, 4, 2, 5).reshape(B, self.nout, g * ps, g * ps)
         return o
 
-    #: tile-count buckets of :meth:`graphed`: a batch is zero-padded up to the next one, so a server
-    #: seeing images of many sizes keeps at most len(GRAPH_BUCKETS) graphs (each holds a private
-    #: memory pool with the whole forward's intermediates) instead of one per exact tile count
-    GRAPH_BUCKETS = (1, 2, 4, 8, 16, 32, 64)
-    #: capture attempts per bucket before that bucket stays eager for the process
+    #: graphs kept by :meth:`graphed`, one per exact tile count, least recently used evicted: each
+    #: holds a private memory pool with the whole forward's intermediates, so a server seeing images
+    #: of many sizes must not keep one per size forever.  Exact counts, not padded buckets: padding the
+    #: 9 tiles of one 512^2 image to a 16-tile bucket cost 40 % of the batch-1 latency (15.3 vs 11.0 ms,
+    #: profiles/r06/bench_1gpu_s12.json), and a 72-tile batch above a 64 bucket ran eagerly.
+    GRAPH_MAX = int(os.environ.get("BE_CPSAM_GRAPH_MAX", "8"))
+    #: largest tile count replayed from a graph (larger batches run eagerly)
+    GRAPH_MAX_TILES = 256
+    #: capture attempts per tile count before that count stays eager for the process
     GRAPH_MAX_TRIES = 3
     #: BE_CPSAM_GRAPH=0 turns graph replay off (every call runs the eager forward)
     GRAPH = os.environ.get("BE_CPSAM_GRAPH", "1") != "0"
 
     @torch.no_grad()
     def graphed(self, x: torch.Tensor) -> torch.Tensor:
-        """:meth:`__call__` replayed from a HIP graph per tile-count bucket (static input buffer,
-        zero-padded to the bucket; the output is a fresh copy).  Falls back to the eager forward
-        off-GPU, above the largest bucket, with BE_CPSAM_GRAPH=0, and when a capture fails (counted
-        per bucket: after GRAPH_MAX_TRIES failures the bucket stays eager)."""
+        """:meth:`__call__` replayed from a HIP graph per tile count (static input buffer; the output
+        is a fresh copy), at most GRAPH_MAX graphs alive (LRU).  Falls back to the eager forward
+        off-GPU, above GRAPH_MAX_TILES, with BE_CPSAM_GRAPH=0, and when a capture fails (counted per
+        tile count: after GRAPH_MAX_TRIES failures that count stays eager)."""
+        import collections
+
         B = x.shape[0]
-        if not (x.is_cuda and self.device.type == "cuda") or not self.GRAPH or B > self.GRAPH_BUCKETS[-1]:
+        if (not (x.is_cuda and self.device.type == "cuda") or not self.GRAPH or B > self.GRAPH_MAX_TILES
+                or self.GRAPH_MAX <= 0):
             return self(x)
-        bucket = next(b for b in self.GRAPH_BUCKETS if b >= B)
-        graphs = self.__dict__.setdefault("_graphs", {})
-        key = (bucket, tuple(x.shape[1:]))
+        graphs = self.__dict__.setdefault("_graphs", collections.OrderedDict())
+        fails = self.__dict__.setdefault("_graph_fails", {})
+        key = tuple(x.shape)
+        if fails.get(key, 0) >= self.GRAPH_MAX_TRIES:
+            return self(x)
         ent = graphs.get(key)
-        if isinstance(ent, int):  # earlier capture attempts failed
-            if ent >= self.GRAPH_MAX_TRIES:
-                return self(x)
-            ent = None
         if ent is None:
-            xs = torch.zeros((bucket,) + tuple(x.shape[1:]), device=self.device, dtype=torch.bfloat16)
-            xs[:B].copy_(x)
+            while len(graphs) >= self.GRAPH_MAX:
+                graphs.popitem(last=False)  # least recently used: its pool returns to the allocator
+            xs = torch.empty(x.shape, device=self.device, dtype=torch.bfloat16)
+            xs.copy_(x)
             side = torch.cuda.Stream(self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(side):
@@ -327,13 +334,12 @@ class CPSAMEngine:
                 with torch.cuda.graph(gr, capture_error_mode="thread_local"):
                     out = self(xs)
             except Exception:  # noqa: BLE001 -- counted; the request itself runs eagerly
-                graphs[key] = int(graphs.get(key) or 0) + 1
+                fails[key] = fails.get(key, 0) + 1
                 return self(x)
             ent = graphs[key] = (gr, xs, out)
+        graphs.move_to_end(key)
         gr, xs, out = ent
-        xs[:B].copy_(x)
-        if B < bucket:
-            xs[B:].zero_()
+        xs.copy_(x)
         gr.replay()
-        return out[:B].clone()
+        return out.clone()
 

@@ -124,3 +124,10 @@ def test_cpsam_engine_vit_l_matches_fp32(gpu, gemm, monkeypatch):
     assert torch.equal(g1, out)
     rel2 = ((g2 - eng(x * 0.5)).norm() / g2.norm()).item()
     assert rel2 == 0.0, rel2
+    # one graph per exact tile count (no padding), least recently used evicted past GRAPH_MAX
+    monkeypatch.setattr(CPSAMEngine, "GRAPH_MAX", 2)
+    g3 = eng.graphed(x[:1])
+    assert torch.equal(g3, eng(x[:1]))
+    x3 = torch.randn(3, 3, 256, 256, device=gpu)
+    assert torch.equal(eng.graphed(x3), eng(x3))
+    assert list(eng._graphs) == [(1, 3, 256, 256), (3, 3, 256, 256)]  # the 2-tile graph was the LRU
