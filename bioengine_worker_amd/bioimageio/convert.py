@@ -22,7 +22,14 @@
    (:class:`HipConvStride2x2`); in 3-D, ``ConvTranspose3d(k=2, s=2)`` becomes a 1x1x1 MFMA conv to
    8*Cout + the ``vol3d.hip`` depth-to-space scatter (:class:`HipConvTranspose3x2`) and
    ``MaxPool3d(2)`` the ``vol3d.hip`` NDHWC pooling kernel (:class:`HipMaxPool3d`), so a 3-D U-Net
-   runs no library convolution.
+   runs no library convolution;
+7. 2-D models run their forward under a deferred-fusion scope (:class:`DeferredFusion`): a
+   ``torch.cat`` along channels of two channels-last bf16 tensors and a ``MaxPool2d(2)``
+   (:class:`HipMaxPool2d`) return an unfilled placeholder, and the :class:`HipConv2d` that consumes
+   it reads the sources directly (``be_conv2d_concat`` / the 2x2 max-pool halo loader), so the U-Net
+   decoder's skip concatenation and the encoder's pooling never make a copy.  Any other consumer of
+   a placeholder sees it filled first (the scope intercepts every torch call while it is pending),
+   so the rewrite cannot change a model's results.  ``BE_UNET_LAZY=0`` turns it off.
 
 TorchScript-only weights go through :mod:`.ts_convert` (frozen graph rewrite).  Convolutions that
 do not match (3x3 strided, dilated, grouped, 5x5, ...) stay on MIOpen.
@@ -33,7 +40,13 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.conv import PackedConv, fused_conv2d
+import os
+import threading
+import weakref
+
+from torch.overrides import TorchFunctionMode
+
+from ..ops.conv import PackedConv, fused_conv2d, fused_conv2d_concat
 from ..ops.conv3d import PackedConv3d, depth2space3d, fused_conv3d, maxpool3d_ndhwc
 
 
@@ -85,11 +98,27 @@ class HipConv2d(nn.Module):
         self._dev = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        # first, before ANY tensor access (which would make the scope fill a placeholder): is x a
+        # deferred cat / max-pool this conv can read from its sources?
+        scope = getattr(_tls, "scope", None)
+        if scope is not None and scope.pending and not self.nchw_out:
+            ent = scope.take(x, self._fusible)
+            if ent is not None:
+                src = ent[2]
+                if src.is_cuda and self._dev != src.device:
+                    self.pc.to(src.device)
+                    self._dev = src.device
+                if ent[1] == "cat":
+                    a, b = (t.permute(0, 2, 3, 1) for t in ent[2:])
+                    y = fused_conv2d_concat(a, b, self.pc, post_relu=self.post_relu)
+                else:
+                    y = fused_conv2d(src.permute(0, 2, 3, 1), self.pc, inmode="pool2", post_relu=self.post_relu)
+                return y.permute(0, 3, 1, 2)
         if not x.is_cuda:  # CPU: reference math (bf16-rounded like the kernel)
             y = F.conv2d(x.float(), self.pc.w.to(x.device), None if self.pc.bias is None else self.pc.bias.to(x.device),
                          padding=self.pc.ks // 2)
             y = torch.relu(y) if self.post_relu else y
-            return y.to(x.dtype)
+            return y.to(x.dtype).contiguous(memory_format=torch.channels_last)  # the GPU path's layout
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
@@ -103,8 +132,196 @@ class HipConv2d(nn.Module):
         y = fused_conv2d(xh, self.pc, post_relu=self.post_relu)  # [N, H, W, Cout] bf16
         return y.permute(0, 3, 1, 2)  # channels-last view, no copy
 
+    def _fusible(self, ent: tuple) -> bool:
+        if ent[1] == "cat":
+            return self.pc.ks == 3 and self.pc.cin_pad == ent[2].shape[1] + ent[3].shape[1]
+        return self.pc.cin_pad == ent[2].shape[1]  # pool: any kernel size, the loader pools 2x2
+
     def extra_repr(self) -> str:
         return f"{self.cin}, {self.cout}, k={self.pc.ks}, post_relu={self.post_relu}"
+
+
+# ---- deferred cat / max-pool fusion (item 7 of the module docstring) ------------------------------
+_tls = threading.local()
+#: BE_UNET_LAZY=0: no deferred fusion (A/B)
+LAZY = os.environ.get("BE_UNET_LAZY", "1") != "0"
+
+
+def _nhwc_dense(t: torch.Tensor) -> bool:
+    return t.dim() == 4 and t.permute(0, 2, 3, 1).is_contiguous()
+
+
+class DeferredFusion(TorchFunctionMode):
+    """Scope of one model forward.  ``torch.cat([a, b], dim=1)`` of two channels-last bf16 tensors
+    (channels % 8 == 0) and :class:`HipMaxPool2d` return an unfilled channels-last placeholder and
+    record its sources; a :class:`HipConv2d` that receives a placeholder reads the sources itself.
+    The placeholder stays pending (held weakly): any other torch call that touches it fills it
+    first, an in-place write to one of its sources fills it before the write, and leaving the scope
+    fills every placeholder still alive (returned, or kept by the model).  The mode sees every torch
+    function call made while it is active, so results are those of the eager model; a placeholder
+    that only a HIP conv ever read is freed unfilled -- the copy that is saved.  Nothing is deferred
+    when a source requires grad."""
+
+    #: tests only: defer on CPU tensors too (the consumers then run their reference math)
+    ALLOW_CPU = False
+
+    def __init__(self):
+        super().__init__()
+        self.pending: dict[int, tuple] = {}  # id(placeholder) -> (weakref(placeholder), kind, *sources)
+        self.deferred = 0
+        self.filled = 0
+
+    def _ok_src(self, t: torch.Tensor) -> bool:
+        return ((t.is_cuda or self.ALLOW_CPU) and t.dtype == torch.bfloat16 and not t.requires_grad
+                and _nhwc_dense(t) and not self._is_pending(t))
+
+    def _is_pending(self, t) -> bool:
+        ent = self.pending.get(id(t))
+        return ent is not None and ent[0]() is t
+
+    def _add(self, ph: torch.Tensor, kind: str, *srcs) -> torch.Tensor:
+        self.pending[id(ph)] = (weakref.ref(ph), kind, *srcs)
+        self.deferred += 1
+        return ph
+
+    def defer_pool(self, x: torch.Tensor) -> torch.Tensor | None:
+        if not (x.dim() == 4 and self._ok_src(x) and x.shape[2] >= 2 and x.shape[3] >= 2):
+            return None
+        N, C, H, W = x.shape
+        ph = torch.empty((N, C, H // 2, W // 2), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        return self._add(ph, "pool", x)
+
+    def _defer_cat(self, args, kwargs) -> torch.Tensor | None:
+        if "out" in kwargs or not args:
+            return None
+        ts = args[0]
+        dim = args[1] if len(args) > 1 else kwargs.get("dim", 0)
+        if not isinstance(ts, (list, tuple)) or len(ts) != 2 or dim not in (1, -3):
+            return None
+        a, b = ts
+        if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and a.dim() == 4 and b.dim() == 4):
+            return None
+        if not (self._ok_src(a) and self._ok_src(b) and a.device == b.device and a.shape[0] == b.shape[0]
+                and a.shape[2:] == b.shape[2:] and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0):
+            return None
+        N, _, H, W = a.shape
+        ph = torch.empty((N, a.shape[1] + b.shape[1], H, W), dtype=a.dtype, device=a.device,
+                         memory_format=torch.channels_last)
+        return self._add(ph, "cat", a, b)
+
+    def take(self, x: torch.Tensor, fusible) -> tuple | None:
+        """(placeholder, kind, *sources) if ``x`` is a pending placeholder and ``fusible`` accepts it.
+        The entry stays pending: the placeholder is filled if anything else touches it later."""
+        ent = self.pending.get(id(x))
+        if ent is None or ent[0]() is not x:
+            return None
+        ent = (x,) + ent[1:]
+        return ent if fusible(ent) else None
+
+    def _fill_key(self, key: int) -> None:
+        wr, kind, *srcs = self.pending.pop(key)
+        ph = wr()
+        if ph is None:
+            return
+        if kind == "cat":
+            torch.cat(srcs, dim=1, out=ph)
+        else:
+            ph.copy_(F.max_pool2d(srcs[0], 2))
+        self.filled += 1
+
+    def _fill_in(self, obj) -> None:
+        if isinstance(obj, torch.Tensor):
+            if self._is_pending(obj):
+                self._fill_key(id(obj))
+        elif isinstance(obj, (list, tuple)):
+            for o in obj:
+                self._fill_in(o)
+        elif isinstance(obj, dict):
+            for o in obj.values():
+                self._fill_in(o)
+
+    @staticmethod
+    def _written(func, args, kwargs) -> list:
+        name = getattr(func, "__name__", "")
+        out = []
+        if args and isinstance(args[0], torch.Tensor) and (
+                (name.endswith("_") and not name.endswith("__")) or name == "__setitem__"
+                or (name.startswith("__i") and name.endswith("__"))):
+            out.append(args[0])
+        o = kwargs.get("out")
+        if isinstance(o, torch.Tensor):
+            out.append(o)
+        elif isinstance(o, (list, tuple)):
+            out.extend(t for t in o if isinstance(t, torch.Tensor))
+        return out
+
+    def _fill_readers_of(self, written: list) -> None:
+        """Fill every pending placeholder with a source in the storage ``written`` is about to change."""
+        ptrs = {t.untyped_storage().data_ptr() for t in written}
+        for key, ent in list(self.pending.items()):
+            if any(s.untyped_storage().data_ptr() in ptrs for s in ent[2:]):
+                self._fill_key(key)
+
+    def flush(self) -> None:
+        for key in list(self.pending):
+            if key in self.pending:
+                self._fill_key(key)
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is torch.cat:
+            ph = self._defer_cat(args, kwargs)
+            if ph is not None:
+                return ph
+        if self.pending:
+            self._fill_in(args)
+            self._fill_in(kwargs)
+            written = self._written(func, args, kwargs)
+            if written and self.pending:
+                self._fill_readers_of(written)
+        return func(*args, **kwargs)
+
+
+class HipMaxPool2d(nn.Module):
+    """``MaxPool2d(2)``: inside a :class:`DeferredFusion` scope a placeholder the next HIP conv pools
+    in its halo loader (inmode ``pool2``); elsewhere ``F.max_pool2d``."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        scope = getattr(_tls, "scope", None)
+        if scope is not None:
+            ph = scope.defer_pool(x)
+            if ph is not None:
+                return ph
+        return F.max_pool2d(x, 2)
+
+
+def _mp2_ok(m) -> bool:
+    two = lambda v: v == 2 or v == (2, 2)  # noqa: E731
+    return (type(m) is nn.MaxPool2d and two(m.kernel_size) and two(m.stride if m.stride is not None else 2)
+            and m.padding in (0, (0, 0)) and m.dilation in (1, (1, 1)) and not m.ceil_mode
+            and not m.return_indices)
+
+
+def _install_deferred_fusion(model: nn.Module) -> None:
+    orig = model.forward
+
+    def forward(*args, **kwargs):
+        x = args[0] if args else None
+        if not (isinstance(x, torch.Tensor) and (x.is_cuda or DeferredFusion.ALLOW_CPU)) or not LAZY:
+            return orig(*args, **kwargs)
+        prev = getattr(_tls, "scope", None)
+        scope = DeferredFusion()
+        _tls.scope = scope
+        try:
+            with scope:
+                out = orig(*args, **kwargs)
+                scope.flush()
+        finally:
+            _tls.scope = prev
+        model._be_fusion_stats = (scope.deferred, scope.filled)
+        return out
+
+    model.forward = forward
 
 
 class HipConv3d(nn.Module):
@@ -226,6 +443,16 @@ class HipConvTranspose2x2(nn.Module):
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
+        scope = getattr(_tls, "scope", None)
+        if scope is not None and scope.pending and not self.nchw_out:
+            ent = scope.take(x, self._fusible)
+            if ent is not None:  # a deferred cat / max-pool: read its sources in the halo loader
+                if ent[1] == "cat":
+                    a, b = (t.permute(0, 2, 3, 1) for t in ent[2:])
+                    y = fused_conv2d_concat(a, b, self.pc, post_relu=self.post_relu)
+                else:
+                    y = fused_conv2d(ent[2].permute(0, 2, 3, 1), self.pc, inmode="pool2", post_relu=self.post_relu)
+                return y.permute(0, 3, 1, 2)
         N, C, H, W = x.shape
         xh = x.to(torch.bfloat16).permute(0, 2, 3, 1)
         if C != self.pc.cin_pad:
@@ -319,6 +546,16 @@ class HipConvStride2x2(nn.Module):
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
+        scope = getattr(_tls, "scope", None)
+        if scope is not None and scope.pending and not self.nchw_out:
+            ent = scope.take(x, self._fusible)
+            if ent is not None:  # a deferred cat / max-pool: read its sources in the halo loader
+                if ent[1] == "cat":
+                    a, b = (t.permute(0, 2, 3, 1) for t in ent[2:])
+                    y = fused_conv2d_concat(a, b, self.pc, post_relu=self.post_relu)
+                else:
+                    y = fused_conv2d(ent[2].permute(0, 2, 3, 1), self.pc, inmode="pool2", post_relu=self.post_relu)
+                return y.permute(0, 3, 1, 2)
         N, C, H, W = x.shape
         xh = x.to(torch.bfloat16).permute(0, 2, 3, 1)[:, : H // 2 * 2, : W // 2 * 2]
         xs = xh.reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4 * C)
@@ -396,6 +633,11 @@ def _rewrite(mod: nn.Module, stats: dict) -> None:
                     stats["pool3d"] += 1
                     i += 1
                     continue
+                if _mp2_ok(m):
+                    child._modules[k] = HipMaxPool2d()
+                    stats["pool2d"] += 1
+                    i += 1
+                    continue
                 if _s2_ok(m):
                     relu = i + 1 < len(items) and isinstance(items[i + 1][1], nn.ReLU)
                     child._modules[k] = HipConvStride2x2(m, post_relu=relu)
@@ -435,6 +677,9 @@ def _rewrite(mod: nn.Module, stats: dict) -> None:
         elif _mp3_ok(child):
             setattr(mod, name, HipMaxPool3d())
             stats["pool3d"] += 1
+        elif _mp2_ok(child):
+            setattr(mod, name, HipMaxPool2d())
+            stats["pool2d"] += 1
         elif _s2_ok(child):
             setattr(mod, name, HipConvStride2x2(child))
             stats["strided"] += 1
@@ -451,8 +696,10 @@ def optimize_for_mi355x(model: nn.Module, device=None) -> tuple[nn.Module, dict]
     """In-place graph pass (model must be in eval mode).  Returns (model, stats)."""
     model.eval()
     stats = {"convs": 0, "bn_folded": 0, "relu_fused": 0, "skipped": 0, "norm_fused": 0, "norm_unfused": 0,
-             "conv_transpose": 0, "strided": 0, "pool3d": 0}
+             "conv_transpose": 0, "strided": 0, "pool3d": 0, "pool2d": 0}
     _rewrite(model, stats)
+    if any(isinstance(m, HipConv2d) for m in model.modules()):
+        _install_deferred_fusion(model)
     if device is not None:
         model.to(device)
     model.to(torch.bfloat16)

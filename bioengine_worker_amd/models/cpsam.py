@@ -242,7 +242,7 @@ class CPSAMEngine:
                 return F.linear(x, w, b)
 
             def lin_gelu(x, w, b):
-                return torch._addmm_activation(b, x, w.t(), use_gelu=True)
+                return torch._addmm_activation(b.to(x.dtype), x, w.t(), use_gelu=True)
             return lin, lin_gelu
         from ..ops import gemm_mt
 

@@ -279,3 +279,25 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
         qshift_ns, _native.stream(x.device),
     )
     return out
+
+
+def fused_conv2d_concat(xa: torch.Tensor, xb: torch.Tensor, pc: PackedConv, *, post_relu: bool = False,
+                        nw: int | None = None) -> torch.Tensor:
+    """3x3 conv (+ bias, + ReLU) of the channel concatenation [xa, xb] of two NHWC tensors
+    ([N, H, W, Ca] and [N, H, W, Cb], ``pc`` packed for Ca + Cb input channels) without materialising
+    it: ``be_conv2d_concat`` (INMODE 4) picks each 8-channel group's source in the halo loader.  Same
+    K order and accumulation as :func:`fused_conv2d` on ``torch.cat([xa, xb], -1)``."""
+    N, H, W, Ca = xa.shape
+    Cb = xb.shape[-1]
+    assert xb.shape[:3] == (N, H, W) and pc.ks == 3 and pc.cin_pad == Ca + Cb
+    if not xa.is_cuda:
+        return fused_conv2d(torch.cat([xa, xb], -1), pc, post_relu=post_relu)
+    assert xa.dtype == xb.dtype == torch.bfloat16 and xa.is_contiguous() and xb.is_contiguous()
+    assert Ca % 8 == 0 and Cb % 8 == 0 and pc.cout % 4 == 0
+    if pc.wp.device != xa.device:
+        pc.to(xa.device)
+    out = torch.empty(N, H, W, pc.cout, device=xa.device, dtype=torch.bfloat16)
+    _native.call("be_conv2d_concat", _native.ptr(xa), _native.ptr(xb), _native.ptr(pc.wp), _native.ptr(pc.bias),
+                 _native.ptr(out), N, H, W, Ca, Cb, pc.cout, pc.ck, pc.tco, int(bool(post_relu)),
+                 int(nw or choose_nw(pc, H, W)), _native.stream(xa.device))
+    return out

@@ -82,6 +82,8 @@ struct ConvArgs {
   int qshift_ns;
   // INMODE 3 (3x3x3 conv as ONE 2-D launch over the N * zD slices): the K axis stacks the three
   // depth taps, stacked channel dz * zC + c = channel c of slice z + dz - 1 (zero outside the volume)
+  // INMODE 4 (conv of a channel concatenation, the U-Net decoder's cat([skip, up])): channels
+  // [0, zC) come from x ([N, H, W, zC]), channels [zC, Cin) from x2 ([N, H, W, Cin - zC])
   int zD, zC;
 };
 
@@ -167,6 +169,11 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
           const int zz = n % a.zD + dz;
           if (zz >= 0 && zz < a.zD)
             r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)(n + dz) * a.Hs + gy) * a.Ws + gx) * a.zC + cz);
+        } else if (INMODE == 4) {  // zC % 8 == 0 (host-checked): an 8-channel group never straddles the seam
+          if (c < a.zC)
+            r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.H + gy) * a.W + gx) * a.zC + c);
+          else
+            r = *reinterpret_cast<const u32x4*>(a.x2 + (((size_t)n * a.H + gy) * a.W + gx) * (a.Cin - a.zC) + (c - a.zC));
         } else if (INMODE == 1) {
           r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * a.Cin + c);
         } else {
@@ -665,6 +672,16 @@ int dispatch_tco(int tco, int inmode, bool x2, int nw, const ConvArgs& a, hipStr
 }  // namespace
 
 template <int CK>
+int dispatch_concat(int tco, int nw, const ConvArgs& a, hipStream_t s) {
+  switch (tco) {
+    case 16: return dispatch_nw<3, CK, 16, 4, false>(nw, a, s);
+    case 32: return dispatch_nw<3, CK, 32, 4, false>(nw, a, s);
+    case 64: return dispatch_nw<3, CK, 64, 4, false>(nw, a, s);
+  }
+  return -2;
+}
+
+template <int CK>
 int dispatch_ztaps(int tco, int nw, const ConvArgs& a, hipStream_t s) {
   switch (tco) {
     case 16: return dispatch_nw<3, CK, 16, 3, false>(nw, a, s);
@@ -732,6 +749,24 @@ int be_conv3d_ztaps(const void* x, const void* w, const float* bias, void* out, 
   a.persist_blocks = g_persist_blocks;
   a.zD = D; a.zC = zC;
   return ck == 8 ? dispatch_ztaps<8>(tco, nw, a, stream) : dispatch_ztaps<32>(tco, nw, a, stream);
+}
+
+// 3x3 / stride 1 / zero-pad 1 conv of the channel concatenation [xa (Ca channels), xb (Cb)] of two
+// NHWC bf16 tensors of one spatial shape, without materialising it: the halo loader picks the source
+// per 8-channel group (INMODE 4).  The U-Net decoder's torch.cat([skip, up]) copy (~22 % of the 2-D EM
+// line's inference kernel time, profiles/r06/em2d/) disappears.  w: the packed layout of the conv over
+// Ca + Cb input channels; bias (+ ReLU) in the epilogue.
+int be_conv2d_concat(const void* xa, const void* xb, const void* w, const float* bias, void* out, int N, int H, int W,
+                     int Ca, int Cb, int Cout, int ck, int tco, int relu, int nw, hipStream_t stream) {
+  if (Ca % 8 != 0 || Cb % 8 != 0 || (Ca + Cb) % ck != 0 || Cout % 4 != 0 || (ck != 8 && ck != 32)) return -10;
+  ConvArgs a = {};
+  a.x = (const bf16_t*)xa; a.x2 = (const bf16_t*)xb; a.w = (const bf16_t*)w; a.bias = bias; a.out = out;
+  a.N = N; a.H = H; a.W = W; a.Hs = H; a.Ws = W; a.Cin = Ca + Cb; a.Cout = Cout; a.cout_valid = Cout;
+  a.nchunk = (Ca + Cb) / ck; a.KP = be_conv2d_packed_kp(3, ck);
+  a.prelu = relu ? 2 : 0;
+  a.persist_blocks = g_persist_blocks;
+  a.zC = Ca;
+  return ck == 8 ? dispatch_concat<8>(tco, nw, a, stream) : dispatch_concat<32>(tco, nw, a, stream);
 }
 
 }  // extern "C"

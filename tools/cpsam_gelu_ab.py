@@ -3,9 +3,13 @@ against hipBLASLt's fused GELU_BIAS epilogue ("ltgelu", tanh-approximated GELU).
 alternating arms; prints per-arm forward ms over 72 tiles (8 images x 9 tiles of 256^2) and the
 output cosine / max-abs difference against the lib arm."""
 import json
+import os
+import sys
 import time
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
 
 from bioengine_worker_amd.models.cpsam import CPSAM, CPSAMEngine
 

@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 6, s14: deferred cat / max-pool fusion of the 2-D graph pass (tests, then the EM 2-D line A/B
+# on a 64 x 2048^2 slab, 768/64/16 tiles) and the CPSAM exact-size graph test
+set -o pipefail
+mkdir -p gpurun_out/r06/s14
+cd /root/repo
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_deferred_fusion.py tests/test_transformer_gpu.py -m gpu > gpurun_out/r06/s14/tests.log 2>&1 || { tail -30 gpurun_out/r06/s14/tests.log; exit 1; }
+tail -3 gpurun_out/r06/s14/tests.log
+for arm in 1 0 1 0; do
+  BE_UNET_LAZY=$arm timeout -k 10 300 python -u tools/em2d_bench.py --em-z 64 --sweep 768:64:16 > gpurun_out/r06/s14/em2d_lazy$arm.log 2>&1 || { tail -20 gpurun_out/r06/s14/em2d_lazy$arm.log; exit 1; }
+  python - "$arm" <<'PY'
+import json, sys
+for l in open(f"gpurun_out/r06/s14/em2d_lazy{sys.argv[1]}.log"):
+    if l.startswith("{"):
+        d = json.loads(l); c = d["em_volume_config"]; t = c["stage_timings_s_rank0"]
+        print("lazy", sys.argv[1], round(d["em_volume_voxels_per_sec"] / 1e6, 1), "Mvox/s inference", t["inference"], "label", t["label"], "stats", t["stats"])
+PY
+done
