@@ -536,7 +536,8 @@ def bench_cpsam_infer(dev, batch: int = 8, steps: int = 4, lat_n: int = 10) -> d
     """Cellpose-SAM inference -- the reference app's default ``infer`` model
     (apps/cellpose-finetuning/main.py:4966-5144, bf16 Transformer :126-127): 512x512x3 images through
     cellpose 4's 256-tile / 0.1-overlap path (9 tiles per image), the ViT-L/8 engine (HIP attention,
-    rel-pos, LayerNorm, bias-GELU; hipBLASLt linear layers after the A/B against the in-house GEMM)
+    rel-pos, LayerNorm; hipBLASLt linear layers after the A/B against the in-house GEMM, lin1's bias +
+    GELU in hipBLASLt's GELU_BIAS epilogue)
     replayed from its HIP graph, taper blend, dynamics (niter 200), flow QC and fill holes.
     Random-init weights, synthetic images."""
     from bioengine_worker_amd.cellpose.pipeline import CellposeRunner, EvalParams, synthetic_cells
@@ -571,7 +572,10 @@ def bench_cpsam_infer(dev, batch: int = 8, steps: int = 4, lat_n: int = 10) -> d
             "cpsam_infer_p50_ms_batch1": round(lat[len(lat) // 2], 2),
             "cpsam_infer_config": {"model": "Cellpose-SAM ViT-L/8 (dim 1024, 24 blocks), random init",
                                    "image": [512, 512, 3], "batch": batch, "tiles": "256 / 0.1 overlap (9 per image)",
-                                   "gemm": "in-house macro-tile MFMA (gemm_mt)" if gemm == "mt" else "hipBLASLt",
+                                   "gemm": {"mt": "in-house macro-tile MFMA (gemm_mt)",
+                                            "ltgelu": "hipBLASLt; lin1 + bias + GELU (tanh approximation) in one "
+                                                      "GEMM epilogue (exact-GELU path: BE_CPSAM_INFER_GEMM=lib)"}
+                                           .get(gemm, "hipBLASLt + HIP bias/exact-GELU pass"),
                                    "graph": "one HIP graph per tile count", "masks": "dynamics niter 200, QC 0.4"}}
 
 

@@ -216,11 +216,14 @@ class CPSAMEngine:
         self.out_w = bf(net.out.weight.reshape(net.out.weight.shape[0], -1))
         self.out_b = bf(net.out.bias)
 
-    #: GEMM backend of the inference engine: "lib" (PyTorch -> hipBLASLt, default) or "mt" (the
-    #: framework's macro-tile MFMA GEMM with the bias / GELU epilogues).  Measured on MI355X at 512^2 x
-    #: batch 8: lib 99.7 img/s, mt 84.4 / 84.8 (profiles/r05/cpsam/infer_mt_vs_lib_s23.jsonl): the
-    #: in-house GEMM trails hipBLASLt by 10-15 % per forward shape, so the library stays the default.
-    GEMM = os.environ.get("BE_CPSAM_INFER_GEMM", "lib")
+    #: GEMM backend of the inference engine: "ltgelu" (default: hipBLASLt, lin1 with its GELU_BIAS
+    #: epilogue = tanh-approximated GELU fused into the GEMM), "lib" (hipBLASLt + the exact-erf HIP
+    #: bias_gelu_ pass) or "mt" / "hyb" (the framework's macro-tile MFMA GEMM).  Measured on MI355X,
+    #: 72 tiles of 256^2 (profiles/r06/cpsam/gelu_ab_s13.jsonl): ltgelu 62.9 ms, lib 66.8 ms per
+    #: forward; flows cosine 0.99992 against the exact-GELU path (max abs 0.07 of 4.8).  Earlier:
+    #: lib 99.7 img/s, mt 84.4 (profiles/r05/cpsam/infer_mt_vs_lib_s23.jsonl).  Fine-tuning
+    #: (train/cpsam_engine.py) keeps the exact GELU.
+    GEMM = os.environ.get("BE_CPSAM_INFER_GEMM", "ltgelu")
     #: rel-pos terms: "hip" (relpos.hip MFMA kernel, default) or "torch" (fp32 einsums; A/B only)
     RELPOS = os.environ.get("BE_CPSAM_RELPOS", "hip")
 

@@ -103,7 +103,7 @@ def test_cpsam_engine_matches_fp32(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gemm", ["mt", "lib"])
+@pytest.mark.parametrize("gemm", ["mt", "lib", "ltgelu"])
 def test_cpsam_engine_vit_l_matches_fp32(gpu, gemm, monkeypatch):
     """The inference engine at the reference's ViT-L/8 shapes (dim 1024, 24 blocks, 16 heads, 1024
     tokens) against the fp32 CPSAM.forward, eager and replayed from its HIP graph; every linear layer
