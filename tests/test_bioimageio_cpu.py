@@ -186,3 +186,17 @@ def test_model_cache_recovers_from_dead_downloader_and_stale_leases(tmp_path, mo
     cache.cache_size_bytes = 10  # force eviction of everything not in use
     asyncio.run(cache.ensure_space(0))
     assert not d.exists()
+
+
+def test_chunked_mean_std_matches_direct():
+    """processing._mean_std: chunk moments combined exactly (the EM line's per-tile normalisation)."""
+    import torch
+
+    from bioengine_worker_amd.bioimageio.processing import _mean_std
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3, 2, 256, 384, generator=g) * 7 + 3
+    for dims in ([2, 3], [1, 2, 3], [3]):
+        m, s = _mean_std(x, dims)
+        assert torch.allclose(m, x.mean(dim=dims, keepdim=True), atol=1e-5)
+        assert torch.allclose(s, x.std(dim=dims, keepdim=True, unbiased=False), rtol=1e-5)
