@@ -443,16 +443,6 @@ class HipConvTranspose2x2(nn.Module):
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
-        scope = getattr(_tls, "scope", None)
-        if scope is not None and scope.pending and not self.nchw_out:
-            ent = scope.take(x, self._fusible)
-            if ent is not None:  # a deferred cat / max-pool: read its sources in the halo loader
-                if ent[1] == "cat":
-                    a, b = (t.permute(0, 2, 3, 1) for t in ent[2:])
-                    y = fused_conv2d_concat(a, b, self.pc, post_relu=self.post_relu)
-                else:
-                    y = fused_conv2d(ent[2].permute(0, 2, 3, 1), self.pc, inmode="pool2", post_relu=self.post_relu)
-                return y.permute(0, 3, 1, 2)
         N, C, H, W = x.shape
         xh = x.to(torch.bfloat16).permute(0, 2, 3, 1)
         if C != self.pc.cin_pad:
@@ -546,16 +536,6 @@ class HipConvStride2x2(nn.Module):
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
-        scope = getattr(_tls, "scope", None)
-        if scope is not None and scope.pending and not self.nchw_out:
-            ent = scope.take(x, self._fusible)
-            if ent is not None:  # a deferred cat / max-pool: read its sources in the halo loader
-                if ent[1] == "cat":
-                    a, b = (t.permute(0, 2, 3, 1) for t in ent[2:])
-                    y = fused_conv2d_concat(a, b, self.pc, post_relu=self.post_relu)
-                else:
-                    y = fused_conv2d(ent[2].permute(0, 2, 3, 1), self.pc, inmode="pool2", post_relu=self.post_relu)
-                return y.permute(0, 3, 1, 2)
         N, C, H, W = x.shape
         xh = x.to(torch.bfloat16).permute(0, 2, 3, 1)[:, : H // 2 * 2, : W // 2 * 2]
         xs = xh.reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4 * C)
