@@ -47,7 +47,8 @@ import weakref
 from torch.overrides import TorchFunctionMode
 
 from ..ops.conv import PackedConv, fused_conv2d, fused_conv2d_concat
-from ..ops.conv3d import PackedConv3d, depth2space3d, fused_conv3d, maxpool3d_ndhwc
+from ..ops.conv3d import (PackedConv3d, concat3d_fusible, depth2space3d, fused_conv3d, fused_conv3d_concat,
+                          maxpool3d_ndhwc)
 
 
 def _eligible(c: nn.Module) -> bool:
@@ -148,7 +149,10 @@ LAZY = os.environ.get("BE_UNET_LAZY", "1") != "0"
 
 
 def _nhwc_dense(t: torch.Tensor) -> bool:
-    return t.dim() == 4 and t.permute(0, 2, 3, 1).is_contiguous()
+    """Channels-last dense (an NHWC / NDHWC buffer viewed as NCHW / NCDHW)."""
+    if t.dim() == 4:
+        return t.permute(0, 2, 3, 1).is_contiguous()
+    return t.dim() == 5 and t.permute(0, 2, 3, 4, 1).is_contiguous()
 
 
 class DeferredFusion(TorchFunctionMode):
@@ -196,17 +200,18 @@ class DeferredFusion(TorchFunctionMode):
             return None
         ts = args[0]
         dim = args[1] if len(args) > 1 else kwargs.get("dim", 0)
-        if not isinstance(ts, (list, tuple)) or len(ts) != 2 or dim not in (1, -3):
+        if not isinstance(ts, (list, tuple)) or len(ts) != 2 or dim not in (1, -3, -4):
             return None
         a, b = ts
-        if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and a.dim() == 4 and b.dim() == 4):
+        if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and a.dim() == b.dim()
+                and a.dim() in (4, 5) and dim in (1, 1 - a.dim())):
             return None
         if not (self._ok_src(a) and self._ok_src(b) and a.device == b.device and a.shape[0] == b.shape[0]
                 and a.shape[2:] == b.shape[2:] and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0):
             return None
-        N, _, H, W = a.shape
-        ph = torch.empty((N, a.shape[1] + b.shape[1], H, W), dtype=a.dtype, device=a.device,
-                         memory_format=torch.channels_last)
+        shape = (a.shape[0], a.shape[1] + b.shape[1]) + tuple(a.shape[2:])
+        fmt = torch.channels_last if a.dim() == 4 else torch.channels_last_3d
+        ph = torch.empty(shape, dtype=a.dtype, device=a.device, memory_format=fmt)
         return self._add(ph, "cat", a, b)
 
     def take(self, x: torch.Tensor, fusible) -> tuple | None:
@@ -337,11 +342,20 @@ class HipConv3d(nn.Module):
         self._dev = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        scope = getattr(_tls, "scope", None)  # a deferred cat: checked before any tensor access (see HipConv2d)
+        if scope is not None and scope.pending and not self.nchw_out:
+            ent = scope.take(x, lambda e: e[1] == "cat" and concat3d_fusible(self.pc, e[2].shape[1], e[3].shape[1]))
+            if ent is not None:
+                a, b = (t.permute(0, 2, 3, 4, 1) for t in ent[2:])
+                if a.is_cuda and self._dev != a.device:
+                    self.pc.to(a.device)
+                    self._dev = a.device
+                return fused_conv3d_concat(a, b, self.pc, post_relu=self.post_relu).permute(0, 4, 1, 2, 3)
         if not x.is_cuda:  # CPU: fp32 reference math in the input dtype
             y = F.conv3d(x.float(), self.pc.w.to(x.device),
                          None if self.pc.bias is None else self.pc.bias.to(x.device), padding=self.pc.ks // 2)
             y = torch.relu(y) if self.post_relu else y
-            return y.to(x.dtype)
+            return y.to(x.dtype).contiguous(memory_format=torch.channels_last_3d)  # the GPU path's layout
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
@@ -678,7 +692,7 @@ def optimize_for_mi355x(model: nn.Module, device=None) -> tuple[nn.Module, dict]
     stats = {"convs": 0, "bn_folded": 0, "relu_fused": 0, "skipped": 0, "norm_fused": 0, "norm_unfused": 0,
              "conv_transpose": 0, "strided": 0, "pool3d": 0, "pool2d": 0}
     _rewrite(model, stats)
-    if any(isinstance(m, HipConv2d) for m in model.modules()):
+    if any(isinstance(m, (HipConv2d, HipConv3d)) for m in model.modules()):
         _install_deferred_fusion(model)
     if device is not None:
         model.to(device)

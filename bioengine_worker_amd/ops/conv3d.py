@@ -132,6 +132,32 @@ def fused_conv3d(x: torch.Tensor, pc: PackedConv3d, post_relu: bool = False) -> 
     return out
 
 
+def fused_conv3d_concat(xa: torch.Tensor, xb: torch.Tensor, pc: PackedConv3d, post_relu: bool = False) -> torch.Tensor:
+    """3x3x3 conv of the channel concatenation [xa, xb] of two NDHWC volumes without materialising it
+    (``be_conv3d_ztaps_concat``, INMODE 5); same K order and accumulation as :func:`fused_conv3d` on
+    ``torch.cat([xa, xb], -1)`` along the z-tap path."""
+    N, D, H, W, Ca = xa.shape
+    Cb = xb.shape[-1]
+    assert xb.shape[:4] == (N, D, H, W) and pc.ks == 3 and pc.cin_pad == Ca + Cb
+    if not xa.is_cuda:
+        return fused_conv3d(torch.cat([xa, xb], -1), pc, post_relu)
+    zt = pc.ztap
+    assert xa.dtype == xb.dtype == torch.bfloat16 and xa.is_contiguous() and xb.is_contiguous()
+    assert Ca % 8 == 0 and Cb % 8 == 0 and (Ca + Cb) % zt.ck == 0 and pc.cout % 4 == 0
+    out = torch.empty(N, D, H, W, pc.cout, device=xa.device, dtype=torch.bfloat16)
+    _native.call("be_conv3d_ztaps_concat", _native.ptr(xa), _native.ptr(xb), _native.ptr(zt.wp), _native.ptr(zt.bias),
+                 _native.ptr(out), N, D, H, W, Ca, Cb, pc.cout, zt.ck, zt.tco, int(post_relu), 4,
+                 _native.stream(xa.device))
+    return out
+
+
+def concat3d_fusible(pc: PackedConv3d, ca: int, cb: int) -> bool:
+    """Whether :func:`fused_conv3d_concat` takes this conv over a [ca | cb]-channel concatenation."""
+    return (os.environ.get("BE_CONV3D", "ztaps") == "ztaps" and pc.ks == 3 and pc.cout % 4 == 0
+            and pc.cin_pad == ca + cb and pc.ztap.cin_pad == 3 * (ca + cb) and (ca + cb) % pc.ztap.ck == 0
+            and ca % 8 == 0 and cb % 8 == 0)
+
+
 def maxpool3d_ndhwc(x: torch.Tensor) -> torch.Tensor:
     """MaxPool3d(2) (floor mode) of NDHWC [N, D, H, W, C] -> [N, D/2, H/2, W/2, C] (``vol3d.hip``)."""
     N, D, H, W, C = x.shape

@@ -84,7 +84,9 @@ struct ConvArgs {
   // depth taps, stacked channel dz * zC + c = channel c of slice z + dz - 1 (zero outside the volume)
   // INMODE 4 (conv of a channel concatenation, the U-Net decoder's cat([skip, up])): channels
   // [0, zC) come from x ([N, H, W, zC]), channels [zC, Cin) from x2 ([N, H, W, Cin - zC])
-  int zD, zC;
+  // INMODE 5 (INMODE 3 over a concatenation, the 3-D decoder): stacked channel dz * zC + c is
+  // channel c of slice z + dz - 1 of x ([.., zA]) for c < zA, else channel c - zA of x2 ([.., zC - zA])
+  int zD, zC, zA;
 };
 
 // Block order of the one-block-per-tile kernel.  Tile-major (grid x = tile, y = cout block) sends
@@ -169,6 +171,16 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
           const int zz = n % a.zD + dz;
           if (zz >= 0 && zz < a.zD)
             r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)(n + dz) * a.Hs + gy) * a.Ws + gx) * a.zC + cz);
+        } else if (INMODE == 5) {
+          const int dz = c / a.zC - 1, cz = c - (dz + 1) * a.zC;
+          const int zz = n % a.zD + dz;
+          if (zz >= 0 && zz < a.zD) {
+            const size_t pix = ((size_t)(n + dz) * a.Hs + gy) * a.Ws + gx;
+            if (cz < a.zA)
+              r = *reinterpret_cast<const u32x4*>(a.x + pix * a.zA + cz);
+            else
+              r = *reinterpret_cast<const u32x4*>(a.x2 + pix * (a.zC - a.zA) + (cz - a.zA));
+          }
         } else if (INMODE == 4) {  // zC % 8 == 0 (host-checked): an 8-channel group never straddles the seam
           if (c < a.zC)
             r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.H + gy) * a.W + gx) * a.zC + c);
@@ -681,12 +693,12 @@ int dispatch_concat(int tco, int nw, const ConvArgs& a, hipStream_t s) {
   return -2;
 }
 
-template <int CK>
+template <int CK, int MODE = 3>
 int dispatch_ztaps(int tco, int nw, const ConvArgs& a, hipStream_t s) {
   switch (tco) {
-    case 16: return dispatch_nw<3, CK, 16, 3, false>(nw, a, s);
-    case 32: return dispatch_nw<3, CK, 32, 3, false>(nw, a, s);
-    case 64: return dispatch_nw<3, CK, 64, 3, false>(nw, a, s);
+    case 16: return dispatch_nw<3, CK, 16, MODE, false>(nw, a, s);
+    case 32: return dispatch_nw<3, CK, 32, MODE, false>(nw, a, s);
+    case 64: return dispatch_nw<3, CK, 64, MODE, false>(nw, a, s);
   }
   return -2;
 }
@@ -749,6 +761,23 @@ int be_conv3d_ztaps(const void* x, const void* w, const float* bias, void* out, 
   a.persist_blocks = g_persist_blocks;
   a.zD = D; a.zC = zC;
   return ck == 8 ? dispatch_ztaps<8>(tco, nw, a, stream) : dispatch_ztaps<32>(tco, nw, a, stream);
+}
+
+// be_conv3d_ztaps over the channel concatenation [xa (Ca channels), xb (Cb)] of two NDHWC bf16 volumes
+// of one shape (INMODE 5): the 3-D U-Net decoder's torch.cat([skip, up]) is never materialised.
+// w: the z-tap stacked packed layout for zC = Ca + Cb input channels.
+int be_conv3d_ztaps_concat(const void* xa, const void* xb, const void* w, const float* bias, void* out, int N, int D,
+                           int H, int W, int Ca, int Cb, int Cout, int ck, int tco, int relu, int nw, hipStream_t stream) {
+  const int zC = Ca + Cb;
+  if (Ca % 8 != 0 || Cb % 8 != 0 || zC % ck != 0 || Cout % 4 != 0 || (ck != 8 && ck != 32)) return -10;
+  ConvArgs a = {};
+  a.x = (const bf16_t*)xa; a.x2 = (const bf16_t*)xb; a.w = (const bf16_t*)w; a.bias = bias; a.out = out;
+  a.N = N * D; a.H = H; a.W = W; a.Hs = H; a.Ws = W; a.Cin = 3 * zC; a.Cout = Cout; a.cout_valid = Cout;
+  a.nchunk = 3 * zC / ck; a.KP = be_conv2d_packed_kp(3, ck);
+  a.prelu = relu ? 2 : 0;
+  a.persist_blocks = g_persist_blocks;
+  a.zD = D; a.zC = zC; a.zA = Ca;
+  return ck == 8 ? dispatch_ztaps<8, 5>(tco, nw, a, stream) : dispatch_ztaps<32, 5>(tco, nw, a, stream);
 }
 
 // 3x3 / stride 1 / zero-pad 1 conv of the channel concatenation [xa (Ca channels), xb (Cb)] of two

@@ -122,3 +122,70 @@ def test_conv2d_concat_matches_fp32(ca, cb, cout):
     ref = torch.relu(F.conv2d(x32, w.to(torch.bfloat16).float(), bias, padding=1)).permute(0, 2, 3, 1)
     err = (y.float() - ref).abs().max().item()
     assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
+
+
+class TinyUNet3d(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.enc = nn.Sequential(nn.Conv3d(8, 16, 3, padding=1), nn.ReLU())
+        self.mid = nn.Sequential(nn.Conv3d(16, 16, 3, padding=1), nn.ReLU())
+        self.dec = nn.Sequential(nn.Conv3d(32, 16, 3, padding=1), nn.ReLU())
+
+    def forward(self, x):
+        s = self.enc(x)
+        return self.dec(torch.cat([s, self.mid(s)], dim=1))
+
+
+def test_deferred_fusion_3d_cpu(monkeypatch):
+    torch.manual_seed(0)
+    model, st = cv.optimize_for_mi355x(TinyUNet3d().eval())
+    assert st["convs"] == 3
+    x = torch.randn(1, 8, 6, 16, 16).to(torch.bfloat16).contiguous(memory_format=torch.channels_last_3d)
+    with torch.no_grad():
+        ref = model(x).float()
+        monkeypatch.setattr(cv.DeferredFusion, "ALLOW_CPU", True)
+        out = model(x).float()
+    assert model._be_fusion_stats == (1, 0)
+    err = (out - ref).abs().max().item()
+    assert err <= 0.05 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ca,cb,cout", [(16, 16, 16), (32, 32, 32), (64, 64, 64)])
+def test_conv3d_concat_matches_fp32(ca, cb, cout):
+    from bioengine_worker_amd.ops.conv3d import PackedConv3d, fused_conv3d, fused_conv3d_concat
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(1)
+    N, D, H, W = 2, 9, 21, 40
+    a = torch.randn(N, D, H, W, ca, device=dev, generator=g).to(torch.bfloat16)
+    b = torch.randn(N, D, H, W, cb, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(cout, ca + cb, 3, 3, 3, device=dev, generator=g) / (5 * (ca + cb) ** 0.5)
+    bias = torch.randn(cout, device=dev, generator=g)
+    pc = PackedConv3d(w, bias)
+    pc.to(dev)
+    y = fused_conv3d_concat(a, b, pc, post_relu=True)
+    ycat = fused_conv3d(torch.cat([a, b], -1).contiguous(), pc, post_relu=True)
+    assert torch.equal(y, ycat)
+    x32 = torch.cat([a, b], -1).float().permute(0, 4, 1, 2, 3)
+    ref = torch.relu(F.conv3d(x32, w.to(torch.bfloat16).float(), bias, padding=1)).permute(0, 2, 3, 4, 1)
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 1e-2, err
+
+
+@pytest.mark.gpu
+def test_unet3d_deferred_fusion_bit_identical(tmp_path, monkeypatch):
+    from bioengine_worker_amd.bioimageio.package import write_unet3d_package
+    from bioengine_worker_amd.bioimageio.runner import PredictionPipeline
+
+    dev = torch.device("cuda", 0)
+    root = tmp_path / "unet3d"
+    write_unet3d_package(root, "unet3d", in_channels=1, out_channels=1, features=(16, 32, 64, 128),
+                         test_shape=(1, 1, 16, 32, 32))
+    pipe = PredictionPipeline(root, device=dev)
+    x = torch.rand(2, 1, 32, 64, 64, device=dev)
+    fused = next(iter(pipe.predict_tensors(x).values())).float()
+    assert pipe.model._be_fusion_stats == (3, 0)  # the three decoder concatenations, none filled
+    monkeypatch.setattr(cv, "LAZY", False)
+    plain = next(iter(pipe.predict_tensors(x).values())).float()
+    assert torch.equal(fused, plain), (fused - plain).abs().max().item()

@@ -16,3 +16,13 @@ for l in open(f"gpurun_out/r06/s14/em2d_lazy{sys.argv[1]}.log"):
         print("lazy", sys.argv[1], round(d["em_volume_voxels_per_sec"] / 1e6, 1), "Mvox/s inference", t["inference"], "label", t["label"], "stats", t["stats"])
 PY
 done
+for arm in 1 0; do
+  BE_UNET_LAZY=$arm timeout -k 10 300 python -u tools/em3d_bench.py --em3d-z 64 --sweep 64:256:4 > gpurun_out/r06/s14/em3d_lazy$arm.log 2>&1 || { tail -20 gpurun_out/r06/s14/em3d_lazy$arm.log; exit 1; }
+  python - "$arm" <<'PY'
+import json, sys
+for l in open(f"gpurun_out/r06/s14/em3d_lazy{sys.argv[1]}.log"):
+    if l.startswith("{"):
+        d = json.loads(l); c = d["em_volume3d_config"]; t = c["stage_timings_s_rank0"]
+        print("3d lazy", sys.argv[1], round(d["em_volume3d_voxels_per_sec"] / 1e6, 1), "Mvox/s inference", t["inference"], "label", t["label"])
+PY
+done
