@@ -397,7 +397,8 @@ def bench_em_volume(args, world, rank, dev) -> dict:
         out = {"em_volume_voxels_per_sec": round(vox / dt, 1),
                "em_volume_config": {"volume": [Z * world, YX, YX], "slab_per_gpu": [Z, YX, YX], "tile": tile,
                                     "overlap": ov, "tiles_per_call": args.em_tile_batch,
-                                    "model": "BioImage.IO 2-D U-Net 32-64-128-256 (random init, graph pass)",
+                                    "model": "BioImage.IO 2-D U-Net 32-64-128-256 (random init, graph pass: "
+                                             "HIP convs, skip concatenation and max-pool read in the conv loaders)",
                                     "source": "memory-mapped .npy slab per rank", "split_touching": True,
                                     "gather": "rank0 (dist.gather of int32 labels)", "seconds": round(dt, 3),
                                     "n_instances": res["n_instances"],
@@ -465,8 +466,9 @@ def bench_em_volume3d(args, world, rank, dev) -> dict:
                "em_volume3d_config": {"volume": [Z * world, YX, YX], "slab_per_gpu": [Z, YX, YX],
                                       "tile": [kw["tile_z"], kw["tile"], kw["tile"]], "overlap": [8, 16, 16],
                                       "tiles_per_call": kw["batch"],
-                                      "model": "BioImage.IO 3-D U-Net 16-32-64-128 (random init, graph pass, "
-                                               "implicit-GEMM 3x3x3 conv)",
+                                      "model": "BioImage.IO 3-D U-Net 16-32-64-128 (random init, graph pass: "
+                                               "3x3x3 convs as z-tap launches of the 2-D MFMA kernel, skip "
+                                               "concatenation read in the decoder conv's loader)",
                                       "split_touching": True, "gather": "rank0", "seconds": round(dt, 3),
                                       "n_instances": res["n_instances"], "stage_timings_s_rank0": timings}}
         del slab, full, res
