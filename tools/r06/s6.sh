@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r06/s6
 cd /root/repo
-export BE_BENCH_BACKEND=gloo BE_BENCH_SHARED_GPU=1
+export BE_BENCH_BACKEND=gloo BE_BENCH_SHARED_GPU=1 PYTHONFAULTHANDLER=1
 timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 3 --warmup 1 --train-steps 3 > gpurun_out/r06/s6/rehearsal_w2.log 2>&1
 rc=$?
 grep '^{"metric"' gpurun_out/r06/s6/rehearsal_w2.log > gpurun_out/r06/s6/rehearsal_w2.json
