@@ -62,6 +62,27 @@ def _dist_setup(ngpus: int):
     return world, rank, local
 
 
+_STAGE = {"name": "start", "t0": time.time()}
+
+
+def _progress(stage: str, rank: int = 0) -> None:
+    """One stderr line per bench section (and a heartbeat thread repeating the current one every
+    60 s): a long multi-rank run shows where it is, and a native crash names its section."""
+    _STAGE["name"] = stage
+    print(f"[bench r{rank} +{time.time() - _STAGE['t0']:.0f}s] {stage}", file=sys.stderr, flush=True)
+    if not _STAGE.get("hb"):
+        import threading
+
+        def beat():
+            while True:
+                time.sleep(60)
+                print(f"[bench r{rank} +{time.time() - _STAGE['t0']:.0f}s] ... {_STAGE['name']}", file=sys.stderr,
+                      flush=True)
+
+        _STAGE["hb"] = threading.Thread(target=beat, daemon=True)
+        _STAGE["hb"].start()
+
+
 def _barrier(world):
     if world > 1:
         dist.barrier()
@@ -674,6 +695,7 @@ def main():
 
     _native.hip()  # fail loudly if the kernels are missing
 
+    _progress("headline", rank)
     dt, runner, imgs, p, extra = bench_infer(args, world, rank, dev)
     total_imgs = args.batch * args.steps * world
     value = total_imgs / dt
@@ -705,6 +727,7 @@ def main():
     }
     out.update(extra)
     if not args.no_extras:
+        _progress("latency / reference algorithm / masks", rank)
         try:
             if rank == 0:
                 p50, p95 = bench_latency(runner, imgs, p)
@@ -722,11 +745,13 @@ def main():
         except Exception as e:  # extras must never take the headline down
             out["extras_error"] = f"latency/ref: {type(e).__name__}: {e}"
         if world == 1 and not args.no_served:
+            _progress("served cellpose", rank)
             try:
                 out.update(bench_served(args.served_seconds))
             except Exception as e:  # noqa: BLE001
                 out["extras_error_served"] = f"{type(e).__name__}: {e}"
         if rank == 0:
+            _progress("vit embed", rank)
             try:
                 out["vit_embed_imgs_per_s"] = round(bench_vit_embed(dev), 1)  # per GPU, batch 64, fp8
                 out["vit_embed_config"] = {"model": "DINOv2 ViT-B/14", "image": 224, "batch": 64,
@@ -734,10 +759,12 @@ def main():
             except Exception as e:  # noqa: BLE001
                 out["extras_error_vit"] = f"{type(e).__name__}: {e}"
         if world == 1 and not args.no_served:
+            _progress("served search", rank)
             try:
                 out.update(bench_served_search(args.served_seconds))
             except Exception as e:  # noqa: BLE001
                 out["extras_error_served_search"] = f"{type(e).__name__}: {e}"
+        _progress("cpnet fine-tune", rank)
         try:
             tdt = bench_train(args, world, rank, dev)
             out["finetune_samples_per_sec"] = round(args.train_batch * args.train_steps * world / tdt, 2)
@@ -750,10 +777,12 @@ def main():
         except Exception as e:
             out["extras_error_train"] = f"{type(e).__name__}: {e}"
         if not args.no_em:
+            _progress("em 2-d", rank)
             try:
                 out.update(bench_em_volume(args, world, rank, dev))
             except Exception as e:  # noqa: BLE001
                 out["extras_error_em"] = f"{type(e).__name__}: {e}"
+            _progress("em 3-d", rank)
             try:
                 out.update(bench_em_volume3d(args, world, rank, dev))
             except Exception as e:  # noqa: BLE001
@@ -763,6 +792,7 @@ def main():
                 out.update(bench_model_runner_cpu())
             except Exception as e:  # noqa: BLE001
                 out["extras_error_model_runner"] = f"{type(e).__name__}: {e}"
+        _progress("cpsam fine-tune", rank)
         try:
             sps, ms = bench_train_cpsam(args, world, rank, dev, args.cpsam_batch, args.train_steps)
             out["finetune_cpsam_samples_per_sec"] = round(sps, 2)
@@ -772,6 +802,7 @@ def main():
                                             "HIP fwd/bwd engine, segmented HIP-graph step, RCCL bucketed fp32 all-reduce overlapped",
                                             "parallelism": f"dp{world}"}
             if world > 1:  # the ZeRO-1 optimizer on the same DP step
+                _progress("cpsam fine-tune, zero-1", rank)
                 try:
                     spz, msz = bench_train_cpsam(args, world, rank, dev, args.cpsam_batch, args.train_steps, zero=True)
                     out["finetune_cpsam_zero_samples_per_sec"] = round(spz, 2)
@@ -800,6 +831,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             out["extras_error_train_cpsam"] = f"{type(e).__name__}: {e}"
         if rank == 0:
+            _progress("cpsam inference", rank)
             try:
                 out.update(bench_cpsam_infer(dev))
             except Exception as e:  # noqa: BLE001
@@ -820,6 +852,7 @@ def main():
             except Exception as e:  # noqa: BLE001
                 out["extras_error_train_autograd"] = f"{type(e).__name__}: {e}"
     if world > 1 and not args.no_extras and not args.no_served:
+        _progress("served node", rank)
         out.update(bench_served_node(args, world, rank))
     if rank == 0:
         print(json.dumps(out), flush=True)
