@@ -351,6 +351,21 @@ def exchange_halos(x: torch.Tensor, halo: int, group=None) -> tuple[torch.Tensor
     return (out.bool() if x.dtype == torch.bool else out), lo, hi
 
 
+def label_counts(labels: torch.Tensor, n: int) -> torch.Tensor:
+    """int64 [n + 1] voxel counts of labels 1..n (index 0 = 0).  On the GPU the LDS-hash chunk
+    counter (``be_em_label_counts``): torch.bincount over a 256 x 2048^2 int32 slab of the 3-D EM line
+    died with SIGFPE (profiles/r06/rehearsal/), and its per-voxel atomics serialise on large
+    components anyway."""
+    if labels.is_cuda and labels.dtype == torch.int32 and labels.is_contiguous():
+        counts = torch.empty(n + 1, dtype=torch.int32, device=labels.device)
+        _native.call("be_em_label_counts", _native.ptr(labels), labels.numel(), _native.ptr(counts), n + 1,
+                     _native.stream(labels.device))
+        return counts.to(torch.int64)
+    cnt = torch.bincount(labels.reshape(-1).long(), minlength=n + 1)[: n + 1].to(torch.int64)
+    cnt[0] = 0
+    return cnt
+
+
 def split_instances_halo(mask: torch.Tensor, group=None, min_size: int = 300, closing_radius: int = 4,
                          min_distance: int = 8, halo: int | None = None,
                          timings: dict | None = None) -> tuple[torch.Tensor, int]:
@@ -382,7 +397,7 @@ def split_instances_halo(mask: torch.Tensor, group=None, min_size: int = 300, cl
     Zg = sum(depths)
     # 1. remove small objects with GLOBAL component sizes
     labels, n = label_sharded(mask, group)
-    cnt = torch.bincount(labels.reshape(-1).long(), minlength=n + 1)[: n + 1].to(torch.int64)
+    cnt = label_counts(labels, n)
     dist.all_reduce(cnt, group=group)
     big = cnt >= min_size
     big[0] = False

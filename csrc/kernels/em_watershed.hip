@@ -281,7 +281,8 @@ __device__ __forceinline__ void cs_insert(int* keys, int* vals, int r, int c, in
   atomicAdd(counts + r, c);  // crowded map: global
 }
 
-__global__ __launch_bounds__(256) void comp_count_kernel(const int* __restrict__ roots, long long n, int* __restrict__ counts) {
+__global__ __launch_bounds__(256) void comp_count_kernel(const int* __restrict__ roots, long long n, int* __restrict__ counts,
+                                                         int bg) {
   __shared__ int keys[CS_HASH], vals[CS_HASH];
   const int tid = threadIdx.x, lane = tid & 63;
   for (int i = tid; i < CS_HASH; i += 256) { keys[i] = -1; vals[i] = 0; }
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(256) void comp_count_kernel(const int* __restrict__
   const long long base = (long long)blockIdx.x * CS_CHUNK;
   for (int it = 0; it < CS_CHUNK / 256; ++it) {
     const long long i = base + (long long)it * 256 + tid;
-    const int r = i < n ? roots[i] : -1;
+    int r = i < n ? roots[i] : -1;
+    if (r == bg) r = -1;
     const int r0 = __shfl(r, 0, 64);
     if (__all(r == r0)) {
       if (lane == 0 && r0 >= 0) cs_insert(keys, vals, r0, 64, counts);
@@ -321,11 +323,24 @@ int be_component_keep(const int* roots, long long n, int* counts, int min_size, 
   if (n == 0) return 0;
   (void)hipMemsetAsync(counts, 0, (size_t)n * sizeof(int), s);
   const long long nchunk = (n + CS_CHUNK - 1) / CS_CHUNK;
-  hipLaunchKernelGGL(comp_count_kernel, dim3((unsigned)nchunk), dim3(256), 0, s, roots, n, counts);
+  hipLaunchKernelGGL(comp_count_kernel, dim3((unsigned)nchunk), dim3(256), 0, s, roots, n, counts, -1);
   hipLaunchKernelGGL(comp_keep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, roots, n, counts, min_size, out);
   return BE_CHECK_LAUNCH();
 }
 
+
+// counts[l] = voxels with label l for l in [1, nbins) (labels: int32 in [0, nbins), 0 = background,
+// counts[0] = 0), with the LDS-hash chunk counter above.  Replaces torch.bincount on the sharded EM
+// path, which died with SIGFPE on a 256 x 2048^2 slab of the 3-D line (profiles/r06/rehearsal/).
+int be_em_label_counts(const int* labels, long long n, int* counts, int nbins, hipStream_t s) {
+  if (nbins <= 0) return -10;
+  (void)hipMemsetAsync(counts, 0, (size_t)nbins * sizeof(int), s);
+  if (n == 0) return 0;
+  const long long nchunk = (n + CS_CHUNK - 1) / CS_CHUNK;
+  if (nchunk >= (1LL << 31)) return -11;
+  hipLaunchKernelGGL(comp_count_kernel, dim3((unsigned)nchunk), dim3(256), 0, s, labels, n, counts, 0);
+  return BE_CHECK_LAUNCH();
+}
 
 // Marker watershed on elev (e.g. -EDT) restricted to mask (uint8, optional), markers int32 (>0),
 // D = 1 for 2-D.  key: [n] uint64 scratch, flags: [n] uint8 scratch, changed: 1 int (device).

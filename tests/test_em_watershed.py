@@ -268,3 +268,21 @@ def test_edt2d_bounded_search_and_fallback_rows(gpu):
     got = mito.edt(torch.from_numpy(m).to(gpu)).cpu().numpy()
     want = ndimage.distance_transform_edt(m)
     assert np.abs(got - want).max() < 1e-3
+
+
+@pytest.mark.gpu
+def test_em_label_counts_matches_bincount():
+    """be_em_label_counts (LDS-hash chunk counter) against torch.bincount: sparse labels, one huge
+    component, an empty (all-background) slab, and a ragged last chunk."""
+    from bioengine_worker_amd.em.volume import label_counts
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    lab = torch.randint(0, 5000, (7, 301, 257), device=dev, generator=g, dtype=torch.int32)
+    lab[:, 100:250, 20:200] = 17  # a large component (wave-uniform inserts)
+    lab[2] = 0
+    ref = torch.bincount(lab.reshape(-1).long(), minlength=5000)
+    ref[0] = 0
+    assert torch.equal(label_counts(lab, 4999), ref)
+    z = torch.zeros(3, 64, 64, device=dev, dtype=torch.int32)
+    assert torch.equal(label_counts(z, 0), torch.zeros(1, dtype=torch.int64, device=dev))
