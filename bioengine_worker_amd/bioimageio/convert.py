@@ -46,7 +46,7 @@ import weakref
 
 from torch.overrides import TorchFunctionMode
 
-from ..ops.conv import PackedConv, fused_conv2d, fused_conv2d_concat
+from ..ops.conv import PackedConv, depth_to_space2, fused_conv2d, fused_conv2d_concat
 from ..ops.conv3d import (PackedConv3d, concat3d_fusible, depth2space3d, fused_conv3d, fused_conv3d_concat,
                           maxpool3d_ndhwc)
 
@@ -110,8 +110,12 @@ class HipConv2d(nn.Module):
                     self.pc.to(src.device)
                     self._dev = src.device
                 if ent[1] == "cat":
-                    a, b = (t.permute(0, 2, 3, 1) for t in ent[2:])
-                    y = fused_conv2d_concat(a, b, self.pc, post_relu=self.post_relu)
+                    a = ent[2].permute(0, 2, 3, 1)
+                    d2s = scope.source_d2s(ent[3])
+                    if d2s is not None:  # the up-conv's sub-pixel output, read before its shuffle
+                        y = fused_conv2d_concat(a, d2s[0], self.pc, post_relu=self.post_relu, xb_d2s=True)
+                    else:
+                        y = fused_conv2d_concat(a, ent[3].permute(0, 2, 3, 1), self.pc, post_relu=self.post_relu)
                 else:
                     y = fused_conv2d(src.permute(0, 2, 3, 1), self.pc, inmode="pool2", post_relu=self.post_relu)
                 return y.permute(0, 3, 1, 2)
@@ -136,7 +140,9 @@ class HipConv2d(nn.Module):
     def _fusible(self, ent: tuple) -> bool:
         if ent[1] == "cat":
             return self.pc.ks == 3 and self.pc.cin_pad == ent[2].shape[1] + ent[3].shape[1]
-        return self.pc.cin_pad == ent[2].shape[1]  # pool: any kernel size, the loader pools 2x2
+        if ent[1] == "pool":
+            return self.pc.cin_pad == ent[2].shape[1]  # any kernel size: the loader pools 2x2
+        return False
 
     def extra_repr(self) -> str:
         return f"{self.cin}, {self.cout}, k={self.pc.ks}, post_relu={self.post_relu}"
@@ -146,6 +152,13 @@ class HipConv2d(nn.Module):
 _tls = threading.local()
 #: BE_UNET_LAZY=0: no deferred fusion (A/B)
 LAZY = os.environ.get("BE_UNET_LAZY", "1") != "0"
+
+
+# tensor metadata reads: they never need a placeholder's data, so they do not fill it
+_META = {torch.Tensor.shape.__get__, torch.Tensor.dtype.__get__, torch.Tensor.device.__get__,
+         torch.Tensor.is_cuda.__get__, torch.Tensor.requires_grad.__get__, torch.Tensor.ndim.__get__,
+         torch.Tensor.layout.__get__, torch.Tensor.dim, torch.Tensor.size, torch.Tensor.stride,
+         torch.Tensor.is_contiguous, torch.Tensor.numel}
 
 
 def _nhwc_dense(t: torch.Tensor) -> bool:
@@ -183,6 +196,24 @@ class DeferredFusion(TorchFunctionMode):
         ent = self.pending.get(id(t))
         return ent is not None and ent[0]() is t
 
+    def _kind(self, t) -> str | None:
+        ent = self.pending.get(id(t))
+        return ent[1] if ent is not None and ent[0]() is t else None
+
+    def source_d2s(self, t) -> tuple | None:
+        """(y, c) if ``t`` is a pending 2x2 depth-to-space placeholder of y [N, H, W, 4c]."""
+        ent = self.pending.get(id(t))
+        return ent[2:] if ent is not None and ent[0]() is t and ent[1] == "d2s" else None
+
+    def defer_d2s(self, y: torch.Tensor, c: int) -> torch.Tensor | None:
+        """Placeholder for the depth-to-space of y [N, H, W, 4c] (NHWC bf16), [N, c, 2H, 2W] channels-last."""
+        if not ((y.is_cuda or self.ALLOW_CPU) and y.dtype == torch.bfloat16 and y.is_contiguous()
+                and not y.requires_grad and c % 8 == 0):
+            return None
+        N, H, W, _ = y.shape
+        ph = torch.empty((N, c, 2 * H, 2 * W), dtype=y.dtype, device=y.device, memory_format=torch.channels_last)
+        return self._add(ph, "d2s", y, c)
+
     def _add(self, ph: torch.Tensor, kind: str, *srcs) -> torch.Tensor:
         self.pending[id(ph)] = (weakref.ref(ph), kind, *srcs)
         self.deferred += 1
@@ -206,7 +237,8 @@ class DeferredFusion(TorchFunctionMode):
         if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor) and a.dim() == b.dim()
                 and a.dim() in (4, 5) and dim in (1, 1 - a.dim())):
             return None
-        if not (self._ok_src(a) and self._ok_src(b) and a.device == b.device and a.shape[0] == b.shape[0]
+        b_ok = self._ok_src(b) or (a.dim() == 4 and self._kind(b) == "d2s")
+        if not (self._ok_src(a) and b_ok and a.device == b.device and a.shape[0] == b.shape[0]
                 and a.shape[2:] == b.shape[2:] and a.shape[1] % 8 == 0 and b.shape[1] % 8 == 0):
             return None
         shape = (a.shape[0], a.shape[1] + b.shape[1]) + tuple(a.shape[2:])
@@ -229,7 +261,10 @@ class DeferredFusion(TorchFunctionMode):
         if ph is None:
             return
         if kind == "cat":
+            self._fill_in(srcs)  # a source may be a deferred depth-to-space
             torch.cat(srcs, dim=1, out=ph)
+        elif kind == "d2s":
+            ph.permute(0, 2, 3, 1).copy_(depth_to_space2(srcs[0], srcs[1]))
         else:
             ph.copy_(F.max_pool2d(srcs[0], 2))
         self.filled += 1
@@ -268,7 +303,9 @@ class DeferredFusion(TorchFunctionMode):
                 self._fill_key(key)
 
     def flush(self) -> None:
-        for key in list(self.pending):
+        # newest first: a consumer entry (a cat) holds its deferred sources; dropping it first lets a
+        # source that nothing else kept die unfilled
+        for key in reversed(list(self.pending)):
             if key in self.pending:
                 self._fill_key(key)
 
@@ -278,7 +315,7 @@ class DeferredFusion(TorchFunctionMode):
             ph = self._defer_cat(args, kwargs)
             if ph is not None:
                 return ph
-        if self.pending:
+        if self.pending and func not in _META:
             self._fill_in(args)
             self._fill_in(kwargs)
             written = self._written(func, args, kwargs)
@@ -452,7 +489,8 @@ class HipConvTranspose2x2(nn.Module):
         self._dev = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if not x.is_cuda:
+        scope = getattr(_tls, "scope", None)  # (on CPU only in tests: DeferredFusion.ALLOW_CPU)
+        if not x.is_cuda and scope is None:
             return self.ref.to(x.device).float()(x.float()).to(x.dtype)
         if self._dev != x.device:
             self.pc.to(x.device)
@@ -462,8 +500,11 @@ class HipConvTranspose2x2(nn.Module):
         if C != self.pc.cin_pad:
             xh = F.pad(xh, (0, self.pc.cin_pad - C))
         y = fused_conv2d(xh.contiguous(), self.pc)  # [N, H, W, 4*Cout]
-        y = y.view(N, H, W, 2, 2, self.cout).permute(0, 1, 3, 2, 4, 5).reshape(N, 2 * H, 2 * W, self.cout)
-        return y.permute(0, 3, 1, 2)
+        if scope is not None:  # a decoder concatenation can read the sub-pixel layout in place
+            ph = scope.defer_d2s(y, self.cout)
+            if ph is not None:
+                return ph
+        return depth_to_space2(y, self.cout).permute(0, 3, 1, 2)
 
     def extra_repr(self) -> str:
         return f"{self.cin}, {self.cout}, k=2, s=2 (1x1 MFMA + depth-to-space)"

@@ -281,17 +281,30 @@ def fused_conv2d(x: torch.Tensor, pc: PackedConv, *, x2=None, scale=None, shift=
     return out
 
 
+def depth_to_space2(y: torch.Tensor, c: int) -> torch.Tensor:
+    """[N, H, W, 4 c] (channel (2 dy + dx) * c + k) -> [N, 2H, 2W, c] NHWC (a copy)."""
+    N, H, W, _ = y.shape
+    return y.view(N, H, W, 2, 2, c).permute(0, 1, 3, 2, 4, 5).reshape(N, 2 * H, 2 * W, c)
+
+
 def fused_conv2d_concat(xa: torch.Tensor, xb: torch.Tensor, pc: PackedConv, *, post_relu: bool = False,
-                        nw: int | None = None) -> torch.Tensor:
+                        nw: int | None = None, xb_d2s: bool = False) -> torch.Tensor:
     """3x3 conv (+ bias, + ReLU) of the channel concatenation [xa, xb] of two NHWC tensors
     ([N, H, W, Ca] and [N, H, W, Cb], ``pc`` packed for Ca + Cb input channels) without materialising
     it: ``be_conv2d_concat`` (INMODE 4) picks each 8-channel group's source in the halo loader.  Same
-    K order and accumulation as :func:`fused_conv2d` on ``torch.cat([xa, xb], -1)``."""
+    K order and accumulation as :func:`fused_conv2d` on ``torch.cat([xa, xb], -1)``.  ``xb_d2s``: xb is
+    [N, H/2, W/2, 4 Cb], a 2x2 transposed conv's sub-pixel channels before the depth-to-space shuffle
+    (INMODE 6 reads it in place)."""
     N, H, W, Ca = xa.shape
-    Cb = xb.shape[-1]
-    assert xb.shape[:3] == (N, H, W) and pc.ks == 3 and pc.cin_pad == Ca + Cb
+    Cb = xb.shape[-1] // 4 if xb_d2s else xb.shape[-1]
+    if xb_d2s:
+        assert xb.shape[:3] == (N, H // 2, W // 2) and H % 2 == 0 and W % 2 == 0
+    else:
+        assert xb.shape[:3] == (N, H, W)
+    assert pc.ks == 3 and pc.cin_pad == Ca + Cb
     if not xa.is_cuda:
-        return fused_conv2d(torch.cat([xa, xb], -1), pc, post_relu=post_relu)
+        xbf = depth_to_space2(xb, Cb) if xb_d2s else xb
+        return fused_conv2d(torch.cat([xa, xbf], -1), pc, post_relu=post_relu)
     assert xa.dtype == xb.dtype == torch.bfloat16 and xa.is_contiguous() and xb.is_contiguous()
     assert Ca % 8 == 0 and Cb % 8 == 0 and pc.cout % 4 == 0
     if pc.wp.device != xa.device:
@@ -299,5 +312,5 @@ def fused_conv2d_concat(xa: torch.Tensor, xb: torch.Tensor, pc: PackedConv, *, p
     out = torch.empty(N, H, W, pc.cout, device=xa.device, dtype=torch.bfloat16)
     _native.call("be_conv2d_concat", _native.ptr(xa), _native.ptr(xb), _native.ptr(pc.wp), _native.ptr(pc.bias),
                  _native.ptr(out), N, H, W, Ca, Cb, pc.cout, pc.ck, pc.tco, int(bool(post_relu)),
-                 int(nw or choose_nw(pc, H, W)), _native.stream(xa.device))
+                 int(nw or choose_nw(pc, H, W)), int(bool(xb_d2s)), _native.stream(xa.device))
     return out

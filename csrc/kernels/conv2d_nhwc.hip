@@ -186,6 +186,14 @@ __device__ __forceinline__ void issue_chunk(const ConvArgs& a, int n, int ty0, i
             r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.H + gy) * a.W + gx) * a.zC + c);
           else
             r = *reinterpret_cast<const u32x4*>(a.x2 + (((size_t)n * a.H + gy) * a.W + gx) * (a.Cin - a.zC) + (c - a.zC));
+        } else if (INMODE == 6) {  // INMODE 4 with x2 still in the 2x2 transposed conv's sub-pixel layout
+          if (c < a.zC) {
+            r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.H + gy) * a.W + gx) * a.zC + c);
+          } else {
+            const int cb = a.Cin - a.zC, sub = (gy & 1) * 2 + (gx & 1);
+            r = *reinterpret_cast<const u32x4*>(
+                a.x2 + (((size_t)n * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * (4 * cb) + sub * cb + (c - a.zC));
+          }
         } else if (INMODE == 1) {
           r = *reinterpret_cast<const u32x4*>(a.x + (((size_t)n * a.Hs + (gy >> 1)) * a.Ws + (gx >> 1)) * a.Cin + c);
         } else {
@@ -683,12 +691,12 @@ int dispatch_tco(int tco, int inmode, bool x2, int nw, const ConvArgs& a, hipStr
 
 }  // namespace
 
-template <int CK>
+template <int CK, int MODE>
 int dispatch_concat(int tco, int nw, const ConvArgs& a, hipStream_t s) {
   switch (tco) {
-    case 16: return dispatch_nw<3, CK, 16, 4, false>(nw, a, s);
-    case 32: return dispatch_nw<3, CK, 32, 4, false>(nw, a, s);
-    case 64: return dispatch_nw<3, CK, 64, 4, false>(nw, a, s);
+    case 16: return dispatch_nw<3, CK, 16, MODE, false>(nw, a, s);
+    case 32: return dispatch_nw<3, CK, 32, MODE, false>(nw, a, s);
+    case 64: return dispatch_nw<3, CK, 64, MODE, false>(nw, a, s);
   }
   return -2;
 }
@@ -785,9 +793,13 @@ int be_conv3d_ztaps_concat(const void* xa, const void* xb, const void* w, const 
 // per 8-channel group (INMODE 4).  The U-Net decoder's torch.cat([skip, up]) copy (~22 % of the 2-D EM
 // line's inference kernel time, profiles/r06/em2d/) disappears.  w: the packed layout of the conv over
 // Ca + Cb input channels; bias (+ ReLU) in the epilogue.
+// xb_d2s = 1: xb is [N, H/2, W/2, 4 * Cb] with channel (2 dy + dx) * Cb + c = channel c of pixel
+// (2y + dy, 2x + dx) -- the 1x1 MFMA conv half of ConvTranspose2d(k=2, s=2), read before its
+// depth-to-space shuffle (INMODE 6; H, W even).
 int be_conv2d_concat(const void* xa, const void* xb, const void* w, const float* bias, void* out, int N, int H, int W,
-                     int Ca, int Cb, int Cout, int ck, int tco, int relu, int nw, hipStream_t stream) {
+                     int Ca, int Cb, int Cout, int ck, int tco, int relu, int nw, int xb_d2s, hipStream_t stream) {
   if (Ca % 8 != 0 || Cb % 8 != 0 || (Ca + Cb) % ck != 0 || Cout % 4 != 0 || (ck != 8 && ck != 32)) return -10;
+  if (xb_d2s && ((H | W) & 1)) return -11;
   ConvArgs a = {};
   a.x = (const bf16_t*)xa; a.x2 = (const bf16_t*)xb; a.w = (const bf16_t*)w; a.bias = bias; a.out = out;
   a.N = N; a.H = H; a.W = W; a.Hs = H; a.Ws = W; a.Cin = Ca + Cb; a.Cout = Cout; a.cout_valid = Cout;
@@ -795,7 +807,8 @@ int be_conv2d_concat(const void* xa, const void* xb, const void* w, const float*
   a.prelu = relu ? 2 : 0;
   a.persist_blocks = g_persist_blocks;
   a.zC = Ca;
-  return ck == 8 ? dispatch_concat<8>(tco, nw, a, stream) : dispatch_concat<32>(tco, nw, a, stream);
+  if (xb_d2s) return ck == 8 ? dispatch_concat<8, 6>(tco, nw, a, stream) : dispatch_concat<32, 6>(tco, nw, a, stream);
+  return ck == 8 ? dispatch_concat<8, 4>(tco, nw, a, stream) : dispatch_concat<32, 4>(tco, nw, a, stream);
 }
 
 }  // extern "C"

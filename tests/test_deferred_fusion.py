@@ -64,6 +64,37 @@ def test_deferred_fusion_cpu_matches_eager(monkeypatch, leak_cat):
     assert err <= 0.05 * ref.abs().max().item() + 1e-2, err
 
 
+class TinyUp(nn.Module):
+    """up-conv -> cat -> conv (the decoder step), plus an optional second use of the up-conv output."""
+
+    def __init__(self, leak_up: bool = False):
+        super().__init__()
+        self.up = nn.ConvTranspose2d(32, 16, 2, stride=2)
+        self.dec = nn.Sequential(nn.Conv2d(32, 16, 3, padding=1), nn.ReLU())
+        self.leak_up = leak_up
+
+    def forward(self, x, s):
+        u = self.up(x)
+        y = self.dec(torch.cat([s, u], dim=1)).float()
+        return y + u.float().mean() if self.leak_up else y
+
+
+@pytest.mark.parametrize("leak_up", [False, True])
+def test_deferred_depth_to_space_cpu(monkeypatch, leak_up):
+    torch.manual_seed(1)
+    model, st = cv.optimize_for_mi355x(TinyUp(leak_up).eval())
+    assert st["conv_transpose"] == 1
+    x = torch.randn(2, 32, 8, 12).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    s = torch.randn(2, 16, 16, 24).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        ref = model(x, s)
+        monkeypatch.setattr(cv.DeferredFusion, "ALLOW_CPU", True)
+        out = model(x, s)
+    assert model._be_fusion_stats == (2, 1 if leak_up else 0)
+    err = (out - ref).abs().max().item()
+    assert err <= 0.05 * ref.abs().max().item() + 1e-2, err
+
+
 def test_scope_fills_on_any_other_use(monkeypatch):
     monkeypatch.setattr(cv.DeferredFusion, "ALLOW_CPU", True)
     a = torch.randn(1, 8, 4, 4).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -94,7 +125,7 @@ def test_unet2d_deferred_fusion_bit_identical(tmp_path, monkeypatch):
     x = torch.rand(4, 1, 256, 256, device=dev)
     fused = next(iter(pipe.predict_tensors(x).values())).float()
     assert pipe.convert_stats["pool2d"] == 3
-    assert pipe.model._be_fusion_stats == (6, 0)  # 3 pools + 3 concatenations deferred, none filled
+    assert pipe.model._be_fusion_stats == (9, 0)  # 3 pools, 3 up-conv shuffles, 3 concatenations; none filled
     monkeypatch.setattr(cv, "LAZY", False)
     plain = next(iter(pipe.predict_tensors(x).values())).float()
     assert torch.equal(fused, plain), (fused - plain).abs().max().item()
@@ -189,3 +220,22 @@ def test_unet3d_deferred_fusion_bit_identical(tmp_path, monkeypatch):
     monkeypatch.setattr(cv, "LAZY", False)
     plain = next(iter(pipe.predict_tensors(x).values())).float()
     assert torch.equal(fused, plain), (fused - plain).abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ca,cb", [(32, 32), (64, 64), (16, 16)])
+def test_conv2d_concat_subpixel_source_identical(ca, cb):
+    """INMODE 6 (the second source read in the 2x2 transposed conv's sub-pixel layout) is bit-identical
+    to INMODE 4 on the shuffled tensor."""
+    from bioengine_worker_amd.ops.conv import PackedConv, depth_to_space2, fused_conv2d_concat
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(2)
+    N, H, W = 2, 38, 70
+    a = torch.randn(N, H, W, ca, device=dev, generator=g).to(torch.bfloat16)
+    y4 = torch.randn(N, H // 2, W // 2, 4 * cb, device=dev, generator=g).to(torch.bfloat16)
+    w = torch.randn(32, ca + cb, 3, 3, device=dev, generator=g) / (3 * (ca + cb) ** 0.5)
+    pc = PackedConv.from_weight(w, torch.randn(32, device=dev, generator=g))
+    y = fused_conv2d_concat(a, y4, pc, post_relu=True, xb_d2s=True)
+    ref = fused_conv2d_concat(a, depth_to_space2(y4, cb).contiguous(), pc, post_relu=True)
+    assert torch.equal(y, ref)
