@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 6, s18: the sub-pixel concat source (INMODE 6): GPU tests, then the 2-D EM line A/B (64 x 2048^2)
+set -o pipefail
+mkdir -p gpurun_out/r06/s18
+cd /root/repo
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_deferred_fusion.py -m gpu > gpurun_out/r06/s18/tests.log 2>&1 || { tail -30 gpurun_out/r06/s18/tests.log; exit 1; }
+tail -2 gpurun_out/r06/s18/tests.log
+for arm in 1 0 1 0; do
+  BE_UNET_LAZY=$arm timeout -k 10 300 python -u tools/em2d_bench.py --em-z 64 --sweep 768:64:16 > gpurun_out/r06/s18/em2d_lazy$arm.log 2>&1 || { tail -20 gpurun_out/r06/s18/em2d_lazy$arm.log; exit 1; }
+  python - "$arm" <<'PY'
+import json, sys
+for l in open(f"gpurun_out/r06/s18/em2d_lazy{sys.argv[1]}.log"):
+    if l.startswith("{"):
+        d = json.loads(l); c = d["em_volume_config"]; t = c["stage_timings_s_rank0"]
+        print("lazy", sys.argv[1], round(d["em_volume_voxels_per_sec"] / 1e6, 1), "Mvox/s inference", t["inference"], "label", t["label"])
+PY
+done
