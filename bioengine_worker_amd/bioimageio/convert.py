@@ -123,7 +123,9 @@ class HipConv2d(nn.Module):
             y = F.conv2d(x.float(), self.pc.w.to(x.device), None if self.pc.bias is None else self.pc.bias.to(x.device),
                          padding=self.pc.ks // 2)
             y = torch.relu(y) if self.post_relu else y
-            return y.to(x.dtype).contiguous(memory_format=torch.channels_last)  # the GPU path's layout
+            y = y.to(x.dtype)
+            # the GPU path's layout, for the deferral tests (a scope exists on CPU only with ALLOW_CPU)
+            return y.contiguous(memory_format=torch.channels_last) if scope is not None else y
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
@@ -392,7 +394,8 @@ class HipConv3d(nn.Module):
             y = F.conv3d(x.float(), self.pc.w.to(x.device),
                          None if self.pc.bias is None else self.pc.bias.to(x.device), padding=self.pc.ks // 2)
             y = torch.relu(y) if self.post_relu else y
-            return y.to(x.dtype).contiguous(memory_format=torch.channels_last_3d)  # the GPU path's layout
+            y = y.to(x.dtype)
+            return y.contiguous(memory_format=torch.channels_last_3d) if scope is not None else y
         if self._dev != x.device:
             self.pc.to(x.device)
             self._dev = x.device
