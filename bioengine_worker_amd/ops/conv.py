@@ -71,11 +71,13 @@ class PackedConv:
 
     @classmethod
     def from_weight(cls, weight: torch.Tensor, bias: torch.Tensor | None = None, cin_pad: int | None = None,
-                    cout_pad_to: int | None = None) -> "PackedConv":
+                    cout_pad_to: int | None = None, exact_cin: bool = False) -> "PackedConv":
+        """``exact_cin``: keep a multiple-of-8 channel count as is (8-channel K chunks) instead of
+        padding it to a multiple of 32 (the 3-D U-Net's 16-channel layers, see ops/conv3d.py)."""
         cout, cin, ks, ks2 = weight.shape
         assert ks == ks2 and ks in (1, 3), "only 1x1 / 3x3 convs"
         cin_pad = cin_pad or _round_up(cin, 8)
-        if cin_pad % 32 and cin_pad != 8:
+        if cin_pad % 32 and cin_pad != 8 and not (exact_cin and cin_pad % 8 == 0):
             cin_pad = _round_up(cin_pad, 32)
         ck, tco = cls.choose(cin_pad, cout, ks)
         cout_k = max(cout, cout_pad_to or 0)

@@ -49,8 +49,13 @@ class PackedConv3d:
         self.w = weight.detach().float()
         self.bias = None if bias is None else bias.detach().float()
         self.cin, self.cout = cin, cout
+        # NARROW (default): a 16-channel layer keeps 16 input channels (8-channel K chunks) instead of
+        # being padded to 32 -- no padded copy of the activation in front of every such conv, a third
+        # fewer MFMA K steps, and the 1-channel stem takes the z-tap path too (BE_CONV3D_NARROW=0: the
+        # round-6 s8 layout, A/B)
+        narrow = os.environ.get("BE_CONV3D_NARROW", "1") != "0"
         self.taps = [PackedConv.from_weight(self.w[:, :, dz], self.bias if dz == kd // 2 else None,
-                                            cout_pad_to=cout_pad_to) for dz in range(kd)]
+                                            cout_pad_to=cout_pad_to, exact_cin=narrow) for dz in range(kd)]
         self.cin_pad = self.taps[0].cin_pad
         if kd == 3:
             # implicit-GEMM weights [Cout][kpad], k = (9 dz + 3 dy + dx) * cin_pad + c, zero-padded to 64
@@ -62,7 +67,7 @@ class PackedConv3d:
             # z-tap stacked 2-D weights for be_conv3d_ztaps: W'[co][dz * cin_pad + c][ky][kx]
             wz = F.pad(self.w, (0, 0, 0, 0, 0, 0, 0, self.cin_pad - cin)).permute(0, 2, 1, 3, 4)
             self.ztap = PackedConv.from_weight(wz.reshape(cout, 3 * self.cin_pad, 3, 3), self.bias,
-                                               cin_pad=3 * self.cin_pad)
+                                               cin_pad=3 * self.cin_pad, exact_cin=narrow)
 
     def to(self, device) -> "PackedConv3d":
         for t in self.taps:
