@@ -71,15 +71,19 @@ class PackedConv:
 
     @classmethod
     def from_weight(cls, weight: torch.Tensor, bias: torch.Tensor | None = None, cin_pad: int | None = None,
-                    cout_pad_to: int | None = None, exact_cin: bool = False) -> "PackedConv":
+                    cout_pad_to: int | None = None, exact_cin: bool = False, ck16: bool = False) -> "PackedConv":
         """``exact_cin``: keep a multiple-of-8 channel count as is (8-channel K chunks) instead of
-        padding it to a multiple of 32 (the 3-D U-Net's 16-channel layers, see ops/conv3d.py)."""
+        padding it to a multiple of 32 (the 3-D U-Net's 16-channel layers, see ops/conv3d.py);
+        ``ck16``: 16-channel K chunks when the count is an odd multiple of 16 (3x3 only; the z-tap
+        kernel's CK = 16 build)."""
         cout, cin, ks, ks2 = weight.shape
         assert ks == ks2 and ks in (1, 3), "only 1x1 / 3x3 convs"
         cin_pad = cin_pad or _round_up(cin, 8)
         if cin_pad % 32 and cin_pad != 8 and not (exact_cin and cin_pad % 8 == 0):
             cin_pad = _round_up(cin_pad, 32)
         ck, tco = cls.choose(cin_pad, cout, ks)
+        if ck16 and ks == 3 and ck == 8 and cin_pad % 16 == 0:
+            ck = 16
         cout_k = max(cout, cout_pad_to or 0)
         cout_pad = _round_up(cout_k, tco)
         kp = ((ks * ks * ck + 31) // 32) * 32

@@ -66,8 +66,11 @@ class PackedConv3d:
             self.b_mt = (self.bias if self.bias is not None else torch.zeros(cout)).float().contiguous()
             # z-tap stacked 2-D weights for be_conv3d_ztaps: W'[co][dz * cin_pad + c][ky][kx]
             wz = F.pad(self.w, (0, 0, 0, 0, 0, 0, 0, self.cin_pad - cin)).permute(0, 2, 1, 3, 4)
+            # BE_CONV3D_CK16=1: 16-channel K chunks for the 16-channel layers (5 instead of 6 K steps per
+            # 16 channels, half the chunk iterations; A/B)
+            ck16 = os.environ.get("BE_CONV3D_CK16", "0") == "1"
             self.ztap = PackedConv.from_weight(wz.reshape(cout, 3 * self.cin_pad, 3, 3), self.bias,
-                                               cin_pad=3 * self.cin_pad, exact_cin=narrow)
+                                               cin_pad=3 * self.cin_pad, exact_cin=narrow, ck16=ck16)
 
     def to(self, device) -> "PackedConv3d":
         for t in self.taps:

@@ -110,7 +110,8 @@ struct Cfg {
   static constexpr int TH = 2 * NW;
   static constexpr int HH = TH + KS - 1;
   static constexpr int HW_ = TW + KS - 1;
-  static constexpr int PSTR = CK == 8 ? 24 : CK + 16;  // dwords/pixel = 8 (mod 16) for CK=32/64; CK=8: 12
+  // dwords/pixel = 8 (mod 16) for CK = 16 / 32 / 64 (CK = 16 needs no pad: 8 dwords); CK = 8: 12
+  static constexpr int PSTR = CK == 8 ? 24 : (CK == 16 ? 16 : CK + 16);
   static constexpr int KSTEPS = (KS * KS * CK + 31) / 32;
   static constexpr int KPL = KSTEPS * 32;
   static constexpr int WSTR = KPL + 16;
@@ -760,7 +761,7 @@ int be_conv2d_nhwc(const void* x, const void* x2, const float* pscale, const flo
 // ~3x from L2 instead of 27x (the implicit-GEMM gather of be_conv3d_mt).
 int be_conv3d_ztaps(const void* x, const void* w, const float* bias, void* out, int N, int D, int H, int W, int zC,
                     int Cout, int ck, int tco, int relu, int nw, hipStream_t stream) {
-  if (zC % ck != 0 || Cout % 4 != 0 || (ck != 8 && ck != 32)) return -10;
+  if (zC % ck != 0 || Cout % 4 != 0 || (ck != 8 && ck != 16 && ck != 32)) return -10;
   ConvArgs a = {};
   a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.bias = bias; a.out = out;
   a.N = N * D; a.H = H; a.W = W; a.Hs = H; a.Ws = W; a.Cin = 3 * zC; a.Cout = Cout; a.cout_valid = Cout;
@@ -768,6 +769,7 @@ int be_conv3d_ztaps(const void* x, const void* w, const float* bias, void* out, 
   a.prelu = relu ? 2 : 0;
   a.persist_blocks = g_persist_blocks;
   a.zD = D; a.zC = zC;
+  if (ck == 16) return dispatch_ztaps<16>(tco, nw, a, stream);  // the 16-channel 3-D U-Net layers
   return ck == 8 ? dispatch_ztaps<8>(tco, nw, a, stream) : dispatch_ztaps<32>(tco, nw, a, stream);
 }
 

@@ -186,12 +186,15 @@ def test_head_1x1x1_small_cout(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ck16", ["0", "1"])
 @pytest.mark.parametrize("N,D,H,W,Cin,Cout", [(1, 8, 40, 72, 32, 64), (2, 5, 33, 20, 16, 32), (1, 6, 20, 36, 16, 16),
-                                              (1, 4, 24, 40, 128, 64)])
-def test_conv3d_ztaps_single_rounding(gpu, N, D, H, W, Cin, Cout, monkeypatch):
+                                              (1, 4, 24, 40, 128, 64), (1, 5, 18, 34, 1, 16)])
+def test_conv3d_ztaps_single_rounding(gpu, N, D, H, W, Cin, Cout, ck16, monkeypatch):
     """BE_CONV3D=ztaps: the 3x3x3 conv as ONE launch of the LDS-staged 2-D kernel with the depth taps
-    stacked on K, fp32 accumulation over all 27 taps, one bf16 rounding (same bound as the igemm)."""
+    stacked on K, fp32 accumulation over all 27 taps, one bf16 rounding (same bound as the igemm);
+    16- and 1-channel inputs unpadded (8-channel chunks, or 16 with BE_CONV3D_CK16=1)."""
     monkeypatch.setenv("BE_CONV3D", "ztaps")
+    monkeypatch.setenv("BE_CONV3D_CK16", ck16)
     g = torch.Generator().manual_seed(N * 1000 + D * 10 + Cin)
     w = torch.randn(Cout, Cin, 3, 3, 3, generator=g) / (27 * Cin) ** 0.5
     b = torch.randn(Cout, generator=g) * 0.1
