@@ -16,13 +16,14 @@ for l in open(f"gpurun_out/r06/s18/em2d_lazy{sys.argv[1]}.log"):
         print("lazy", sys.argv[1], round(d["em_volume_voxels_per_sec"] / 1e6, 1), "Mvox/s inference", t["inference"], "label", t["label"])
 PY
 done
-for arm in 1 0 1 0; do
-  BE_CONV3D_NARROW=$arm timeout -k 10 300 python -u tools/em3d_bench.py --em3d-z 64 --sweep 64:256:4 > gpurun_out/r06/s18/em3d_narrow$arm.log 2>&1 || { tail -20 gpurun_out/r06/s18/em3d_narrow$arm.log; exit 1; }
+for arm in n1c0 n1c1 n0c0 n1c0 n1c1; do
+  nar=${arm:1:1}; c16=${arm:3:1}
+  BE_CONV3D_NARROW=$nar BE_CONV3D_CK16=$c16 timeout -k 10 300 python -u tools/em3d_bench.py --em3d-z 64 --sweep 64:256:4 > gpurun_out/r06/s18/em3d_$arm.log 2>&1 || { tail -20 gpurun_out/r06/s18/em3d_$arm.log; exit 1; }
   python - "$arm" <<'PY'
 import json, sys
-for l in open(f"gpurun_out/r06/s18/em3d_narrow{sys.argv[1]}.log"):
+for l in open(f"gpurun_out/r06/s18/em3d_{sys.argv[1]}.log"):
     if l.startswith("{"):
         d = json.loads(l); c = d["em_volume3d_config"]; t = c["stage_timings_s_rank0"]
-        print("3d narrow", sys.argv[1], round(d["em_volume3d_voxels_per_sec"] / 1e6, 1), "Mvox/s inference", t["inference"], "label", t["label"])
+        print("3d", sys.argv[1], round(d["em_volume3d_voxels_per_sec"] / 1e6, 1), "Mvox/s inference", t["inference"], "label", t["label"])
 PY
 done
