@@ -40,6 +40,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import collections
 import os
 import threading
 import weakref
@@ -109,13 +110,12 @@ class HipConv2d(nn.Module):
                 if src.is_cuda and self._dev != src.device:
                     self.pc.to(src.device)
                     self._dev = src.device
-                if ent[1] == "cat":
-                    a = ent[2].permute(0, 2, 3, 1)
-                    d2s = scope.source_d2s(ent[3])
-                    if d2s is not None:  # the up-conv's sub-pixel output, read before its shuffle
-                        y = fused_conv2d_concat(a, d2s[0], self.pc, post_relu=self.post_relu, xb_d2s=True)
-                    else:
-                        y = fused_conv2d_concat(a, ent[3].permute(0, 2, 3, 1), self.pc, post_relu=self.post_relu)
+                if ent[1] == "cat_d2s":  # the up-conv's sub-pixel output, read before its shuffle
+                    y = fused_conv2d_concat(ent[2].permute(0, 2, 3, 1), ent[3], self.pc, post_relu=self.post_relu,
+                                            xb_d2s=True)
+                elif ent[1] == "cat":
+                    y = fused_conv2d_concat(ent[2].permute(0, 2, 3, 1), ent[3].permute(0, 2, 3, 1), self.pc,
+                                            post_relu=self.post_relu)
                 else:
                     y = fused_conv2d(src.permute(0, 2, 3, 1), self.pc, inmode="pool2", post_relu=self.post_relu)
                 return y.permute(0, 3, 1, 2)
@@ -142,6 +142,8 @@ class HipConv2d(nn.Module):
     def _fusible(self, ent: tuple) -> bool:
         if ent[1] == "cat":
             return self.pc.ks == 3 and self.pc.cin_pad == ent[2].shape[1] + ent[3].shape[1]
+        if ent[1] == "cat_d2s":
+            return self.pc.ks == 3 and self.pc.cin_pad == ent[2].shape[1] + ent[4]
         if ent[1] == "pool":
             return self.pc.cin_pad == ent[2].shape[1]  # any kernel size: the loader pools 2x2
         return False
@@ -189,6 +191,7 @@ class DeferredFusion(TorchFunctionMode):
         self.pending: dict[int, tuple] = {}  # id(placeholder) -> (weakref(placeholder), kind, *sources)
         self.deferred = 0
         self.filled = 0
+        self.filled_kinds: collections.Counter = collections.Counter()
 
     def _ok_src(self, t: torch.Tensor) -> bool:
         return ((t.is_cuda or self.ALLOW_CPU) and t.dtype == torch.bfloat16 and not t.requires_grad
@@ -246,6 +249,9 @@ class DeferredFusion(TorchFunctionMode):
         shape = (a.shape[0], a.shape[1] + b.shape[1]) + tuple(a.shape[2:])
         fmt = torch.channels_last if a.dim() == 4 else torch.channels_last_3d
         ph = torch.empty(shape, dtype=a.dtype, device=a.device, memory_format=fmt)
+        d2s = self.source_d2s(b)
+        if d2s is not None:  # hold the up-conv's sub-pixel output, not its (unfilled) placeholder
+            return self._add(ph, "cat_d2s", a, d2s[0], d2s[1])
         return self._add(ph, "cat", a, b)
 
     def take(self, x: torch.Tensor, fusible) -> tuple | None:
@@ -263,13 +269,15 @@ class DeferredFusion(TorchFunctionMode):
         if ph is None:
             return
         if kind == "cat":
-            self._fill_in(srcs)  # a source may be a deferred depth-to-space
             torch.cat(srcs, dim=1, out=ph)
+        elif kind == "cat_d2s":
+            torch.cat([srcs[0], depth_to_space2(srcs[1], srcs[2]).permute(0, 3, 1, 2)], dim=1, out=ph)
         elif kind == "d2s":
             ph.permute(0, 2, 3, 1).copy_(depth_to_space2(srcs[0], srcs[1]))
         else:
             ph.copy_(F.max_pool2d(srcs[0], 2))
         self.filled += 1
+        self.filled_kinds[kind] += 1
 
     def _fill_in(self, obj) -> None:
         if isinstance(obj, torch.Tensor):
@@ -301,7 +309,8 @@ class DeferredFusion(TorchFunctionMode):
         """Fill every pending placeholder with a source in the storage ``written`` is about to change."""
         ptrs = {t.untyped_storage().data_ptr() for t in written}
         for key, ent in list(self.pending.items()):
-            if any(s.untyped_storage().data_ptr() in ptrs for s in ent[2:]):
+            if key in self.pending and any(isinstance(s, torch.Tensor) and s.untyped_storage().data_ptr() in ptrs
+                                           for s in ent[2:]):
                 self._fill_key(key)
 
     def flush(self) -> None:
@@ -363,6 +372,7 @@ def _install_deferred_fusion(model: nn.Module) -> None:
         finally:
             _tls.scope = prev
         model._be_fusion_stats = (scope.deferred, scope.filled)
+        model._be_fusion_filled = dict(scope.filled_kinds)
         return out
 
     model.forward = forward

@@ -125,7 +125,8 @@ def test_unet2d_deferred_fusion_bit_identical(tmp_path, monkeypatch):
     x = torch.rand(4, 1, 256, 256, device=dev)
     fused = next(iter(pipe.predict_tensors(x).values())).float()
     assert pipe.convert_stats["pool2d"] == 3
-    assert pipe.model._be_fusion_stats == (9, 0)  # 3 pools, 3 up-conv shuffles, 3 concatenations; none filled
+    # 3 pools, 3 up-conv shuffles, 3 concatenations; none filled
+    assert pipe.model._be_fusion_stats == (9, 0), pipe.model._be_fusion_filled
     monkeypatch.setattr(cv, "LAZY", False)
     plain = next(iter(pipe.predict_tensors(x).values())).float()
     assert torch.equal(fused, plain), (fused - plain).abs().max().item()
