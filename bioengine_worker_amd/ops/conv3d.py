@@ -49,10 +49,10 @@ class PackedConv3d:
         self.w = weight.detach().float()
         self.bias = None if bias is None else bias.detach().float()
         self.cin, self.cout = cin, cout
-        # NARROW (default): a 16-channel layer keeps 16 input channels (8-channel K chunks) instead of
-        # being padded to 32 -- no padded copy of the activation in front of every such conv, a third
-        # fewer MFMA K steps, and the 1-channel stem takes the z-tap path too (BE_CONV3D_NARROW=0: the
-        # round-6 s8 layout, A/B)
+        # NARROW (default): a 16-channel layer keeps 16 input channels instead of being padded to 32 --
+        # no padded copy of the activation in front of every such conv, fewer MFMA K steps, and the
+        # 1-channel stem takes the z-tap path too: 683 vs 555 M voxel/s (profiles/r06/em3d/
+        # narrow_ck16_ab_s18.txt; BE_CONV3D_NARROW=0: the padded layout, A/B)
         narrow = os.environ.get("BE_CONV3D_NARROW", "1") != "0"
         self.taps = [PackedConv.from_weight(self.w[:, :, dz], self.bias if dz == kd // 2 else None,
                                             cout_pad_to=cout_pad_to, exact_cin=narrow) for dz in range(kd)]
@@ -66,9 +66,10 @@ class PackedConv3d:
             self.b_mt = (self.bias if self.bias is not None else torch.zeros(cout)).float().contiguous()
             # z-tap stacked 2-D weights for be_conv3d_ztaps: W'[co][dz * cin_pad + c][ky][kx]
             wz = F.pad(self.w, (0, 0, 0, 0, 0, 0, 0, self.cin_pad - cin)).permute(0, 2, 1, 3, 4)
-            # BE_CONV3D_CK16=1: 16-channel K chunks for the 16-channel layers (5 instead of 6 K steps per
-            # 16 channels, half the chunk iterations; A/B)
-            ck16 = os.environ.get("BE_CONV3D_CK16", "0") == "1"
+            # 16-channel K chunks for the 16-channel layers (5 instead of 6 K steps per 16 channels, half
+            # the chunk iterations): 707-710 vs 683-684 M voxel/s on the 3-D line's 64 x 2048^2 slab
+            # (profiles/r06/em3d/narrow_ck16_ab_s18.txt); BE_CONV3D_CK16=0: 8-channel chunks (A/B)
+            ck16 = os.environ.get("BE_CONV3D_CK16", "1") == "1"
             self.ztap = PackedConv.from_weight(wz.reshape(cout, 3 * self.cin_pad, 3, 3), self.bias,
                                                cin_pad=3 * self.cin_pad, exact_cin=narrow, ck16=ck16)
 
