@@ -226,12 +226,23 @@ MORPH_BITS = os.environ.get("BE_MORPH_BITS", "1") != "0"
 WS_ACTIVE_TILES = os.environ.get("BE_WS_ACTIVE", "1") != "0"
 
 
+#: relaxation iterations inside a tile per sweep / launches between convergence checks (A/B knobs)
+WS_MAX_LOCAL = int(os.environ.get("BE_WS_MAX_LOCAL", "32"))
+WS_CHECK_EVERY = int(os.environ.get("BE_WS_CHECK_EVERY", "4"))
+#: sweeps of the last watershed_gpu call (reported in the split-stage timings)
+LAST_WS_SWEEPS = 0
+
+
 def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor | None = None,
-                  max_local: int = 32, check_every: int = 4, max_sweeps: int = 100000) -> torch.Tensor:
+                  max_local: int | None = None, check_every: int | None = None,
+                  max_sweeps: int = 100000) -> torch.Tensor:
     """Marker watershed of ``elev`` ([H, W] or [D, H, W] fp32, device) with 4/6-connectivity as the
     parallel minimax-path fixpoint of ``em_watershed.hip`` (skimage ``watershed(elev, markers,
     mask=mask)``; ties between basins may resolve differently from the CPU priority flood).
     Sweeps repeat until no tile changes (checked every ``check_every`` launches)."""
+    global LAST_WS_SWEEPS
+    max_local = WS_MAX_LOCAL if max_local is None else max_local
+    check_every = WS_CHECK_EVERY if check_every is None else check_every
     dev = elev.device
     shape = tuple(elev.shape)
     D, H, W = (1,) + shape if elev.dim() == 2 else shape
@@ -268,6 +279,7 @@ def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor 
         sweeps += check_every
         if int(changed.item()) == 0:
             break
+    LAST_WS_SWEEPS = sweeps
     out = torch.empty(shape, dtype=torch.int32, device=dev)
     _native.call("be_ws_labels", _native.ptr(key), _native.ptr(flags), n, _native.ptr(out), st)
     return out
@@ -465,6 +477,8 @@ def prob_to_instances_3d(mask: torch.Tensor, min_size: int = 300, closing_radius
     else:
         labels = torch.from_numpy(watershed((-dist).cpu().numpy(), markers.cpu().numpy(), closed.cpu().numpy(), conn=1)).to(dev)
     _stage(timings, "watershed", t, dev)
+    if timings is not None and gpu_watershed:
+        timings["ws_sweeps"] = LAST_WS_SWEEPS
     return labels, int(len(peaks))
 
 
