@@ -214,7 +214,10 @@ __global__ __launch_bounds__(256) void edt3_bf(const float* __restrict__ fin, fl
 
 // lower envelope of parabolas along one axis: lines of length L, element stride `st`, line bases
 // from (line / inner) * outer_st + (line % inner) * inner_st.  f == 3e38 marks "no site".
-// only (optional): skip the lines whose flag is 0.
+// only (optional): skip the lines whose flag is 0.  The per-line stacks (parabola sites v, boundaries
+// z) are interleaved across lines -- entry k of line l at k * nlines + l -- so the threads of a wave,
+// which hold neighbouring lines at similar stack depths, touch neighbouring addresses (a line-major
+// stack put every thread's entry on its own cache line).
 __global__ void edt3_axis(const float* __restrict__ fin, float* __restrict__ fout, int* __restrict__ vbuf,
                           double* __restrict__ zbuf, long long nlines, int L, long long st, long long inner,
                           long long inner_st, long long outer_st, int take_sqrt,
@@ -223,25 +226,26 @@ __global__ void edt3_axis(const float* __restrict__ fin, float* __restrict__ fou
   if (line >= nlines) return;
   if (only && !only[line]) return;
   const long long base = (line / inner) * outer_st + (line % inner) * inner_st;
-  int* v = vbuf + line * L;
-  double* z = zbuf + line * (L + 1);
+  int* v = vbuf + line;     // v[k * nlines]
+  double* z = zbuf + line;  // z[k * nlines], k <= L
+  const long long S = nlines;
   int k = -1;
   for (int q = 0; q < L; ++q) {
     const float fq = fin[base + q * st];
     if (fq >= 3.0e38f) continue;
     if (k < 0) {
-      k = 0; v[0] = q; z[0] = -1e300; z[1] = 1e300;
+      k = 0; v[0] = q; z[0] = -1e300; z[S] = 1e300;
       continue;
     }
     double s;
     for (;;) {
-      const int p = v[k];
+      const int p = v[k * S];
       const double fp = fin[base + p * st];
       s = ((double)fq + (double)q * q - (fp + (double)p * p)) / (2.0 * (q - p));
-      if (s <= z[k] && k > 0) { --k; continue; }
+      if (s <= z[k * S] && k > 0) { --k; continue; }
       break;
     }
-    ++k; v[k] = q; z[k] = s; z[k + 1] = 1e300;
+    ++k; v[k * S] = q; z[k * S] = s; z[(k + 1) * S] = 1e300;
   }
   if (k < 0) {
     for (int q = 0; q < L; ++q) fout[base + q * st] = 3.0e38f;
@@ -249,9 +253,10 @@ __global__ void edt3_axis(const float* __restrict__ fin, float* __restrict__ fou
   }
   int j = 0;
   for (int q = 0; q < L; ++q) {
-    while (z[j + 1] < (double)q) ++j;
-    const double d = (double)(q - v[j]);
-    const double r = d * d + (double)fin[base + v[j] * st];
+    while (z[(j + 1) * S] < (double)q) ++j;
+    const int vj = v[j * S];
+    const double d = (double)(q - vj);
+    const double r = d * d + (double)fin[base + vj * st];
     fout[base + q * st] = take_sqrt ? (float)sqrt(r) : (float)r;
   }
 }
