@@ -26,6 +26,8 @@
 // slab.  A voxel whose search passes EDT_RCAP flags its line, and the envelope kernel then redoes
 // exactly the flagged lines (thick objects, columns with no background).  Squared distances are
 // integers below 2^24, exact in fp32, so both paths give the exact transform.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -142,6 +144,123 @@ __global__ __launch_bounds__(WS_TX* WS_TY* TZ) void ws_relax_kernel(const float*
       if (TZ > 1 && bz + 1 < tz_n) dirty_out[tile + txy] = 1;
     }
   }
+}
+
+// Wide-tile variant: TZ x 32 x 32 voxels per 1024-thread block, TZ / (1024 / (32 * 32)) = TZ voxels
+// per thread (one (y, x) column of the tile, z inner).  The flood crosses at most one tile boundary per
+// sweep, so on the EM lines (one basin front spanning the 2048^2 plane) the sweep count is set by
+// W / 16 = 128 tiles of the 16 x 16 kernel; 32 x 32 tiles halve it.  The thread's z voxels are relaxed
+// in order within an iteration (their updates are visible to the next z at once).
+template <int TZ>
+__global__ __launch_bounds__(1024) void ws_relax_wide_kernel(const float* __restrict__ elev,
+                                                             const unsigned char* __restrict__ flags,
+                                                             unsigned long long* __restrict__ key, int D, int H,
+                                                             int W, int tiles_x, int tiles_y, int max_local,
+                                                             int* __restrict__ changed,
+                                                             const unsigned char* __restrict__ dirty_in,
+                                                             unsigned char* __restrict__ dirty_out) {
+  constexpr int TX = 32, TY = 32;
+  constexpr int HX = TX + 2, HY = TY + 2, HZ = TZ == 1 ? 1 : TZ + 2;
+  constexpr int NH = HX * HY * HZ;
+  constexpr int NT = 1024;
+  __shared__ unsigned long long k_s[NH];
+  __shared__ unsigned e_s[NH];
+  __shared__ unsigned char f_s[NH];
+  __shared__ int any_s;
+  const int tid = threadIdx.x;
+  const int bx = blockIdx.x % tiles_x, by = blockIdx.x / tiles_x;
+  const int bz = blockIdx.y;
+  const long long tile = (long long)bz * tiles_x * tiles_y + blockIdx.x;
+  if (dirty_in && !dirty_in[tile]) return;  // workgroup-uniform
+  const int x0 = bx * TX - 1, y0 = by * TY - 1, z0 = TZ == 1 ? bz : bz * TZ - 1;
+  for (int e = tid; e < NH; e += NT) {
+    const int lx = e % HX, ly = (e / HX) % HY, lz = e / (HX * HY);
+    const int gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
+    unsigned long long kv = WS_NONE;
+    unsigned ev = 0xffffffffu;
+    unsigned char fv = 0;
+    if (gx >= 0 && gx < W && gy >= 0 && gy < H && gz >= 0 && gz < D) {
+      const long long g = ((long long)gz * H + gy) * W + gx;
+      kv = key[g];
+      ev = ordered(elev[g]);
+      fv = flags[g];
+    }
+    k_s[e] = kv;
+    e_s[e] = ev;
+    f_s[e] = fv;
+  }
+  if (tid == 0) any_s = 0;
+  __syncthreads();
+  const int tx = tid % TX, ty = tid / TX;
+  const int gx = x0 + 1 + tx, gy = y0 + 1 + ty;
+  const int c0 = (TZ == 1 ? 0 : 1) * HX * HY + (ty + 1) * HX + (tx + 1);
+  bool act[TZ];
+  unsigned ep[TZ];
+#pragma unroll
+  for (int z = 0; z < TZ; ++z) {
+    const int c = c0 + z * HX * HY;
+    const int gz = TZ == 1 ? z0 : z0 + 1 + z;
+    act[z] = gx < W && gy < H && gz < D && (f_s[c] & 1) && !(f_s[c] & 2);
+    ep[z] = e_s[c];
+  }
+  unsigned mine = 0;  // bit z: voxel z improved at least once
+  for (int it = 0; it < max_local; ++it) {
+    bool ch = false;
+#pragma unroll
+    for (int z = 0; z < TZ; ++z) {
+      if (!act[z]) continue;
+      const int c = c0 + z * HX * HY;
+      auto mn = [](unsigned long long a, unsigned long long b) { return a < b ? a : b; };
+      unsigned long long bn = mn(k_s[c - 1], k_s[c + 1]);
+      bn = mn(bn, mn(k_s[c - HX], k_s[c + HX]));
+      if (TZ > 1) bn = mn(bn, mn(k_s[c - HX * HY], k_s[c + HX * HY]));
+      if (bn != WS_NONE) {
+        const unsigned cq = (unsigned)(bn >> 32);
+        const unsigned hq = (unsigned)((bn >> WS_LABEL_BITS) & WS_HOP_MAX);
+        const unsigned lab = (unsigned)(bn & WS_LABEL_MASK);
+        const unsigned long long nk = pack_key(ep[z] > cq ? ep[z] : cq, ep[z] > cq ? 0u : hq + 1u, lab);
+        if (nk != k_s[c]) {
+          k_s[c] = nk;
+          ch = true;
+          mine |= 1u << z;
+        }
+      }
+    }
+    if (__syncthreads_or(ch) == 0) break;
+  }
+  if (mine) {
+#pragma unroll
+    for (int z = 0; z < TZ; ++z)
+      if (mine & (1u << z)) {
+        const int gz = TZ == 1 ? z0 : z0 + 1 + z;
+        key[((long long)gz * H + gy) * W + gx] = k_s[c0 + z * HX * HY];
+      }
+    any_s = 1;
+  }
+  __syncthreads();
+  if (tid == 0 && any_s) {
+    atomicOr(changed, 1);
+    if (dirty_out) {
+      const int tz_n = TZ == 1 ? D : (D + TZ - 1) / TZ;
+      const long long txy = (long long)tiles_x * tiles_y;
+      dirty_out[tile] = 1;
+      if (bx > 0) dirty_out[tile - 1] = 1;
+      if (bx + 1 < tiles_x) dirty_out[tile + 1] = 1;
+      if (by > 0) dirty_out[tile - tiles_x] = 1;
+      if (by + 1 < tiles_y) dirty_out[tile + tiles_x] = 1;
+      if (TZ > 1 && bz > 0) dirty_out[tile - txy] = 1;
+      if (TZ > 1 && bz + 1 < tz_n) dirty_out[tile + txy] = 1;
+    }
+  }
+}
+
+// BE_WS_TILE=16: the 16 x 16 (x 4) tiles of round 5 (A/B); default 32: ws_relax_wide_kernel
+static int ws_tile() {
+  static int t = [] {
+    const char* e = getenv("BE_WS_TILE");
+    return (e && atoi(e) == 16) ? 16 : 32;
+  }();
+  return t;
 }
 
 __global__ void ws_init_kernel(const float* __restrict__ elev, const int* __restrict__ markers,
@@ -359,6 +478,16 @@ int be_ws_init(const float* elev, const int* markers, const unsigned char* mask,
 
 int be_ws_relax(const float* elev, const unsigned char* flags, unsigned long long* key, int D, int H, int W, int max_local,
                 int* changed, hipStream_t s) {
+  if (ws_tile() == 32) {
+    const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32;
+    if (D == 1)
+      hipLaunchKernelGGL(ws_relax_wide_kernel<1>, dim3(tiles_x * tiles_y, 1), dim3(1024), 0, s, elev, flags, key, D, H, W,
+                         tiles_x, tiles_y, max_local, changed, nullptr, nullptr);
+    else
+      hipLaunchKernelGGL(ws_relax_wide_kernel<4>, dim3(tiles_x * tiles_y, (D + 3) / 4), dim3(1024), 0, s, elev, flags, key,
+                         D, H, W, tiles_x, tiles_y, max_local, changed, nullptr, nullptr);
+    return BE_CHECK_LAUNCH();
+  }
   const int tiles_x = (W + WS_TX - 1) / WS_TX, tiles_y = (H + WS_TY - 1) / WS_TY;
   if (D == 1) {
     hipLaunchKernelGGL(ws_relax_kernel<1>, dim3(tiles_x * tiles_y, 1), dim3(WS_TX * WS_TY), 0, s, elev, flags, key, D, H, W,
@@ -373,7 +502,8 @@ int be_ws_relax(const float* elev, const unsigned char* flags, unsigned long lon
 
 // Number of relaxation tiles (the size of the dirty-tile arrays of be_ws_relax_active).
 long long be_ws_tiles(int D, int H, int W) {
-  const long long txy = (long long)((W + WS_TX - 1) / WS_TX) * ((H + WS_TY - 1) / WS_TY);
+  const int t = ws_tile() == 32 ? 32 : WS_TX;
+  const long long txy = (long long)((W + t - 1) / t) * ((H + t - 1) / t);
   return D == 1 ? txy : txy * ((D + 3) / 4);
 }
 
@@ -381,8 +511,18 @@ long long be_ws_tiles(int D, int H, int W) {
 // changed and their face neighbours are flagged in dirty_out, which this call zeroes first.
 int be_ws_relax_active(const float* elev, const unsigned char* flags, unsigned long long* key, int D, int H, int W,
                        int max_local, int* changed, const unsigned char* dirty_in, unsigned char* dirty_out, hipStream_t s) {
-  const int tiles_x = (W + WS_TX - 1) / WS_TX, tiles_y = (H + WS_TY - 1) / WS_TY;
   (void)hipMemsetAsync(dirty_out, 0, (size_t)be_ws_tiles(D, H, W), s);
+  if (ws_tile() == 32) {
+    const int tiles_x = (W + 31) / 32, tiles_y = (H + 31) / 32;
+    if (D == 1)
+      hipLaunchKernelGGL(ws_relax_wide_kernel<1>, dim3(tiles_x * tiles_y, 1), dim3(1024), 0, s, elev, flags, key, D, H, W,
+                         tiles_x, tiles_y, max_local, changed, dirty_in, dirty_out);
+    else
+      hipLaunchKernelGGL(ws_relax_wide_kernel<4>, dim3(tiles_x * tiles_y, (D + 3) / 4), dim3(1024), 0, s, elev, flags, key,
+                         D, H, W, tiles_x, tiles_y, max_local, changed, dirty_in, dirty_out);
+    return BE_CHECK_LAUNCH();
+  }
+  const int tiles_x = (W + WS_TX - 1) / WS_TX, tiles_y = (H + WS_TY - 1) / WS_TY;
   if (D == 1) {
     hipLaunchKernelGGL(ws_relax_kernel<1>, dim3(tiles_x * tiles_y, 1), dim3(WS_TX * WS_TY), 0, s, elev, flags, key, D, H, W,
                        tiles_x, tiles_y, max_local, changed, dirty_in, dirty_out);
