@@ -231,6 +231,8 @@ WS_MAX_LOCAL = int(os.environ.get("BE_WS_MAX_LOCAL", "64"))  # 32: 0.063 s, 64: 
 WS_CHECK_EVERY = int(os.environ.get("BE_WS_CHECK_EVERY", "4"))
 #: sweeps of the last watershed_gpu call (reported in the split-stage timings)
 LAST_WS_SWEEPS = 0
+#: wide watershed tiles when the volume has more than this many voxels per marker (a basin ~64^3)
+WS_WIDE_VOXELS_PER_BASIN = 64 ** 3
 
 
 def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor | None = None,
@@ -248,7 +250,8 @@ def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor 
     D, H, W = (1,) + shape if elev.dim() == 2 else shape
     n = D * H * W
     mk = markers.to(torch.int32).contiguous()
-    if int(mk.max()) > _ws_max_label():
+    nmk = int(mk.max()) if mk.numel() else 0
+    if nmk > _ws_max_label():
         raise ValueError(f"watershed_gpu supports up to {_ws_max_label()} markers")
     e = elev.float().contiguous()
     m = mask.to(torch.uint8).contiguous() if mask is not None else None
@@ -256,6 +259,10 @@ def watershed_gpu(elev: torch.Tensor, markers: torch.Tensor, mask: torch.Tensor 
     flags = torch.empty(n, dtype=torch.uint8, device=dev)
     changed = torch.zeros(1, dtype=torch.int32, device=dev)
     st = _native.stream(dev)
+    # tile width from the marker density: wide (32) tiles when the basins are large (fewer sweeps for
+    # a front spanning the volume), 16 when many small basins keep the active front sparse
+    # (profiles/r06/README.md §10)
+    _native.call("be_ws_set_tile", 32 if nmk * WS_WIDE_VOXELS_PER_BASIN < n else 16)
     _native.call("be_ws_init", _native.ptr(e), _native.ptr(mk), _native.ptr(m), n, _native.ptr(key), _native.ptr(flags), st)
     sweeps = 0
     if WS_ACTIVE_TILES:

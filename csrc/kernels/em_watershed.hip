@@ -254,13 +254,19 @@ __global__ __launch_bounds__(1024) void ws_relax_wide_kernel(const float* __rest
   }
 }
 
-// BE_WS_TILE=16: the 16 x 16 (x 4) tiles of round 5 (A/B); default 32: ws_relax_wide_kernel
+// Tile width of the relaxation sweeps: 32 (ws_relax_wide_kernel) or 16 (the 16 x 16 (x 4) kernel).
+// Wide tiles halve the sweeps when few basins span the volume (3-D EM line: 136 -> 72 sweeps, 0.27 ->
+// 0.20 s) but cost more per active tile when many small basins keep the front sparse (2-D EM line,
+// ~10^4 basins: 0.27 -> 0.35 s), so the host picks per call from the marker density
+// (be_ws_set_tile); BE_WS_TILE=16 / 32 pins it.
+static int g_ws_tile = 0;
 static int ws_tile() {
-  static int t = [] {
+  static int env = [] {
     const char* e = getenv("BE_WS_TILE");
-    return (e && atoi(e) == 16) ? 16 : 32;
+    return e ? (atoi(e) == 16 ? 16 : 32) : 0;
   }();
-  return t;
+  if (env) return env;
+  return g_ws_tile == 16 ? 16 : 32;
 }
 
 __global__ void ws_init_kernel(const float* __restrict__ elev, const int* __restrict__ markers,
@@ -541,6 +547,12 @@ int be_ws_labels(const unsigned long long* key, const unsigned char* flags, long
 }
 
 int be_ws_max_label() { return (int)WS_LABEL_MASK; }
+
+// 16 or 32: the tile width of the following be_ws_tiles / be_ws_relax* calls (unless BE_WS_TILE is set)
+int be_ws_set_tile(int t) {
+  g_ws_tile = t == 16 ? 16 : 32;
+  return 0;
+}
 
 // 3-D EDT of fg [D, H, W] uint8 -> dist fp32.  tmp: [D*H*W] fp32; v: [D*H*W + D*max(H, W)] int
 // scratch (the tail holds the per-line fallback flags); z: [D*H*W + D*max(H, W)] double scratch
