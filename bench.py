@@ -257,8 +257,10 @@ def bench_served(seconds: float = 4.0, concurrency=(1, 64)) -> dict:
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     import serve_bench
 
+    # BE_SERVE_TIMELINE=PATH: per level, the start times of the requests at or above p99 and this
+    # process's GC pauses (tools/serve_bench.py --timeline)
     a = _ap.Namespace(size=512, concurrency=list(concurrency), seconds=seconds, gpus=1, replica_mode="process",
-                      max_ongoing=64, model="cyto3", profile=None)
+                      max_ongoing=64, model="cyto3", profile=None, timeline=os.environ.get("BE_SERVE_TIMELINE"))
     res = asyncio.run(serve_bench.main_async(a))
     out = {}
     for r in res:
