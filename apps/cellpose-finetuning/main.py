@@ -283,8 +283,11 @@ class CellposeFinetune:
         return sid
 
     # ------------------------------------------------------------------ lifecycle
-    #: batch sizes the replica runs once at start-up, largest first (BE_CELLPOSE_PREWARM=0 skips it)
-    PREWARM_BATCHES = (32, 16, 8, 4, 2, 1)
+    #: batch sizes the replica runs once at start-up, largest first (BE_CELLPOSE_PREWARM=0 skips it):
+    #: EVERY size the batcher can form (1..32), not only powers of two -- the c = 64 serving tail of
+    #: round 6 came as ~30 ms stalls at the first batch of a new size (3, 5, ...: allocator growth and
+    #: per-shape plans on the request path; profiles/r06/README.md §4)
+    PREWARM_BATCHES = tuple(range(32, 0, -1))
 
     async def async_init(self) -> None:
         await self._runner(self.default_model)

@@ -24,6 +24,10 @@ def test_async_init_prewarms_every_batch_size(tmp_path, monkeypatch):
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     cls = mod.CellposeFinetune.func_or_class
+    # the default covers every size the batcher can form (max_batch_size 32), largest first
+    assert cls.PREWARM_BATCHES == tuple(range(32, 0, -1))
+    # the mechanism on a CPU-sized subset (odd sizes included): each runs as one whole batch
+    monkeypatch.setattr(cls, "PREWARM_BATCHES", (7, 5, 3, 2, 1))
     app = cls(default_model="cyto3")
 
     async def main():
